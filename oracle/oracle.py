@@ -1,0 +1,133 @@
+"""ctypes front-end to oracle/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+The CPU restatement of the reference hot path (see sv_oracle.c's header for the file:line map).
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module; the
+product (supervillain_amd) never does.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from supervillain_amd._abi import SvRng, SvStats, rng_from_numpy, rng_to_numpy
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, 'liboracle.so')
+        if not os.path.exists(path):
+            raise RuntimeError(f'{path} is missing: run `make -C oracle` (or __graft_entry__.build())')
+        L = ctypes.CDLL(path)
+        P = ctypes.POINTER
+        i32, i64, f64, vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
+        L.sv_o_raw.argtypes = [P(SvRng), i64, vp]
+        L.sv_o_uniform.argtypes = [P(SvRng), f64, f64, i64, vp]
+        L.sv_o_integers.argtypes = [P(SvRng), ctypes.c_uint32, i64, vp]
+        L.sv_o_colors.argtypes = [i32, vp]
+        L.sv_o_villain_neighborhood.argtypes = [i32, f64, i64, f64, i64, vp, vp, i32, P(SvRng), vp]
+        L.sv_o_villain_action.argtypes = [i32, f64, vp, vp]
+        L.sv_o_villain_action.restype = f64
+        L.sv_o_worldline_coexact.argtypes = [i32, f64, f64, i64, vp, vp, i32, i32, P(SvRng), vp]
+        L.sv_o_worldline_plaquette_seq.argtypes = [i32, f64, f64, vp, vp, i32, vp, P(SvRng), vp]
+        L.sv_o_worldline_plaquette_cb.argtypes = [i32, f64, f64, vp, vp, i32, i32, P(SvRng), vp]
+        _LIB = L
+    return _LIB
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _stats_array(k):
+    return (SvStats * max(k, 1))()
+
+
+def raw(gen, count):
+    r = rng_from_numpy(gen)
+    out = np.empty(count, dtype=np.uint64)
+    lib().sv_o_raw(ctypes.byref(r), count, _ptr(out))
+    rng_to_numpy(r, gen)
+    return out
+
+
+def uniform(gen, low, high, count):
+    r = rng_from_numpy(gen)
+    out = np.empty(count, dtype=np.float64)
+    lib().sv_o_uniform(ctypes.byref(r), low, high, count, _ptr(out))
+    rng_to_numpy(r, gen)
+    return out
+
+
+def integers(gen, k, count):
+    r = rng_from_numpy(gen)
+    out = np.empty(count, dtype=np.int64)
+    lib().sv_o_integers(ctypes.byref(r), k, count, _ptr(out))
+    rng_to_numpy(r, gen)
+    return out
+
+
+def colors(N):
+    out = np.empty(N * N, dtype=np.int32)
+    ncol = lib().sv_o_colors(N, _ptr(out))
+    return ncol, out.reshape(N, N)
+
+
+def villain_neighborhood(N, kappa, W, phi, n, sweeps, gen, interval_phi=np.pi, interval_n=1):
+    """Run `sweeps` NeighborhoodUpdate sweeps in place on (phi (N,N) f64, n (2,N,N) i64)."""
+    assert phi.dtype == np.float64 and n.dtype == np.int64
+    assert phi.flags.c_contiguous and n.flags.c_contiguous
+    r = rng_from_numpy(gen)
+    st = _stats_array(sweeps)
+    rc = lib().sv_o_villain_neighborhood(N, kappa, int(W), interval_phi, int(interval_n), _ptr(phi), _ptr(n),
+                                         sweeps, ctypes.byref(r), st)
+    if rc != 0:
+        raise ValueError('oracle rejected the arguments')
+    rng_to_numpy(r, gen)
+    return [st[i] for i in range(sweeps)]
+
+
+def villain_action(N, kappa, phi, n):
+    return lib().sv_o_villain_action(N, kappa, _ptr(phi), _ptr(n))
+
+
+def worldline_coexact(N, kappa, W_eff, m, v, sweeps, gen, interval_t=1):
+    assert m.dtype == np.int64 and m.flags.c_contiguous and v.flags.c_contiguous
+    v_is_float = int(v.dtype == np.float64)
+    assert v_is_float or v.dtype == np.int64
+    r = rng_from_numpy(gen)
+    st = _stats_array(sweeps)
+    rc = lib().sv_o_worldline_coexact(N, kappa, float(W_eff), int(interval_t), _ptr(m), _ptr(v), v_is_float,
+                                      sweeps, ctypes.byref(r), st)
+    if rc != 0:
+        raise ValueError('oracle rejected the arguments')
+    rng_to_numpy(r, gen)
+    return [st[i] for i in range(sweeps)]
+
+
+def worldline_plaquette_seq(N, kappa, W_eff, m, v, order, gen):
+    v_is_float = int(v.dtype == np.float64)
+    order = np.ascontiguousarray(order, dtype=np.int64)
+    r = rng_from_numpy(gen)
+    st = _stats_array(1)
+    rc = lib().sv_o_worldline_plaquette_seq(N, kappa, float(W_eff), _ptr(m), _ptr(v), v_is_float, _ptr(order),
+                                            ctypes.byref(r), st)
+    if rc != 0:
+        raise ValueError('oracle rejected the arguments')
+    rng_to_numpy(r, gen)
+    return st[0]
+
+
+def worldline_plaquette_cb(N, kappa, W_eff, m, v, sweeps, gen):
+    v_is_float = int(v.dtype == np.float64)
+    r = rng_from_numpy(gen)
+    st = _stats_array(sweeps)
+    rc = lib().sv_o_worldline_plaquette_cb(N, kappa, float(W_eff), _ptr(m), _ptr(v), v_is_float, sweeps,
+                                           ctypes.byref(r), st)
+    if rc != 0:
+        raise ValueError('oracle rejected the arguments')
+    rng_to_numpy(r, gen)
+    return [st[i] for i in range(sweeps)]

@@ -1,0 +1,535 @@
+/*
+ * sv_oracle.c -- CPU restatement of the reference hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * This file is the parity checker for the HIP product path, never part of it: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load liboracle.so.  It is pinned
+ * against golden vectors captured from the reference itself (tests/golden/, made by
+ * tools/make_golden.py through tools/refshim.py in the survey container).
+ *
+ * What it restates (all citations are /root/reference paths):
+ *   - NumPy's Generator(PCG64) draw semantics used by the generators (third-party, NumPy 2.2.6 in
+ *     this image): PCG64 XSL-RR 128/64 step-then-output, uniform() as
+ *     low + range*((u64>>11)*2^-53), choice(seq,k) == seq[integers(0,len)] via the buffered 32-bit
+ *     Lemire rejection sampler whose half-word buffer lives in the bit generator state.
+ *   - NeighborhoodUpdate.step     supervillain/generator/villain/neighborhood.py:59-137
+ *   - CoexactUpdate.step          supervillain/generator/worldline/coexact.py:53-128
+ *   - PlaquetteUpdate.step        supervillain/generator/worldline/plaquette.py:35-104 (visit order
+ *     supplied by the caller, since the reference draws it from NumPy's global MT19937)
+ *   - the D=2 operators d/delta/face_sum/coface_sum in the reference's summation order
+ *     supervillain/lattice/reference.py:9-81, _operator_tables compact.py:143-174,
+ *     coface_sum_at compact.py:1185-1247, delta_sparse compact.py:1042-1116
+ *   - Lattice.checkerboarding     supervillain/lattice/compact.py:191-239 (odd N: 4 colours built
+ *     from FFT-convention coordinates, lattice/__init__.py:4-9, compact.py:36-53)
+ * plus one chain the reference does not have: the checkerboard PlaquetteUpdate variant the GPU
+ * runs in mode="checkerboard" (defined in DESIGN.md); here it is the bit-exact oracle for that mode.
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off, no fast-math: the op order IS the spec).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef unsigned __int128 u128;
+
+typedef struct {
+    uint64_t state_hi, state_lo, inc_hi, inc_lo;
+    int32_t has_uint32;
+    uint32_t uinteger;
+} sv_rng;
+
+typedef struct {
+    int64_t accepted;
+    int64_t proposed;
+    double acceptance_sum; /* sum of per-proposal Metropolis probabilities in this sweep */
+    int64_t rejections;    /* Lemire rejections met in this sweep (diagnostic) */
+} sv_stats;
+
+/* ---------------------------------------------------------------- PCG64 (NumPy) */
+static const u128 PCG_MULT = (((u128)0x2360ED051FC65DA4ULL) << 64) | (u128)0x4385DF649FCCF645ULL;
+
+typedef struct {
+    u128 s, inc;
+    int has;
+    uint32_t buf;
+} pcg;
+
+static pcg pcg_load(const sv_rng *r) {
+    pcg g;
+    g.s = (((u128)r->state_hi) << 64) | r->state_lo;
+    g.inc = (((u128)r->inc_hi) << 64) | r->inc_lo;
+    g.has = r->has_uint32;
+    g.buf = r->uinteger;
+    return g;
+}
+
+static void pcg_store(const pcg *g, sv_rng *r) {
+    r->state_hi = (uint64_t)(g->s >> 64);
+    r->state_lo = (uint64_t)g->s;
+    r->has_uint32 = g->has;
+    r->uinteger = g->buf;
+}
+
+static inline uint64_t pcg_u64(pcg *g) {
+    g->s = g->s * PCG_MULT + g->inc; /* advance first ... */
+    uint64_t x = (uint64_t)(g->s >> 64) ^ (uint64_t)g->s;
+    unsigned rot = (unsigned)(g->s >> 122);
+    return (x >> rot) | (x << ((64u - rot) & 63u)); /* ... then XSL-RR output */
+}
+
+static inline double pcg_double(pcg *g) { return (double)(pcg_u64(g) >> 11) * (1.0 / 9007199254740992.0); }
+
+static inline double pcg_uniform(pcg *g, double low, double range) {
+    double d = pcg_double(g);
+    double t = range * d;
+    return low + t;
+}
+
+static inline uint32_t pcg_u32(pcg *g) {
+    if (g->has) {
+        g->has = 0;
+        return g->buf;
+    }
+    uint64_t x = pcg_u64(g);
+    g->has = 1;
+    g->buf = (uint32_t)(x >> 32);
+    return (uint32_t)x;
+}
+
+/* integers(0, k) for 1 <= k <= 2^32 via NumPy's buffered bounded Lemire (32-bit path).
+ * k == 1 consumes nothing (NumPy returns `off` when rng == 0). */
+static inline uint32_t pcg_bounded(pcg *g, uint32_t k, int64_t *rejections) {
+    if (k <= 1) return 0;
+    uint32_t thr = (uint32_t)((0u - k) % k); /* (2^32 - k) mod k */
+    uint64_t m = (uint64_t)pcg_u32(g) * (uint64_t)k;
+    uint32_t left = (uint32_t)m;
+    if (left < k) {
+        while (left < thr) {
+            if (rejections) (*rejections)++;
+            m = (uint64_t)pcg_u32(g) * (uint64_t)k;
+            left = (uint32_t)m;
+        }
+    }
+    return (uint32_t)(m >> 32);
+}
+
+/* ---------------------------------------------------------------- KAT helpers */
+int sv_o_raw(sv_rng *r, int64_t count, uint64_t *out) {
+    pcg g = pcg_load(r);
+    for (int64_t i = 0; i < count; i++) out[i] = pcg_u64(&g);
+    pcg_store(&g, r);
+    return 0;
+}
+
+int sv_o_uniform(sv_rng *r, double low, double high, int64_t count, double *out) {
+    pcg g = pcg_load(r);
+    double range = high - low;
+    for (int64_t i = 0; i < count; i++) out[i] = pcg_uniform(&g, low, range);
+    pcg_store(&g, r);
+    return 0;
+}
+
+int sv_o_integers(sv_rng *r, uint32_t k, int64_t count, int64_t *out) {
+    pcg g = pcg_load(r);
+    for (int64_t i = 0; i < count; i++) out[i] = pcg_bounded(&g, k, NULL);
+    pcg_store(&g, r);
+    return 0;
+}
+
+/* ---------------------------------------------------------------- lattice (D=2) */
+static inline int64_t wrap(int64_t i, int64_t N) { return ((i % N) + N) % N; }
+
+/* FFT-convention coordinate, lattice/__init__.py:4-9: [0..N//2] then [-N//2+1 .. -1]. */
+static inline int64_t fftc(int64_t i, int64_t N) { return i <= N / 2 ? i : i - N; }
+
+/* Colour of every site and the colour count, compact.py:191-239 for D=2.
+ * Even N: parity of the coordinate sum.  Odd N: 4 colours ordered (b,c) =
+ * (0,0),(0,1),(1,0),(1,1) with b the hyperoctant pair and c the parity. */
+int sv_o_colors(int32_t N, int32_t *color_of_site) {
+    int64_t V = (int64_t)N * N;
+    for (int64_t t = 0; t < N; t++)
+        for (int64_t x = 0; x < N; x++) {
+            int64_t c0 = fftc(t, N), c1 = fftc(x, N);
+            int par = (int)((((c0 + c1) % 2) + 2) % 2);
+            int col;
+            if (N % 2 == 0) {
+                col = par;
+            } else {
+                int b0 = (c0 >= 0 && c1 >= 0) || (c0 < 0 && c1 < 0);
+                int b = b0 ? 0 : 1;
+                col = 2 * b + par;
+            }
+            color_of_site[t * N + x] = col;
+        }
+    (void)V;
+    return N % 2 == 0 ? 2 : 4;
+}
+
+/* Colour site lists in np.where (row-major) order. */
+typedef struct {
+    int ncol;
+    int64_t count[4];
+    int64_t *sites[4];
+} colors_t;
+
+static colors_t colors_make(int32_t N) {
+    colors_t C;
+    int64_t V = (int64_t)N * N;
+    int32_t *col = (int32_t *)malloc(sizeof(int32_t) * V);
+    C.ncol = sv_o_colors(N, col);
+    for (int c = 0; c < 4; c++) {
+        C.count[c] = 0;
+        C.sites[c] = (int64_t *)malloc(sizeof(int64_t) * (V + 1));
+    }
+    for (int64_t s = 0; s < V; s++) {
+        int c = col[s];
+        C.sites[c][C.count[c]++] = s;
+    }
+    free(col);
+    return C;
+}
+
+static void colors_free(colors_t *C) {
+    for (int c = 0; c < 4; c++) free(C->sites[c]);
+}
+
+/* neighbours: e0 moves t (axis 0, rows), e1 moves x (axis 1, columns) */
+static inline int64_t fwd(int64_t s, int mu, int64_t N) {
+    int64_t t = s / N, x = s % N;
+    if (mu == 0) t = (t + 1) % N; else x = (x + 1) % N;
+    return t * N + x;
+}
+static inline int64_t bwd(int64_t s, int mu, int64_t N) {
+    int64_t t = s / N, x = s % N;
+    if (mu == 0) t = (t + N - 1) % N; else x = (x + N - 1) % N;
+    return t * N + x;
+}
+
+#define TWO_PI 6.283185307179586 /* Python's 2*np.pi, rounded once */
+
+/* ---------------------------------------------------------------- Villain NeighborhoodUpdate */
+/* One sweep of neighborhood.py:59-137 on D=2.  phi: (N,N) f64, n: (2,N,N) i64, in place. */
+static void villain_sweep(int64_t N, double kappa, int64_t W, double interval_phi, int64_t interval_n,
+                          double *phi, int64_t *n, pcg *g, const colors_t *C, sv_stats *st, double *work) {
+    int64_t V = N * N;
+    double *metro = work;          /* V */
+    double *r = metro + V;         /* 2V */
+    double *cphi = r + 2 * V;      /* V */
+    double *dSl = cphi + V;        /* 2V */
+    int64_t *cn = (int64_t *)(dSl + 2 * V); /* 2V */
+    int64_t *acc = cn + 2 * V;     /* V (per-site accepted flag for the current colour) */
+    const double half_kappa = kappa / 2.0;
+    const uint32_t k = (uint32_t)(2 * interval_n + 1);
+    const double range_phi = interval_phi - (-interval_phi);
+
+    memset(st, 0, sizeof(*st));
+    for (int64_t s = 0; s < V; s++) metro[s] = pcg_uniform(g, 0.0, 1.0); /* :87 */
+    for (int mu = 0; mu < 2; mu++)                                         /* :91 */
+        for (int64_t s = 0; s < V; s++)
+            r[mu * V + s] = (0.0 + (phi[fwd(s, mu, N)] - phi[s])) - TWO_PI * (double)n[mu * V + s];
+
+    for (int c = 0; c < C->ncol; c++) { /* :93 */
+        const int64_t nc = C->count[c];
+        const int64_t *sites = C->sites[c];
+        for (int64_t s = 0; s < V; s++) cphi[s] = 0.0;
+        for (int64_t l = 0; l < 2 * V; l++) cn[l] = 0;
+        for (int64_t i = 0; i < nc; i++) cphi[sites[i]] = pcg_uniform(g, -interval_phi, range_phi); /* :98 */
+        for (int mu = 0; mu < 2; mu++) { /* :104-107 */
+            for (int64_t i = 0; i < nc; i++)
+                cn[mu * V + sites[i]] = W * ((int64_t)pcg_bounded(g, k, &st->rejections) - interval_n);
+            for (int64_t i = 0; i < nc; i++)
+                cn[mu * V + bwd(sites[i], mu, N)] = W * ((int64_t)pcg_bounded(g, k, &st->rejections) - interval_n);
+        }
+        /* :110-112  change_r = d(change_phi) - 2 pi change_n ; dS_link ; face_sum */
+        for (int mu = 0; mu < 2; mu++)
+            for (int64_t s = 0; s < V; s++) {
+                double cr = (0.0 + (cphi[fwd(s, mu, N)] - cphi[s])) - TWO_PI * (double)cn[mu * V + s];
+                double a = half_kappa * cr;
+                double b = (2.0 * r[mu * V + s]) + cr;
+                dSl[mu * V + s] = a * b;
+            }
+        for (int64_t i = 0; i < nc; i++) { /* :115-118 */
+            int64_t s = sites[i];
+            double dS = 0.0;
+            dS += dSl[0 * V + s];
+            dS += dSl[0 * V + bwd(s, 0, N)];
+            dS += dSl[1 * V + s];
+            dS += dSl[1 * V + bwd(s, 1, N)];
+            double p = exp(-dS);
+            p = p < 0.0 ? 0.0 : p;
+            p = p > 1.0 ? 1.0 : p;
+            int a = metro[s] < p;
+            acc[s] = a;
+            st->accepted += a;
+            st->acceptance_sum += p;
+        }
+        for (int64_t i = 0; i < nc; i++) { /* :121-125 */
+            int64_t s = sites[i];
+            double a = (double)acc[s];
+            cphi[s] = cphi[s] * a;
+            for (int mu = 0; mu < 2; mu++) {
+                cn[mu * V + s] *= acc[s];
+                cn[mu * V + bwd(s, mu, N)] *= acc[s];
+            }
+        }
+        for (int64_t s = 0; s < V; s++) phi[s] = phi[s] + cphi[s]; /* :127 */
+        for (int64_t l = 0; l < 2 * V; l++) n[l] = n[l] + cn[l];    /* :128 */
+        for (int mu = 0; mu < 2; mu++)                              /* :129 */
+            for (int64_t s = 0; s < V; s++) {
+                double dcp = 0.0 + (cphi[fwd(s, mu, N)] - cphi[s]);
+                r[mu * V + s] = (r[mu * V + s] + dcp) - TWO_PI * (double)cn[mu * V + s];
+            }
+    }
+    st->proposed = V;
+}
+
+int sv_o_villain_neighborhood(int32_t N, double kappa, int64_t W, double interval_phi, int64_t interval_n,
+                              double *phi, int64_t *n, int32_t sweeps, sv_rng *rng, sv_stats *stats) {
+    if (N < 2 || sweeps < 0) return -1;
+    int64_t V = (int64_t)N * N;
+    colors_t C = colors_make(N);
+    double *work = (double *)malloc(sizeof(double) * 6 * V + sizeof(int64_t) * 3 * V);
+    pcg g = pcg_load(rng);
+    for (int32_t s = 0; s < sweeps; s++)
+        villain_sweep(N, kappa, W, interval_phi, interval_n, phi, n, &g, &C, &stats[s], work);
+    pcg_store(&g, rng);
+    free(work);
+    colors_free(&C);
+    return 0;
+}
+
+/* Villain action, villain.py:51-66 (sequential sum; the reference uses NumPy pairwise). */
+double sv_o_villain_action(int32_t N, double kappa, const double *phi, const int64_t *n) {
+    int64_t V = (int64_t)N * N;
+    double S = 0.0;
+    for (int mu = 0; mu < 2; mu++)
+        for (int64_t s = 0; s < V; s++) {
+            double l = (0.0 + (phi[fwd(s, mu, N)] - phi[s])) - TWO_PI * (double)n[mu * V + s];
+            S += l * l;
+        }
+    return (kappa / 2.0) * S;
+}
+
+/* ---------------------------------------------------------------- Worldline helpers */
+/* delta(v)/_W for a D=2 two-form v (comp (0,1)), reference.py:27-45 with table rows
+ * ('delta',2) = (0,0,1,-1),(1,0,0,+1): dv0[x] = 0 - (-1)(v[x]-v[x-e1]), dv1[x] = 0 - (+1)(v[x]-v[x-e0]).
+ * coexact.py:80 / plaquette.py:53 then divide by _W (worldline.py:49). */
+static void delta_v_by_W(int64_t N, const void *v, int v_is_float, double Weff, double *dvw) {
+    int64_t V = N * N;
+    for (int64_t s = 0; s < V; s++) {
+        int64_t b1 = bwd(s, 1, N), b0 = bwd(s, 0, N);
+        double d0, d1;
+        if (v_is_float) {
+            const double *vf = (const double *)v;
+            double a = vf[s] - vf[b1];
+            double b = vf[s] - vf[b0];
+            d0 = 0.0 - (-a);
+            d1 = 0.0 - b;
+        } else {
+            const int64_t *vi = (const int64_t *)v;
+            d0 = (double)(0 - (-(vi[s] - vi[b1])));
+            d1 = (double)(0 - (vi[s] - vi[b0]));
+        }
+        dvw[s] = d0 / Weff;
+        dvw[V + s] = d1 / Weff;
+    }
+}
+
+/* ---------------------------------------------------------------- Worldline CoexactUpdate */
+/* coexact.py:53-128 on D=2 (one 2-form component).  ts = (-it..-1, 1..it).
+ * Plaquette at x with value t changes  m0[x] += t, m0[x+e1] -= t, m1[x] -= t, m1[x+e0] += t
+ * (delta_sparse with ('delta',2) rows), and dS sums dS_link in coface_sum_at row order
+ * ('coface_sum',1) = (0,1,0,1),(0,0,1,1):  dl1[x], dl1[x+e0], dl0[x], dl0[x+e1]. */
+int sv_o_worldline_coexact(int32_t N_, double kappa, double Weff, int64_t interval_t, int64_t *m, const void *v,
+                           int32_t v_is_float, int32_t sweeps, sv_rng *rng, sv_stats *stats) {
+    int64_t N = N_, V = N * N;
+    if (N < 2 || interval_t < 1) return -1;
+    colors_t C = colors_make(N_);
+    double *dvw = (double *)malloc(sizeof(double) * 2 * V);
+    double *metro = (double *)malloc(sizeof(double) * V);
+    int64_t *tv = (int64_t *)malloc(sizeof(int64_t) * V);
+    delta_v_by_W(N, v, v_is_float, Weff, dvw);
+    const double c = 0.5 / kappa;
+    const uint32_t k = (uint32_t)(2 * interval_t);
+    pcg g = pcg_load(rng);
+    for (int32_t sw = 0; sw < sweeps; sw++) {
+        sv_stats *st = &stats[sw];
+        memset(st, 0, sizeof(*st));
+        for (int64_t s = 0; s < V; s++) metro[s] = pcg_uniform(&g, 0.0, 1.0); /* :89 */
+        for (int col = 0; col < C.ncol; col++) {
+            const int64_t nc = C.count[col];
+            const int64_t *sites = C.sites[col];
+            for (int64_t i = 0; i < nc; i++) { /* :99 choice(ts) */
+                int64_t j = (int64_t)pcg_bounded(&g, k, &st->rejections);
+                tv[i] = j < interval_t ? j - interval_t : j - interval_t + 1;
+            }
+            for (int64_t i = 0; i < nc; i++) {
+                int64_t x = sites[i], t = tv[i];
+                int64_t xe0 = fwd(x, 0, N), xe1 = fwd(x, 1, N);
+                /* links and their cm, in coface order */
+                int64_t L[4] = {V + x, V + xe0, x, xe1};
+                int64_t cm[4] = {-t, +t, +t, -t};
+                double dS = 0.0;
+                for (int q = 0; q < 4; q++) {
+                    double a = c * (double)cm[q];
+                    double f = (double)m[L[q]] - dvw[L[q]];
+                    double b = (2.0 * f) + (double)cm[q];
+                    dS += a * b;
+                }
+                double p = exp(-dS);
+                p = p < 0.0 ? 0.0 : p;
+                p = p > 1.0 ? 1.0 : p;
+                int a = metro[x] < p;
+                st->accepted += a;
+                st->acceptance_sum += p;
+                if (a) { /* :120 (links of same-colour plaquettes are disjoint) */
+                    m[x] += t;
+                    m[xe1] -= t;
+                    m[V + x] -= t;
+                    m[V + xe0] += t;
+                }
+            }
+        }
+        st->proposed = V;
+    }
+    pcg_store(&g, rng);
+    free(dvw);
+    free(metro);
+    free(tv);
+    colors_free(&C);
+    return 0;
+}
+
+/* ---------------------------------------------------------------- Worldline PlaquetteUpdate */
+/* plaquette.py:35-104 on D=2 with the visit order supplied (order[i] = row-major site of the i-th
+ * entry of np.random.permutation(L.coordinates)).  One sweep. */
+int sv_o_worldline_plaquette_seq(int32_t N_, double kappa, double Weff, int64_t *m, void *v, int32_t v_is_float,
+                                 const int64_t *order, sv_rng *rng, sv_stats *st) {
+    int64_t N = N_, V = N * N;
+    if (N < 2) return -1;
+    double *f = (double *)malloc(sizeof(double) * 2 * V);
+    int64_t *cm = (int64_t *)malloc(sizeof(int64_t) * V);
+    int64_t *cv = (int64_t *)malloc(sizeof(int64_t) * V);
+    double *met = (double *)malloc(sizeof(double) * V);
+    memset(st, 0, sizeof(*st));
+    delta_v_by_W(N, v, v_is_float, Weff, f);
+    for (int64_t l = 0; l < 2 * V; l++) f[l] = (double)m[l] - f[l]; /* :53 */
+    pcg g = pcg_load(rng);
+    for (int64_t i = 0; i < V; i++) cm[i] = pcg_bounded(&g, 2, &st->rejections) ? 1 : -1;          /* :58 */
+    for (int64_t i = 0; i < V; i++) cv[i] = (int64_t)pcg_bounded(&g, 3, &st->rejections) - 1;       /* :59 */
+    for (int64_t i = 0; i < V; i++) met[i] = pcg_uniform(&g, 0.0, 1.0);                           /* :60 */
+    pcg_store(&g, rng);
+    for (int64_t i = 0; i < V; i++) { /* :63-101 */
+        int64_t x = order[i];
+        int64_t xm = fwd(x, 0, N), xn = fwd(x, 1, N);
+        double df = (double)cm[i] - (double)cv[i] / Weff;
+        double dS = df / kappa * ((((f[x] + f[V + xm]) - f[xn]) - f[V + x]) + 2.0 * df);
+        double p = exp(-dS);
+        p = p < 0.0 ? 0.0 : p;
+        p = p > 1.0 ? 1.0 : p;
+        st->acceptance_sum += p;
+        if (met[i] < p) {
+            m[x] += cm[i];
+            m[V + xm] += cm[i];
+            m[xn] += -cm[i];
+            m[V + x] += -cm[i];
+            if (v_is_float) ((double *)v)[x] += (double)cv[i];
+            else ((int64_t *)v)[x] += cv[i];
+            f[x] += df;
+            f[V + xm] += df;
+            f[xn] -= df;
+            f[V + x] -= df;
+            st->accepted++;
+        }
+    }
+    st->proposed = V;
+    free(f);
+    free(cm);
+    free(cv);
+    free(met);
+    return 0;
+}
+
+/* Checkerboard PlaquetteUpdate (this build's GPU-native chain, DESIGN.md "Plaquette modes").
+ * Per sweep: metropolis = uniform(0,1,V) in row-major order; then per colour c (compact.py
+ * checkerboarding): cm = choice([-1,1], n_c), cv = choice([-1,0,1], n_c).  Each colour pass
+ * evaluates f = m - delta(v)/W FRESH from the current fields (same expression and order as
+ * plaquette.py:53,84-85), accepts with metropolis[x] < clip(exp(-dS),0,1), and applies the
+ * plaquette.py:91-96 field changes.  Same-colour plaquettes share no link, so the pass is
+ * order-independent. */
+int sv_o_worldline_plaquette_cb(int32_t N_, double kappa, double Weff, int64_t *m, void *v, int32_t v_is_float,
+                                int32_t sweeps, sv_rng *rng, sv_stats *stats) {
+    int64_t N = N_, V = N * N;
+    if (N < 2) return -1;
+    colors_t C = colors_make(N_);
+    double *metro = (double *)malloc(sizeof(double) * V);
+    int64_t *cm = (int64_t *)malloc(sizeof(int64_t) * V);
+    int64_t *cv = (int64_t *)malloc(sizeof(int64_t) * V);
+    pcg g = pcg_load(rng);
+    for (int32_t sw = 0; sw < sweeps; sw++) {
+        sv_stats *st = &stats[sw];
+        memset(st, 0, sizeof(*st));
+        for (int64_t s = 0; s < V; s++) metro[s] = pcg_uniform(&g, 0.0, 1.0);
+        for (int col = 0; col < C.ncol; col++) {
+            const int64_t nc = C.count[col];
+            const int64_t *sites = C.sites[col];
+            for (int64_t i = 0; i < nc; i++) cm[i] = pcg_bounded(&g, 2, &st->rejections) ? 1 : -1;
+            for (int64_t i = 0; i < nc; i++) cv[i] = (int64_t)pcg_bounded(&g, 3, &st->rejections) - 1;
+            for (int64_t i = 0; i < nc; i++) {
+                int64_t x = sites[i];
+                int64_t xm = fwd(x, 0, N), xn = fwd(x, 1, N);
+                /* f on the four boundary links, fresh: f_l = m_l - dvw_l */
+                int64_t links[4] = {x, V + xm, xn, V + x};
+                double fl[4];
+                for (int q = 0; q < 4; q++) {
+                    int64_t l = links[q];
+                    int64_t s = l % V;
+                    int mu = (int)(l / V);
+                    double dv;
+                    if (mu == 0) {
+                        int64_t b1 = bwd(s, 1, N);
+                        if (v_is_float) {
+                            const double *vf = (const double *)v;
+                            dv = 0.0 - (-(vf[s] - vf[b1]));
+                        } else {
+                            const int64_t *vi = (const int64_t *)v;
+                            dv = (double)(vi[s] - vi[b1]);
+                        }
+                    } else {
+                        int64_t b0 = bwd(s, 0, N);
+                        if (v_is_float) {
+                            const double *vf = (const double *)v;
+                            dv = 0.0 - (vf[s] - vf[b0]);
+                        } else {
+                            const int64_t *vi = (const int64_t *)v;
+                            dv = (double)(0 - (vi[s] - vi[b0]));
+                        }
+                    }
+                    fl[q] = (double)m[l] - dv / Weff;
+                }
+                double df = (double)cm[i] - (double)cv[i] / Weff;
+                double dS = df / kappa * ((((fl[0] + fl[1]) - fl[2]) - fl[3]) + 2.0 * df);
+                double p = exp(-dS);
+                p = p < 0.0 ? 0.0 : p;
+                p = p > 1.0 ? 1.0 : p;
+                st->acceptance_sum += p;
+                if (metro[x] < p) {
+                    m[x] += cm[i];
+                    m[V + xm] += cm[i];
+                    m[xn] -= cm[i];
+                    m[V + x] -= cm[i];
+                    if (v_is_float) ((double *)v)[x] += (double)cv[i];
+                    else ((int64_t *)v)[x] += cv[i];
+                    st->accepted++;
+                }
+            }
+        }
+        st->proposed = V;
+    }
+    pcg_store(&g, rng);
+    free(metro);
+    free(cm);
+    free(cv);
+    colors_free(&C);
+    return 0;
+}

@@ -1,0 +1,40 @@
+"""Loader for the golden fixtures in tests/golden/ (made by tools/make_golden.py from the reference)."""
+import os
+
+import numpy as np
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+
+
+def cases(name):
+    z = np.load(os.path.join(HERE, name), allow_pickle=False)
+    out = []
+    for i in range(int(z['count'])):
+        prefix = f'{i}/'
+        c = {k[len(prefix):]: z[k] for k in z.files if k.startswith(prefix)}
+        for k, v in list(c.items()):
+            if v.shape == () and v.dtype.kind in 'iuf':
+                c[k] = v.item()
+            elif v.shape == () and v.dtype.kind == 'U':
+                c[k] = str(v)
+        out.append(c)
+    return out
+
+
+def generator_from(state):
+    """A NumPy Generator(PCG64) positioned at a recorded state (6 uint64: s_hi s_lo inc_hi inc_lo has buf)."""
+    s = [int(x) for x in state]
+    g = np.random.Generator(np.random.PCG64())
+    st = g.bit_generator.state
+    st['state'] = {'state': (s[0] << 64) | s[1], 'inc': (s[2] << 64) | s[3]}
+    st['has_uint32'] = s[4]
+    st['uinteger'] = s[5]
+    g.bit_generator.state = st
+    return g
+
+
+def state_of(gen):
+    st = gen.bit_generator.state
+    s, inc = st['state']['state'], st['state']['inc']
+    return np.array([s >> 64, s & ((1 << 64) - 1), inc >> 64, inc & ((1 << 64) - 1), st['has_uint32'],
+                     st['uinteger']], dtype=np.uint64)

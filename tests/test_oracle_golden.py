@@ -1,0 +1,91 @@
+"""Pin the CPU oracle (oracle/sv_oracle.c) to golden vectors captured from the reference.
+
+The oracle is only trusted as the GPU path's checker because of these tests.
+"""
+import numpy as np
+import pytest
+
+from tests.golden import cases, generator_from, state_of
+
+
+def test_rng_kat(oracle_lib):
+    O = oracle_lib
+    for c in cases('rng_kat.npz'):
+        g = generator_from(c['rng0'])
+        if len(c['raw']):
+            assert (O.raw(g, len(c['raw'])) == c['raw']).all()
+        assert (O.uniform(g, 0.0, 1.0, len(c['uniform01'])) == c['uniform01']).all()
+        if len(c['uniform_pi']):
+            assert (O.uniform(g, -np.pi, np.pi, len(c['uniform_pi'])) == c['uniform_pi']).all()
+        assert (O.integers(g, 3, len(c['choice3'])) - 1 == c['choice3']).all()
+        assert (O.uniform(g, 0.0, 1.0, len(c['uniform_after'])) == c['uniform_after']).all()
+        assert (2 * O.integers(g, 2, len(c['choice2'])) - 1 == c['choice2']).all()
+        assert (O.integers(g, 5, len(c['choice5'])) - 2 == c['choice5']).all()
+        assert (state_of(g) == c['rng1']).all()
+
+
+def test_checkerboarding(oracle_lib):
+    for c in cases('checkerboarding.npz'):
+        ncol, col = oracle_lib.colors(c['N'])
+        assert ncol == c['colors'].max() + 1
+        assert (col == c['colors']).all()
+
+
+def _villain(O, c):
+    g = generator_from(c['rng0'])
+    phi, n = c['phi0'].copy(), c['n0'].copy()
+    st = O.villain_neighborhood(c['N'], c['kappa'], c['W'], phi, n, c['sweeps'], g,
+                                interval_phi=c['interval_phi'], interval_n=c['interval_n'])
+    return g, phi, n, st
+
+
+@pytest.mark.parametrize('fixture', ['villain_neighborhood.npz', 'villain_rejections.npz'])
+def test_villain_neighborhood(oracle_lib, fixture):
+    for c in cases(fixture):
+        g, phi, n, st = _villain(oracle_lib, c)
+        assert (phi == c['phi']).all(), (c['N'], c['kappa'])
+        assert (n == c['n']).all()
+        assert (state_of(g) == c['rng1']).all()
+        assert np.cumsum([s.accepted for s in st])[-1] == c['accepted'][-1]
+        V = c['N'] ** 2
+        acc = np.cumsum([s.acceptance_sum / V for s in st])
+        np.testing.assert_allclose(acc, c['acceptance'], rtol=1e-12, atol=1e-15)
+        np.testing.assert_allclose(oracle_lib.villain_action(c['N'], c['kappa'], phi, n), c['action'], rtol=1e-12)
+
+
+def test_rejection_fixtures_really_reject(oracle_lib):
+    hit = 0
+    for c in cases('villain_rejections.npz'):
+        _, _, _, st = _villain(oracle_lib, c)
+        hit += sum(s.rejections for s in st) > 0
+    assert hit >= 6
+
+
+def test_worldline_coexact(oracle_lib):
+    for c in cases('worldline_coexact.npz'):
+        g = generator_from(c['rng0'])
+        m = np.zeros((2, c['N'], c['N']), dtype=np.int64)
+        st = oracle_lib.worldline_coexact(c['N'], c['kappa'], c['W_eff'], m, np.ascontiguousarray(c['v']),
+                                          c['sweeps'], g, interval_t=c['interval_t'])
+        assert (m == c['m']).all(), (c['N'], c['W'])
+        assert (state_of(g) == c['rng1']).all()
+        assert np.cumsum([s.accepted for s in st])[-1] == c['accepted'][-1]
+        V = c['N'] ** 2
+        np.testing.assert_allclose(np.cumsum([s.acceptance_sum / V for s in st]), c['acceptance'], rtol=1e-12)
+
+
+def test_worldline_plaquette_sequential(oracle_lib):
+    for c in cases('worldline_plaquette.npz'):
+        N = c['N']
+        g = generator_from(c['rng0'])
+        m = np.zeros((2, N, N), dtype=np.int64)
+        v = np.zeros((N, N), dtype=np.float64 if np.isinf(c['W']) else np.int64)
+        acc, tot = 0, 0.0
+        for k in range(c['sweeps']):
+            st = oracle_lib.worldline_plaquette_seq(N, c['kappa'], c['W_eff'], m, v, c['order'][k], g)
+            acc += st.accepted
+            tot += st.acceptance_sum
+            assert acc == c['accepted'][k]
+            np.testing.assert_allclose(tot, c['acceptance'][k], rtol=1e-12)
+        assert (m == c['m']).all() and (v == c['v']).all()
+        assert (state_of(g) == c['rng1']).all()
