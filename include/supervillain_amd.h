@@ -1,0 +1,115 @@
+/*
+ * supervillain_amd.h -- C-ABI of libsvhip.so, the MI355X (gfx950) Metropolis sweep engine behind the
+ * supervillain generator plugin API.
+ *
+ * The reference (evanberkowitz/supervillain, pure Python/NumPy) has no native boundary of its own:
+ * its generators are duck-typed Python objects called as `generator.step(cfg) -> cfg`
+ * (supervillain/generator/generator.py:5-17) from Ensemble.generate (supervillain/ensemble.py:89-92),
+ * Sequentially.step (generator/combining.py:38-40) and KeepEvery.step (combining.py:100-104).
+ * This header is the boundary a binding of that protocol needs: plain pointers and sizes, no torch
+ * types.  the supervillain_amd.generator classes bind it with ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *   - Every function returns 0 on success and a negative code on failure; sv_last_error(ctx) then
+ *     holds the message.  Calls are synchronous on return.
+ *   - Host arrays are borrowed, C-contiguous, row-major (component axis first, then (t, x)), exactly
+ *     the reference's Form layout (supervillain/lattice/compact.py:244-261): phi (1,N,N) float64,
+ *     n and m (2,N,N) int64, v (1,N,N) int64 (float64 when W is infinite, worldline.py:110-112).
+ *   - Randomness: the generator's NumPy Generator(PCG64) state crosses as sv_rng and is advanced
+ *     exactly as the reference's NumPy calls would advance it, so a seeded device chain equals the
+ *     seeded reference chain (integers bit-exact, floats bit-exact up to exp() rounding).
+ *   - A context (sv_ctx) owns one HIP device and stream; it is not thread-safe.
+ */
+#ifndef SUPERVILLAIN_AMD_H
+#define SUPERVILLAIN_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct sv_ctx sv_ctx;
+typedef struct sv_villain sv_villain;
+typedef struct sv_worldline sv_worldline;
+
+/* NumPy PCG64 bit-generator state: bit_generator.state['state'] = {state, inc} as 128-bit halves,
+ * plus the half-word buffer ('has_uint32', 'uinteger') NumPy's bounded sampler keeps there. */
+typedef struct sv_rng {
+    uint64_t state_hi, state_lo, inc_hi, inc_lo;
+    int32_t has_uint32;
+    uint32_t uinteger;
+} sv_rng;
+
+/* Per-sweep counters.  The generators fold these exactly like the reference does, e.g.
+ * neighborhood.py:131-135: proposed += V, accepted += accepted, acceptance += acceptance_sum / V. */
+typedef struct sv_stats {
+    int64_t accepted;
+    int64_t proposed;
+    double acceptance_sum;
+    int64_t rejections; /* NumPy Lemire rejections met (diagnostic; they shift the stream) */
+} sv_stats;
+
+/* ---- context ------------------------------------------------------------------------------ */
+int sv_ctx_create(int device, sv_ctx **out);
+int sv_ctx_destroy(sv_ctx *ctx);
+const char *sv_last_error(sv_ctx *ctx);
+int sv_device_count(void);
+/* Measurement hooks: when enabled, every sweep-kernel launch is bracketed by hipEvents on the
+ * context's stream; sv_ctx_kernel_time returns the summed kernel time and launch count since enable. */
+int sv_ctx_set_timing(sv_ctx *ctx, int32_t enable);
+int sv_ctx_kernel_time(sv_ctx *ctx, double *ms_total, int64_t *launches);
+const char *sv_build_info(void);
+
+/* ---- Villain (phi, n): NeighborhoodUpdate ------------------------------------------------- */
+/* Replaces NeighborhoodUpdate.step, supervillain/generator/villain/neighborhood.py:59-137
+ * (constructor arguments kappa, W from the Villain action villain.py:41-45; interval_phi,
+ * interval_n from neighborhood.py:38).  Runs `sweeps` consecutive steps; stats has `sweeps`
+ * entries.  phi/n are read, updated and written back in place. */
+int sv_villain_neighborhood(sv_ctx *ctx, int32_t N, double kappa, int64_t W, double interval_phi, int64_t interval_n,
+                            double *phi, int64_t *n, int32_t sweeps, sv_rng *rng, sv_stats *stats);
+
+/* Device-resident form of the same (what a KeepEvery stride or a benchmark folds into one call). */
+int sv_villain_create(sv_ctx *ctx, int32_t N, sv_villain **out);
+int sv_villain_destroy(sv_villain *st);
+int sv_villain_upload(sv_villain *st, const double *phi, const int64_t *n);
+int sv_villain_download(sv_villain *st, double *phi, int64_t *n);
+/* path: 0 = auto (fused two-colour sweep kernel for even N, per-colour kernels otherwise),
+ *       1 = per-colour kernels (any N), 2 = fused (even N only). */
+int sv_villain_run(sv_villain *st, double kappa, int64_t W, double interval_phi, int64_t interval_n, int32_t sweeps,
+                   sv_rng *rng, sv_stats *stats, int32_t path);
+/* Inline observables of the current state (observable/action.py:25-31, energy.py:25-30,
+ * winding.py:30-37, wrapping.py:17-25): out[0]=S (villain.py:51-66), out[1]=sum (dn)^2, out[2..3]=sum n_mu */
+int sv_villain_observables(sv_villain *st, double kappa, double *out);
+
+/* ---- Worldline (m, v): CoexactUpdate, PlaquetteUpdate ------------------------------------- */
+/* W_eff is Worldline._W (worldline.py:49): W, or 2*pi when W is infinite; v_is_float selects the
+ * float64 v layout used at W = infinity. */
+int sv_worldline_create(sv_ctx *ctx, int32_t N, int32_t v_is_float, sv_worldline **out);
+int sv_worldline_destroy(sv_worldline *st);
+int sv_worldline_upload(sv_worldline *st, const int64_t *m, const void *v);
+int sv_worldline_download(sv_worldline *st, int64_t *m, void *v);
+
+/* Replaces CoexactUpdate.step, supervillain/generator/worldline/coexact.py:53-128 (interval_t from
+ * coexact.py:32).  v is read only. */
+int sv_worldline_coexact_run(sv_worldline *st, double kappa, double W_eff, int64_t interval_t, int32_t sweeps,
+                             sv_rng *rng, sv_stats *stats);
+int sv_worldline_coexact(sv_ctx *ctx, int32_t N, double kappa, double W_eff, int64_t interval_t, int64_t *m,
+                         const void *v, int32_t v_is_float, int32_t sweeps, sv_rng *rng, sv_stats *stats);
+
+/* Replaces PlaquetteUpdate.step, supervillain/generator/worldline/plaquette.py:35-104, in the
+ * reference's own visit order: `order` (N*N row-major site indices) is the row-major image of the
+ * permutation the reference draws from NumPy's global RandomState (plaquette.py:63).  One sweep. */
+int sv_worldline_plaquette_ordered_run(sv_worldline *st, double kappa, double W_eff, const int64_t *order,
+                                       sv_rng *rng, sv_stats *stats);
+/* Checkerboard variant (a different, equally valid chain): colour passes instead of the
+ * random sequential order.  `sweeps` consecutive sweeps. */
+int sv_worldline_plaquette_checkerboard_run(sv_worldline *st, double kappa, double W_eff, int32_t sweeps, sv_rng *rng,
+                                            sv_stats *stats);
+int sv_worldline_plaquette(sv_ctx *ctx, int32_t N, double kappa, double W_eff, int64_t *m, void *v,
+                           int32_t v_is_float, const int64_t *order, sv_rng *rng, sv_stats *stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,121 @@
+"""Loader for libsvhip.so, the HIP/gfx950 engine behind the generators (C-ABI: include/supervillain_amd.h).
+
+There is no CPU fallback: if the library or a HIP device is missing, every generator step raises.
+"""
+import ctypes
+import os
+import threading
+
+from supervillain_amd._abi import SvRng, SvStats
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libsvhip.so')
+_LIB = None
+_LOCK = threading.RLock()
+_CONTEXTS = {}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib():
+    """The loaded libsvhip.so (raises NativeError if it has not been built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(f'{LIB_PATH} is missing; build it with `python -c "import __graft_entry__ as g; g.build()"` '
+                              '(or `make -C supervillain_amd/csrc`).  There is no CPU fallback.')
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.POINTER
+        i32, i64, f64, vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
+        L.sv_ctx_create.argtypes = [ctypes.c_int, P(vp)]
+        L.sv_ctx_destroy.argtypes = [vp]
+        L.sv_last_error.argtypes = [vp]
+        L.sv_last_error.restype = ctypes.c_char_p
+        L.sv_device_count.argtypes = []
+        L.sv_build_info.restype = ctypes.c_char_p
+        L.sv_ctx_set_timing.argtypes = [vp, i32]
+        L.sv_ctx_kernel_time.argtypes = [vp, P(f64), P(i64)]
+        L.sv_villain_neighborhood.argtypes = [vp, i32, f64, i64, f64, i64, vp, vp, i32, P(SvRng), P(SvStats)]
+        L.sv_villain_create.argtypes = [vp, i32, P(vp)]
+        L.sv_villain_destroy.argtypes = [vp]
+        L.sv_villain_upload.argtypes = [vp, vp, vp]
+        L.sv_villain_download.argtypes = [vp, vp, vp]
+        L.sv_villain_run.argtypes = [vp, f64, i64, f64, i64, i32, P(SvRng), P(SvStats), i32]
+        L.sv_villain_observables.argtypes = [vp, f64, vp]
+        L.sv_worldline_create.argtypes = [vp, i32, i32, P(vp)]
+        L.sv_worldline_destroy.argtypes = [vp]
+        L.sv_worldline_upload.argtypes = [vp, vp, vp]
+        L.sv_worldline_download.argtypes = [vp, vp, vp]
+        L.sv_worldline_coexact_run.argtypes = [vp, f64, f64, i64, i32, P(SvRng), P(SvStats)]
+        L.sv_worldline_coexact.argtypes = [vp, i32, f64, f64, i64, vp, vp, i32, i32, P(SvRng), P(SvStats)]
+        L.sv_worldline_plaquette_ordered_run.argtypes = [vp, f64, f64, vp, P(SvRng), P(SvStats)]
+        L.sv_worldline_plaquette_checkerboard_run.argtypes = [vp, f64, f64, i32, P(SvRng), P(SvStats)]
+        L.sv_worldline_plaquette.argtypes = [vp, i32, f64, f64, vp, vp, i32, vp, P(SvRng), P(SvStats)]
+        _LIB = L
+        return L
+
+
+EXPORTED = ('sv_ctx_create', 'sv_ctx_destroy', 'sv_last_error', 'sv_device_count', 'sv_build_info',
+            'sv_ctx_set_timing', 'sv_ctx_kernel_time',
+            'sv_villain_neighborhood', 'sv_villain_create', 'sv_villain_destroy', 'sv_villain_upload',
+            'sv_villain_download', 'sv_villain_run', 'sv_villain_observables', 'sv_worldline_create',
+            'sv_worldline_destroy', 'sv_worldline_upload', 'sv_worldline_download', 'sv_worldline_coexact_run',
+            'sv_worldline_coexact', 'sv_worldline_plaquette_ordered_run',
+            'sv_worldline_plaquette_checkerboard_run', 'sv_worldline_plaquette')
+
+
+def default_device():
+    for var in ('SV_DEVICE', 'LOCAL_RANK'):
+        if var in os.environ:
+            return int(os.environ[var])
+    return 0
+
+
+class Context:
+    """One HIP device + stream (sv_ctx).  Not thread-safe, like the reference's generators."""
+
+    def __init__(self, device):
+        self.device = device
+        h = ctypes.c_void_p()
+        rc = lib().sv_ctx_create(device, ctypes.byref(h))
+        if rc != 0 or not h.value:
+            raise NativeError(f'cannot open HIP device {device} (sv_ctx_create returned {rc}); '
+                              'the supervillain_amd generators run only on an MI355X')
+        self.handle = h
+
+    def check(self, rc, what):
+        if rc != 0:
+            msg = lib().sv_last_error(self.handle)
+            raise NativeError(f'{what} failed: {msg.decode() if msg else rc}')
+
+    def __del__(self):
+        try:
+            if _LIB is not None and self.handle:
+                _LIB.sv_ctx_destroy(self.handle)
+        except Exception:
+            pass
+
+
+def context(device=None):
+    if device is None:
+        device = default_device()
+    with _LOCK:
+        ctx = _CONTEXTS.get(device)
+        if ctx is None:
+            ctx = Context(device)
+            _CONTEXTS[device] = ctx
+        return ctx
+
+
+def ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def stats_array(k):
+    return (SvStats * max(k, 1))()

@@ -1,0 +1,177 @@
+// capi.hip -- context management of libsvhip.so (see include/supervillain_amd.h).
+#include <cstring>
+
+#include "common.h"
+
+const sv::JumpTables *sv_ctx::jump_tables(uint64_t inc_hi, uint64_t inc_lo) {
+    auto key = std::make_pair(inc_hi, inc_lo);
+    auto it = tables.find(key);
+    if (it != tables.end()) return it->second;
+    sv::JumpTables *h = new sv::JumpTables(sv::make_tables(sv::u128{inc_lo, inc_hi}));
+    sv::JumpTables *d = nullptr;
+    SV_HIP(hipMalloc(&d, sizeof(sv::JumpTables)));
+    SV_HIP(hipMemcpy(d, h, sizeof(sv::JumpTables), hipMemcpyHostToDevice));
+    delete h;
+    if (tables.size() > 64) {  // a long-lived context seeing many generators: drop the cache
+        for (auto &kv : tables) (void)hipFree(kv.second);
+        tables.clear();
+    }
+    tables[key] = d;
+    return d;
+}
+
+void sv_ctx::ensure_blocks(size_t n) {
+    if (n <= blocks_cap) return;
+    SV_HIP(hipStreamSynchronize(stream));
+    if (d_blocks) SV_HIP(hipFree(d_blocks));
+    blocks_cap = std::max(n, 2 * blocks_cap);
+    SV_HIP(hipMalloc(&d_blocks, blocks_cap * sizeof(sv::Block)));
+}
+
+void sv_ctx::ensure_skips(size_t n) {
+    if (n <= skips_cap) return;
+    SV_HIP(hipStreamSynchronize(stream));
+    if (d_skips) SV_HIP(hipFree(d_skips));
+    skips_cap = std::max<size_t>(std::max(n, 2 * skips_cap), 64);
+    SV_HIP(hipMalloc(&d_skips, skips_cap * sizeof(uint32_t)));
+}
+
+void sv_ctx::ensure_stats(size_t n) {
+    if (n <= stats_cap) return;
+    SV_HIP(hipStreamSynchronize(stream));
+    if (d_stats) SV_HIP(hipFree(d_stats));
+    stats_cap = std::max(n, 2 * stats_cap);
+    SV_HIP(hipMalloc(&d_stats, stats_cap * sizeof(sv_stats)));
+}
+
+static hipEvent_t take_event(std::vector<hipEvent_t> &pool) {
+    if (!pool.empty()) {
+        hipEvent_t e = pool.back();
+        pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    SV_HIP(hipEventCreate(&e));
+    return e;
+}
+
+void sv_ctx::time_begin(hipEvent_t *a) {
+    *a = nullptr;
+    if (!timing) return;
+    *a = take_event(ev_pool);
+    SV_HIP(hipEventRecord(*a, stream));
+}
+
+void sv_ctx::time_end(hipEvent_t a) {
+    if (!timing || !a) return;
+    hipEvent_t b = take_event(ev_pool);
+    SV_HIP(hipEventRecord(b, stream));
+    ev_pending.push_back({a, b});
+}
+
+void sv_ctx::time_collect() {
+    for (auto &p : ev_pending) {
+        float ms = 0.f;
+        SV_HIP(hipEventSynchronize(p.second));
+        SV_HIP(hipEventElapsedTime(&ms, p.first, p.second));
+        timed_ms += ms;
+        timed_launches += 1;
+        ev_pool.push_back(p.first);
+        ev_pool.push_back(p.second);
+    }
+    ev_pending.clear();
+}
+
+void sv_ctx::time_discard() {
+    for (auto &p : ev_pending) {
+        ev_pool.push_back(p.first);
+        ev_pool.push_back(p.second);
+    }
+    ev_pending.clear();
+}
+
+extern "C" {
+
+int sv_ctx_set_timing(sv_ctx *ctx, int32_t enable) {
+    if (!ctx) return -1;
+    ctx->timing = enable != 0;
+    ctx->timed_ms = 0.0;
+    ctx->timed_launches = 0;
+    return 0;
+}
+
+int sv_ctx_kernel_time(sv_ctx *ctx, double *ms_total, int64_t *launches) {
+    if (!ctx) return -1;
+    try {
+        ctx->time_collect();
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+    if (ms_total) *ms_total = ctx->timed_ms;
+    if (launches) *launches = ctx->timed_launches;
+    return 0;
+}
+
+int sv_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char *sv_build_info(void) {
+    return "libsvhip gfx950 (PCG64 stream replay; fused Villain sweep; Coexact/Plaquette colour passes)";
+}
+
+int sv_ctx_create(int device, sv_ctx **out) {
+    if (!out) return -1;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return -3;  // no such HIP device
+    sv_ctx *ctx = new sv_ctx();
+    try {
+        ctx->device = device;
+        SV_HIP(hipSetDevice(device));
+        SV_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+        SV_HIP(hipMalloc(&ctx->d_abort, sizeof(int32_t)));
+        SV_HIP(hipMalloc(&ctx->d_nreport, sizeof(uint32_t)));
+        SV_HIP(hipMalloc(&ctx->d_reports, sv::MAX_REPORTS * sizeof(sv::Report)));
+        SV_HIP(hipMemset(ctx->d_abort, 0, sizeof(int32_t)));
+        SV_HIP(hipMemset(ctx->d_nreport, 0, sizeof(uint32_t)));
+        ctx->ensure_blocks(64);
+        ctx->ensure_skips(64);
+        ctx->ensure_stats(64);
+        *out = ctx;
+        return 0;
+    } catch (const std::exception &e) {
+        static thread_local std::string last;
+        last = e.what();
+        delete ctx;
+        return -2;
+    }
+}
+
+int sv_ctx_destroy(sv_ctx *ctx) {
+    if (!ctx) return 0;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto &kv : ctx->tables) (void)hipFree(kv.second);
+    for (auto &p : ctx->ev_pending) {
+        (void)hipEventDestroy(p.first);
+        (void)hipEventDestroy(p.second);
+    }
+    for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
+    (void)hipFree(ctx->d_abort);
+    (void)hipFree(ctx->d_nreport);
+    (void)hipFree(ctx->d_reports);
+    (void)hipFree(ctx->d_blocks);
+    (void)hipFree(ctx->d_skips);
+    (void)hipFree(ctx->d_stats);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return 0;
+}
+
+const char *sv_last_error(sv_ctx *ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+
+}  // extern "C"

@@ -1,0 +1,148 @@
+// common.h -- internal declarations shared by the HIP translation units of libsvhip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "pcg64.h"
+#include "supervillain_amd.h"
+
+namespace sv {
+
+// ----------------------------------------------------------------------------------------------
+// RNG blocks.  A sweep consumes the NumPy stream as a fixed sequence of blocks:
+// uniform blocks (one u64 per draw) and bounded blocks (one uint32 per draw through NumPy's
+// buffered Lemire sampler, plus one extra uint32 per rejection).  The host planner walks a cursor
+// through the blocks; kernels address any draw of a block by position.
+struct Block {
+    uint64_t base_lo, base_hi;  // state whose XSL-RR output is this block's u64 #0
+    uint32_t has, buf;          // bounded: a buffered half-word precedes the u64 stream
+    int32_t nskip, skip0;       // bounded: rejected stream positions are skips[skip0 .. skip0+nskip)
+};
+
+struct Cursor {
+    u128 s;  // state BEFORE the next draw
+    uint32_t has, buf;
+};
+
+enum BlockKind { UNIFORM = 0, BOUNDED = 1 };
+
+struct BlockSpec {
+    BlockKind kind;
+    uint32_t count;  // draws
+};
+
+// Host PCG64 helpers
+u128 host_jump(u128 s, u128 inc, uint64_t steps);
+Affine host_power(u128 inc, uint64_t steps);  // the map of `steps` PCG64 steps
+uint64_t host_output_at(u128 s, u128 inc, uint64_t pos);  // X_pos after state s (X_0 = output of one step)
+
+// Plan one block starting at `cur`; advances `cur`.  `skips` is the sorted list of rejected
+// stream positions known for this block (bounded only).
+Block plan_block(Cursor &cur, u128 inc, const BlockSpec &spec, const std::vector<uint32_t> &skips, int32_t skip0);
+
+// Device jump tables for one increment (cached in the context).
+JumpTables make_tables(u128 inc);
+
+// Rejection report written by kernels: the sweep (within the launch batch), block and stream position.
+struct Report {
+    uint32_t sweep, block, pos, pad;
+};
+static constexpr int MAX_REPORTS = 1024;
+
+// Device-side per-call scratch: abort flag, reports, stats accumulators.
+struct DevScratch {
+    int32_t *abort;     // nonzero: a rejection (or overflow) was met; later sweeps exit immediately
+    uint32_t *nreport;  // count of reports
+    Report *reports;
+};
+
+}  // namespace sv
+
+// ----------------------------------------------------------------------------------------------
+// Context and device-resident states (opaque in the C-ABI).
+struct sv_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    std::map<std::pair<uint64_t, uint64_t>, sv::JumpTables *> tables;  // per PCG64 increment (device)
+    // scratch
+    int32_t *d_abort = nullptr;
+    uint32_t *d_nreport = nullptr;
+    sv::Report *d_reports = nullptr;
+    sv::Block *d_blocks = nullptr;
+    size_t blocks_cap = 0;
+    uint32_t *d_skips = nullptr;
+    size_t skips_cap = 0;
+    sv_stats *d_stats = nullptr;
+    size_t stats_cap = 0;
+    // pinned host staging
+    sv::Block *h_blocks = nullptr;
+    size_t h_blocks_cap = 0;
+    // optional per-launch timing of the sweep kernels (hipEvents on ctx->stream)
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
+    double timed_ms = 0.0;
+    int64_t timed_launches = 0;
+    void time_begin(hipEvent_t *a);
+    void time_end(hipEvent_t a);
+    void time_collect();  // after a stream sync
+    void time_discard();  // drop pending (unsynchronized-safe: after a stream sync)
+
+    const sv::JumpTables *jump_tables(uint64_t inc_hi, uint64_t inc_lo);
+    void ensure_blocks(size_t n);
+    void ensure_skips(size_t n);
+    void ensure_stats(size_t n);
+};
+
+struct sv_villain {
+    sv_ctx *ctx = nullptr;
+    int32_t N = 0;
+    double *phi[2] = {nullptr, nullptr};  // ping-pong (fused sweep reads one, writes the other)
+    int64_t *n[2] = {nullptr, nullptr};
+    int cur = 0;
+    double *r = nullptr;        // generic path: residual r = d(phi) - 2 pi n, kept incrementally
+    double *snap_phi = nullptr;  // generic path snapshot
+    int64_t *snap_n = nullptr;
+    int32_t *sites = nullptr;    // generic path: colour site lists (row-major), concatenated
+    int32_t ncol = 0;
+    int64_t count[4] = {0, 0, 0, 0};
+    int64_t offset[4] = {0, 0, 0, 0};
+    std::vector<int64_t> partial;  // host scratch
+};
+
+struct sv_worldline {
+    sv_ctx *ctx = nullptr;
+    int32_t N = 0;
+    int32_t v_is_float = 0;
+    int64_t *m = nullptr;
+    void *v = nullptr;  // int64 or double (N*N)
+    int64_t *snap_m = nullptr;
+    void *snap_v = nullptr;
+    double *f = nullptr;         // sequential plaquette: f = m - delta(v)/W kept incrementally
+    int32_t *order = nullptr;    // sequential plaquette: visit order (row-major site per position)
+    int32_t *pos = nullptr;      // sequential plaquette: inverse of order
+    int32_t *done = nullptr;     // sequential plaquette: round in which a plaquette was processed (0 = not yet)
+    int32_t *sites = nullptr;
+    int32_t ncol = 0;
+    int64_t count[4] = {0, 0, 0, 0};
+    int64_t offset[4] = {0, 0, 0, 0};
+};
+
+#define SV_HIP(call)                                                                                   \
+    do {                                                                                               \
+        hipError_t e_ = (call);                                                                        \
+        if (e_ != hipSuccess)                                                                          \
+            throw std::runtime_error(std::string(#call) + " failed: " + hipGetErrorString(e_));       \
+    } while (0)
+
+namespace sv {
+// colour lists for D=2 (compact.py:191-239); returns ncol, fills site lists in row-major order
+int build_colors(int32_t N, std::vector<int32_t> &sites, int64_t count[4], int64_t offset[4]);
+}  // namespace sv

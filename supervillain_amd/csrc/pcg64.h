@@ -1,0 +1,108 @@
+// pcg64.h -- NumPy PCG64 stream arithmetic for host and device (gfx950).
+//
+// The generators replay NumPy's Generator(PCG64) stream exactly (the reference draws every random
+// number from `self.rng`, e.g. supervillain/generator/villain/neighborhood.py:87,98,105-107).  A GPU
+// lane cannot step the stream serially, so every draw is addressed by its POSITION: PCG64 is an LCG,
+// k steps are the affine map  s -> A_k s + C_k  (mod 2^128), and a lane reaches position p of a block
+// by composing the block's base state with (A_p, C_p) from small tables.  Output is XSL-RR 128/64 of
+// the advanced state (NumPy advances first, then outputs).
+#pragma once
+#include <stdint.h>
+
+#ifndef SV_HD
+#define SV_HD __host__ __device__ __forceinline__
+#endif
+
+namespace sv {
+
+struct u128 {
+    uint64_t lo, hi;
+};
+
+SV_HD uint64_t mulhi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul64hi(a, b);
+#else
+    return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+// low 128 bits of a*b
+SV_HD u128 mul(u128 a, u128 b) {
+    u128 r;
+    r.lo = a.lo * b.lo;
+    r.hi = mulhi64(a.lo, b.lo) + a.lo * b.hi + a.hi * b.lo;
+    return r;
+}
+
+SV_HD u128 add(u128 a, u128 b) {
+    u128 r;
+    r.lo = a.lo + b.lo;
+    r.hi = a.hi + b.hi + (r.lo < a.lo ? 1u : 0u);
+    return r;
+}
+
+// affine map s -> A s + C
+struct Affine {
+    u128 A, C;
+};
+
+SV_HD u128 apply(const Affine &f, u128 s) { return add(mul(f.A, s), f.C); }
+
+// f after g  (apply g first, then f):  A = Af Ag, C = Af Cg + Cf
+SV_HD Affine compose(const Affine &f, const Affine &g) {
+    Affine r;
+    r.A = mul(f.A, g.A);
+    r.C = add(mul(f.A, g.C), f.C);
+    return r;
+}
+
+SV_HD uint64_t xsl_rr(u128 s) {
+    uint64_t x = s.hi ^ s.lo;
+    unsigned rot = (unsigned)(s.hi >> 58);
+    return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+
+static constexpr uint64_t MULT_HI = 0x2360ED051FC65DA4ull;
+static constexpr uint64_t MULT_LO = 0x4385DF649FCCF645ull;
+
+SV_HD u128 mult() { return u128{MULT_LO, MULT_HI}; }
+
+SV_HD Affine step_map(u128 inc) { return Affine{mult(), inc}; }
+
+SV_HD Affine identity() { return Affine{u128{1, 0}, u128{0, 0}}; }
+
+// NumPy next_double: (u64 >> 11) * 2^-53
+SV_HD double to_double(uint64_t x) { return (double)(x >> 11) * (1.0 / 9007199254740992.0); }
+
+// Jump tables for one increment: LEVELS digits of DIGIT_BITS bits, entry [l][d] = map of d * 2^(l*DIGIT_BITS) steps.
+// Plus a "small" table of maps for 0..SMALL-1 steps (the per-lane offsets inside a row).
+static constexpr int JUMP_LEVELS = 4;
+static constexpr int JUMP_DIGIT_BITS = 8;
+static constexpr int JUMP_DIGITS = 1 << JUMP_DIGIT_BITS;
+static constexpr int SMALL = 256;
+
+struct JumpTables {
+    Affine level[JUMP_LEVELS][JUMP_DIGITS];
+    Affine small[SMALL];
+};
+
+// s advanced by p steps, p < 2^32, using the level tables.
+SV_HD u128 jump(const JumpTables *T, u128 s, uint32_t p) {
+#pragma unroll
+    for (int l = 0; l < JUMP_LEVELS; l++) {
+        uint32_t d = (p >> (l * JUMP_DIGIT_BITS)) & (JUMP_DIGITS - 1);
+        if (d) s = apply(T->level[l][d], s);
+    }
+    return s;
+}
+
+// Lemire bounded draw on one uint32 (NumPy buffered_bounded_lemire_uint32, 32-bit path):
+// returns the index, sets *reject when this uint32 is rejected (leftover < threshold).
+SV_HD uint32_t lemire(uint32_t x, uint32_t k, uint32_t thr, bool *reject) {
+    uint64_t m = (uint64_t)x * (uint64_t)k;
+    *reject = (uint32_t)m < thr;
+    return (uint32_t)(m >> 32);
+}
+
+}  // namespace sv

@@ -1,0 +1,1133 @@
+// villain.hip -- NeighborhoodUpdate (supervillain/generator/villain/neighborhood.py:59-137) on gfx950.
+//
+// Two device paths, both bit-exact replays of the reference chain under a fixed NumPy seed:
+//
+//  * generic (any N, incl. odd N's four colours): one kernel per colour pass, the residual
+//    r = d(phi) - 2 pi n kept in HBM and updated incrementally exactly as neighborhood.py:129 does.
+//
+//  * fused (even N): ONE kernel per sweep.  A workgroup owns a column strip of <=125 columns and
+//    TH rows and streams down it with a ring of LDS rows: colour-0 decisions for rows t+2.., then
+//    colour-1 decisions for rows t+1.. (reading the colour-0 results, including the incrementally
+//    updated r, from LDS), then writes finished rows t.. .  Halo decisions (one row/column of
+//    colour-1 and two of colour-0 beyond the strip) are recomputed redundantly -- every draw is
+//    addressed by its global NumPy stream position, so neighbouring strips agree bit-for-bit.
+//    HBM traffic is one read and one write of (phi, n) per sweep: 48 B/site instead of the
+//    88 B/site of two colour passes.
+//
+// Floating point follows the reference op by op (compile with -ffp-contract=off):
+//   d(phi) on link (mu,x):   0.0 + (phi[x+e] - phi[x])                 (lattice/reference.py:9-24)
+//   change_r:               (0.0 + (cphi[x+e] - cphi[x])) - (2pi)*cn   (neighborhood.py:110)
+//   dS_link:                ((kappa/2) * cr) * ((2*r) + cr)            (neighborhood.py:111)
+//   face_sum:               (((0 + f0[x]) + f0[x-e0]) + f1[x]) + f1[x-e1]  (reference.py:48-64)
+//   r update:               (r + d(cphi)) - (2pi)*cn                  (neighborhood.py:129)
+#include <cstdlib>
+
+#include "common.h"
+
+namespace sv {
+
+#define TWO_PI 6.283185307179586
+
+struct VParams {
+    int32_t N;
+    double half_kappa;
+    int64_t W;
+    double lo_phi, range_phi;  // uniform(-interval_phi, +interval_phi): low, high - low
+    int64_t interval_n;
+    uint32_t k, thr;           // choice over 2*interval_n+1 values; Lemire threshold
+};
+
+// Block order inside one sweep's descriptor array:
+//   [0] metropolis (uniform V), then per colour c: [1+5c] dphi (uniform), [2+5c] fwd mu=0,
+//   [3+5c] bwd mu=0, [4+5c] fwd mu=1, [5+5c] bwd mu=1 (bounded choice).
+__device__ __forceinline__ u128 block_base(const Block &b) { return u128{b.base_lo, b.base_hi}; }
+
+__device__ __forceinline__ void report(const DevScratch &S, uint32_t sweep, uint32_t block, uint32_t pos) {
+    uint32_t i = atomicAdd(S.nreport, 1u);
+    if (i < (uint32_t)MAX_REPORTS) S.reports[i] = Report{sweep, block, pos, 0};
+    __hip_atomic_store(S.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// stream position of bounded draw d, accounting for known rejected positions (sorted)
+__device__ __forceinline__ uint32_t skip_pos(const Block &b, const uint32_t *skips, uint32_t d) {
+    uint32_t q = d;
+    for (int i = 0; i < b.nskip; i++)
+        if (skips[b.skip0 + i] <= q) q++;
+    return q;
+}
+
+// uint32 at stream position q of a bounded block, by full jump from the block base
+__device__ __forceinline__ uint32_t bounded_word(const JumpTables *T, const Block &b, uint32_t q) {
+    if (b.has && q == 0) return b.buf;
+    uint32_t qq = q - b.has;
+    uint64_t X = xsl_rr(jump(T, block_base(b), qq >> 1));
+    return (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
+}
+
+// bounded draw d (index into the choice array), any path; reports rejections
+__device__ __forceinline__ int64_t bounded_draw(const JumpTables *T, const Block &b, const uint32_t *skips, uint32_t d,
+                                                const VParams &P, const DevScratch &S, uint32_t sweep, uint32_t bidx) {
+    uint32_t q = skip_pos(b, skips, d);
+    bool rej;
+    uint32_t idx = lemire(bounded_word(T, b, q), P.k, P.thr, &rej);
+    if (rej) report(S, sweep, bidx, q);
+    return P.W * ((int64_t)idx - P.interval_n);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+__device__ __forceinline__ void flush_stats(sv_stats *st, int64_t acc, double psum) {
+    // one atomic pair per wave
+    unsigned long long a = (unsigned long long)acc;
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+    psum = wave_sum(psum);
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd((unsigned long long *)&st->accepted, a);
+        atomicAdd(&st->acceptance_sum, psum);
+    }
+}
+
+// ================================================================================================
+// generic path
+// ================================================================================================
+
+// r = d(phi) - 2 pi n at sweep start (neighborhood.py:91); also phi <- phi + 0.0 (see DESIGN.md:
+// every site receives `phi + change_phi` with change_phi = +0.0 in some colour pass).
+__global__ void villain_r_init(int32_t N, double *phi, const int64_t *n, double *r, const int32_t *abort) {
+    if (*(volatile const int32_t *)abort) return;
+    int64_t V = (int64_t)N * N;
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < V; s += (int64_t)gridDim.x * blockDim.x) {
+        int64_t t = s / N, x = s - t * N;
+        int64_t f0 = ((t + 1 == N) ? 0 : t + 1) * N + x;
+        int64_t f1 = t * N + ((x + 1 == N) ? 0 : x + 1);
+        double p = phi[s];
+        r[s] = (0.0 + (phi[f0] - p)) - TWO_PI * (double)n[s];
+        r[V + s] = (0.0 + (phi[f1] - p)) - TWO_PI * (double)n[V + s];
+    }
+}
+
+__global__ void villain_phi_normalize(int32_t N, double *phi, const int32_t *abort) {
+    if (*(volatile const int32_t *)abort) return;
+    int64_t V = (int64_t)N * N;
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < V; s += (int64_t)gridDim.x * blockDim.x)
+        phi[s] = phi[s] + 0.0;
+}
+
+__global__ __launch_bounds__(256) void villain_pass_generic(VParams P, double *phi, int64_t *n, double *r,
+                                                            const int32_t *sites, int64_t nc, int color,
+                                                            const Block *blocks, const uint32_t *skips,
+                                                            const JumpTables *T, sv_stats *stat, DevScratch S,
+                                                            uint32_t sweep) {
+    if (*(volatile const int32_t *)S.abort) return;
+    const int64_t N = P.N, V = N * N;
+    int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    int64_t acc_count = 0;
+    double psum = 0.0;
+    if (i < nc) {
+        const int64_t s = sites[i];
+        const int64_t t = s / N, x = s - t * N;
+        const int64_t b0s = ((t == 0) ? N - 1 : t - 1) * N + x;  // x - e0
+        const int64_t b1s = t * N + ((x == 0) ? N - 1 : x - 1);  // x - e1
+        const Block &BM = blocks[0];
+        const int bb = 1 + 5 * color;
+        const double u = 0.0 + 1.0 * to_double(xsl_rr(jump(T, block_base(BM), (uint32_t)s)));
+        const double dphi = P.lo_phi + P.range_phi * to_double(xsl_rr(jump(T, block_base(blocks[bb]), (uint32_t)i)));
+        int64_t cn[4] = {0, 0, 0, 0};  // f0, b0, f1, b1
+        if (P.k > 1) {
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                cn[q] = bounded_draw(T, blocks[bb + 1 + q], skips, (uint32_t)i, P, S, sweep, (uint32_t)(bb + 1 + q));
+        }
+        const int64_t L[4] = {s, b0s, V + s, V + b1s};
+        double rr[4], cr[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) rr[q] = r[L[q]];
+        cr[0] = (0.0 + (0.0 - dphi)) - TWO_PI * (double)cn[0];
+        cr[1] = (0.0 + (dphi - 0.0)) - TWO_PI * (double)cn[1];
+        cr[2] = (0.0 + (0.0 - dphi)) - TWO_PI * (double)cn[2];
+        cr[3] = (0.0 + (dphi - 0.0)) - TWO_PI * (double)cn[3];
+        double dS = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            double a = P.half_kappa * cr[q];
+            double b = (2.0 * rr[q]) + cr[q];
+            dS += a * b;
+        }
+        double p = exp(-dS);
+        p = p < 0.0 ? 0.0 : p;
+        p = p > 1.0 ? 1.0 : p;
+        const int acc = u < p;
+        acc_count = acc;
+        psum = p;
+        const double cphi = dphi * (double)acc;
+        phi[s] = phi[s] + cphi;
+        const double dcp_f = 0.0 + (0.0 - cphi);
+        const double dcp_b = 0.0 + (cphi - 0.0);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            int64_t c = cn[q] * acc;
+            n[L[q]] = n[L[q]] + c;
+            r[L[q]] = (rr[q] + ((q & 1) ? dcp_b : dcp_f)) - TWO_PI * (double)c;
+        }
+    }
+    flush_stats(stat, acc_count, psum);
+}
+
+// ================================================================================================
+// fused path (even N)
+// ================================================================================================
+
+static constexpr uint32_t OVERFLOW_BLOCK = 0xFFFFu;  // report tag: state not representable on this path
+static constexpr int FW_MAX = 123;     // colour-0 sites per region row <= 63, so lane 63 is always spare
+static constexpr int RW = FW_MAX + 5;  // 128 region columns: x0-2 .. x1+2
+static constexpr int SMALL_LDS = 128;  // small-offset maps cached in LDS (in-row offsets are <= w+4)
+
+template <int NW>
+struct FusedGeom {
+    static constexpr int R = 2 * NW + 3;  // ring rows: outputs t.. up to prefetched rows t+2+2NW
+};
+
+struct FArgs {
+    VParams P;
+    const double *phi_in;
+    const int64_t *n_in;
+    double *phi_out;
+    int64_t *n_out;
+    int32_t nsx, TH, nsy;  // column strips, rows per strip tile, row tiles
+    const Block *blocks;   // this sweep's 11 descriptors
+    const uint32_t *skips;
+    const JumpTables *T;
+    Affine adv[3];  // advance a row base by NW rows: [0] NW*N draws, [1] NW*N/2, [2] NW*N/4
+    sv_stats *stat;
+    DevScratch S;
+    uint32_t sweep;
+};
+
+// v mod N for v in [-2N, 3N) without a division
+__device__ __forceinline__ int32_t wrapN(int32_t v, int32_t N) {
+    v = v < 0 ? v + N : v;
+    v = v < 0 ? v + N : v;
+    v = v >= N ? v - N : v;
+    v = v >= N ? v - N : v;
+    return v;
+}
+
+__device__ __forceinline__ u128 readlane128(u128 v, int lane) {
+    u128 r;
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v.lo, lane);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v.lo >> 32), lane);
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v.hi, lane);
+    const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v.hi >> 32), lane);
+    r.lo = ((uint64_t)b << 32) | a;
+    r.hi = ((uint64_t)d << 32) | c;
+    return r;
+}
+
+// Row-base position of block type `ty` (0 metropolis, 1 dphi, 2..5 bounded words) for global row gq.
+// Bases sit at column xb, the strip's first non-wrapped region column.
+__device__ __forceinline__ int64_t base_pos(int ty, int64_t gq, int64_t N, int64_t xb, uint32_t has) {
+    const int64_t lin = gq * N + xb;
+    if (ty == 0) return lin;
+    const int64_t rank = lin >> 1;
+    if (ty == 1) return rank;
+    const int64_t p = rank - (int64_t)has;
+    return p < 0 ? 0 : (p >> 1);
+}
+
+struct Draws {
+    double u, dphi;
+    int64_t cn[4];
+};
+
+// Slow paths (branched around when no lane needs them).  The trailing wait keeps table loads from
+// leaving a pending-VMEM hazard on merged values, which would drain the row prefetch early.
+__device__ __forceinline__ u128 full_jump(const JumpTables *T, const Block *blk, uint32_t pos) {
+    u128 r = jump(T, block_base(*blk), pos);
+    __builtin_amdgcn_s_waitcnt(0);
+    return r;
+}
+
+__device__ __forceinline__ u128 from_base(const JumpTables *T, const Block *blk, const Affine *sm, u128 base,
+                                          int64_t bpos, int64_t pos) {
+    const int64_t off = pos - bpos;
+    u128 st;
+    if (off >= 0 && off < SMALL_LDS) st = apply(sm[off], base);
+    else st = full_jump(T, blk, (uint32_t)pos);
+    return st;
+}
+
+__device__ __forceinline__ int64_t choice_value(const FArgs &A, uint32_t word, uint32_t bidx, uint32_t spos) {
+    bool rej;
+    const uint32_t idx = lemire(word, A.P.k, A.P.thr, &rej);
+    if (rej) report(A.S, A.sweep, bidx, spos);
+    return A.P.W * ((int64_t)idx - A.P.interval_n);
+}
+
+// General draws: any strip (wrapped columns), skips, mismatched buffers.  6 compositions per site.
+__device__ __forceinline__ Draws draws_general(const FArgs &A, int c, bool active, int64_t gq, int64_t gx, int64_t xb,
+                                               const u128 *bases, const Affine *sm) {
+    const JumpTables *T = A.T;
+    const int64_t N = A.P.N;
+    const int bb = 1 + 5 * c;
+    const int64_t lin = gq * N + gx, rank = lin >> 1;
+    Draws D;
+    D.u = 0.0;
+    D.dphi = 0.0;
+    D.cn[0] = D.cn[1] = D.cn[2] = D.cn[3] = 0;
+    if (!active) return D;
+    D.u = 0.0 + 1.0 * to_double(xsl_rr(from_base(T, &A.blocks[0], sm, bases[0], gq * N + xb, lin)));
+    D.dphi = A.P.lo_phi + A.P.range_phi * to_double(xsl_rr(from_base(T, &A.blocks[bb], sm, bases[1], (gq * N + xb) >> 1, rank)));
+    if (A.P.k > 1) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const Block *B = &A.blocks[bb + 1 + q];
+            uint32_t word, spos = (uint32_t)rank;
+            if (B->nskip == 0) {
+                const int64_t qq = rank - (int64_t)B->has;
+                const int64_t wi = qq < 0 ? 0 : (qq >> 1);
+                const uint64_t X = xsl_rr(from_base(T, B, sm, bases[2 + q], base_pos(2, gq, N, xb, B->has), wi));
+                word = (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
+                if (qq < 0) word = B->buf;  // has && rank == 0: the buffered half-word
+            } else {
+                spos = skip_pos(*B, A.skips, (uint32_t)rank);
+                word = bounded_word(T, *B, spos);
+                __builtin_amdgcn_s_waitcnt(0);
+            }
+            D.cn[q] = choice_value(A, word, (uint32_t)(bb + 1 + q), spos);
+        }
+    }
+    return D;
+}
+
+// Fast draws for interior strips (no wrapped columns, no skips, equal buffers within each
+// forward/backward pair).  4 compositions per site: the fwd and bwd choice blocks of a direction
+// read the SAME u64 word for two adjacent lanes (its two 32-bit halves), so each lane of a pair
+// computes one block's word and swaps the other half with its partner.
+__device__ __forceinline__ Draws draws_fast(const FArgs &A, int c, bool active, int32_t lane, uint32_t rowlin,
+                                            uint32_t xs, uint32_t gx, uint32_t xb, const u128 *bases,
+                                            const Affine *sm) {
+    const int bb = 1 + 5 * c;
+    const uint32_t lin = rowlin + gx, rank = lin >> 1;
+    const uint32_t PM = rowlin + xb, PR = PM >> 1;
+    Draws D;
+    {
+        const u128 st = apply(sm[(gx - xb) & (SMALL_LDS - 1)], bases[0]);
+        D.u = 0.0 + 1.0 * to_double(xsl_rr(st));
+    }
+    {
+        const u128 st = apply(sm[(rank - PR) & (SMALL_LDS - 1)], bases[1]);
+        D.dphi = A.P.lo_phi + A.P.range_phi * to_double(xsl_rr(st));
+    }
+    D.cn[0] = D.cn[1] = D.cn[2] = D.cn[3] = 0;
+    if (A.P.k > 1) {
+        const uint32_t R0 = (rowlin + xs) >> 1;  // rank of lane 0
+#pragma unroll
+        for (int mu = 0; mu < 2; mu++) {
+            const Block &F = A.blocks[bb + 1 + 2 * mu];
+            const uint32_t h = F.has;
+            const uint32_t P = (R0 - h) & 1u;                        // pairing parity of this row
+            const uint32_t PW = (PR - h) >> 1;                       // word index of the row base
+            uint32_t qq = rank - h;
+            if (lane == 63 && P) qq = R0 - h;                        // lane 63 serves lane 0's word
+            const uint32_t half = (lane == 63 && P) ? 0u : (qq & 1u);
+            const uint32_t w = qq >> 1;
+            const u128 st = apply(sm[(w - PW) & (SMALL_LDS - 1)], half ? bases[3 + 2 * mu] : bases[2 + 2 * mu]);
+            const uint64_t X = xsl_rr(st);
+            // lo lanes computed the fwd word (send its high half), hi lanes the bwd word (send its low half)
+            const uint32_t send = half ? (uint32_t)X : (uint32_t)(X >> 32);
+            const int partner = half ? (lane == 0 ? 63 : lane - 1) : lane + 1;
+            const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute(partner << 2, (int)send);
+            const uint32_t wf = half ? got : (uint32_t)X;
+            const uint32_t wb = half ? (uint32_t)(X >> 32) : got;
+            if (active) {
+                D.cn[2 * mu] = choice_value(A, wf, (uint32_t)(bb + 1 + 2 * mu), rank);
+                D.cn[2 * mu + 1] = choice_value(A, wb, (uint32_t)(bb + 2 + 2 * mu), rank);
+            }
+        }
+    }
+    return D;
+}
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
+    constexpr int R = FusedGeom<NW>::R;
+    constexpr int nthreads = NW * 64;
+    constexpr int PF = (NW * RW + nthreads - 1) / nthreads;  // prefetched elements per thread
+    __shared__ double s_phi[R][RW];
+    __shared__ double s_r0[R][RW];
+    __shared__ double s_r1[R][RW];
+    __shared__ int32_t s_n0[R][RW];
+    __shared__ int32_t s_n1[R][RW];
+    __shared__ Affine s_small[SMALL_LDS];
+    __shared__ int32_t s_bad;
+
+    if (*(volatile const int32_t *)A.S.abort) return;
+
+    const int32_t N = A.P.N;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t V = (int64_t)N * N;
+
+    // XCD-aware tile order: blocks b, b+8, ... share an XCD; give each XCD a contiguous run of tiles
+    const int G = A.nsx * A.nsy;
+    int b = blockIdx.x;
+    {
+        const int per = G / 8, rem = G % 8;
+        const int xcd = b & 7, k = b >> 3;
+        b = xcd * per + (xcd < rem ? xcd : rem) + k;
+    }
+    const int ix = b % A.nsx, iy = b / A.nsx;
+    const int32_t x0 = (int32_t)((int64_t)ix * N / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * N / A.nsx);
+    const int32_t w = x1 - x0;
+    const int32_t t0 = iy * A.TH;
+    const int32_t t1 = t0 + A.TH < N ? t0 + A.TH : N;
+    const int32_t rbase = t0 - 2;  // local row 0
+    const int32_t cols = w + 5;
+    const int32_t xb = x0 - 2 < 0 ? 0 : x0 - 2;  // row bases at the first non-wrapped region column
+    const bool interior = x0 >= 4 && x1 + 2 < N;
+
+    for (int e = threadIdx.x; e < SMALL_LDS; e += nthreads) s_small[e] = A.T->small[e];
+    if (threadIdx.x == 0) s_bad = 0;
+
+    // fast draws need, per colour, no skips and equal buffers within each fwd/bwd pair
+    bool fast[2];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        const Block *B = &A.blocks[2 + 5 * c];
+        fast[c] = interior && B[0].nskip == 0 && B[1].nskip == 0 && B[2].nskip == 0 && B[3].nskip == 0 &&
+                  B[0].has == B[1].has && B[2].has == B[3].has;
+    }
+
+    // ---- register prefetch of region rows [ra, ra+NW) (clipped to [t0-2, t1+2])
+    double pf_phi[PF];
+    int64_t pf_n0[PF], pf_n1[PF];
+    int pf_rr[PF], pf_cc[PF], pf_gx[PF];
+#pragma unroll
+    for (int k = 0; k < PF; k++) {
+        const int e = threadIdx.x + k * nthreads;
+        pf_rr[k] = e / cols;
+        pf_cc[k] = e - pf_rr[k] * cols;
+        pf_gx[k] = wrapN(x0 - 2 + pf_cc[k], N);
+    }
+    auto prefetch = [&](int32_t ra) {
+#pragma unroll
+        for (int k = 0; k < PF; k++) {
+            const int32_t q = ra + pf_rr[k];
+            if (pf_rr[k] < NW && q >= t0 - 2 && q <= t1 + 2) {
+                const int64_t g = (int64_t)wrapN(q, N) * N + pf_gx[k];
+                pf_phi[k] = A.phi_in[g];
+                pf_n0[k] = A.n_in[g];
+                pf_n1[k] = A.n_in[V + g];
+            }
+        }
+    };
+    auto commit = [&](int32_t ra) {
+#pragma unroll
+        for (int k = 0; k < PF; k++) {
+            const int32_t q = ra + pf_rr[k];
+            if (pf_rr[k] < NW && q >= t0 - 2 && q <= t1 + 2) {
+                const int slot = (q - rbase) % R, cc = pf_cc[k];
+                s_phi[slot][cc] = pf_phi[k];
+                const int64_t a = pf_n0[k], c = pf_n1[k];
+                if (a > (1LL << 30) || a < -(1LL << 30) || c > (1LL << 30) || c < -(1LL << 30)) s_bad = 1;
+                s_n0[slot][cc] = (int32_t)a;
+                s_n1[slot][cc] = (int32_t)c;
+            }
+        }
+    };
+
+    // ---- per-wave running row bases: lane 8c+ty holds block ty's base for this wave's colour-c row
+    const bool base_lane = (lane & 7) < 6 && lane < 16;
+    const int bc = lane >> 3, bty = lane & 7;
+    const int bblk = bty == 0 ? 0 : 1 + 5 * bc + bty - 1;
+    const uint32_t bhas = (base_lane && bty >= 2) ? A.blocks[bblk].has : 0u;
+    const int32_t tfirst = t0 - 3;
+    int32_t brow = tfirst + 2 - bc + wave;  // D0 row t+2+wave, D1 row t+1+wave
+    u128 bases{0, 0};
+    if (base_lane) bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)base_pos(bty, wrapN(brow, N), N, xb, bhas));
+    __builtin_amdgcn_s_waitcnt(0);
+
+    int64_t acc_count = 0;
+    double psum = 0.0;
+
+    // coalesced stores of finished rows [ra, ra+NW) (clipped to the tile) from the ring
+    auto store_rows = [&](int32_t ra) {
+        const int32_t r0 = ra < t0 ? t0 : ra, r1 = ra + NW < t1 ? ra + NW : t1;
+        const int total = r1 > r0 ? (r1 - r0) * w : 0;
+        for (int e = threadIdx.x; e < total; e += nthreads) {
+            const int rr = e / w, cc = e - rr * w;
+            const int32_t q = r0 + rr;
+            const int slot = (q - rbase) % R, cx = cc + 2;
+            const int64_t g = (int64_t)q * N + x0 + cc;  // tile sites never wrap
+            A.phi_out[g] = s_phi[slot][cx];
+            A.n_out[g] = (int64_t)s_n0[slot][cx];
+            A.n_out[V + g] = (int64_t)s_n1[slot][cx];
+        }
+    };
+
+    for (int32_t ra = t0 - 2; ra < tfirst + 3 + NW; ra += NW) {
+        prefetch(ra);
+        commit(ra);
+    }
+    __syncthreads();
+
+    for (int32_t t = tfirst; t < t1; t += NW) {
+        prefetch(t + 3 + NW);  // rows for the next step; committed during phase C
+        store_rows(t - NW);    // rows finished by the previous step (their slots are recycled in phase C)
+        // ---------------- phase B: colour-0 decisions on row q = t+2+wave (+ stores of rows t-NW..t-1)
+        {
+            const int32_t q = t + 2 + wave;
+            const bool row_ok = (q >= t0 - 1) && (q <= t1 + 1);
+            const int32_t gq = wrapN(q, N);
+            const int32_t xs = (x0 - 1) + ((q + x0 - 1) & 1);  // (q + x) even
+            const int32_t x = xs + 2 * lane;
+            const bool active = row_ok && x <= x1 + 1;
+            u128 bs[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) bs[k] = readlane128(bases, k);
+            Draws D;
+            if (fast[0])
+                D = draws_fast(A, 0, active, lane, (uint32_t)gq * (uint32_t)N, (uint32_t)xs, (uint32_t)x, (uint32_t)xb,
+                               bs, s_small);
+            else
+                D = draws_general(A, 0, active, gq, wrapN(x, N), xb, bs, s_small);
+            if (active) {
+                const int lr = q - rbase;
+                const int sm = (lr - 1) % R, s0 = lr % R, sp = (lr + 1) % R;
+                const int cx = x - (x0 - 2);
+                const double ph = s_phi[s0][cx];
+                // r0 on the four links: f0=(0,q,x), b0=(0,q-1,x), f1=(1,q,x), b1=(1,q,x-1)
+                const int32_t n_f0 = s_n0[s0][cx], n_b0 = s_n0[sm][cx], n_f1 = s_n1[s0][cx], n_b1 = s_n1[s0][cx - 1];
+                double r0[4];
+                r0[0] = (0.0 + (s_phi[sp][cx] - ph)) - TWO_PI * (double)n_f0;
+                r0[1] = (0.0 + (ph - s_phi[sm][cx])) - TWO_PI * (double)n_b0;
+                r0[2] = (0.0 + (s_phi[s0][cx + 1] - ph)) - TWO_PI * (double)n_f1;
+                r0[3] = (0.0 + (ph - s_phi[s0][cx - 1])) - TWO_PI * (double)n_b1;
+                double cr[4];
+                cr[0] = (0.0 + (0.0 - D.dphi)) - TWO_PI * (double)D.cn[0];
+                cr[1] = (0.0 + (D.dphi - 0.0)) - TWO_PI * (double)D.cn[1];
+                cr[2] = (0.0 + (0.0 - D.dphi)) - TWO_PI * (double)D.cn[2];
+                cr[3] = (0.0 + (D.dphi - 0.0)) - TWO_PI * (double)D.cn[3];
+                double dS = 0.0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const double a = A.P.half_kappa * cr[k];
+                    const double bb2 = (2.0 * r0[k]) + cr[k];
+                    dS += a * bb2;
+                }
+                double p = exp(-dS);
+                p = p < 0.0 ? 0.0 : p;
+                p = p > 1.0 ? 1.0 : p;
+                const int acc = D.u < p;
+                const bool own = q >= t0 && q < t1 && x >= x0 && x < x1;
+                if (own) {  // count each site once; colour-0 phi is final after this pass
+                    acc_count += acc;
+                    psum += p;
+                }
+                const double cphi = D.dphi * (double)acc;
+                s_phi[s0][cx] = (ph + cphi) + 0.0;  // final colour-0 phi (the colour-1 pass adds +0.0)
+                const double dcp_f = 0.0 + (0.0 - cphi);
+                const double dcp_b = 0.0 + (cphi - 0.0);
+                const int32_t c0 = (int32_t)(D.cn[0] * acc), c1 = (int32_t)(D.cn[1] * acc);
+                const int32_t c2 = (int32_t)(D.cn[2] * acc), c3 = (int32_t)(D.cn[3] * acc);
+                s_n0[s0][cx] = n_f0 + c0;
+                s_n0[sm][cx] = n_b0 + c1;
+                s_n1[s0][cx] = n_f1 + c2;
+                s_n1[s0][cx - 1] = n_b1 + c3;
+                s_r0[s0][cx] = (r0[0] + dcp_f) - TWO_PI * (double)c0;
+                s_r0[sm][cx] = (r0[1] + dcp_b) - TWO_PI * (double)c1;
+                s_r1[s0][cx] = (r0[2] + dcp_f) - TWO_PI * (double)c2;
+                s_r1[s0][cx - 1] = (r0[3] + dcp_b) - TWO_PI * (double)c3;
+            }
+        }
+        __syncthreads();
+        // ---------------- phase C: colour-1 decisions on row q = t+1+wave; rows t.. become final
+        {
+            const int32_t q = t + 1 + wave;
+            const bool row_ok = (q >= t0) && (q <= t1);
+            const int32_t gq = wrapN(q, N);
+            const int32_t xs = x0 + ((q + x0 + 1) & 1);  // (q + x) odd
+            const int32_t x = xs + 2 * lane;
+            const bool active = row_ok && x <= x1;
+            u128 bs[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) bs[k] = readlane128(bases, 8 + k);
+            Draws D;
+            if (fast[1])
+                D = draws_fast(A, 1, active, lane, (uint32_t)gq * (uint32_t)N, (uint32_t)xs, (uint32_t)x, (uint32_t)xb,
+                               bs, s_small);
+            else
+                D = draws_general(A, 1, active, gq, wrapN(x, N), xb, bs, s_small);
+            if (active) {
+                const int lr = q - rbase;
+                const int sm = (lr - 1) % R, s0 = lr % R;
+                const int cx = x - (x0 - 2);
+                const double ph = s_phi[s0][cx];
+                double ri[4];
+                ri[0] = s_r0[s0][cx];
+                ri[1] = s_r0[sm][cx];
+                ri[2] = s_r1[s0][cx];
+                ri[3] = s_r1[s0][cx - 1];
+                double cr[4];
+                cr[0] = (0.0 + (0.0 - D.dphi)) - TWO_PI * (double)D.cn[0];
+                cr[1] = (0.0 + (D.dphi - 0.0)) - TWO_PI * (double)D.cn[1];
+                cr[2] = (0.0 + (0.0 - D.dphi)) - TWO_PI * (double)D.cn[2];
+                cr[3] = (0.0 + (D.dphi - 0.0)) - TWO_PI * (double)D.cn[3];
+                double dS = 0.0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const double a = A.P.half_kappa * cr[k];
+                    const double bb2 = (2.0 * ri[k]) + cr[k];
+                    dS += a * bb2;
+                }
+                double p = exp(-dS);
+                p = p < 0.0 ? 0.0 : p;
+                p = p > 1.0 ? 1.0 : p;
+                const int acc = D.u < p;
+                if (q >= t0 && q < t1 && x >= x0 && x < x1) {
+                    acc_count += acc;
+                    psum += p;
+                }
+                const double cphi = D.dphi * (double)acc;
+                s_phi[s0][cx] = (ph + 0.0) + cphi;
+                s_n0[s0][cx] += (int32_t)(D.cn[0] * acc);
+                s_n0[sm][cx] += (int32_t)(D.cn[1] * acc);
+                s_n1[s0][cx] += (int32_t)(D.cn[2] * acc);
+                s_n1[s0][cx - 1] += (int32_t)(D.cn[3] * acc);
+            }
+        }
+        commit(t + 3 + NW);  // slots of rows [t-NW, t): not read in phase C
+        // advance the row bases by NW rows (one affine map; a full jump where the row wraps)
+        if (base_lane) {
+            const int64_t p_old = base_pos(bty, wrapN(brow, N), N, xb, bhas);
+            const int64_t p_new = base_pos(bty, wrapN(brow + NW, N), N, xb, bhas);
+            const int ai = bty == 0 ? 0 : (bty == 1 ? 1 : 2);
+            const int64_t step = bty == 0 ? (int64_t)NW * N : (bty == 1 ? (int64_t)NW * N / 2 : (int64_t)NW * N / 4);
+            if (p_new - p_old == step) bases = apply(A.adv[ai], bases);
+            else bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)p_new);
+            brow += NW;
+        }
+        __syncthreads();
+    }
+    {
+        // the last step's rows; the loop ended with a barrier
+        int32_t tl = tfirst;
+        while (tl + NW < t1) tl += NW;
+        store_rows(tl);
+    }
+    if (s_bad && threadIdx.x == 0) {
+        // |n| too large for the int32 LDS image: the host falls back to the generic path
+        report(A.S, A.sweep, OVERFLOW_BLOCK, 0);
+    }
+    flush_stats(A.stat, acc_count, psum);
+}
+
+template __global__ void villain_sweep_fused<2>(FArgs);
+template __global__ void villain_sweep_fused<4>(FArgs);
+template __global__ void villain_sweep_fused<6>(FArgs);
+
+// ================================================================================================
+// observables (fused reductions over the current state)
+// ================================================================================================
+__global__ void villain_observables_kernel(int32_t N, double half_kappa, const double *phi, const int64_t *n,
+                                           double *out) {
+    const int64_t V = (int64_t)N * N;
+    double s_act = 0.0, s_w2 = 0.0, s_n0 = 0.0, s_n1 = 0.0;
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < V; s += (int64_t)gridDim.x * blockDim.x) {
+        int64_t t = s / N, x = s - t * N;
+        int64_t f0 = ((t + 1 == N) ? 0 : t + 1) * N + x;
+        int64_t f1 = t * N + ((x + 1 == N) ? 0 : x + 1);
+        double p = phi[s];
+        double l0 = (0.0 + (phi[f0] - p)) - TWO_PI * (double)n[s];
+        double l1 = (0.0 + (phi[f1] - p)) - TWO_PI * (double)n[V + s];
+        s_act += l0 * l0 + l1 * l1;
+        // (dn)_01[x] = (n1[x+e0] - n1[x]) - (n0[x+e1] - n0[x])   (d on 1-forms, rows (0,1,0,+1),(0,0,1,-1))
+        int64_t dn = (n[V + f0] - n[V + s]) - (n[f1] - n[s]);
+        s_w2 += (double)(dn * dn);
+        s_n0 += (double)n[s];
+        s_n1 += (double)n[V + s];
+    }
+    s_act = wave_sum(s_act);
+    s_w2 = wave_sum(s_w2);
+    s_n0 = wave_sum(s_n0);
+    s_n1 = wave_sum(s_n1);
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&out[0], half_kappa * s_act);
+        atomicAdd(&out[1], s_w2);
+        atomicAdd(&out[2], s_n0);
+        atomicAdd(&out[3], s_n1);
+    }
+}
+
+}  // namespace sv
+
+// ==================================================================================================
+// host drivers
+// ==================================================================================================
+using namespace sv;
+
+namespace {
+
+struct VillainPlan {
+    std::vector<BlockSpec> specs;  // per sweep
+};
+
+std::vector<BlockSpec> villain_specs(const sv_villain *st, bool has_bounded) {
+    std::vector<BlockSpec> s;
+    int64_t V = (int64_t)st->N * st->N;
+    s.push_back({UNIFORM, (uint32_t)V});
+    for (int c = 0; c < st->ncol; c++) {
+        uint32_t nc = (uint32_t)st->count[c];
+        s.push_back({UNIFORM, nc});
+        for (int q = 0; q < 4; q++) s.push_back({BOUNDED, has_bounded ? nc : 0u});
+    }
+    return s;
+}
+
+// Skip lists keyed by (sweep index within the call, block index)
+using SkipMap = std::map<std::pair<int, int>, std::vector<uint32_t>>;
+
+// plan `count` sweeps starting at sweep `first`, writing descriptors to ctx host staging
+void plan_sweeps(sv_ctx *ctx, Cursor &cur, u128 inc, const std::vector<BlockSpec> &specs, int first, int count,
+                 const SkipMap &skips, std::vector<Block> &blocks, std::vector<uint32_t> &skipvec) {
+    blocks.clear();
+    skipvec.clear();
+    static const std::vector<uint32_t> none;
+    for (int sw = first; sw < first + count; sw++) {
+        for (int bi = 0; bi < (int)specs.size(); bi++) {
+            auto it = skips.find({sw, bi});
+            const std::vector<uint32_t> &sk = it == skips.end() ? none : it->second;
+            Block b = plan_block(cur, inc, specs[bi], sk, (int32_t)skipvec.size());
+            skipvec.insert(skipvec.end(), sk.begin(), sk.end());
+            blocks.push_back(b);
+        }
+    }
+}
+
+void upload_plan(sv_ctx *ctx, const std::vector<Block> &blocks, const std::vector<uint32_t> &skipvec) {
+    ctx->ensure_blocks(blocks.size());
+    ctx->ensure_skips(skipvec.size() + 1);
+    SV_HIP(hipMemcpyAsync(ctx->d_blocks, blocks.data(), blocks.size() * sizeof(Block), hipMemcpyHostToDevice,
+                          ctx->stream));
+    if (!skipvec.empty())
+        SV_HIP(hipMemcpyAsync(ctx->d_skips, skipvec.data(), skipvec.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                              ctx->stream));
+}
+
+VParams make_params(int32_t N, double kappa, int64_t W, double interval_phi, int64_t interval_n) {
+    VParams P;
+    P.N = N;
+    P.half_kappa = kappa / 2.0;
+    P.W = W;
+    P.lo_phi = -interval_phi;
+    P.range_phi = interval_phi - (-interval_phi);
+    P.interval_n = interval_n;
+    P.k = (uint32_t)(2 * interval_n + 1);
+    P.thr = P.k > 1 ? (uint32_t)((0u - P.k) % P.k) : 0u;
+    return P;
+}
+
+DevScratch scratch(sv_ctx *ctx) { return DevScratch{ctx->d_abort, ctx->d_nreport, ctx->d_reports}; }
+
+struct AbortInfo {
+    int32_t abort;
+    std::vector<Report> reports;
+};
+
+AbortInfo read_abort(sv_ctx *ctx) {
+    AbortInfo a;
+    uint32_t nrep = 0;
+    SV_HIP(hipMemcpyAsync(&a.abort, ctx->d_abort, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    SV_HIP(hipMemcpyAsync(&nrep, ctx->d_nreport, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    SV_HIP(hipStreamSynchronize(ctx->stream));
+    if (nrep > (uint32_t)MAX_REPORTS) nrep = MAX_REPORTS;
+    a.reports.resize(nrep);
+    if (nrep) {
+        SV_HIP(hipMemcpyAsync(a.reports.data(), ctx->d_reports, nrep * sizeof(Report), hipMemcpyDeviceToHost,
+                              ctx->stream));
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    return a;
+}
+
+void clear_abort(sv_ctx *ctx) {
+    SV_HIP(hipMemsetAsync(ctx->d_abort, 0, sizeof(int32_t), ctx->stream));
+    SV_HIP(hipMemsetAsync(ctx->d_nreport, 0, sizeof(uint32_t), ctx->stream));
+}
+
+// Add the rejected positions of the earliest reported (sweep, block) to the skip map.
+// Returns that sweep index (relative to the batch start).
+int absorb_reports(const AbortInfo &a, int first, SkipMap &skips) {
+    if (a.reports.empty()) throw std::runtime_error("device aborted without a rejection report");
+    std::pair<uint32_t, uint32_t> best{~0u, ~0u};
+    for (const Report &r : a.reports)
+        if (std::make_pair(r.sweep, r.block) < best) best = {r.sweep, r.block};
+    auto &lst = skips[{first + (int)best.first, (int)best.second}];
+    for (const Report &r : a.reports)
+        if (r.sweep == best.first && r.block == best.second) lst.push_back(r.pos);
+    std::sort(lst.begin(), lst.end());
+    lst.erase(std::unique(lst.begin(), lst.end()), lst.end());
+    return (int)best.first;
+}
+
+// Tunables (overridable for experiments with SV_FUSED_NW in {2,4,6} and SV_FUSED_TH)
+int fused_nw() {
+    const char *e = getenv("SV_FUSED_NW");
+    int v = e ? atoi(e) : 4;
+    return (v == 2 || v == 4 || v == 6) ? v : 4;
+}
+int fused_th() {
+    const char *e = getenv("SV_FUSED_TH");
+    int v = e ? atoi(e) : 64;
+    return v >= 8 ? v : 64;
+}
+
+bool fused_ok(int32_t N) { return N % 2 == 0 && N >= 4; }
+
+void run_generic(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u128 inc, sv_stats *stats) {
+    sv_ctx *ctx = st->ctx;
+    const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
+    const int64_t V = (int64_t)st->N * st->N;
+    auto specs = villain_specs(st, P.k > 1);
+    const int nb = (int)specs.size();
+    SkipMap skips;
+    std::vector<Block> blocks;
+    std::vector<uint32_t> skipvec;
+    ctx->ensure_stats(1);
+    double *phi = st->phi[st->cur];
+    int64_t *n = st->n[st->cur];
+    for (int sw = 0; sw < sweeps; sw++) {
+        SV_HIP(hipMemcpyAsync(st->snap_phi, phi, V * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+        SV_HIP(hipMemcpyAsync(st->snap_n, n, 2 * V * sizeof(int64_t), hipMemcpyDeviceToDevice, ctx->stream));
+        for (int attempt = 0;; attempt++) {
+            if (attempt > 64) throw std::runtime_error("rejection replay did not converge");
+            Cursor c = cur;
+            plan_sweeps(ctx, c, inc, specs, sw, 1, skips, blocks, skipvec);
+            upload_plan(ctx, blocks, skipvec);
+            clear_abort(ctx);
+            SV_HIP(hipMemsetAsync(ctx->d_stats, 0, sizeof(sv_stats), ctx->stream));
+            const int grid = (int)std::min<int64_t>((V + 255) / 256, 4096);
+            villain_phi_normalize<<<grid, 256, 0, ctx->stream>>>(st->N, phi, ctx->d_abort);
+            villain_r_init<<<grid, 256, 0, ctx->stream>>>(st->N, phi, n, st->r, ctx->d_abort);
+            for (int col = 0; col < st->ncol; col++) {
+                int64_t nc = st->count[col];
+                if (!nc) continue;
+                villain_pass_generic<<<(int)((nc + 255) / 256), 256, 0, ctx->stream>>>(
+                    P, phi, n, st->r, st->sites + st->offset[col], nc, col, ctx->d_blocks, ctx->d_skips, T,
+                    ctx->d_stats, scratch(ctx), 0u);
+            }
+            SV_HIP(hipGetLastError());
+            AbortInfo a = read_abort(ctx);
+            if (!a.abort) {
+                cur = c;
+                break;
+            }
+            absorb_reports(a, sw, skips);
+            SV_HIP(hipMemcpyAsync(phi, st->snap_phi, V * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+            SV_HIP(hipMemcpyAsync(n, st->snap_n, 2 * V * sizeof(int64_t), hipMemcpyDeviceToDevice, ctx->stream));
+        }
+        SV_HIP(hipMemcpyAsync(&stats[sw], ctx->d_stats, sizeof(sv_stats), hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+        stats[sw].proposed = V;
+        // rejections actually met in this sweep
+        int64_t rj = 0;
+        for (int bi = 0; bi < nb; bi++) {
+            auto it = skips.find({sw, bi});
+            if (it != skips.end()) rj += (int64_t)it->second.size();
+        }
+        stats[sw].rejections = rj;
+    }
+}
+
+// returns false if the fused path cannot represent the state (|n| too large): caller falls back
+bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u128 inc, sv_stats *stats,
+               int &done_sweeps) {
+    sv_ctx *ctx = st->ctx;
+    const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
+    const int32_t N = st->N;
+    const int64_t V = (int64_t)N * N;
+    auto specs = villain_specs(st, P.k > 1);
+    const int nb = (int)specs.size();
+    const int nsx = (N + FW_MAX - 1) / FW_MAX;
+    const int NWv = fused_nw();
+    const int TH = fused_th();
+    const int nsy = (N + TH - 1) / TH;
+    const int grid = nsx * nsy;
+    const int BATCH = 64;
+    // row-base advance maps for NW rows: NW*N metropolis draws, NW*N/2 ranks, NW*N/4 words
+    if ((int64_t)NWv * N % 4) throw std::invalid_argument("fused path needs NW*N divisible by 4");
+    const Affine adv[3] = {host_power(inc, (uint64_t)NWv * N), host_power(inc, (uint64_t)NWv * N / 2),
+                           host_power(inc, (uint64_t)NWv * N / 4)};
+    SkipMap skips;
+    std::vector<Block> blocks;
+    std::vector<uint32_t> skipvec;
+    int sw = 0;
+    while (sw < sweeps) {
+        const int count = std::min(BATCH, sweeps - sw);
+        Cursor c = cur;
+        plan_sweeps(ctx, c, inc, specs, sw, count, skips, blocks, skipvec);
+        upload_plan(ctx, blocks, skipvec);
+        clear_abort(ctx);
+        ctx->ensure_stats(count);
+        SV_HIP(hipMemsetAsync(ctx->d_stats, 0, count * sizeof(sv_stats), ctx->stream));
+        const int cur0 = st->cur;
+        for (int k = 0; k < count; k++) {
+            FArgs A;
+            A.P = P;
+            A.phi_in = st->phi[st->cur];
+            A.n_in = st->n[st->cur];
+            A.phi_out = st->phi[st->cur ^ 1];
+            A.n_out = st->n[st->cur ^ 1];
+            A.nsx = nsx;
+            A.TH = TH;
+            A.nsy = nsy;
+            A.blocks = ctx->d_blocks + (size_t)k * nb;
+            A.skips = ctx->d_skips;
+            A.T = T;
+            A.adv[0] = adv[0];
+            A.adv[1] = adv[1];
+            A.adv[2] = adv[2];
+            A.stat = ctx->d_stats + k;
+            A.S = scratch(ctx);
+            A.sweep = (uint32_t)k;
+            hipEvent_t ev;
+            ctx->time_begin(&ev);
+            if (NWv == 2) villain_sweep_fused<2><<<grid, 2 * 64, 0, ctx->stream>>>(A);
+            else if (NWv == 6) villain_sweep_fused<6><<<grid, 6 * 64, 0, ctx->stream>>>(A);
+            else villain_sweep_fused<4><<<grid, 4 * 64, 0, ctx->stream>>>(A);
+            ctx->time_end(ev);
+            st->cur ^= 1;
+        }
+        SV_HIP(hipGetLastError());
+        AbortInfo a = read_abort(ctx);
+        if (a.abort) ctx->time_discard();  // aborted launches exit early: keep the average honest
+        ctx->time_collect();
+        if (!a.abort) {
+            SV_HIP(hipMemcpyAsync(stats + sw, ctx->d_stats, count * sizeof(sv_stats), hipMemcpyDeviceToHost,
+                                  ctx->stream));
+            SV_HIP(hipStreamSynchronize(ctx->stream));
+            for (int k = 0; k < count; k++) {
+                stats[sw + k].proposed = V;
+                int64_t rj = 0;
+                for (int bi = 0; bi < nb; bi++) {
+                    auto it = skips.find({sw + k, bi});
+                    if (it != skips.end()) rj += (int64_t)it->second.size();
+                }
+                stats[sw + k].rejections = rj;
+            }
+            cur = c;
+            sw += count;
+            continue;
+        }
+        // earliest failing (sweep, block); an overflow tag sorts after every rejection of its sweep
+        uint32_t first_bad = ~0u;
+        bool overflow = false;
+        {
+            std::pair<uint32_t, uint32_t> best{~0u, ~0u};
+            for (const Report &r : a.reports)
+                if (std::make_pair(r.sweep, r.block) < best) best = {r.sweep, r.block};
+            first_bad = best.first;
+            overflow = best.second == OVERFLOW_BLOCK;
+        }
+        if (overflow) {
+            const int bad = (int)first_bad;
+            if (bad > 0) {
+                Cursor c2 = cur;
+                std::vector<Block> b2;
+                std::vector<uint32_t> s2;
+                plan_sweeps(ctx, c2, inc, specs, sw, bad, skips, b2, s2);
+                SV_HIP(hipMemcpyAsync(stats + sw, ctx->d_stats, bad * sizeof(sv_stats), hipMemcpyDeviceToHost,
+                                      ctx->stream));
+                SV_HIP(hipStreamSynchronize(ctx->stream));
+                for (int k = 0; k < bad; k++) {
+                    stats[sw + k].proposed = V;
+                    int64_t rj = 0;
+                    for (int bi = 0; bi < nb; bi++) {
+                        auto it = skips.find({sw + k, bi});
+                        if (it != skips.end()) rj += (int64_t)it->second.size();
+                    }
+                    stats[sw + k].rejections = rj;
+                }
+                cur = c2;
+            }
+            st->cur = cur0 ^ (bad & 1);
+            done_sweeps = sw + bad;
+            return false;
+        }
+        const int bad = absorb_reports(a, sw, skips);
+        // sweeps before `bad` in this batch are valid: keep them
+        if (bad > 0) {
+            Cursor c2 = cur;
+            std::vector<Block> b2;
+            std::vector<uint32_t> s2;
+            plan_sweeps(ctx, c2, inc, specs, sw, bad, skips, b2, s2);
+            SV_HIP(hipMemcpyAsync(stats + sw, ctx->d_stats, bad * sizeof(sv_stats), hipMemcpyDeviceToHost,
+                                  ctx->stream));
+            SV_HIP(hipStreamSynchronize(ctx->stream));
+            for (int k = 0; k < bad; k++) {
+                stats[sw + k].proposed = V;
+                int64_t rj = 0;
+                for (int bi = 0; bi < nb; bi++) {
+                    auto it = skips.find({sw + k, bi});
+                    if (it != skips.end()) rj += (int64_t)it->second.size();
+                }
+                stats[sw + k].rejections = rj;
+            }
+            cur = c2;
+        }
+        st->cur = cur0 ^ (bad & 1);
+        sw += bad;
+    }
+    done_sweeps = sweeps;
+    return true;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------- C-ABI (Villain)
+extern "C" {
+
+int sv_villain_create(sv_ctx *ctx, int32_t N, sv_villain **out) {
+    try {
+        if (!ctx || !out) return -1;
+        if (N < 2) throw std::invalid_argument("N must be >= 2");
+        SV_HIP(hipSetDevice(ctx->device));
+        sv_villain *st = new sv_villain();
+        st->ctx = ctx;
+        st->N = N;
+        const size_t V = (size_t)N * N;
+        for (int i = 0; i < 2; i++) {
+            SV_HIP(hipMalloc(&st->phi[i], V * sizeof(double)));
+            SV_HIP(hipMalloc(&st->n[i], 2 * V * sizeof(int64_t)));
+        }
+        SV_HIP(hipMalloc(&st->r, 2 * V * sizeof(double)));
+        SV_HIP(hipMalloc(&st->snap_phi, V * sizeof(double)));
+        SV_HIP(hipMalloc(&st->snap_n, 2 * V * sizeof(int64_t)));
+        std::vector<int32_t> sites;
+        st->ncol = build_colors(N, sites, st->count, st->offset);
+        SV_HIP(hipMalloc(&st->sites, sites.size() * sizeof(int32_t)));
+        SV_HIP(hipMemcpy(st->sites, sites.data(), sites.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+        *out = st;
+        return 0;
+    } catch (const std::exception &e) {
+        if (ctx) ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_villain_destroy(sv_villain *st) {
+    if (!st) return 0;
+    (void)hipSetDevice(st->ctx->device);
+    for (int i = 0; i < 2; i++) {
+        (void)hipFree(st->phi[i]);
+        (void)hipFree(st->n[i]);
+    }
+    (void)hipFree(st->r);
+    (void)hipFree(st->snap_phi);
+    (void)hipFree(st->snap_n);
+    (void)hipFree(st->sites);
+    delete st;
+    return 0;
+}
+
+int sv_villain_upload(sv_villain *st, const double *phi, const int64_t *n) {
+    try {
+        const size_t V = (size_t)st->N * st->N;
+        SV_HIP(hipSetDevice(st->ctx->device));
+        SV_HIP(hipMemcpyAsync(st->phi[st->cur], phi, V * sizeof(double), hipMemcpyHostToDevice, st->ctx->stream));
+        SV_HIP(hipMemcpyAsync(st->n[st->cur], n, 2 * V * sizeof(int64_t), hipMemcpyHostToDevice, st->ctx->stream));
+        SV_HIP(hipStreamSynchronize(st->ctx->stream));
+        return 0;
+    } catch (const std::exception &e) {
+        st->ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_villain_download(sv_villain *st, double *phi, int64_t *n) {
+    try {
+        const size_t V = (size_t)st->N * st->N;
+        SV_HIP(hipSetDevice(st->ctx->device));
+        SV_HIP(hipMemcpyAsync(phi, st->phi[st->cur], V * sizeof(double), hipMemcpyDeviceToHost, st->ctx->stream));
+        SV_HIP(hipMemcpyAsync(n, st->n[st->cur], 2 * V * sizeof(int64_t), hipMemcpyDeviceToHost, st->ctx->stream));
+        SV_HIP(hipStreamSynchronize(st->ctx->stream));
+        return 0;
+    } catch (const std::exception &e) {
+        st->ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_villain_run(sv_villain *st, double kappa, int64_t W, double interval_phi, int64_t interval_n, int32_t sweeps,
+                   sv_rng *rng, sv_stats *stats, int32_t path) {
+    if (!st || !rng || (sweeps > 0 && !stats)) return -1;
+    sv_ctx *ctx = st->ctx;
+    try {
+        if (sweeps < 0) throw std::invalid_argument("sweeps must be >= 0");
+        if (interval_n < 0) throw std::invalid_argument("interval_n must be >= 0");
+        if (interval_n > (1 << 20)) throw std::invalid_argument("interval_n too large");
+        SV_HIP(hipSetDevice(ctx->device));
+        VParams P = make_params(st->N, kappa, W, interval_phi, interval_n);
+        u128 inc{rng->inc_lo, rng->inc_hi};
+        Cursor cur{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
+        const bool small_dn = (W < 0 ? -W : W) * interval_n < (1LL << 28);
+        bool use_fused = path == 2 || (path == 0 && fused_ok(st->N) && small_dn);
+        if (path == 2 && !fused_ok(st->N)) throw std::invalid_argument("fused path needs even N >= 4");
+        int done = 0;
+        if (use_fused && sweeps > 0) {
+            // run as many sweeps as possible fused; on int32 overflow fall back for the rest
+            bool all = run_fused(st, P, sweeps, cur, inc, stats, done);
+            if (!all && path == 2) throw std::runtime_error("|n| exceeds the fused path's int32 LDS image");
+        }
+        if (done < sweeps) {
+            // generic path works on phi[cur], n[cur] in place
+            run_generic(st, P, sweeps - done, cur, inc, stats + done);
+        }
+        rng->state_hi = cur.s.hi;
+        rng->state_lo = cur.s.lo;
+        rng->has_uint32 = (int32_t)cur.has;
+        rng->uinteger = cur.buf;
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_villain_neighborhood(sv_ctx *ctx, int32_t N, double kappa, int64_t W, double interval_phi, int64_t interval_n,
+                            double *phi, int64_t *n, int32_t sweeps, sv_rng *rng, sv_stats *stats) {
+    sv_villain *st = nullptr;
+    int rc = sv_villain_create(ctx, N, &st);
+    if (rc) return rc;
+    rc = sv_villain_upload(st, phi, n);
+    if (!rc) rc = sv_villain_run(st, kappa, W, interval_phi, interval_n, sweeps, rng, stats, 0);
+    if (!rc) rc = sv_villain_download(st, phi, n);
+    sv_villain_destroy(st);
+    return rc;
+}
+
+int sv_villain_observables(sv_villain *st, double kappa, double *out) {
+    try {
+        sv_ctx *ctx = st->ctx;
+        SV_HIP(hipSetDevice(ctx->device));
+        double *d = nullptr;
+        SV_HIP(hipMallocAsync((void **)&d, 4 * sizeof(double), ctx->stream));
+        SV_HIP(hipMemsetAsync(d, 0, 4 * sizeof(double), ctx->stream));
+        const int64_t V = (int64_t)st->N * st->N;
+        const int grid = (int)std::min<int64_t>((V + 255) / 256, 2048);
+        villain_observables_kernel<<<grid, 256, 0, ctx->stream>>>(st->N, kappa / 2.0, st->phi[st->cur], st->n[st->cur],
+                                                                   d);
+        SV_HIP(hipMemcpyAsync(out, d, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipFreeAsync(d, ctx->stream));
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+        return 0;
+    } catch (const std::exception &e) {
+        st->ctx->err = e.what();
+        return -2;
+    }
+}
+
+}  // extern "C"

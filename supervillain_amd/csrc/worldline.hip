@@ -1,0 +1,692 @@
+// worldline.hip -- CoexactUpdate and PlaquetteUpdate on gfx950.
+//
+//  * CoexactUpdate (supervillain/generator/worldline/coexact.py:53-128): one kernel per colour pass,
+//    m patched in place; delta(v)/W is formed on the fly from v (frozen for the sweep, coexact.py:80).
+//    Bit-exact replay of the seeded reference chain.
+//  * PlaquetteUpdate, reference order (plaquette.py:35-104): the visit order is the permutation the
+//    reference draws from NumPy's global RandomState; the host hands it over.  Sequential semantics
+//    are kept exactly by dependency ROUNDS: a plaquette is processed once every earlier-visited
+//    plaquette sharing one of its links is done; plaquettes processed in one round share no link,
+//    so the result (m, v and the incrementally updated f = m - delta(v)/W) is bit-identical to the
+//    sequential loop.
+//  * PlaquetteUpdate, checkerboard: this build's GPU-native chain: colour passes with f
+//    evaluated fresh.  Oracle: oracle/sv_oracle.c sv_o_worldline_plaquette_cb.
+#include <algorithm>
+
+#include "common.h"
+
+namespace sv {
+
+#define TWO_PI_W 6.283185307179586
+
+__device__ __forceinline__ u128 wbase(const Block &b) { return u128{b.base_lo, b.base_hi}; }
+
+__device__ __forceinline__ void wreport(const DevScratch &S, uint32_t sweep, uint32_t block, uint32_t pos) {
+    uint32_t i = atomicAdd(S.nreport, 1u);
+    if (i < (uint32_t)MAX_REPORTS) S.reports[i] = Report{sweep, block, pos, 0};
+    __hip_atomic_store(S.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint32_t wbounded(const JumpTables *T, const Block &b, const uint32_t *skips, uint32_t d,
+                                             uint32_t k, uint32_t thr, const DevScratch &S, uint32_t sweep,
+                                             uint32_t bidx) {
+    uint32_t q = d;
+    for (int i = 0; i < b.nskip; i++)
+        if (skips[b.skip0 + i] <= q) q++;
+    uint32_t word;
+    if (b.has && q == 0) {
+        word = b.buf;
+    } else {
+        uint32_t qq = q - b.has;
+        uint64_t X = xsl_rr(jump(T, wbase(b), qq >> 1));
+        word = (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
+    }
+    bool rej;
+    uint32_t idx = lemire(word, k, thr, &rej);
+    if (rej) wreport(S, sweep, bidx, q);
+    return idx;
+}
+
+__device__ __forceinline__ double wsum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+__device__ __forceinline__ void wflush(sv_stats *st, int64_t acc, double psum) {
+    unsigned long long a = (unsigned long long)acc;
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+    psum = wsum(psum);
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd((unsigned long long *)&st->accepted, a);
+        atomicAdd(&st->acceptance_sum, psum);
+    }
+}
+
+// delta(v)/W on link (mu, s) of a D=2 two-form v, exactly as reference_delta + coexact.py:80:
+//   dv0[s] = 0 - (-1)(v[s] - v[s-e1]),  dv1[s] = 0 - (+1)(v[s] - v[s-e0]);  then / W_eff
+template <bool VF>
+__device__ __forceinline__ double dvw_link(const void *v, int64_t N, int mu, int64_t s, double Weff) {
+    const int64_t t = s / N, x = s - t * N;
+    const int64_t nb = mu == 0 ? t * N + (x == 0 ? N - 1 : x - 1) : (t == 0 ? N - 1 : t - 1) * N + x;
+    double d;
+    if (VF) {
+        const double *vf = (const double *)v;
+        double diff = vf[s] - vf[nb];
+        d = mu == 0 ? 0.0 - (-diff) : 0.0 - diff;
+    } else {
+        const int64_t *vi = (const int64_t *)v;
+        int64_t diff = vi[s] - vi[nb];
+        d = mu == 0 ? (double)(0 - (-diff)) : (double)(0 - diff);
+    }
+    return d / Weff;
+}
+
+struct WParams {
+    int32_t N;
+    double kappa, Weff;
+    double c;  // 0.5 / kappa
+    int64_t it;
+    uint32_t k, thr;
+};
+
+// ------------------------------------------------------------------------------------------------
+// CoexactUpdate colour pass.  Blocks per sweep: [0] metropolis (uniform V), [1+c] t for colour c.
+template <bool VF>
+__global__ __launch_bounds__(256) void coexact_pass(WParams P, int64_t *m, const void *v, const int32_t *sites,
+                                                    int64_t nc, int color, const Block *blocks, const uint32_t *skips,
+                                                    const JumpTables *T, sv_stats *stat, DevScratch S,
+                                                    uint32_t sweep) {
+    if (*(volatile const int32_t *)S.abort) return;
+    const int64_t N = P.N, V = N * N;
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    int64_t acc_count = 0;
+    double psum = 0.0;
+    if (i < nc) {
+        const int64_t x = sites[i];
+        const int64_t tt = x / N, xx = x - tt * N;
+        const int64_t xe0 = ((tt + 1 == N) ? 0 : tt + 1) * N + xx;
+        const int64_t xe1 = tt * N + ((xx + 1 == N) ? 0 : xx + 1);
+        const double u = 0.0 + 1.0 * to_double(xsl_rr(jump(T, wbase(blocks[0]), (uint32_t)x)));
+        const uint32_t j = wbounded(T, blocks[1 + color], skips, (uint32_t)i, P.k, P.thr, S, sweep, 1 + color);
+        const int64_t t = (int64_t)j < P.it ? (int64_t)j - P.it : (int64_t)j - P.it + 1;
+        // coface_sum_at order ('coface_sum',1) rows (0,1,0,1),(0,0,1,1): l1[x], l1[x+e0], l0[x], l0[x+e1]
+        const int mus[4] = {1, 1, 0, 0};
+        const int64_t ss[4] = {x, xe0, x, xe1};
+        const int64_t cm[4] = {-t, +t, +t, -t};
+        double dS = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int64_t l = mus[q] * V + ss[q];
+            const double a = P.c * (double)cm[q];
+            const double f = (double)m[l] - dvw_link<VF>(v, N, mus[q], ss[q], P.Weff);
+            const double b = (2.0 * f) + (double)cm[q];
+            dS += a * b;
+        }
+        double p = exp(-dS);
+        p = p < 0.0 ? 0.0 : p;
+        p = p > 1.0 ? 1.0 : p;
+        const int acc = u < p;
+        acc_count = acc;
+        psum = p;
+        if (acc) {  // delta_sparse(..., t*accepted, out=m): m0[x]+=t, m0[x+e1]-=t, m1[x]-=t, m1[x+e0]+=t
+            m[x] += t;
+            m[xe1] -= t;
+            m[V + x] -= t;
+            m[V + xe0] += t;
+        }
+    }
+    wflush(stat, acc_count, psum);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Checkerboard PlaquetteUpdate colour pass.  Blocks per sweep: [0] metropolis (uniform V),
+// per colour c: [1+2c] change_m = choice([-1,1]), [2+2c] change_v = choice([-1,0,1]).
+template <bool VF>
+__global__ __launch_bounds__(256) void plaquette_cb_pass(WParams P, int64_t *m, void *v, const int32_t *sites,
+                                                         int64_t nc, int color, const Block *blocks,
+                                                         const uint32_t *skips, const JumpTables *T, sv_stats *stat,
+                                                         DevScratch S, uint32_t sweep) {
+    if (*(volatile const int32_t *)S.abort) return;
+    const int64_t N = P.N, V = N * N;
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    int64_t acc_count = 0;
+    double psum = 0.0;
+    if (i < nc) {
+        const int64_t x = sites[i];
+        const int64_t tt = x / N, xx = x - tt * N;
+        const int64_t xm = ((tt + 1 == N) ? 0 : tt + 1) * N + xx;  // here + e_mu (mu = 0)
+        const int64_t xn = tt * N + ((xx + 1 == N) ? 0 : xx + 1);  // here + e_nu (nu = 1)
+        const double u = 0.0 + 1.0 * to_double(xsl_rr(jump(T, wbase(blocks[0]), (uint32_t)x)));
+        const uint32_t jm = wbounded(T, blocks[1 + 2 * color], skips, (uint32_t)i, 2u, 0u, S, sweep, 1 + 2 * color);
+        const uint32_t jv = wbounded(T, blocks[2 + 2 * color], skips, (uint32_t)i, 3u, 1u, S, sweep, 2 + 2 * color);
+        const int64_t cm = jm ? 1 : -1, cv = (int64_t)jv - 1;
+        const double f1 = (double)m[x] - dvw_link<VF>(v, N, 0, x, P.Weff);
+        const double f2 = (double)m[V + xm] - dvw_link<VF>(v, N, 1, xm, P.Weff);
+        const double f3 = (double)m[xn] - dvw_link<VF>(v, N, 0, xn, P.Weff);
+        const double f4 = (double)m[V + x] - dvw_link<VF>(v, N, 1, x, P.Weff);
+        const double df = (double)cm - (double)cv / P.Weff;
+        const double dS = df / P.kappa * ((((f1 + f2) - f3) - f4) + 2.0 * df);
+        double p = exp(-dS);
+        p = p < 0.0 ? 0.0 : p;
+        p = p > 1.0 ? 1.0 : p;
+        const int acc = u < p;
+        acc_count = acc;
+        psum = p;
+        if (acc) {
+            m[x] += cm;
+            m[V + xm] += cm;
+            m[xn] -= cm;
+            m[V + x] -= cm;
+            if (VF) ((double *)v)[x] += (double)cv;
+            else ((int64_t *)v)[x] += cv;
+        }
+    }
+    wflush(stat, acc_count, psum);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Reference-order PlaquetteUpdate.
+template <bool VF>
+__global__ void plaquette_ordered_init(WParams P, const int64_t *m, const void *v, double *f, const int32_t *order,
+                                       int32_t *pos, int32_t *done) {
+    const int64_t N = P.N, V = N * N;
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < V; s += (int64_t)gridDim.x * blockDim.x) {
+        pos[order[s]] = (int32_t)s;
+        done[s] = 0;
+        // f = m - delta(v)/W   (plaquette.py:53)
+        f[s] = (double)m[s] - dvw_link<VF>(v, N, 0, s, P.Weff);
+        f[V + s] = (double)m[V + s] - dvw_link<VF>(v, N, 1, s, P.Weff);
+    }
+}
+
+// Blocks: [0] change_m (k=2, V), [1] change_v (k=3, V), [2] metropolis (uniform V); draw index =
+// visit position (plaquette.py:58-60, 66-69).
+template <bool VF>
+__global__ __launch_bounds__(256) void plaquette_ordered_round(WParams P, int64_t *m, void *v, double *f,
+                                                               const int32_t *pos, int32_t *done, int32_t round,
+                                                               const Block *blocks, const uint32_t *skips,
+                                                               const JumpTables *T, sv_stats *stat, DevScratch S,
+                                                               uint32_t *remaining) {
+    if (*(volatile const int32_t *)S.abort) return;
+    const int64_t N = P.N, V = N * N;
+    int64_t acc_count = 0;
+    double psum = 0.0;
+    uint32_t left = 0;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < V; x += (int64_t)gridDim.x * blockDim.x) {
+        if (done[x]) continue;
+        const int64_t tt = x / N, xx = x - tt * N;
+        const int64_t xm = ((tt + 1 == N) ? 0 : tt + 1) * N + xx;
+        const int64_t xn = tt * N + ((xx + 1 == N) ? 0 : xx + 1);
+        const int64_t xmb = ((tt == 0) ? N - 1 : tt - 1) * N + xx;
+        const int64_t xnb = tt * N + ((xx == 0) ? N - 1 : xx - 1);
+        const int32_t me = pos[x];
+        const int64_t nbs[4] = {xm, xn, xmb, xnb};
+        bool ready = true;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int64_t y = nbs[q];
+            if (pos[y] < me) {
+                const int32_t dy = __hip_atomic_load(&done[y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (dy == 0 || dy >= round) ready = false;
+            }
+        }
+        if (!ready) {
+            left++;
+            continue;
+        }
+        const uint32_t idx = (uint32_t)me;
+        const uint32_t jm = wbounded(T, blocks[0], skips, idx, 2u, 0u, S, 0, 0);
+        const uint32_t jv = wbounded(T, blocks[1], skips, idx, 3u, 1u, S, 0, 1);
+        const double met = 0.0 + 1.0 * to_double(xsl_rr(jump(T, wbase(blocks[2]), idx)));
+        const int64_t cm = jm ? 1 : -1, cv = (int64_t)jv - 1;
+        const double f1 = f[x], f2 = f[V + xm], f3 = f[xn], f4 = f[V + x];
+        const double df = (double)cm - (double)cv / P.Weff;
+        const double dS = df / P.kappa * ((((f1 + f2) - f3) - f4) + 2.0 * df);
+        double p = exp(-dS);
+        p = p < 0.0 ? 0.0 : p;
+        p = p > 1.0 ? 1.0 : p;
+        psum += p;
+        if (met < p) {
+            m[x] += cm;
+            m[V + xm] += cm;
+            m[xn] += -cm;
+            m[V + x] += -cm;
+            if (VF) ((double *)v)[x] += (double)cv;
+            else ((int64_t *)v)[x] += cv;
+            f[x] += df;
+            f[V + xm] += df;
+            f[xn] -= df;
+            f[V + x] -= df;
+            acc_count++;
+        }
+        __hip_atomic_store(&done[x], round, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    wflush(stat, acc_count, psum);
+    unsigned long long l = left;
+    for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o);
+    if ((threadIdx.x & 63) == 0 && l) atomicAdd(remaining, (uint32_t)l);
+}
+
+}  // namespace sv
+
+using namespace sv;
+
+namespace {
+
+using SkipMap = std::map<std::pair<int, int>, std::vector<uint32_t>>;
+
+void wplan(Cursor &cur, u128 inc, const std::vector<BlockSpec> &specs, int first, int count, const SkipMap &skips,
+           std::vector<Block> &blocks, std::vector<uint32_t> &skipvec) {
+    blocks.clear();
+    skipvec.clear();
+    static const std::vector<uint32_t> none;
+    for (int sw = first; sw < first + count; sw++)
+        for (int bi = 0; bi < (int)specs.size(); bi++) {
+            auto it = skips.find({sw, bi});
+            const std::vector<uint32_t> &sk = it == skips.end() ? none : it->second;
+            blocks.push_back(plan_block(cur, inc, specs[bi], sk, (int32_t)skipvec.size()));
+            skipvec.insert(skipvec.end(), sk.begin(), sk.end());
+        }
+}
+
+void wupload(sv_ctx *ctx, const std::vector<Block> &blocks, const std::vector<uint32_t> &skipvec) {
+    ctx->ensure_blocks(blocks.size());
+    ctx->ensure_skips(skipvec.size() + 1);
+    SV_HIP(hipMemcpyAsync(ctx->d_blocks, blocks.data(), blocks.size() * sizeof(Block), hipMemcpyHostToDevice,
+                          ctx->stream));
+    if (!skipvec.empty())
+        SV_HIP(hipMemcpyAsync(ctx->d_skips, skipvec.data(), skipvec.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                              ctx->stream));
+}
+
+void wclear(sv_ctx *ctx) {
+    SV_HIP(hipMemsetAsync(ctx->d_abort, 0, sizeof(int32_t), ctx->stream));
+    SV_HIP(hipMemsetAsync(ctx->d_nreport, 0, sizeof(uint32_t), ctx->stream));
+}
+
+bool wcheck(sv_ctx *ctx, std::vector<Report> &reps) {
+    int32_t ab = 0;
+    uint32_t nrep = 0;
+    SV_HIP(hipMemcpyAsync(&ab, ctx->d_abort, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    SV_HIP(hipMemcpyAsync(&nrep, ctx->d_nreport, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    SV_HIP(hipStreamSynchronize(ctx->stream));
+    reps.clear();
+    if (!ab) return false;
+    if (nrep > (uint32_t)MAX_REPORTS) nrep = MAX_REPORTS;
+    reps.resize(nrep);
+    if (nrep) {
+        SV_HIP(hipMemcpyAsync(reps.data(), ctx->d_reports, nrep * sizeof(Report), hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    if (reps.empty()) throw std::runtime_error("device aborted without a rejection report");
+    return true;
+}
+
+int wabsorb(const std::vector<Report> &reps, int first, SkipMap &skips) {
+    std::pair<uint32_t, uint32_t> best{~0u, ~0u};
+    for (const Report &r : reps)
+        if (std::make_pair(r.sweep, r.block) < best) best = {r.sweep, r.block};
+    auto &lst = skips[{first + (int)best.first, (int)best.second}];
+    for (const Report &r : reps)
+        if (r.sweep == best.first && r.block == best.second) lst.push_back(r.pos);
+    std::sort(lst.begin(), lst.end());
+    lst.erase(std::unique(lst.begin(), lst.end()), lst.end());
+    return (int)best.first;
+}
+
+WParams wparams(int32_t N, double kappa, double Weff, int64_t it) {
+    WParams P;
+    P.N = N;
+    P.kappa = kappa;
+    P.Weff = Weff;
+    P.c = 0.5 / kappa;
+    P.it = it;
+    P.k = (uint32_t)(2 * it);
+    P.thr = (uint32_t)((0u - P.k) % P.k);
+    return P;
+}
+
+DevScratch wscratch(sv_ctx *ctx) { return DevScratch{ctx->d_abort, ctx->d_nreport, ctx->d_reports}; }
+
+void snapshot(sv_worldline *st, bool restore) {
+    sv_ctx *ctx = st->ctx;
+    const size_t V = (size_t)st->N * st->N;
+    const size_t vb = V * (st->v_is_float ? sizeof(double) : sizeof(int64_t));
+    if (!restore) {
+        SV_HIP(hipMemcpyAsync(st->snap_m, st->m, 2 * V * sizeof(int64_t), hipMemcpyDeviceToDevice, ctx->stream));
+        SV_HIP(hipMemcpyAsync(st->snap_v, st->v, vb, hipMemcpyDeviceToDevice, ctx->stream));
+    } else {
+        SV_HIP(hipMemcpyAsync(st->m, st->snap_m, 2 * V * sizeof(int64_t), hipMemcpyDeviceToDevice, ctx->stream));
+        SV_HIP(hipMemcpyAsync(st->v, st->snap_v, vb, hipMemcpyDeviceToDevice, ctx->stream));
+    }
+}
+
+// Batched colour-pass runner with snapshot + replay on a rejection.
+template <typename Launch>
+void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, int32_t sweeps, Cursor &cur, u128 inc,
+                       sv_stats *stats, Launch launch) {
+    sv_ctx *ctx = st->ctx;
+    const int nb = (int)specs.size();
+    const int64_t V = (int64_t)st->N * st->N;
+    const int BATCH = 64;
+    SkipMap skips;
+    std::vector<Block> blocks;
+    std::vector<uint32_t> skipvec;
+    std::vector<Report> reps;
+    int sw = 0;
+    while (sw < sweeps) {
+        const int count = std::min(BATCH, sweeps - sw);
+        snapshot(st, false);
+        for (int attempt = 0;; attempt++) {
+            if (attempt > 256) throw std::runtime_error("rejection replay did not converge");
+            Cursor c = cur;
+            wplan(c, inc, specs, sw, count, skips, blocks, skipvec);
+            wupload(ctx, blocks, skipvec);
+            wclear(ctx);
+            ctx->ensure_stats(count);
+            SV_HIP(hipMemsetAsync(ctx->d_stats, 0, count * sizeof(sv_stats), ctx->stream));
+            for (int k = 0; k < count; k++) launch(ctx->d_blocks + (size_t)k * nb, ctx->d_stats + k, (uint32_t)k);
+            SV_HIP(hipGetLastError());
+            if (!wcheck(ctx, reps)) {
+                cur = c;
+                break;
+            }
+            wabsorb(reps, sw, skips);
+            snapshot(st, true);
+        }
+        SV_HIP(hipMemcpyAsync(stats + sw, ctx->d_stats, count * sizeof(sv_stats), hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+        for (int k = 0; k < count; k++) {
+            stats[sw + k].proposed = V;
+            int64_t rj = 0;
+            for (int bi = 0; bi < nb; bi++) {
+                auto it = skips.find({sw + k, bi});
+                if (it != skips.end()) rj += (int64_t)it->second.size();
+            }
+            stats[sw + k].rejections = rj;
+        }
+        sw += count;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int sv_worldline_create(sv_ctx *ctx, int32_t N, int32_t v_is_float, sv_worldline **out) {
+    try {
+        if (!ctx || !out) return -1;
+        if (N < 2) throw std::invalid_argument("N must be >= 2");
+        SV_HIP(hipSetDevice(ctx->device));
+        sv_worldline *st = new sv_worldline();
+        st->ctx = ctx;
+        st->N = N;
+        st->v_is_float = v_is_float ? 1 : 0;
+        const size_t V = (size_t)N * N;
+        const size_t vb = V * (st->v_is_float ? sizeof(double) : sizeof(int64_t));
+        SV_HIP(hipMalloc(&st->m, 2 * V * sizeof(int64_t)));
+        SV_HIP(hipMalloc(&st->v, vb));
+        SV_HIP(hipMalloc(&st->snap_m, 2 * V * sizeof(int64_t)));
+        SV_HIP(hipMalloc(&st->snap_v, vb));
+        std::vector<int32_t> sites;
+        st->ncol = build_colors(N, sites, st->count, st->offset);
+        SV_HIP(hipMalloc(&st->sites, sites.size() * sizeof(int32_t)));
+        SV_HIP(hipMemcpy(st->sites, sites.data(), sites.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+        *out = st;
+        return 0;
+    } catch (const std::exception &e) {
+        if (ctx) ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_worldline_destroy(sv_worldline *st) {
+    if (!st) return 0;
+    (void)hipSetDevice(st->ctx->device);
+    (void)hipFree(st->m);
+    (void)hipFree(st->v);
+    (void)hipFree(st->snap_m);
+    (void)hipFree(st->snap_v);
+    (void)hipFree(st->sites);
+    if (st->f) (void)hipFree(st->f);
+    if (st->order) (void)hipFree(st->order);
+    if (st->pos) (void)hipFree(st->pos);
+    if (st->done) (void)hipFree(st->done);
+    delete st;
+    return 0;
+}
+
+int sv_worldline_upload(sv_worldline *st, const int64_t *m, const void *v) {
+    try {
+        const size_t V = (size_t)st->N * st->N;
+        const size_t vb = V * (st->v_is_float ? sizeof(double) : sizeof(int64_t));
+        SV_HIP(hipSetDevice(st->ctx->device));
+        SV_HIP(hipMemcpyAsync(st->m, m, 2 * V * sizeof(int64_t), hipMemcpyHostToDevice, st->ctx->stream));
+        SV_HIP(hipMemcpyAsync(st->v, v, vb, hipMemcpyHostToDevice, st->ctx->stream));
+        SV_HIP(hipStreamSynchronize(st->ctx->stream));
+        return 0;
+    } catch (const std::exception &e) {
+        st->ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_worldline_download(sv_worldline *st, int64_t *m, void *v) {
+    try {
+        const size_t V = (size_t)st->N * st->N;
+        const size_t vb = V * (st->v_is_float ? sizeof(double) : sizeof(int64_t));
+        SV_HIP(hipSetDevice(st->ctx->device));
+        SV_HIP(hipMemcpyAsync(m, st->m, 2 * V * sizeof(int64_t), hipMemcpyDeviceToHost, st->ctx->stream));
+        if (v) SV_HIP(hipMemcpyAsync(v, st->v, vb, hipMemcpyDeviceToHost, st->ctx->stream));
+        SV_HIP(hipStreamSynchronize(st->ctx->stream));
+        return 0;
+    } catch (const std::exception &e) {
+        st->ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_worldline_coexact_run(sv_worldline *st, double kappa, double W_eff, int64_t interval_t, int32_t sweeps,
+                             sv_rng *rng, sv_stats *stats) {
+    if (!st || !rng || (sweeps > 0 && !stats)) return -1;
+    sv_ctx *ctx = st->ctx;
+    try {
+        if (interval_t < 1 || interval_t > (1 << 20)) throw std::invalid_argument("interval_t must be in [1, 2^20]");
+        SV_HIP(hipSetDevice(ctx->device));
+        WParams P = wparams(st->N, kappa, W_eff, interval_t);
+        u128 inc{rng->inc_lo, rng->inc_hi};
+        Cursor cur{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
+        const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
+        std::vector<BlockSpec> specs;
+        specs.push_back({UNIFORM, (uint32_t)((int64_t)st->N * st->N)});
+        for (int c = 0; c < st->ncol; c++) specs.push_back({BOUNDED, (uint32_t)st->count[c]});
+        run_colour_sweeps(st, specs, sweeps, cur, inc, stats, [&](const Block *blocks, sv_stats *stat, uint32_t k) {
+            for (int c = 0; c < st->ncol; c++) {
+                const int64_t nc = st->count[c];
+                if (!nc) continue;
+                const int grid = (int)((nc + 255) / 256);
+                if (st->v_is_float)
+                    coexact_pass<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->sites + st->offset[c], nc,
+                                                                      c, blocks, ctx->d_skips, T, stat,
+                                                                      wscratch(ctx), k);
+                else
+                    coexact_pass<false><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->sites + st->offset[c], nc,
+                                                                       c, blocks, ctx->d_skips, T, stat,
+                                                                       wscratch(ctx), k);
+            }
+        });
+        rng->state_hi = cur.s.hi;
+        rng->state_lo = cur.s.lo;
+        rng->has_uint32 = (int32_t)cur.has;
+        rng->uinteger = cur.buf;
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_worldline_coexact(sv_ctx *ctx, int32_t N, double kappa, double W_eff, int64_t interval_t, int64_t *m,
+                         const void *v, int32_t v_is_float, int32_t sweeps, sv_rng *rng, sv_stats *stats) {
+    sv_worldline *st = nullptr;
+    int rc = sv_worldline_create(ctx, N, v_is_float, &st);
+    if (rc) return rc;
+    rc = sv_worldline_upload(st, m, v);
+    if (!rc) rc = sv_worldline_coexact_run(st, kappa, W_eff, interval_t, sweeps, rng, stats);
+    if (!rc) rc = sv_worldline_download(st, m, nullptr);
+    sv_worldline_destroy(st);
+    return rc;
+}
+
+int sv_worldline_plaquette_checkerboard_run(sv_worldline *st, double kappa, double W_eff, int32_t sweeps, sv_rng *rng,
+                                            sv_stats *stats) {
+    if (!st || !rng || (sweeps > 0 && !stats)) return -1;
+    sv_ctx *ctx = st->ctx;
+    try {
+        SV_HIP(hipSetDevice(ctx->device));
+        WParams P = wparams(st->N, kappa, W_eff, 1);
+        u128 inc{rng->inc_lo, rng->inc_hi};
+        Cursor cur{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
+        const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
+        std::vector<BlockSpec> specs;
+        specs.push_back({UNIFORM, (uint32_t)((int64_t)st->N * st->N)});
+        for (int c = 0; c < st->ncol; c++) {
+            specs.push_back({BOUNDED, (uint32_t)st->count[c]});
+            specs.push_back({BOUNDED, (uint32_t)st->count[c]});
+        }
+        run_colour_sweeps(st, specs, sweeps, cur, inc, stats, [&](const Block *blocks, sv_stats *stat, uint32_t k) {
+            for (int c = 0; c < st->ncol; c++) {
+                const int64_t nc = st->count[c];
+                if (!nc) continue;
+                const int grid = (int)((nc + 255) / 256);
+                if (st->v_is_float)
+                    plaquette_cb_pass<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->sites + st->offset[c],
+                                                                           nc, c, blocks, ctx->d_skips, T, stat,
+                                                                           wscratch(ctx), k);
+                else
+                    plaquette_cb_pass<false><<<grid, 256, 0, ctx->stream>>>(
+                        P, st->m, st->v, st->sites + st->offset[c], nc, c, blocks, ctx->d_skips, T, stat,
+                        wscratch(ctx), k);
+            }
+        });
+        rng->state_hi = cur.s.hi;
+        rng->state_lo = cur.s.lo;
+        rng->has_uint32 = (int32_t)cur.has;
+        rng->uinteger = cur.buf;
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_worldline_plaquette_ordered_run(sv_worldline *st, double kappa, double W_eff, const int64_t *order,
+                                       sv_rng *rng, sv_stats *stats) {
+    if (!st || !rng || !stats || !order) return -1;
+    sv_ctx *ctx = st->ctx;
+    try {
+        SV_HIP(hipSetDevice(ctx->device));
+        const int64_t N = st->N, V = N * N;
+        WParams P = wparams(st->N, kappa, W_eff, 1);
+        u128 inc{rng->inc_lo, rng->inc_hi};
+        Cursor cur{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
+        const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
+        if (!st->f) {
+            SV_HIP(hipMalloc(&st->f, 2 * V * sizeof(double)));
+            SV_HIP(hipMalloc(&st->order, V * sizeof(int32_t)));
+            SV_HIP(hipMalloc(&st->pos, V * sizeof(int32_t)));
+            SV_HIP(hipMalloc(&st->done, (V + 1) * sizeof(int32_t)));
+        }
+        std::vector<int32_t> ord(V);
+        std::vector<char> seen(V, 0);
+        for (int64_t i = 0; i < V; i++) {
+            if (order[i] < 0 || order[i] >= V || seen[order[i]]) throw std::invalid_argument("order is not a permutation");
+            seen[order[i]] = 1;
+            ord[i] = (int32_t)order[i];
+        }
+        SV_HIP(hipMemcpyAsync(st->order, ord.data(), V * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+        std::vector<BlockSpec> specs = {{BOUNDED, (uint32_t)V}, {BOUNDED, (uint32_t)V}, {UNIFORM, (uint32_t)V}};
+        SkipMap skips;
+        std::vector<Block> blocks;
+        std::vector<uint32_t> skipvec;
+        std::vector<Report> reps;
+        uint32_t *d_rem = nullptr;  // plaquettes still waiting after a chunk of rounds
+        SV_HIP(hipMallocAsync((void **)&d_rem, sizeof(uint32_t), ctx->stream));
+        snapshot(st, false);
+        ctx->ensure_stats(1);
+        const int grid = (int)std::min<int64_t>((V + 255) / 256, 8192);
+        for (int attempt = 0;; attempt++) {
+            if (attempt > 256) throw std::runtime_error("rejection replay did not converge");
+            Cursor c = cur;
+            wplan(c, inc, specs, 0, 1, skips, blocks, skipvec);
+            wupload(ctx, blocks, skipvec);
+            wclear(ctx);
+            SV_HIP(hipMemsetAsync(ctx->d_stats, 0, sizeof(sv_stats), ctx->stream));
+            if (st->v_is_float)
+                plaquette_ordered_init<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f, st->order, st->pos,
+                                                                             st->done);
+            else
+                plaquette_ordered_init<false><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f, st->order,
+                                                                              st->pos, st->done);
+            int32_t round = 1;
+            for (;;) {
+                const int CHUNK = 8;
+                for (int k = 0; k < CHUNK; k++, round++) {
+                    SV_HIP(hipMemsetAsync(d_rem, 0, sizeof(uint32_t), ctx->stream));
+                    if (st->v_is_float)
+                        plaquette_ordered_round<true><<<grid, 256, 0, ctx->stream>>>(
+                            P, st->m, st->v, st->f, st->pos, st->done, round, ctx->d_blocks, ctx->d_skips, T,
+                            ctx->d_stats, wscratch(ctx), d_rem);
+                    else
+                        plaquette_ordered_round<false><<<grid, 256, 0, ctx->stream>>>(
+                            P, st->m, st->v, st->f, st->pos, st->done, round, ctx->d_blocks, ctx->d_skips, T,
+                            ctx->d_stats, wscratch(ctx), d_rem);
+                }
+                SV_HIP(hipGetLastError());
+                uint32_t rem = 0;
+                SV_HIP(hipMemcpyAsync(&rem, d_rem, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+                SV_HIP(hipStreamSynchronize(ctx->stream));
+                int32_t ab = 0;
+                SV_HIP(hipMemcpy(&ab, ctx->d_abort, sizeof(int32_t), hipMemcpyDeviceToHost));
+                if (rem == 0 || ab) break;
+                if (round > 1 << 20) throw std::runtime_error("plaquette rounds did not terminate");
+            }
+            if (!wcheck(ctx, reps)) {
+                cur = c;
+                break;
+            }
+            wabsorb(reps, 0, skips);
+            snapshot(st, true);
+        }
+        SV_HIP(hipMemcpyAsync(stats, ctx->d_stats, sizeof(sv_stats), hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipFreeAsync(d_rem, ctx->stream));
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+        stats->proposed = V;
+        int64_t rj = 0;
+        for (auto &kv : skips) rj += (int64_t)kv.second.size();
+        stats->rejections = rj;
+        rng->state_hi = cur.s.hi;
+        rng->state_lo = cur.s.lo;
+        rng->has_uint32 = (int32_t)cur.has;
+        rng->uinteger = cur.buf;
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_worldline_plaquette(sv_ctx *ctx, int32_t N, double kappa, double W_eff, int64_t *m, void *v,
+                           int32_t v_is_float, const int64_t *order, sv_rng *rng, sv_stats *stats) {
+    sv_worldline *st = nullptr;
+    int rc = sv_worldline_create(ctx, N, v_is_float, &st);
+    if (rc) return rc;
+    rc = sv_worldline_upload(st, m, v);
+    if (!rc) rc = sv_worldline_plaquette_ordered_run(st, kappa, W_eff, order, rng, stats);
+    if (!rc) rc = sv_worldline_download(st, m, v);
+    sv_worldline_destroy(st);
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,180 @@
+"""Worldline hot-path generators on the MI355X.
+
+CoexactUpdate   supervillain/generator/worldline/coexact.py:12-194
+PlaquetteUpdate supervillain/generator/worldline/plaquette.py:9-113
+
+Same constructors, attributes, `step` contracts and `report()` texts as the reference; the sweeps
+run in libsvhip.so (include/supervillain_amd.h) replaying `self.rng`'s NumPy PCG64 stream.
+"""
+import ctypes
+
+import numpy as np
+
+from supervillain_amd import _native
+from supervillain_amd.generator._common import DeviceState, rng_from_numpy, rng_to_numpy, wrap_like
+from supervillain_amd.generator.generator import Generator
+
+
+def _is_worldline(action):
+    return type(action).__name__ == 'Worldline' and hasattr(action, '_W') and hasattr(action, 'Lattice')
+
+
+class _WorldlineDevice(DeviceState):
+    def _state(self):
+        L = self.Action.Lattice
+        if L.D != 2:
+            raise NotImplementedError(f'the MI355X {self} is implemented for D=2 lattices')
+        v_float = not (self.Action.W < float('inf'))
+        dev = self.__dict__.get('_dev')
+        if dev is None or dev[1] != (L.N, v_float):
+            ctx = self._device_context()
+            h = ctypes.c_void_p()
+            ctx.check(_native.lib().sv_worldline_create(ctx.handle, L.N, int(v_float), ctypes.byref(h)),
+                      'sv_worldline_create')
+            dev = (ctx, (L.N, v_float), h)
+            self._dev = dev
+        return dev
+
+    def __del__(self):
+        dev = self.__dict__.get('_dev')
+        if dev is not None and _native._LIB is not None:
+            try:
+                _native._LIB.sv_worldline_destroy(dev[2])
+            except Exception:
+                pass
+
+    def _fields(self, cfg):
+        N = self.Action.Lattice.N
+        m = np.array(cfg['m'], dtype=np.int64, order='C', copy=True).reshape(2, N, N)
+        v_float = not (self.Action.W < float('inf'))
+        v = np.array(cfg['v'], dtype=np.float64 if v_float else np.int64, order='C', copy=True).reshape(1, N, N)
+        return m, v
+
+
+class CoexactUpdate(_WorldlineDevice, Generator):
+    r'''Changes m by delta t with t = ±1..±interval_t on one plaquette colour at a time (coexact.py:12-31).'''
+
+    def __init__(self, action, interval_t=1, *, device=None):
+        if not _is_worldline(action):
+            raise ValueError('Need a Worldline action')
+        self.Action = action
+        self.Lattice = action.Lattice
+        self.kappa = action.kappa
+        self.interval_t = interval_t
+        self.ts = tuple(range(-interval_t, 0)) + tuple(range(1, interval_t + 1))
+        self.rng = np.random.default_rng()
+        self.accepted = 0
+        self.proposed = 0
+        self.acceptance = 0.
+        self.sweeps = 0
+        self.device = device
+
+    def __str__(self):
+        return 'SiteUpdate'  # sic: the reference's CoexactUpdate.__str__ (coexact.py:50-51)
+
+    def _advance(self, cfg, sweeps):
+        ctx, _, h = self._state()
+        m, v = self._fields(cfg)
+        L = _native.lib()
+        st = _native.stats_array(sweeps)
+        r = rng_from_numpy(self.rng)
+        ctx.check(L.sv_worldline_upload(h, _native.ptr(m), _native.ptr(v)), 'sv_worldline_upload')
+        ctx.check(L.sv_worldline_coexact_run(h, float(self.kappa), float(self.Action._W), int(self.interval_t),
+                                             sweeps, ctypes.byref(r), st), 'sv_worldline_coexact_run')
+        ctx.check(L.sv_worldline_download(h, _native.ptr(m), None), 'sv_worldline_download')
+        rng_to_numpy(r, self.rng)
+        P = self.Lattice.cells_of_degree[2]
+        for k in range(sweeps):  # coexact.py:122-124
+            self.sweeps += 1
+            self.proposed += P
+            self.acceptance += st[k].acceptance_sum / P
+            self.accepted += int(st[k].accepted)
+        return cfg | {'m': wrap_like(cfg['m'], m, 1, self.Lattice)}
+
+    def step(self, cfg):
+        return self._advance(cfg, 1)
+
+    def _steps(self, cfg, count):
+        return self._advance(cfg, count)
+
+    def report(self):
+        return (
+            f'There were {self.accepted} coexact proposals accepted of {self.proposed} proposed updates.'
+            + '\n' +
+            f'    {self.accepted/self.proposed:.6f} acceptance rate'
+            + '\n' +
+            f'    {self.acceptance / self.sweeps:.6f} average Metropolis acceptance probability.'
+        )
+
+
+class PlaquetteUpdate(_WorldlineDevice, Generator):
+    r'''Single-plaquette Metropolis on the 4 boundary links of m and on v (plaquette.py:9-22).
+
+    mode='reference' (default) keeps the reference's chain: every sweep visits the plaquettes in the
+    order np.random.permutation(L.coordinates) draws from NumPy's global RandomState, exactly as
+    plaquette.py:63 does, and the device processes them in dependency rounds that reproduce the
+    sequential loop bit-for-bit.  mode='checkerboard' is the GPU-native variant: colour
+    passes, no global-RandomState draw, a different but equally valid chain.
+    '''
+
+    def __init__(self, action, *, mode='reference', device=None):
+        if not _is_worldline(action):
+            raise ValueError('The PlaquetteUpdate requires the Worldline action.')
+        if mode not in ('reference', 'checkerboard'):
+            raise ValueError("mode must be 'reference' or 'checkerboard'")
+        self.Action = action
+        self.accepted = 0
+        self.proposed = 0
+        self.rng = np.random.default_rng()
+        self.acceptance = 0.
+        self.mode = mode
+        self.device = device
+
+    def __str__(self):
+        return 'PlaquetteUpdate'
+
+    def _advance(self, cfg, sweeps):
+        ctx, _, h = self._state()
+        m, v = self._fields(cfg)
+        Lib = _native.lib()
+        L = self.Action.Lattice
+        r = rng_from_numpy(self.rng)
+        ctx.check(Lib.sv_worldline_upload(h, _native.ptr(m), _native.ptr(v)), 'sv_worldline_upload')
+        kappa, W = float(self.Action.kappa), float(self.Action._W)
+        if self.mode == 'reference':
+            st = _native.stats_array(1)
+            stats = []
+            for _ in range(sweeps):
+                order = np.random.permutation(L.coordinates)  # plaquette.py:63, global RandomState
+                lin = np.ascontiguousarray((order[:, 0] % L.N) * L.N + (order[:, 1] % L.N), dtype=np.int64)
+                ctx.check(Lib.sv_worldline_plaquette_ordered_run(h, kappa, W, _native.ptr(lin), ctypes.byref(r), st),
+                          'sv_worldline_plaquette_ordered_run')
+                stats.append((int(st[0].accepted), st[0].acceptance_sum))
+        else:
+            st = _native.stats_array(sweeps)
+            ctx.check(Lib.sv_worldline_plaquette_checkerboard_run(h, kappa, W, sweeps, ctypes.byref(r), st),
+                      'sv_worldline_plaquette_checkerboard_run')
+            stats = [(int(st[k].accepted), st[k].acceptance_sum) for k in range(sweeps)]
+        ctx.check(Lib.sv_worldline_download(h, _native.ptr(m), _native.ptr(v)), 'sv_worldline_download')
+        rng_to_numpy(r, self.rng)
+        P = L.sites * len(L.components[2])
+        for acc, psum in stats:  # plaquette.py:73, 101-103
+            self.acceptance += psum
+            self.accepted += acc
+            self.proposed += P
+        return cfg | {'m': wrap_like(cfg['m'], m, 1, L), 'v': wrap_like(cfg['v'], v, 2, L)}
+
+    def step(self, cfg):
+        return self._advance(cfg, 1)
+
+    def _steps(self, cfg, count):
+        return self._advance(cfg, count)
+
+    def report(self):
+        return (
+            f'There were {self.accepted} single-plaquette proposals accepted of {self.proposed} proposed updates.'
+            + '\n' +
+            f'    {self.accepted/self.proposed:.6f} acceptance rate'
+            + '\n' +
+            f'    {self.acceptance / self.proposed :.6f} average Metropolis acceptance probability.'
+        )

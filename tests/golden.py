@@ -38,3 +38,26 @@ def state_of(gen):
     s, inc = st['state']['state'], st['state']['inc']
     return np.array([s >> 64, s & ((1 << 64) - 1), inc >> 64, inc & ((1 << 64) - 1), st['has_uint32'],
                      st['uinteger']], dtype=np.uint64)
+
+
+_MULT = 0x2360ED051FC65DA44385DF649FCCF645
+_MINV = pow(_MULT, -1, 1 << 128)
+_M128 = (1 << 128) - 1
+
+
+def crafted_generator(seed, position, half):
+    """A Generator(PCG64) whose raw output `position` has its low (half=0) or high (half=1) 32 bits
+    zero, forcing a NumPy Lemire rejection there (natural rate 2^-32 per draw)."""
+    gen = np.random.default_rng(seed)
+    inc = gen.bit_generator.state['state']['inc']
+    hi = (0x0123456789ABCDEF ^ (seed * 0x9E3779B1)) & ((1 << 58) - 1)
+    out = 0xDEADBEEF00000000 if half == 0 else 0x00000000DEADBEEF
+    s = (hi << 64) | (hi ^ out)
+    for _ in range(position + 1):
+        s = ((s - inc) * _MINV) & _M128
+    st = gen.bit_generator.state
+    st['state']['state'] = s
+    st['has_uint32'] = 0
+    st['uinteger'] = 0
+    gen.bit_generator.state = st
+    return gen

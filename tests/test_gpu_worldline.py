@@ -1,0 +1,149 @@
+"""CoexactUpdate and PlaquetteUpdate on the MI355X vs golden vectors and the CPU oracle."""
+import numpy as np
+import pytest
+
+import supervillain_amd as sv
+from tests.golden import cases, crafted_generator, generator_from, state_of
+
+pytestmark = pytest.mark.gpu
+
+
+def coexact_gpu(N, kappa, W, v, sweeps, gen, interval_t=1):
+    L = sv.Lattice2D(N)
+    S = sv.Worldline(L, kappa, W)
+    G = sv.generator.worldline.CoexactUpdate(S, interval_t=interval_t)
+    G.rng = gen
+    cfg = {'m': sv.Form(np.zeros((2, N, N), dtype=int), degree=1, lattice=L),
+           'v': sv.Form(v.reshape(1, N, N), degree=2, lattice=L)}
+    acc, accept = [], []
+    for _ in range(sweeps):
+        cfg = cfg | G.step(cfg)
+        acc.append(G.accepted)
+        accept.append(G.acceptance)
+    return G, S, cfg, acc, accept
+
+
+def test_coexact_golden():
+    for c in cases('worldline_coexact.npz'):
+        G, S, cfg, acc, accept = coexact_gpu(c['N'], c['kappa'], c['W'], c['v'], c['sweeps'],
+                                             generator_from(c['rng0']), c['interval_t'])
+        assert (np.asarray(cfg['m']) == c['m']).all(), (c['N'], c['W'])
+        assert (state_of(G.rng) == c['rng1']).all()
+        assert acc == list(c['accepted'])
+        np.testing.assert_allclose(accept, c['acceptance'], rtol=1e-12)
+        assert S.valid(cfg)
+        assert np.asarray(cfg['m']).dtype == np.int64
+
+
+@pytest.mark.parametrize('N,W', [(64, 1), (130, 3), (256, float('inf')), (63, 2)])
+def test_coexact_oracle(N, W, oracle_lib):
+    r = np.random.default_rng(N)
+    v = r.integers(-3, 4, (N, N)) if W < float('inf') else r.standard_normal((N, N))
+    G, S, cfg, acc, _ = coexact_gpu(N, 0.5, W, v, 5, np.random.default_rng(N + 1))
+    m = np.zeros((2, N, N), dtype=np.int64)
+    g = np.random.default_rng(N + 1)
+    oracle_lib.worldline_coexact(N, 0.5, S._W, m, np.ascontiguousarray(v), 5, g)
+    assert (np.asarray(cfg['m']) == m).all() and G.rng.bit_generator.state == g.bit_generator.state
+
+
+def test_coexact_forced_rejection(oracle_lib):
+    """interval_t=3 draws from 6 values, whose Lemire sampler can reject: force one."""
+    N = 16
+    V = N * N
+    v = np.random.default_rng(3).integers(-3, 4, (N, N))
+    for pos, half in [(V + 5, 0), (V + V // 4 + 2, 1)]:
+        G, S, cfg, _, _ = coexact_gpu(N, 0.5, 1, v, 3, crafted_generator(pos, pos, half), interval_t=3)
+        m = np.zeros((2, N, N), dtype=np.int64)
+        g = crafted_generator(pos, pos, half)
+        st = oracle_lib.worldline_coexact(N, 0.5, 1.0, m, np.ascontiguousarray(v), 3, g, interval_t=3)
+        assert sum(s.rejections for s in st) >= 1
+        assert (np.asarray(cfg['m']) == m).all() and G.rng.bit_generator.state == g.bit_generator.state
+
+
+def test_plaquette_reference_order_golden():
+    for c in cases('worldline_plaquette.npz'):
+        N = c['N']
+        L = sv.Lattice2D(N)
+        S = sv.Worldline(L, c['kappa'], c['W'])
+        G = sv.generator.worldline.PlaquetteUpdate(S)
+        G.rng = generator_from(c['rng0'])
+        cfg = S.configurations(1)[0]
+        saved = np.random.get_state()
+        np.random.seed(c['np_seed'])
+        try:
+            for k in range(c['sweeps']):
+                cfg = cfg | G.step(cfg)
+                assert G.accepted == c['accepted'][k]
+                np.testing.assert_allclose(G.acceptance, c['acceptance'][k], rtol=1e-12)
+        finally:
+            np.random.set_state(saved)
+        assert (np.asarray(cfg['m']) == c['m']).all() and (np.asarray(cfg['v'])[0] == c['v']).all()
+        assert (state_of(G.rng) == c['rng1']).all()
+        assert S.valid(cfg)
+
+
+@pytest.mark.parametrize('N,W', [(32, 1), (64, 2), (100, float('inf'))])
+def test_plaquette_reference_order_oracle(N, W, oracle_lib):
+    L = sv.Lattice2D(N)
+    S = sv.Worldline(L, 0.4, W)
+    G = sv.generator.worldline.PlaquetteUpdate(S)
+    G.rng = np.random.default_rng(5)
+    cfg = S.configurations(1)[0]
+    saved = np.random.get_state()
+    np.random.seed(77)
+    orders = []
+    for _ in range(3):
+        st = np.random.get_state()
+        o = np.random.permutation(L.coordinates)
+        np.random.set_state(st)
+        orders.append((o[:, 0] % N) * N + (o[:, 1] % N))
+        cfg = cfg | G.step(cfg)
+    np.random.set_state(saved)
+    m = np.zeros((2, N, N), dtype=np.int64)
+    v = np.zeros((N, N), dtype=np.float64 if W == float('inf') else np.int64)
+    g = np.random.default_rng(5)
+    for o in orders:
+        oracle_lib.worldline_plaquette_seq(N, 0.4, S._W, m, v, o, g)
+    assert (np.asarray(cfg['m']) == m).all() and (np.asarray(cfg['v'])[0] == v).all()
+    assert G.rng.bit_generator.state == g.bit_generator.state
+
+
+def test_plaquette_reference_order_forced_rejection(oracle_lib):
+    N = 12
+    V = N * N
+    L = sv.Lattice2D(N)
+    S = sv.Worldline(L, 0.4, 1)
+    pos, half = V // 2 + 9, 1  # inside the change_v block (choice over 3 values)
+    G = sv.generator.worldline.PlaquetteUpdate(S)
+    G.rng = crafted_generator(pos, pos, half)
+    saved = np.random.get_state()
+    np.random.seed(3)
+    st0 = np.random.get_state()
+    o = np.random.permutation(L.coordinates)
+    np.random.set_state(st0)
+    cfg = G.step(S.configurations(1)[0])
+    np.random.set_state(saved)
+    m = np.zeros((2, N, N), dtype=np.int64)
+    v = np.zeros((N, N), dtype=np.int64)
+    g = crafted_generator(pos, pos, half)
+    st = oracle_lib.worldline_plaquette_seq(N, 0.4, 1.0, m, v, (o[:, 0] % N) * N + (o[:, 1] % N), g)
+    assert st.rejections >= 1
+    assert (np.asarray(cfg['m']) == m).all() and (np.asarray(cfg['v'])[0] == v).all()
+    assert G.rng.bit_generator.state == g.bit_generator.state
+
+
+@pytest.mark.parametrize('N,W', [(8, 1), (9, 2), (64, float('inf')), (256, 1)])
+def test_plaquette_checkerboard_oracle(N, W, oracle_lib):
+    L = sv.Lattice2D(N)
+    S = sv.Worldline(L, 0.5, W)
+    G = sv.generator.worldline.PlaquetteUpdate(S, mode='checkerboard')
+    G.rng = np.random.default_rng(N)
+    cfg = G._steps(S.configurations(1)[0], 6)
+    m = np.zeros((2, N, N), dtype=np.int64)
+    v = np.zeros((N, N), dtype=np.float64 if W == float('inf') else np.int64)
+    g = np.random.default_rng(N)
+    st = oracle_lib.worldline_plaquette_cb(N, 0.5, S._W, m, v, 6, g)
+    assert (np.asarray(cfg['m']) == m).all() and (np.asarray(cfg['v'])[0] == v).all()
+    assert G.rng.bit_generator.state == g.bit_generator.state
+    assert G.accepted == sum(s.accepted for s in st)
+    assert S.valid(cfg)

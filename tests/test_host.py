@@ -1,0 +1,141 @@
+"""Host-side mirror of the reference interface (CPU): lattice, forms, actions, storage, composition.
+
+The Ensemble/KeepEvery/Sequentially logic is exercised with an oracle-backed stand-in generator
+(test-only) and compared with golden vectors captured from the reference's own Ensemble.generate."""
+import numpy as np
+import pytest
+
+import supervillain_amd as sv
+from supervillain_amd.batch import Batch
+from supervillain_amd.lattice import d, delta
+from tests.golden import cases
+
+
+def test_checkerboarding_matches_reference():
+    for c in cases('checkerboarding.npz'):
+        L = sv.Lattice2D(c['N'])
+        cid = np.full((c['N'], c['N']), -1)
+        for i, color in enumerate(L.checkerboarding):
+            cid[color] = i
+        assert (cid == c['colors']).all()
+
+
+def test_colours_have_no_same_colour_neighbours():
+    for N in range(2, 14):
+        L = sv.Lattice2D(N)
+        cid = np.full((N, N), -1)
+        for i, color in enumerate(L.checkerboarding):
+            cid[color] = i
+        if N > 2:
+            assert (cid != np.roll(cid, 1, 0)).all() and (cid != np.roll(cid, 1, 1)).all()
+
+
+def test_d_delta_nilpotent_and_dtypes():
+    L = sv.Lattice(3, 4)
+    rng = np.random.default_rng(0)
+    f0 = sv.Form(rng.integers(-3, 4, (1, 4, 4, 4)), degree=0, lattice=L)
+    f2 = sv.Form(rng.integers(-3, 4, (3, 4, 4, 4)), degree=2, lattice=L)
+    assert (d(d(f0)) == 0).all()
+    assert (delta(delta(f2)) == 0).all()
+    assert np.asarray(d(f0)).dtype == np.int64 and np.asarray(delta(f2)).dtype == np.int64
+
+
+def test_villain_action_matches_golden(oracle_lib):
+    for c in cases('villain_neighborhood.npz'):
+        L = sv.Lattice2D(c['N'])
+        S = sv.Villain(L, c['kappa'], c['W'])
+        phi = sv.Form(c['phi'][None], degree=0, lattice=L)
+        n = sv.Form(c['n'], degree=1, lattice=L)
+        np.testing.assert_allclose(S(phi, n), c['action'], rtol=1e-12)
+        assert S.valid({'n': n})
+
+
+def test_worldline_action_matches_golden():
+    for c in cases('worldline_coexact.npz'):
+        L = sv.Lattice2D(c['N'])
+        S = sv.Worldline(L, c['kappa'], c['W'])
+        m = sv.Form(c['m'], degree=1, lattice=L)
+        v = sv.Form(c['v'][None], degree=2, lattice=L)
+        assert S.valid({'m': m})
+        np.testing.assert_allclose(S(m, v), c['action'], rtol=1e-12)
+    L = sv.Lattice2D(4)
+    S = sv.Worldline(L, 0.5, 1)
+    bad = L.zeros(1, dtype=int)
+    bad[0, 0, 0] = 1
+    with pytest.raises(ValueError):
+        S(bad, L.zeros(2, dtype=int))
+
+
+def test_batch_rejects_lossy_casts():
+    b = Batch(3, shape=(2,), dtype=int)
+    b[0] = np.array([1.0, 2.0])
+    with pytest.raises(TypeError):
+        b[1] = np.array([1.5, 2.0])
+
+
+def test_generators_reject_wrong_action():
+    L = sv.Lattice2D(4)
+    with pytest.raises(ValueError):
+        sv.generator.villain.NeighborhoodUpdate(sv.Worldline(L, 0.5, 1))
+    with pytest.raises(ValueError):
+        sv.generator.worldline.CoexactUpdate(sv.Villain(L, 0.5, 1))
+    with pytest.raises(ValueError):
+        sv.generator.worldline.PlaquetteUpdate(sv.Villain(L, 0.5, 1))
+
+
+class OracleNeighborhood(sv.generator.Generator):
+    """Test-only stand-in with NeighborhoodUpdate's contract, backed by the CPU oracle."""
+
+    def __init__(self, S, oracle, interval_phi=np.pi):
+        self.Action, self.O, self.interval_phi = S, oracle, interval_phi
+        self.rng = np.random.default_rng()
+        self.accepted = self.proposed = self.sweeps = 0
+        self.acceptance = 0.
+
+    def step(self, cfg):
+        N = self.Action.Lattice.N
+        phi = np.array(cfg['phi'], dtype=float).reshape(N, N).copy()
+        n = np.array(cfg['n'], dtype=np.int64).copy()
+        st = self.O.villain_neighborhood(N, self.Action.kappa, self.Action.W, phi, n, 1, self.rng,
+                                         interval_phi=self.interval_phi)
+        V = N * N
+        self.sweeps += 1
+        self.proposed += V
+        self.acceptance += st[0].acceptance_sum / V
+        self.accepted += st[0].accepted
+        L = self.Action.Lattice
+        return cfg | {'phi': sv.Form(phi[None], degree=0, lattice=L), 'n': sv.Form(n, degree=1, lattice=L)}
+
+    def report(self):
+        return (f'There were {self.accepted} neighborhood proposals accepted of {self.proposed} proposed updates.'
+                + '\n' + f'    {self.accepted/self.proposed:.6f} acceptance rate' + '\n'
+                + f'    {self.acceptance / self.sweeps:.6f} average Metropolis acceptance probability.')
+
+
+def test_ensemble_generate_matches_golden(oracle_lib):
+    c = [x for x in cases('ensemble.npz') if x['kind'] == 'villain_generate'][0]
+    L = sv.Lattice2D(c['N'])
+    S = sv.Villain(L, c['kappa'], c['W'])
+    G = OracleNeighborhood(S, oracle_lib)
+    G.rng = np.random.default_rng(c['seed'])
+    E = sv.Ensemble(S).generate(c['steps'], G, starting_index=c['starting_index'], index_stride=c['index_stride'])
+    assert E.configuration.phi.array.shape == c['phi'].shape and E.configuration.phi.dtype == np.float64
+    assert E.configuration.n.dtype == np.int64
+    assert (E.configuration.phi.array == c['phi']).all() and (E.configuration.n.array == c['n']).all()
+    assert (E.index.array == c['index']).all() and (E.weight.array == c['weight']).all()
+    assert G.report() == c['report']
+    e2 = E.cut(2).every(2)
+    assert len(e2) == len(range(2, c['steps'], 2))
+    assert isinstance(e2.generator, sv.generator.KeepEvery)
+
+
+def test_keepevery_sequentially_matches_golden(oracle_lib):
+    c = [x for x in cases('ensemble.npz') if x['kind'] == 'keepevery_sequentially'][0]
+    L = sv.Lattice2D(c['N'])
+    S = sv.Villain(L, c['kappa'], c['W'])
+    a, b = OracleNeighborhood(S, oracle_lib), OracleNeighborhood(S, oracle_lib, interval_phi=1.0)
+    a.rng, b.rng = np.random.default_rng(8), np.random.default_rng(9)
+    G = sv.generator.KeepEvery(3, sv.generator.Sequentially((a, b)))
+    E = sv.Ensemble(S).generate(c['steps'], G)
+    assert (E.configuration.phi.array == c['phi']).all() and (E.configuration.n.array == c['n']).all()
+    assert G.report() == c['report']
