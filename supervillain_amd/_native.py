@@ -9,7 +9,7 @@ import threading
 from supervillain_amd._abi import SvRng, SvStats
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libsvhip.so')
+LIB_PATH = os.environ.get('SV_LIB_OVERRIDE') or os.path.join(_HERE, 'libsvhip.so')  # override: timing experiments
 _LIB = None
 _LOCK = threading.RLock()
 _CONTEXTS = {}

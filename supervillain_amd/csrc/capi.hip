@@ -62,24 +62,27 @@ void sv_ctx::time_begin(hipEvent_t *a) {
     SV_HIP(hipEventRecord(*a, stream));
 }
 
-void sv_ctx::time_end(hipEvent_t a) {
+void sv_ctx::time_end(hipEvent_t a, int64_t launches) {
     if (!timing || !a) return;
     hipEvent_t b = take_event(ev_pool);
     SV_HIP(hipEventRecord(b, stream));
     ev_pending.push_back({a, b});
+    ev_launches.push_back(launches);
 }
 
 void sv_ctx::time_collect() {
-    for (auto &p : ev_pending) {
+    for (size_t i = 0; i < ev_pending.size(); i++) {
+        auto &p = ev_pending[i];
         float ms = 0.f;
         SV_HIP(hipEventSynchronize(p.second));
         SV_HIP(hipEventElapsedTime(&ms, p.first, p.second));
         timed_ms += ms;
-        timed_launches += 1;
+        timed_launches += ev_launches[i];
         ev_pool.push_back(p.first);
         ev_pool.push_back(p.second);
     }
     ev_pending.clear();
+    ev_launches.clear();
 }
 
 void sv_ctx::time_discard() {
@@ -88,6 +91,7 @@ void sv_ctx::time_discard() {
         ev_pool.push_back(p.second);
     }
     ev_pending.clear();
+    ev_launches.clear();
 }
 
 extern "C" {

@@ -88,10 +88,11 @@ struct sv_ctx {
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
+    std::vector<int64_t> ev_launches;
     double timed_ms = 0.0;
     int64_t timed_launches = 0;
     void time_begin(hipEvent_t *a);
-    void time_end(hipEvent_t a);
+    void time_end(hipEvent_t a, int64_t launches = 1);
     void time_collect();  // after a stream sync
     void time_discard();  // drop pending (unsynchronized-safe: after a stream sync)
 

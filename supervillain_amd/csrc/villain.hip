@@ -20,6 +20,8 @@
 //   dS_link:                ((kappa/2) * cr) * ((2*r) + cr)            (neighborhood.py:111)
 //   face_sum:               (((0 + f0[x]) + f0[x-e0]) + f1[x]) + f1[x-e1]  (reference.py:48-64)
 //   r update:               (r + d(cphi)) - (2pi)*cn                  (neighborhood.py:129)
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 
 #include "common.h"
@@ -216,6 +218,24 @@ __device__ __forceinline__ int32_t wrapN(int32_t v, int32_t N) {
     return v;
 }
 
+#ifndef SV_ABLATE
+#define SV_ABLATE 0  // timing experiments only: 1 = no exp, 2 = no RNG compositions, 3 = both
+#endif
+__device__ __forceinline__ double sv_exp(double x) {
+#if SV_ABLATE & 1
+    return 1.0 + x * 0.5;
+#else
+    return exp(x);
+#endif
+}
+__device__ __forceinline__ u128 sv_apply(const Affine &f, u128 s) {
+#if SV_ABLATE & 2
+    return u128{s.lo ^ f.A.lo, s.hi + f.C.hi};
+#else
+    return apply(f, s);
+#endif
+}
+
 __device__ __forceinline__ u128 readlane128(u128 v, int lane) {
     u128 r;
     const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v.lo, lane);
@@ -240,7 +260,7 @@ __device__ __forceinline__ int64_t base_pos(int ty, int64_t gq, int64_t N, int64
 
 struct Draws {
     double u, dphi;
-    int64_t cn[4];
+    int32_t cn[4];  // W * (choice - interval_n); |W * interval_n| < 2^28 on this path
 };
 
 // Slow paths (branched around when no lane needs them).  The trailing wait keeps table loads from
@@ -260,11 +280,11 @@ __device__ __forceinline__ u128 from_base(const JumpTables *T, const Block *blk,
     return st;
 }
 
-__device__ __forceinline__ int64_t choice_value(const FArgs &A, uint32_t word, uint32_t bidx, uint32_t spos) {
+__device__ __forceinline__ int32_t choice_value(const FArgs &A, uint32_t word, uint32_t bidx, uint32_t spos) {
     bool rej;
     const uint32_t idx = lemire(word, A.P.k, A.P.thr, &rej);
     if (rej) report(A.S, A.sweep, bidx, spos);
-    return A.P.W * ((int64_t)idx - A.P.interval_n);
+    return (int32_t)A.P.W * ((int32_t)idx - (int32_t)A.P.interval_n);
 }
 
 // General draws: any strip (wrapped columns), skips, mismatched buffers.  6 compositions per site.
@@ -315,11 +335,11 @@ __device__ __forceinline__ Draws draws_fast(const FArgs &A, int c, bool active, 
     const uint32_t PM = rowlin + xb, PR = PM >> 1;
     Draws D;
     {
-        const u128 st = apply(sm[(gx - xb) & (SMALL_LDS - 1)], bases[0]);
+        const u128 st = sv_apply(sm[(gx - xb) & (SMALL_LDS - 1)], bases[0]);
         D.u = 0.0 + 1.0 * to_double(xsl_rr(st));
     }
     {
-        const u128 st = apply(sm[(rank - PR) & (SMALL_LDS - 1)], bases[1]);
+        const u128 st = sv_apply(sm[(rank - PR) & (SMALL_LDS - 1)], bases[1]);
         D.dphi = A.P.lo_phi + A.P.range_phi * to_double(xsl_rr(st));
     }
     D.cn[0] = D.cn[1] = D.cn[2] = D.cn[3] = 0;
@@ -335,7 +355,7 @@ __device__ __forceinline__ Draws draws_fast(const FArgs &A, int c, bool active, 
             if (lane == 63 && P) qq = R0 - h;                        // lane 63 serves lane 0's word
             const uint32_t half = (lane == 63 && P) ? 0u : (qq & 1u);
             const uint32_t w = qq >> 1;
-            const u128 st = apply(sm[(w - PW) & (SMALL_LDS - 1)], half ? bases[3 + 2 * mu] : bases[2 + 2 * mu]);
+            const u128 st = sv_apply(sm[(w - PW) & (SMALL_LDS - 1)], half ? bases[3 + 2 * mu] : bases[2 + 2 * mu]);
             const uint64_t X = xsl_rr(st);
             // lo lanes computed the fwd word (send its high half), hi lanes the bwd word (send its low half)
             const uint32_t send = half ? (uint32_t)X : (uint32_t)(X >> 32);
@@ -363,6 +383,8 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
     __shared__ int32_t s_n0[R][RW];
     __shared__ int32_t s_n1[R][RW];
     __shared__ Affine s_small[SMALL_LDS];
+    __shared__ Affine s_adv[3];
+    __shared__ u128 s_base[NW][16];  // per wave: [8c + ty] = block ty's base for the colour-c row
     __shared__ int32_t s_bad;
 
     if (*(volatile const int32_t *)A.S.abort) return;
@@ -390,6 +412,7 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
     const bool interior = x0 >= 4 && x1 + 2 < N;
 
     for (int e = threadIdx.x; e < SMALL_LDS; e += nthreads) s_small[e] = A.T->small[e];
+    if (threadIdx.x < 3) s_adv[threadIdx.x] = A.adv[threadIdx.x];
     if (threadIdx.x == 0) s_bad = 0;
 
     // fast draws need, per colour, no skips and equal buffers within each fwd/bwd pair
@@ -449,6 +472,7 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
     u128 bases{0, 0};
     if (base_lane) bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)base_pos(bty, wrapN(brow, N), N, xb, bhas));
     __builtin_amdgcn_s_waitcnt(0);
+    if (base_lane) s_base[wave][lane] = bases;
 
     int64_t acc_count = 0;
     double psum = 0.0;
@@ -487,7 +511,7 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
             const bool active = row_ok && x <= x1 + 1;
             u128 bs[6];
 #pragma unroll
-            for (int k = 0; k < 6; k++) bs[k] = readlane128(bases, k);
+            for (int k = 0; k < 6; k++) bs[k] = s_base[wave][k];
             Draws D;
             if (fast[0])
                 D = draws_fast(A, 0, active, lane, (uint32_t)gq * (uint32_t)N, (uint32_t)xs, (uint32_t)x, (uint32_t)xb,
@@ -518,7 +542,7 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
                     const double bb2 = (2.0 * r0[k]) + cr[k];
                     dS += a * bb2;
                 }
-                double p = exp(-dS);
+                double p = sv_exp(-dS);
                 p = p < 0.0 ? 0.0 : p;
                 p = p > 1.0 ? 1.0 : p;
                 const int acc = D.u < p;
@@ -531,8 +555,8 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
                 s_phi[s0][cx] = (ph + cphi) + 0.0;  // final colour-0 phi (the colour-1 pass adds +0.0)
                 const double dcp_f = 0.0 + (0.0 - cphi);
                 const double dcp_b = 0.0 + (cphi - 0.0);
-                const int32_t c0 = (int32_t)(D.cn[0] * acc), c1 = (int32_t)(D.cn[1] * acc);
-                const int32_t c2 = (int32_t)(D.cn[2] * acc), c3 = (int32_t)(D.cn[3] * acc);
+                const int32_t c0 = acc ? D.cn[0] : 0, c1 = acc ? D.cn[1] : 0;
+                const int32_t c2 = acc ? D.cn[2] : 0, c3 = acc ? D.cn[3] : 0;
                 s_n0[s0][cx] = n_f0 + c0;
                 s_n0[sm][cx] = n_b0 + c1;
                 s_n1[s0][cx] = n_f1 + c2;
@@ -554,7 +578,7 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
             const bool active = row_ok && x <= x1;
             u128 bs[6];
 #pragma unroll
-            for (int k = 0; k < 6; k++) bs[k] = readlane128(bases, 8 + k);
+            for (int k = 0; k < 6; k++) bs[k] = s_base[wave][8 + k];
             Draws D;
             if (fast[1])
                 D = draws_fast(A, 1, active, lane, (uint32_t)gq * (uint32_t)N, (uint32_t)xs, (uint32_t)x, (uint32_t)xb,
@@ -583,7 +607,7 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
                     const double bb2 = (2.0 * ri[k]) + cr[k];
                     dS += a * bb2;
                 }
-                double p = exp(-dS);
+                double p = sv_exp(-dS);
                 p = p < 0.0 ? 0.0 : p;
                 p = p > 1.0 ? 1.0 : p;
                 const int acc = D.u < p;
@@ -593,10 +617,12 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
                 }
                 const double cphi = D.dphi * (double)acc;
                 s_phi[s0][cx] = (ph + 0.0) + cphi;
-                s_n0[s0][cx] += (int32_t)(D.cn[0] * acc);
-                s_n0[sm][cx] += (int32_t)(D.cn[1] * acc);
-                s_n1[s0][cx] += (int32_t)(D.cn[2] * acc);
-                s_n1[s0][cx - 1] += (int32_t)(D.cn[3] * acc);
+                if (acc) {
+                    s_n0[s0][cx] += D.cn[0];
+                    s_n0[sm][cx] += D.cn[1];
+                    s_n1[s0][cx] += D.cn[2];
+                    s_n1[s0][cx - 1] += D.cn[3];
+                }
             }
         }
         commit(t + 3 + NW);  // slots of rows [t-NW, t): not read in phase C
@@ -606,9 +632,10 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
             const int64_t p_new = base_pos(bty, wrapN(brow + NW, N), N, xb, bhas);
             const int ai = bty == 0 ? 0 : (bty == 1 ? 1 : 2);
             const int64_t step = bty == 0 ? (int64_t)NW * N : (bty == 1 ? (int64_t)NW * N / 2 : (int64_t)NW * N / 4);
-            if (p_new - p_old == step) bases = apply(A.adv[ai], bases);
+            if (p_new - p_old == step) bases = apply(s_adv[ai], bases);
             else bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)p_new);
             brow += NW;
+            s_base[wave][lane] = bases;  // read by this wave only, after the barrier below
         }
         __syncthreads();
     }
@@ -865,15 +892,21 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     std::vector<Block> blocks;
     std::vector<uint32_t> skipvec;
     int sw = 0;
+    const bool dbg = getenv("SV_DEBUG_TIMING") != nullptr;
     while (sw < sweeps) {
         const int count = std::min(BATCH, sweeps - sw);
         Cursor c = cur;
+        auto tp0 = std::chrono::steady_clock::now();
         plan_sweeps(ctx, c, inc, specs, sw, count, skips, blocks, skipvec);
+        auto tp1 = std::chrono::steady_clock::now();
+        if (dbg) fprintf(stderr, "[sv] plan %d sweeps: %.1f us\n", count, std::chrono::duration<double, std::micro>(tp1 - tp0).count());
         upload_plan(ctx, blocks, skipvec);
         clear_abort(ctx);
         ctx->ensure_stats(count);
         SV_HIP(hipMemsetAsync(ctx->d_stats, 0, count * sizeof(sv_stats), ctx->stream));
         const int cur0 = st->cur;
+        hipEvent_t ev;
+        ctx->time_begin(&ev);
         for (int k = 0; k < count; k++) {
             FArgs A;
             A.P = P;
@@ -893,16 +926,19 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             A.stat = ctx->d_stats + k;
             A.S = scratch(ctx);
             A.sweep = (uint32_t)k;
-            hipEvent_t ev;
-            ctx->time_begin(&ev);
             if (NWv == 2) villain_sweep_fused<2><<<grid, 2 * 64, 0, ctx->stream>>>(A);
             else if (NWv == 6) villain_sweep_fused<6><<<grid, 6 * 64, 0, ctx->stream>>>(A);
             else villain_sweep_fused<4><<<grid, 4 * 64, 0, ctx->stream>>>(A);
-            ctx->time_end(ev);
             st->cur ^= 1;
         }
+        ctx->time_end(ev, count);
         SV_HIP(hipGetLastError());
+        auto tp2 = std::chrono::steady_clock::now();
         AbortInfo a = read_abort(ctx);
+        auto tp3 = std::chrono::steady_clock::now();
+        if (dbg)
+            fprintf(stderr, "[sv] launch %.1f us, wait %.1f us\n", std::chrono::duration<double, std::micro>(tp2 - tp1).count(),
+                    std::chrono::duration<double, std::micro>(tp3 - tp2).count());
         if (a.abort) ctx->time_discard();  // aborted launches exit early: keep the average honest
         ctx->time_collect();
         if (!a.abort) {
