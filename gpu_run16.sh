@@ -1,0 +1,3 @@
+set -u
+mkdir -p gpurun_out/r16
+timeout -k 10 300 python -m pytest tests/test_gpu_worldline.py -m gpu -q -p no:cacheprovider -k "reference_order" > gpurun_out/r16/b.log 2>&1; echo "golden+oracle rc=$?"; grep -E "^E |assert" gpurun_out/r16/b.log | head -20; tail -2 gpurun_out/r16/b.log

@@ -127,9 +127,9 @@ struct sv_worldline {
     int64_t *snap_m = nullptr;
     void *snap_v = nullptr;
     double *f = nullptr;         // sequential plaquette: f = m - delta(v)/W kept incrementally
-    int32_t *order = nullptr;    // sequential plaquette: visit order (row-major site per position)
-    int32_t *pos = nullptr;      // sequential plaquette: inverse of order
-    int32_t *done = nullptr;     // sequential plaquette: round in which a plaquette was processed (0 = not yet)
+    int32_t *order = nullptr;    // sequential plaquette: plaquettes grouped by dependency level
+    int32_t *pos = nullptr;      // sequential plaquette: visit position of each plaquette
+    int32_t *done = nullptr;     // (unused)
     int32_t *sites = nullptr;
     int32_t ncol = 0;
     int64_t count[4] = {0, 0, 0, 0};

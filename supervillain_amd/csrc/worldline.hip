@@ -5,10 +5,10 @@
 //    Bit-exact replay of the seeded reference chain.
 //  * PlaquetteUpdate, reference order (plaquette.py:35-104): the visit order is the permutation the
 //    reference draws from NumPy's global RandomState; the host hands it over.  Sequential semantics
-//    are kept exactly by dependency ROUNDS: a plaquette is processed once every earlier-visited
-//    plaquette sharing one of its links is done; plaquettes processed in one round share no link,
-//    so the result (m, v and the incrementally updated f = m - delta(v)/W) is bit-identical to the
-//    sequential loop.
+//    are kept exactly by dependency LEVELS: level(p) = 1 + the highest level among the earlier-visited
+//    plaquettes sharing a link with p.  Plaquettes of one level share no link and depend only on
+//    lower levels, so one launch per level reproduces the sequential loop bit-for-bit (m, v and the
+//    incrementally updated f = m - delta(v)/W).
 //  * PlaquetteUpdate, checkerboard: this build's GPU-native chain: colour passes with f
 //    evaluated fresh.  Oracle: oracle/sv_oracle.c sv_o_worldline_plaquette_cb.
 #include <algorithm>
@@ -186,56 +186,36 @@ __global__ __launch_bounds__(256) void plaquette_cb_pass(WParams P, int64_t *m, 
 }
 
 // ------------------------------------------------------------------------------------------------
-// Reference-order PlaquetteUpdate.
+// Reference-order PlaquetteUpdate: f = m - delta(v)/W once per sweep (plaquette.py:53), then one
+// launch per dependency level.  Blocks: [0] change_m (k=2, V), [1] change_v (k=3, V),
+// [2] metropolis (uniform V); the draw index of a plaquette is its visit position (plaquette.py:58-69).
 template <bool VF>
-__global__ void plaquette_ordered_init(WParams P, const int64_t *m, const void *v, double *f, const int32_t *order,
-                                       int32_t *pos, int32_t *done) {
+__global__ void plaquette_f_init(WParams P, const int64_t *m, const void *v, double *f) {
     const int64_t N = P.N, V = N * N;
     for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < V; s += (int64_t)gridDim.x * blockDim.x) {
-        pos[order[s]] = (int32_t)s;
-        done[s] = 0;
-        // f = m - delta(v)/W   (plaquette.py:53)
         f[s] = (double)m[s] - dvw_link<VF>(v, N, 0, s, P.Weff);
         f[V + s] = (double)m[V + s] - dvw_link<VF>(v, N, 1, s, P.Weff);
     }
 }
 
-// Blocks: [0] change_m (k=2, V), [1] change_v (k=3, V), [2] metropolis (uniform V); draw index =
-// visit position (plaquette.py:58-60, 66-69).
+// One dependency level of the reference-order sweep: every plaquette in `list` has all of its
+// earlier-visited link-sharing neighbours in lower levels, and no two share a link.
 template <bool VF>
-__global__ __launch_bounds__(256) void plaquette_ordered_round(WParams P, int64_t *m, void *v, double *f,
-                                                               const int32_t *pos, int32_t *done, int32_t round,
-                                                               const Block *blocks, const uint32_t *skips,
-                                                               const JumpTables *T, sv_stats *stat, DevScratch S,
-                                                               uint32_t *remaining) {
+__global__ __launch_bounds__(256) void plaquette_level(WParams P, int64_t *m, void *v, double *f, const int32_t *list,
+                                                       int32_t count, const int32_t *pos, const Block *blocks,
+                                                       const uint32_t *skips, const JumpTables *T, sv_stats *stat,
+                                                       DevScratch S) {
     if (*(volatile const int32_t *)S.abort) return;
     const int64_t N = P.N, V = N * N;
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     int64_t acc_count = 0;
     double psum = 0.0;
-    uint32_t left = 0;
-    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < V; x += (int64_t)gridDim.x * blockDim.x) {
-        if (done[x]) continue;
+    if (i < count) {
+        const int64_t x = list[i];
         const int64_t tt = x / N, xx = x - tt * N;
         const int64_t xm = ((tt + 1 == N) ? 0 : tt + 1) * N + xx;
         const int64_t xn = tt * N + ((xx + 1 == N) ? 0 : xx + 1);
-        const int64_t xmb = ((tt == 0) ? N - 1 : tt - 1) * N + xx;
-        const int64_t xnb = tt * N + ((xx == 0) ? N - 1 : xx - 1);
-        const int32_t me = pos[x];
-        const int64_t nbs[4] = {xm, xn, xmb, xnb};
-        bool ready = true;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int64_t y = nbs[q];
-            if (pos[y] < me) {
-                const int32_t dy = __hip_atomic_load(&done[y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (dy == 0 || dy >= round) ready = false;
-            }
-        }
-        if (!ready) {
-            left++;
-            continue;
-        }
-        const uint32_t idx = (uint32_t)me;
+        const uint32_t idx = (uint32_t)pos[x];
         const uint32_t jm = wbounded(T, blocks[0], skips, idx, 2u, 0u, S, 0, 0);
         const uint32_t jv = wbounded(T, blocks[1], skips, idx, 3u, 1u, S, 0, 1);
         const double met = 0.0 + 1.0 * to_double(xsl_rr(jump(T, wbase(blocks[2]), idx)));
@@ -246,7 +226,7 @@ __global__ __launch_bounds__(256) void plaquette_ordered_round(WParams P, int64_
         double p = exp(-dS);
         p = p < 0.0 ? 0.0 : p;
         p = p > 1.0 ? 1.0 : p;
-        psum += p;
+        psum = p;
         if (met < p) {
             m[x] += cm;
             m[V + xm] += cm;
@@ -258,14 +238,10 @@ __global__ __launch_bounds__(256) void plaquette_ordered_round(WParams P, int64_
             f[V + xm] += df;
             f[xn] -= df;
             f[V + x] -= df;
-            acc_count++;
+            acc_count = 1;
         }
-        __hip_atomic_store(&done[x], round, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     wflush(stat, acc_count, psum);
-    unsigned long long l = left;
-    for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o);
-    if ((threadIdx.x & 63) == 0 && l) atomicAdd(remaining, (uint32_t)l);
 }
 
 }  // namespace sv
@@ -598,21 +574,42 @@ int sv_worldline_plaquette_ordered_run(sv_worldline *st, double kappa, double W_
             SV_HIP(hipMalloc(&st->pos, V * sizeof(int32_t)));
             SV_HIP(hipMalloc(&st->done, (V + 1) * sizeof(int32_t)));
         }
-        std::vector<int32_t> ord(V);
-        std::vector<char> seen(V, 0);
+        // Dependency levels of the visit order (host, O(V)): level(p) = 1 + max level of the
+        // earlier-visited plaquettes sharing a link with p (its four nearest neighbours).
+        std::vector<int32_t> pos(V, -1), level(V, 0);
         for (int64_t i = 0; i < V; i++) {
-            if (order[i] < 0 || order[i] >= V || seen[order[i]]) throw std::invalid_argument("order is not a permutation");
-            seen[order[i]] = 1;
-            ord[i] = (int32_t)order[i];
+            const int64_t x = order[i];
+            if (x < 0 || x >= V || pos[x] >= 0) throw std::invalid_argument("order is not a permutation");
+            pos[x] = (int32_t)i;
         }
-        SV_HIP(hipMemcpyAsync(st->order, ord.data(), V * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+        int32_t nlev = 0;
+        for (int64_t i = 0; i < V; i++) {
+            const int64_t x = order[i], t = x / N, xx = x - t * N;
+            const int64_t nb[4] = {((t + 1) % N) * N + xx, ((t + N - 1) % N) * N + xx, t * N + (xx + 1) % N,
+                                   t * N + (xx + N - 1) % N};
+            int32_t l = 0;
+            for (int k = 0; k < 4; k++)
+                if (pos[nb[k]] < i && level[nb[k]] > l) l = level[nb[k]];
+            level[x] = l + 1;
+            if (l + 1 > nlev) nlev = l + 1;
+        }
+        std::vector<int32_t> start(nlev + 2, 0), list(V);
+        for (int64_t x = 0; x < V; x++) start[level[x] + 1]++;
+        for (int l = 1; l <= nlev + 1; l++) start[l] += start[l - 1];
+        {
+            std::vector<int32_t> fill(start.begin(), start.end());
+            for (int64_t i = 0; i < V; i++) {  // visit order inside a level (any order is equivalent)
+                const int64_t x = order[i];
+                list[fill[level[x]]++] = (int32_t)x;
+            }
+        }
+        SV_HIP(hipMemcpyAsync(st->order, list.data(), V * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+        SV_HIP(hipMemcpyAsync(st->pos, pos.data(), V * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
         std::vector<BlockSpec> specs = {{BOUNDED, (uint32_t)V}, {BOUNDED, (uint32_t)V}, {UNIFORM, (uint32_t)V}};
         SkipMap skips;
         std::vector<Block> blocks;
         std::vector<uint32_t> skipvec;
         std::vector<Report> reps;
-        uint32_t *d_rem = nullptr;  // plaquettes still waiting after a chunk of rounds
-        SV_HIP(hipMallocAsync((void **)&d_rem, sizeof(uint32_t), ctx->stream));
         snapshot(st, false);
         ctx->ensure_stats(1);
         const int grid = (int)std::min<int64_t>((V + 255) / 256, 8192);
@@ -624,34 +621,23 @@ int sv_worldline_plaquette_ordered_run(sv_worldline *st, double kappa, double W_
             wclear(ctx);
             SV_HIP(hipMemsetAsync(ctx->d_stats, 0, sizeof(sv_stats), ctx->stream));
             if (st->v_is_float)
-                plaquette_ordered_init<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f, st->order, st->pos,
-                                                                             st->done);
+                plaquette_f_init<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f);
             else
-                plaquette_ordered_init<false><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f, st->order,
-                                                                              st->pos, st->done);
-            int32_t round = 1;
-            for (;;) {
-                const int CHUNK = 8;
-                for (int k = 0; k < CHUNK; k++, round++) {
-                    SV_HIP(hipMemsetAsync(d_rem, 0, sizeof(uint32_t), ctx->stream));
-                    if (st->v_is_float)
-                        plaquette_ordered_round<true><<<grid, 256, 0, ctx->stream>>>(
-                            P, st->m, st->v, st->f, st->pos, st->done, round, ctx->d_blocks, ctx->d_skips, T,
-                            ctx->d_stats, wscratch(ctx), d_rem);
-                    else
-                        plaquette_ordered_round<false><<<grid, 256, 0, ctx->stream>>>(
-                            P, st->m, st->v, st->f, st->pos, st->done, round, ctx->d_blocks, ctx->d_skips, T,
-                            ctx->d_stats, wscratch(ctx), d_rem);
-                }
-                SV_HIP(hipGetLastError());
-                uint32_t rem = 0;
-                SV_HIP(hipMemcpyAsync(&rem, d_rem, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-                SV_HIP(hipStreamSynchronize(ctx->stream));
-                int32_t ab = 0;
-                SV_HIP(hipMemcpy(&ab, ctx->d_abort, sizeof(int32_t), hipMemcpyDeviceToHost));
-                if (rem == 0 || ab) break;
-                if (round > 1 << 20) throw std::runtime_error("plaquette rounds did not terminate");
+                plaquette_f_init<false><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f);
+            for (int l = 1; l <= nlev; l++) {
+                const int32_t cnt = start[l + 1] - start[l];
+                if (!cnt) continue;
+                const int g = (cnt + 255) / 256;
+                if (st->v_is_float)
+                    plaquette_level<true><<<g, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f, st->order + start[l], cnt,
+                                                                      st->pos, ctx->d_blocks, ctx->d_skips, T,
+                                                                      ctx->d_stats, wscratch(ctx));
+                else
+                    plaquette_level<false><<<g, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f, st->order + start[l],
+                                                                       cnt, st->pos, ctx->d_blocks, ctx->d_skips, T,
+                                                                       ctx->d_stats, wscratch(ctx));
             }
+            SV_HIP(hipGetLastError());
             if (!wcheck(ctx, reps)) {
                 cur = c;
                 break;
@@ -660,7 +646,6 @@ int sv_worldline_plaquette_ordered_run(sv_worldline *st, double kappa, double W_
             snapshot(st, true);
         }
         SV_HIP(hipMemcpyAsync(stats, ctx->d_stats, sizeof(sv_stats), hipMemcpyDeviceToHost, ctx->stream));
-        SV_HIP(hipFreeAsync(d_rem, ctx->stream));
         SV_HIP(hipStreamSynchronize(ctx->stream));
         stats->proposed = V;
         int64_t rj = 0;

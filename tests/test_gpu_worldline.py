@@ -89,23 +89,30 @@ def test_plaquette_reference_order_oracle(N, W, oracle_lib):
     G = sv.generator.worldline.PlaquetteUpdate(S)
     G.rng = np.random.default_rng(5)
     cfg = S.configurations(1)[0]
-    saved = np.random.get_state()
-    np.random.seed(77)
-    orders = []
-    for _ in range(3):
-        st = np.random.get_state()
-        o = np.random.permutation(L.coordinates)
-        np.random.set_state(st)
-        orders.append((o[:, 0] % N) * N + (o[:, 1] % N))
-        cfg = cfg | G.step(cfg)
-    np.random.set_state(saved)
     m = np.zeros((2, N, N), dtype=np.int64)
     v = np.zeros((N, N), dtype=np.float64 if W == float('inf') else np.int64)
     g = np.random.default_rng(5)
-    for o in orders:
-        oracle_lib.worldline_plaquette_seq(N, 0.4, S._W, m, v, o, g)
-    assert (np.asarray(cfg['m']) == m).all() and (np.asarray(cfg['v'])[0] == v).all()
-    assert G.rng.bit_generator.state == g.bit_generator.state
+    saved = np.random.get_state()
+    np.random.seed(77)
+    try:
+        for sweep in range(3):
+            st = np.random.get_state()
+            o = np.random.permutation(L.coordinates)
+            np.random.set_state(st)
+            m0, v0, rng0 = m.copy(), v.copy(), state_of(g)
+            cfg = cfg | G.step(cfg)
+            s = oracle_lib.worldline_plaquette_seq(N, 0.4, S._W, m, v, (o[:, 0] % N) * N + (o[:, 1] % N), g)
+            dm = int((np.asarray(cfg['m']) != m).sum())
+            dv = int((np.asarray(cfg['v'])[0] != v).sum())
+            if dm or dv:
+                import os
+                os.makedirs('gpurun_out', exist_ok=True)
+                np.savez(f'gpurun_out/plaq_mismatch_{N}.npz', m0=m0, v0=v0, rng0=rng0, order=o,
+                         m_gpu=np.asarray(cfg['m']), v_gpu=np.asarray(cfg['v'])[0], m_cpu=m, v_cpu=v)
+            assert dm == 0 and dv == 0, (sweep, dm, dv, G.accepted, s.accepted)
+            assert G.rng.bit_generator.state == g.bit_generator.state
+    finally:
+        np.random.set_state(saved)
 
 
 def test_plaquette_reference_order_forced_rejection(oracle_lib):
