@@ -2,10 +2,15 @@
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--L 4096]
 
-A "step" is one NeighborhoodUpdate sweep (neighborhood.py:59-137) of the whole L x L lattice, in the
+A "step" is one NeighborhoodUpdate sweep (neighborhood.py:59-137) of the whole lattice, in the
 reference's own chain semantics (NumPy PCG64 stream replayed on the device, bit-exact parity mode),
-with the fields resident in HBM.  One process per GPU (torch.distributed.run for N>1); each rank runs
-its own L x L chain (seed = rank): weak scaling, no data-path collective (Multi-GPU).
+with the fields resident in HBM.
+
+  N = 1: one L x L lattice on one GPU (the single-lattice fused sweep kernel).
+  N > 1: one process per GPU (torch.distributed.run); ONE lattice of (ty L) x (tx L) sites is
+         domain-decomposed into ty x tx tiles of L x L (1x2, 2x2, 2x4 for N = 2, 4, 8), one tile per
+         GPU, with an RCCL halo exchange every sweep (weak scaling: L x L sites per GPU).  The chain
+         is bit-identical to running that lattice on one GPU.  --strong keeps the lattice at L x L.
 Rank 0 prints one JSON line.
 """
 import argparse
@@ -36,6 +41,9 @@ def parse():
     ap.add_argument('--path', type=int, default=2, help='0 auto, 1 per-colour kernels, 2 fused sweep kernel')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-sweeps', type=int, default=5)
+    ap.add_argument('--strong', action='store_true', help='N>1: decompose one L x L lattice (strong scaling)')
+    ap.add_argument('--tiles', default=None, help='tile grid TYxTX (default from N); with N=1 emulates the '
+                                                   'decomposition on one GPU')
     return ap.parse_args()
 
 
@@ -67,6 +75,92 @@ def cpu_baseline(L, kappa, W, sweeps):
                       'oracle/sv_oracle.c single-threaded'}
 
 
+def max_over_ranks(dist, x):
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def kernel_time(Lib, ctx):
+    ms = ctypes.c_double()
+    launches = ctypes.c_int64()
+    Lib.sv_ctx_kernel_time(ctx.handle, ctypes.byref(ms), ctypes.byref(launches))
+    Lib.sv_ctx_set_timing(ctx.handle, 0)
+    return ms.value / 1e3 / max(launches.value, 1)
+
+
+def report(args, world, sites_per_step, sites_per_launch, elapsed, acc, avg_launch_s, config, traffic_L):
+    achieved = ALG_BYTES_PER_SITE * sites_per_launch / avg_launch_s / 1e9
+    out = {
+        'metric': 'lattice-site updates/sec (sweeps/s × L²), L=4096 Villain, 1→8 MI355X',
+        'value': args.steps * sites_per_step / elapsed,
+        'unit': 'lattice-site updates/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': elapsed / args.steps * 1e3,
+        'higher_is_better': True,
+        'scaling': 'strong' if args.strong else 'weak',
+        'vs_baseline': None,
+        'dtype': 'f64+int64',
+        'data': 'synthetic (cold start, NumPy PCG64 seed 0)',
+        'config': dict(config, kappa=args.kappa, W=args.W, acceptance_rate=acc),
+        'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic_from_profiles(traffic_L),
+                     'kernel': 'villain_sweep_fused', 'avg_launch_us': avg_launch_s * 1e6,
+                     'alg_bytes_per_site': ALG_BYTES_PER_SITE,
+                     'survey_effective_GBps': SURVEY_BYTES_PER_SITE * sites_per_launch / avg_launch_s / 1e9},
+        'cpu_baseline': None,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out['cpu_baseline'] = cpu_baseline(args.L, args.kappa, args.W, args.cpu_sweeps)
+    print(json.dumps(out), flush=True)
+
+
+def run_domain(args, world, rank, local, dist):
+    """N > 1 (or --tiles on one GPU): one lattice, domain-decomposed, RCCL halos."""
+    from supervillain_amd import _native
+    from supervillain_amd.domain import VillainDomain, tile_grid
+    L = args.L
+    if args.tiles:
+        ty, tx = (int(v) for v in args.tiles.lower().split('x'))
+    else:
+        ty, tx = tile_grid(world)
+    Nt, Nx = (L, L) if args.strong else (ty * L, tx * L)
+    kw = dict(kappa=args.kappa, W=args.W)  # device: $SV_DEVICE, else $LOCAL_RANK
+    if world > 1:
+        dom = VillainDomain.distributed(Nt, Nx, (ty, tx), **kw)
+    else:
+        dom = VillainDomain(Nt, Nx, (ty, tx), **kw)
+    dom.cold()
+    gen = np.random.default_rng(0)  # one chain: every rank holds the same stream
+    Lib = _native.lib()
+    if args.warmup:
+        dom.run(args.warmup, gen)
+    Lib.sv_ctx_set_timing(dom.ctx.handle, 1)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    st = dom.run(args.steps, gen)  # synchronous on return
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = max_over_ranks(dist, t1 - t0)
+    avg_launch_s = kernel_time(Lib, dom.ctx)
+    acc = sum(s.accepted for s in st) / (args.steps * Nt * Nx)
+    if rank == 0:
+        config = {'workload': f'{Nt}x{Nx} Villain NeighborhoodUpdate sweep, domain-decomposed into {ty}x{tx} tiles of '
+                              f'{Nt // ty}x{Nx // tx} (one per GPU), RCCL halo exchange every sweep, bit-exact '
+                              'reference chain (PCG64 replay)',
+                  'L': L, 'lattice': [Nt, Nx], 'tiles': [ty, tx], 'path': 'domain',
+                  'parallelism': f'{ty}x{tx} domain decomposition over {world} GPU(s)'}
+        report(args, world, Nt * Nx, Nt * Nx // (ty * tx), elapsed, acc, avg_launch_s, config, Nt // ty)
+    dom.close()
+
+
 def main():
     args = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -78,6 +172,11 @@ def main():
         import torch.distributed as dist
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         dist.init_process_group('gloo', rank=rank, world_size=world)
+    if world > 1 or args.tiles:
+        run_domain(args, world, rank, local, dist)
+        if dist:
+            dist.destroy_process_group()
+        return
 
     from supervillain_amd import _native
     from supervillain_amd._abi import SvRng, rng_from_numpy
@@ -90,7 +189,7 @@ def main():
     phi = np.zeros((L, L))
     n = np.zeros((2, L, L), dtype=np.int64)
     ctx.check(Lib.sv_villain_upload(h, _native.ptr(phi), _native.ptr(n)), 'upload')
-    r = rng_from_numpy(np.random.default_rng(rank))
+    r = rng_from_numpy(np.random.default_rng(0))
 
     def run(k):
         st = _native.stats_array(k)
@@ -101,60 +200,16 @@ def main():
     if args.warmup:
         run(args.warmup)
     Lib.sv_ctx_set_timing(ctx.handle, 1)
-    if dist:
-        dist.barrier()
     t0 = time.perf_counter()
     st = run(args.steps)  # synchronous on return (stream synchronized)
     t1 = time.perf_counter()
-    if dist:
-        dist.barrier()
-    elapsed = t1 - t0
-    ms = ctypes.c_double()
-    launches = ctypes.c_int64()
-    Lib.sv_ctx_kernel_time(ctx.handle, ctypes.byref(ms), ctypes.byref(launches))
-    Lib.sv_ctx_set_timing(ctx.handle, 0)
+    avg_launch_s = kernel_time(Lib, ctx)
     acc = sum(st[i].accepted for i in range(args.steps)) / (args.steps * L * L)
-    if dist:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    if rank == 0:
-        value = world * args.steps * L * L / elapsed
-        avg_launch_s = ms.value / 1e3 / max(launches.value, 1)
-        achieved = ALG_BYTES_PER_SITE * L * L / avg_launch_s / 1e9
-        traffic = traffic_from_profiles(L)
-        out = {
-            'metric': 'lattice-site updates/sec (sweeps/s × L²), L=4096 Villain, 1→8 MI355X',
-            'value': value,
-            'unit': 'lattice-site updates/s',
-            'n_gpus': world,
-            'steps': args.steps,
-            'warmup': args.warmup,
-            'ms_per_step': elapsed / args.steps * 1e3,
-            'higher_is_better': True,
-            'scaling': 'weak',
-            'vs_baseline': None,
-            'dtype': 'f64+int64',
-            'data': 'synthetic (cold start, NumPy PCG64 seed = rank)',
-            'config': {'workload': f'L={L} Villain NeighborhoodUpdate sweep, kappa={args.kappa}, W={args.W}, '
-                                   'bit-exact reference chain (PCG64 replay), fused two-colour sweep kernel',
-                       'L': L, 'kappa': args.kappa, 'W': args.W, 'path': args.path,
-                       'parallelism': f'{world} independent chains (one per GPU)',
-                       'acceptance_rate': acc},
-            'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                         'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
-                         'kernel': 'villain_sweep_fused', 'avg_launch_us': avg_launch_s * 1e6,
-                         'alg_bytes_per_site': ALG_BYTES_PER_SITE,
-                         'survey_effective_GBps': SURVEY_BYTES_PER_SITE * L * L / avg_launch_s / 1e9},
-            'cpu_baseline': None,
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            out['cpu_baseline'] = cpu_baseline(L, args.kappa, args.W, args.cpu_sweeps)
-        print(json.dumps(out), flush=True)
+    config = {'workload': f'L={L} Villain NeighborhoodUpdate sweep, kappa={args.kappa}, W={args.W}, '
+                          'bit-exact reference chain (PCG64 replay), fused two-colour sweep kernel',
+              'L': L, 'lattice': [L, L], 'path': args.path, 'parallelism': 'single GPU'}
+    report(args, 1, L * L, L * L, t1 - t0, acc, avg_launch_s, config, L)
     Lib.sv_villain_destroy(h)
-    if dist:
-        dist.destroy_process_group()
 
 
 if __name__ == '__main__':

@@ -110,6 +110,35 @@ int sv_worldline_plaquette_checkerboard_run(sv_worldline *st, double kappa, doub
 int sv_worldline_plaquette(sv_ctx *ctx, int32_t N, double kappa, double W_eff, int64_t *m, void *v,
                            int32_t v_is_float, const int64_t *order, sv_rng *rng, sv_stats *stats);
 
+
+/* ---- Villain on a domain-decomposed lattice (multi-GPU; SURVEY.md 8e, BASELINE config 4) -------- */
+/* The same chain as sv_villain_* (NeighborhoodUpdate, neighborhood.py:59-137) on an Nt x Nx lattice
+ * (Nt = Nx = N for the reference's square Lattice2D) cut into tiles_t x tiles_x tiles, one halo
+ * exchange per sweep.  nranks == 1: every tile lives on this context's GPU (bit-exact emulation of any
+ * tile grid).  nranks > 1: one tile per rank (rank = tile index, row-major), halos over RCCL; all
+ * ranks must make the same calls with the same arguments (collective), and rank 0's
+ * sv_domain_unique_id bytes must reach every rank (e.g. a torch.distributed broadcast).
+ * Tiles must be even and at least 4 x 4; stats are global (summed over tiles, identical on every rank).
+ * nranks == 1 with a unique id and a 1 x 1 grid: the tile's halos go through RCCL to itself (a one-GPU
+ * check of the RCCL path). */
+typedef struct sv_domain sv_domain;
+#define SV_UNIQUE_ID_BYTES 128
+int sv_domain_unique_id(uint8_t *id /* SV_UNIQUE_ID_BYTES */);
+int sv_domain_create(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t nranks,
+                     int32_t rank, const uint8_t *unique_id, sv_domain **out);
+int sv_domain_destroy(sv_domain *d);
+/* Global (Nt, Nx) row-major host arrays; each rank copies its own tiles.  phi == NULL: cold start. */
+int sv_domain_upload(sv_domain *d, const double *phi, const int64_t *n);
+int sv_domain_download(sv_domain *d, double *phi, int64_t *n);
+int sv_domain_run(sv_domain *d, double kappa, int64_t W, double interval_phi, int64_t interval_n, int32_t sweeps,
+                  sv_rng *rng, sv_stats *stats);
+/* Host-only geometry query (no GPU needed): for each of the 8 halo messages s (in send order) of tile
+ * `rank`: out[10 s ..] = {dy, dx, send_to, src_row0, src_col0, rows, cols, recv_from, dst_row0, dst_col0}
+ * -- the message of direction (dy, dx) is the interior block [src_row0, +rows) x [src_col0, +cols),
+ * and the message of direction s received from `recv_from` fills the ghost block at (dst_row0, dst_col0)
+ * (tile-local coordinates; ghosts are negative or >= the tile extent). */
+int sv_domain_exchange_plan(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t rank, int64_t *out);
+
 #ifdef __cplusplus
 }
 #endif

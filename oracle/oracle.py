@@ -29,6 +29,7 @@ def lib():
         L.sv_o_integers.argtypes = [P(SvRng), ctypes.c_uint32, i64, vp]
         L.sv_o_colors.argtypes = [i32, vp]
         L.sv_o_villain_neighborhood.argtypes = [i32, f64, i64, f64, i64, vp, vp, i32, P(SvRng), vp]
+        L.sv_o_villain_neighborhood_rect.argtypes = [i32, i32, f64, i64, f64, i64, vp, vp, i32, P(SvRng), vp]
         L.sv_o_villain_action.argtypes = [i32, f64, vp, vp]
         L.sv_o_villain_action.restype = f64
         L.sv_o_worldline_coexact.argtypes = [i32, f64, f64, i64, vp, vp, i32, i32, P(SvRng), vp]
@@ -84,6 +85,20 @@ def villain_neighborhood(N, kappa, W, phi, n, sweeps, gen, interval_phi=np.pi, i
     st = _stats_array(sweeps)
     rc = lib().sv_o_villain_neighborhood(N, kappa, int(W), interval_phi, int(interval_n), _ptr(phi), _ptr(n),
                                          sweeps, ctypes.byref(r), st)
+    if rc != 0:
+        raise ValueError('oracle rejected the arguments')
+    rng_to_numpy(r, gen)
+    return [st[i] for i in range(sweeps)]
+
+
+def villain_neighborhood_rect(Nt, Nx, kappa, W, phi, n, sweeps, gen, interval_phi=np.pi, interval_n=1):
+    """The same chain on an even Nt x Nx torus (phi (Nt,Nx), n (2,Nt,Nx)); Nt == Nx is the reference's."""
+    assert phi.dtype == np.float64 and n.dtype == np.int64
+    assert phi.flags.c_contiguous and n.flags.c_contiguous and phi.shape == (Nt, Nx) and n.shape == (2, Nt, Nx)
+    r = rng_from_numpy(gen)
+    st = _stats_array(sweeps)
+    rc = lib().sv_o_villain_neighborhood_rect(Nt, Nx, kappa, int(W), interval_phi, int(interval_n), _ptr(phi), _ptr(n),
+                                              sweeps, ctypes.byref(r), st)
     if rc != 0:
         raise ValueError('oracle rejected the arguments')
     rng_to_numpy(r, gen)

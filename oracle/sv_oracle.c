@@ -193,25 +193,44 @@ static void colors_free(colors_t *C) {
     for (int c = 0; c < 4; c++) free(C->sites[c]);
 }
 
-/* neighbours: e0 moves t (axis 0, rows), e1 moves x (axis 1, columns) */
-static inline int64_t fwd(int64_t s, int mu, int64_t N) {
-    int64_t t = s / N, x = s % N;
-    if (mu == 0) t = (t + 1) % N; else x = (x + 1) % N;
-    return t * N + x;
+/* Even Nt x Nx rectangle (the domain-decomposition extension; the reference's Lattice2D is square):
+ * colours are the parity of t + x, row-major, as compact.py:191-239 gives for even square N. */
+static colors_t colors_make_rect(int32_t Nt, int32_t Nx) {
+    colors_t C;
+    int64_t V = (int64_t)Nt * Nx;
+    C.ncol = 2;
+    for (int c = 0; c < 4; c++) {
+        C.count[c] = 0;
+        C.sites[c] = (int64_t *)malloc(sizeof(int64_t) * (V + 1));
+    }
+    for (int64_t s = 0; s < V; s++) {
+        int c = (int)(((s / Nx) + (s % Nx)) & 1);
+        C.sites[c][C.count[c]++] = s;
+    }
+    return C;
 }
-static inline int64_t bwd(int64_t s, int mu, int64_t N) {
-    int64_t t = s / N, x = s % N;
-    if (mu == 0) t = (t + N - 1) % N; else x = (x + N - 1) % N;
-    return t * N + x;
+
+/* neighbours on an Nt x Nx torus: e0 moves t (axis 0, rows), e1 moves x (axis 1, columns) */
+static inline int64_t fwd2(int64_t s, int mu, int64_t Nt, int64_t Nx) {
+    int64_t t = s / Nx, x = s % Nx;
+    if (mu == 0) t = (t + 1) % Nt; else x = (x + 1) % Nx;
+    return t * Nx + x;
 }
+static inline int64_t bwd2(int64_t s, int mu, int64_t Nt, int64_t Nx) {
+    int64_t t = s / Nx, x = s % Nx;
+    if (mu == 0) t = (t + Nt - 1) % Nt; else x = (x + Nx - 1) % Nx;
+    return t * Nx + x;
+}
+static inline int64_t fwd(int64_t s, int mu, int64_t N) { return fwd2(s, mu, N, N); }
+static inline int64_t bwd(int64_t s, int mu, int64_t N) { return bwd2(s, mu, N, N); }
 
 #define TWO_PI 6.283185307179586 /* Python's 2*np.pi, rounded once */
 
 /* ---------------------------------------------------------------- Villain NeighborhoodUpdate */
 /* One sweep of neighborhood.py:59-137 on D=2.  phi: (N,N) f64, n: (2,N,N) i64, in place. */
-static void villain_sweep(int64_t N, double kappa, int64_t W, double interval_phi, int64_t interval_n,
+static void villain_sweep(int64_t Nt, int64_t Nx, double kappa, int64_t W, double interval_phi, int64_t interval_n,
                           double *phi, int64_t *n, pcg *g, const colors_t *C, sv_stats *st, double *work) {
-    int64_t V = N * N;
+    int64_t V = Nt * Nx;
     double *metro = work;          /* V */
     double *r = metro + V;         /* 2V */
     double *cphi = r + 2 * V;      /* V */
@@ -226,7 +245,7 @@ static void villain_sweep(int64_t N, double kappa, int64_t W, double interval_ph
     for (int64_t s = 0; s < V; s++) metro[s] = pcg_uniform(g, 0.0, 1.0); /* :87 */
     for (int mu = 0; mu < 2; mu++)                                         /* :91 */
         for (int64_t s = 0; s < V; s++)
-            r[mu * V + s] = (0.0 + (phi[fwd(s, mu, N)] - phi[s])) - TWO_PI * (double)n[mu * V + s];
+            r[mu * V + s] = (0.0 + (phi[fwd2(s, mu, Nt, Nx)] - phi[s])) - TWO_PI * (double)n[mu * V + s];
 
     for (int c = 0; c < C->ncol; c++) { /* :93 */
         const int64_t nc = C->count[c];
@@ -238,12 +257,12 @@ static void villain_sweep(int64_t N, double kappa, int64_t W, double interval_ph
             for (int64_t i = 0; i < nc; i++)
                 cn[mu * V + sites[i]] = W * ((int64_t)pcg_bounded(g, k, &st->rejections) - interval_n);
             for (int64_t i = 0; i < nc; i++)
-                cn[mu * V + bwd(sites[i], mu, N)] = W * ((int64_t)pcg_bounded(g, k, &st->rejections) - interval_n);
+                cn[mu * V + bwd2(sites[i], mu, Nt, Nx)] = W * ((int64_t)pcg_bounded(g, k, &st->rejections) - interval_n);
         }
         /* :110-112  change_r = d(change_phi) - 2 pi change_n ; dS_link ; face_sum */
         for (int mu = 0; mu < 2; mu++)
             for (int64_t s = 0; s < V; s++) {
-                double cr = (0.0 + (cphi[fwd(s, mu, N)] - cphi[s])) - TWO_PI * (double)cn[mu * V + s];
+                double cr = (0.0 + (cphi[fwd2(s, mu, Nt, Nx)] - cphi[s])) - TWO_PI * (double)cn[mu * V + s];
                 double a = half_kappa * cr;
                 double b = (2.0 * r[mu * V + s]) + cr;
                 dSl[mu * V + s] = a * b;
@@ -252,9 +271,9 @@ static void villain_sweep(int64_t N, double kappa, int64_t W, double interval_ph
             int64_t s = sites[i];
             double dS = 0.0;
             dS += dSl[0 * V + s];
-            dS += dSl[0 * V + bwd(s, 0, N)];
+            dS += dSl[0 * V + bwd2(s, 0, Nt, Nx)];
             dS += dSl[1 * V + s];
-            dS += dSl[1 * V + bwd(s, 1, N)];
+            dS += dSl[1 * V + bwd2(s, 1, Nt, Nx)];
             double p = exp(-dS);
             p = p < 0.0 ? 0.0 : p;
             p = p > 1.0 ? 1.0 : p;
@@ -269,14 +288,14 @@ static void villain_sweep(int64_t N, double kappa, int64_t W, double interval_ph
             cphi[s] = cphi[s] * a;
             for (int mu = 0; mu < 2; mu++) {
                 cn[mu * V + s] *= acc[s];
-                cn[mu * V + bwd(s, mu, N)] *= acc[s];
+                cn[mu * V + bwd2(s, mu, Nt, Nx)] *= acc[s];
             }
         }
         for (int64_t s = 0; s < V; s++) phi[s] = phi[s] + cphi[s]; /* :127 */
         for (int64_t l = 0; l < 2 * V; l++) n[l] = n[l] + cn[l];    /* :128 */
         for (int mu = 0; mu < 2; mu++)                              /* :129 */
             for (int64_t s = 0; s < V; s++) {
-                double dcp = 0.0 + (cphi[fwd(s, mu, N)] - cphi[s]);
+                double dcp = 0.0 + (cphi[fwd2(s, mu, Nt, Nx)] - cphi[s]);
                 r[mu * V + s] = (r[mu * V + s] + dcp) - TWO_PI * (double)cn[mu * V + s];
             }
     }
@@ -291,7 +310,25 @@ int sv_o_villain_neighborhood(int32_t N, double kappa, int64_t W, double interva
     double *work = (double *)malloc(sizeof(double) * 6 * V + sizeof(int64_t) * 3 * V);
     pcg g = pcg_load(rng);
     for (int32_t s = 0; s < sweeps; s++)
-        villain_sweep(N, kappa, W, interval_phi, interval_n, phi, n, &g, &C, &stats[s], work);
+        villain_sweep(N, N, kappa, W, interval_phi, interval_n, phi, n, &g, &C, &stats[s], work);
+    pcg_store(&g, rng);
+    free(work);
+    colors_free(&C);
+    return 0;
+}
+
+/* The same chain on an even Nt x Nx torus (stream layout unchanged: V = Nt Nx metropolis draws, then
+ * per colour V/2 dphi and 4 x V/2 choices).  Checks the decomposed GPU engine on rectangles. */
+int sv_o_villain_neighborhood_rect(int32_t Nt, int32_t Nx, double kappa, int64_t W, double interval_phi,
+                                   int64_t interval_n, double *phi, int64_t *n, int32_t sweeps, sv_rng *rng,
+                                   sv_stats *stats) {
+    if (Nt < 2 || Nx < 2 || (Nt % 2) || (Nx % 2) || sweeps < 0) return -1;
+    int64_t V = (int64_t)Nt * Nx;
+    colors_t C = colors_make_rect(Nt, Nx);
+    double *work = (double *)malloc(sizeof(double) * 6 * V + sizeof(int64_t) * 3 * V);
+    pcg g = pcg_load(rng);
+    for (int32_t s = 0; s < sweeps; s++)
+        villain_sweep(Nt, Nx, kappa, W, interval_phi, interval_n, phi, n, &g, &C, &stats[s], work);
     pcg_store(&g, rng);
     free(work);
     colors_free(&C);

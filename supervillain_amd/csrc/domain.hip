@@ -1,0 +1,572 @@
+// domain.hip -- NeighborhoodUpdate on a domain-decomposed lattice (BASELINE config 4).
+//
+// The Nt x Nx lattice is cut into tiles_t x tiles_x tiles of Ht x Wt sites.  Each tile lives in HBM
+// with a ghost frame (2 rows above, 3 below, 2 columns left, 3 right: exactly what the fused sweep
+// kernel reads around a tile, villain.hip) and one sweep is
+//
+//     pack (8 halo messages) -> exchange -> unpack into the ghost frame -> fused sweep kernel.
+//
+// Because both colours are decided inside one launch there is ONE exchange per sweep.  Every draw is
+// addressed by its global NumPy stream position and the colouring by global coordinates, so the
+// decomposed chain is bit-identical to the single-lattice chain (and to the reference's).
+//
+// Transport: tiles in the same process (one GPU emulating any tile grid -- the parity tests -- or a
+// tile grid dimension of 1) read each other's send buffers directly; tiles on other ranks exchange
+// through RCCL point-to-point (ncclSend/ncclRecv in one group, over xGMI), on the context's stream.
+//
+// Rejections (NumPy's Lemire sampler rejecting a uint32, which shifts the rest of its block) are
+// found by whichever tile draws the position.  Each halo message carries its sender's abort flag,
+// so an abort spreads one tile-hop per sweep and every tile stops within D sweeps (D = tile-torus
+// radius); the tile states are kept in a ring of R = D + 1 buffers so the input of the failing sweep
+// survives everywhere.  After each batch the ranks all-gather their reports (one collective per
+// batch) and take the same replay decision as the single-lattice driver.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "villain.h"
+
+namespace sv {
+
+static constexpr int GHOST_TOP = 2, GHOST_BOTTOM = 3, GHOST_LEFT = 2, GHOST_RIGHT = 3;
+static constexpr int LEFT_PAD = 16;  // interior starts 128 B-aligned
+static constexpr int DOMAIN_BATCH = 64;
+static constexpr int NDIR = 8;
+
+// direction s = 0..7 <-> (dy, dx) in {-1,0,1}^2 \ {(0,0)}, row-major
+__host__ __device__ inline void dir_of(int s, int &dy, int &dx) {
+    const int k = s < 4 ? s : s + 1;
+    dy = k / 3 - 1;
+    dx = k % 3 - 1;
+}
+inline int opp(int s) { return NDIR - 1 - s; }  // (-dy, -dx)
+
+// Message of direction s (toward the tile at (dy, dx)): the sender's interior rectangle the
+// receiver needs for its ghost block on the opposite side.
+struct Rect {
+    int32_t r0, c0, rows, cols;
+};
+inline Rect send_rect(int s, int32_t Ht, int32_t Wt) {
+    int dy, dx;
+    dir_of(s, dy, dx);
+    Rect R;
+    R.r0 = dy > 0 ? Ht - GHOST_TOP : 0;
+    R.rows = dy == 0 ? Ht : (dy > 0 ? GHOST_TOP : GHOST_BOTTOM);
+    R.c0 = dx > 0 ? Wt - GHOST_LEFT : 0;
+    R.cols = dx == 0 ? Wt : (dx > 0 ? GHOST_LEFT : GHOST_RIGHT);
+    return R;
+}
+// Ghost block filled by the message of direction s (it arrives from the tile at (-dy, -dx)).
+inline Rect recv_rect(int s, int32_t Ht, int32_t Wt) {
+    int dy, dx;
+    dir_of(s, dy, dx);
+    Rect R = send_rect(s, Ht, Wt);
+    R.r0 = dy > 0 ? -GHOST_TOP : (dy == 0 ? 0 : Ht);
+    R.c0 = dx > 0 ? -GHOST_LEFT : (dx == 0 ? 0 : Wt);
+    return R;
+}
+
+struct HaloTable {
+    Rect rect[NDIR];
+    int64_t off[NDIR];  // u64 words; message = [flag, pad, phi[cnt], n0[cnt], n1[cnt]]
+};
+struct HaloSrc {
+    const uint64_t *msg[NDIR];  // message of direction s for this tile's ghost block s
+};
+
+__global__ void halo_pack(const double *phi, const int64_t *n, int64_t pitch, int64_t plane, int64_t org,
+                          HaloTable H, uint64_t *send, const int32_t *abort) {
+    const int s = blockIdx.y;
+    const Rect R = H.rect[s];
+    const int64_t cnt = (int64_t)R.rows * R.cols;
+    uint64_t *m = send + H.off[s];
+    const int32_t ab = *(volatile const int32_t *)abort;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        m[0] = (uint64_t)ab;
+        m[1] = 0;
+    }
+    if (ab) return;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < cnt; e += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t r = (int32_t)(e / R.cols), c = (int32_t)(e - (int64_t)r * R.cols);
+        const int64_t g = org + (int64_t)(R.r0 + r) * pitch + R.c0 + c;
+        m[2 + e] = __double_as_longlong(phi[g]);
+        m[2 + cnt + e] = (uint64_t)n[g];
+        m[2 + 2 * cnt + e] = (uint64_t)n[plane + g];
+    }
+}
+
+__global__ void halo_unpack(double *phi, int64_t *n, int64_t pitch, int64_t plane, int64_t org, HaloTable H,
+                            HaloSrc src, int32_t *abort) {
+    const int s = blockIdx.y;
+    const uint64_t *m = src.msg[s];
+    if (*(volatile const uint64_t *)m) {  // the sender has aborted: stop here too
+        if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    if (*(volatile const int32_t *)abort) return;
+    const Rect R = H.rect[s];
+    const int64_t cnt = (int64_t)R.rows * R.cols;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < cnt; e += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t r = (int32_t)(e / R.cols), c = (int32_t)(e - (int64_t)r * R.cols);
+        const int64_t g = org + (int64_t)(R.r0 + r) * pitch + R.c0 + c;
+        phi[g] = __longlong_as_double((long long)m[2 + e]);
+        n[g] = (int64_t)m[2 + cnt + e];
+        n[plane + g] = (int64_t)m[2 + 2 * cnt + e];
+    }
+}
+
+// Per-tile batch summary, contiguous so that ranks can all-gather it in one collective.
+struct Summary {
+    int32_t abort;
+    uint32_t nreport;
+    uint64_t pad;
+    Report reports[MAX_REPORTS];
+    sv_stats stats[DOMAIN_BATCH];
+};
+
+}  // namespace sv
+
+using namespace svh;
+
+struct sv_domain_tile {
+    int32_t iy = 0, ix = 0, T0 = 0, X0 = 0;
+    int nbr[NDIR] = {0};            // global tile index of the neighbour in direction s
+    std::vector<double *> phi;      // ring of R buffers, ghost layout
+    std::vector<int64_t *> n;
+    uint64_t *send = nullptr, *recv = nullptr;
+    Summary *sum = nullptr;         // device
+};
+
+struct sv_domain {
+    sv_ctx *ctx = nullptr;
+    int32_t Nt = 0, Nx = 0, ty = 1, tx = 1, Ht = 0, Wt = 0;
+    int nranks = 1, rank = 0;
+    int64_t pitch = 0, plane = 0, org = 0;
+    int R = 2, cur = 0;
+    HaloTable H{};
+    int64_t msg_words = 0;
+    std::vector<sv_domain_tile> tiles;  // local tiles (all tiles when nranks == 1)
+    std::vector<int> local_of;          // global tile index -> local index, or -1
+    ncclComm_t comm = nullptr;
+    bool loopback = false;              // 1 rank, 1 tile, halos through RCCL to itself (tests the RCCL path)
+    Summary *gathered = nullptr;        // device, nranks summaries (RCCL mode)
+    std::vector<Summary> host_sum;
+};
+
+namespace {
+
+void check_nccl(ncclResult_t r, const char *what) {
+    if (r != ncclSuccess) throw std::runtime_error(std::string(what) + " failed: " + ncclGetErrorString(r));
+}
+
+int tile_index(const sv_domain *d, int iy, int ix) {
+    iy = ((iy % d->ty) + d->ty) % d->ty;
+    ix = ((ix % d->tx) + d->tx) % d->tx;
+    return iy * d->tx + ix;
+}
+
+void geometry(sv_domain *d) {
+    if (d->Nt % d->ty || d->Nx % d->tx) throw std::invalid_argument("the lattice must divide evenly into tiles");
+    d->Ht = d->Nt / d->ty;
+    d->Wt = d->Nx / d->tx;
+    if (d->Ht % 2 || d->Wt % 2 || d->Ht < 4 || d->Wt < 4)
+        throw std::invalid_argument("tiles must be at least 4 x 4 with even extents");
+    if ((int64_t)d->Nt * d->Nx >= (1LL << 32)) throw std::invalid_argument("lattice too large for 32-bit stream positions");
+    d->pitch = ((LEFT_PAD + d->Wt + GHOST_RIGHT + 15) / 16) * 16;
+    d->plane = (int64_t)(d->Ht + GHOST_TOP + GHOST_BOTTOM) * d->pitch;
+    d->org = (int64_t)GHOST_TOP * d->pitch + LEFT_PAD;
+    // ring depth: an abort travels one tile-hop (8-neighbour torus) per sweep
+    const int D = std::max(d->ty / 2, d->tx / 2);
+    d->R = std::max(2, D + 1);
+    int64_t off = 0;
+    for (int s = 0; s < NDIR; s++) {
+        d->H.rect[s] = send_rect(s, d->Ht, d->Wt);
+        d->H.off[s] = off;
+        off += 2 + 3 * (int64_t)d->H.rect[s].rows * d->H.rect[s].cols;
+    }
+    d->msg_words = off;
+}
+
+HaloTable recv_table(const sv_domain *d) {
+    HaloTable h = d->H;
+    for (int s = 0; s < NDIR; s++) h.rect[s] = recv_rect(s, d->Ht, d->Wt);
+    return h;
+}
+
+void exchange(sv_domain *d) {
+    sv_ctx *ctx = d->ctx;
+    const int slot = d->cur;
+    const int threads = 256;
+    // pack every local tile
+    for (auto &T : d->tiles) {
+        int64_t mx = 0;
+        for (int s = 0; s < NDIR; s++) mx = std::max<int64_t>(mx, (int64_t)d->H.rect[s].rows * d->H.rect[s].cols);
+        dim3 grid((unsigned)std::min<int64_t>((mx + threads - 1) / threads, 1024), NDIR);
+        halo_pack<<<grid, threads, 0, ctx->stream>>>(T.phi[slot], T.n[slot], d->pitch, d->plane, d->org, d->H, T.send,
+                                                     &T.sum->abort);
+    }
+    // remote messages (one tile per rank in RCCL mode)
+    if (d->comm) {
+        sv_domain_tile &T = d->tiles[0];
+        const int me = d->rank;
+        check_nccl(ncclGroupStart(), "ncclGroupStart");
+        for (int s = 0; s < NDIR; s++) {
+            const int peer = T.nbr[s];
+            if (peer == me && !d->loopback) continue;
+            const int64_t w = 2 + 3 * (int64_t)d->H.rect[s].rows * d->H.rect[s].cols;
+            check_nccl(ncclSend(T.send + d->H.off[s], (size_t)w, ncclUint64, peer, d->comm, ctx->stream), "ncclSend");
+        }
+        for (int s = 0; s < NDIR; s++) {
+            const int peer = T.nbr[opp(s)];  // the message of direction s comes from the tile at -s
+            if (peer == me && !d->loopback) continue;
+            const int64_t w = 2 + 3 * (int64_t)d->H.rect[s].rows * d->H.rect[s].cols;
+            check_nccl(ncclRecv(T.recv + d->H.off[s], (size_t)w, ncclUint64, peer, d->comm, ctx->stream), "ncclRecv");
+        }
+        check_nccl(ncclGroupEnd(), "ncclGroupEnd");
+    }
+    // unpack: ghost block s takes the message of direction s from the neighbour at -s
+    const HaloTable HR = recv_table(d);
+    for (auto &T : d->tiles) {
+        HaloSrc src;
+        int64_t mx = 0;
+        for (int s = 0; s < NDIR; s++) {
+            const int peer = T.nbr[opp(s)];
+            const int li = d->local_of[peer];
+            src.msg[s] = (li >= 0 && !d->loopback) ? d->tiles[li].send + d->H.off[s] : T.recv + d->H.off[s];
+            mx = std::max<int64_t>(mx, (int64_t)HR.rect[s].rows * HR.rect[s].cols);
+        }
+        dim3 grid((unsigned)std::min<int64_t>((mx + threads - 1) / threads, 1024), NDIR);
+        halo_unpack<<<grid, threads, 0, ctx->stream>>>(T.phi[slot], T.n[slot], d->pitch, d->plane, d->org, HR, src,
+                                                       &T.sum->abort);
+    }
+}
+
+// Gather every tile's batch summary (local tiles, then all ranks), in global tile order.
+void gather(sv_domain *d) {
+    sv_ctx *ctx = d->ctx;
+    const int ntiles = d->ty * d->tx;
+    d->host_sum.resize(ntiles);
+    if (d->comm) {
+        check_nccl(ncclAllGather(d->tiles[0].sum, d->gathered, sizeof(Summary), ncclChar, d->comm, ctx->stream),
+                   "ncclAllGather");
+        SV_HIP(hipMemcpyAsync(d->host_sum.data(), d->gathered, ntiles * sizeof(Summary), hipMemcpyDeviceToHost,
+                              ctx->stream));
+    } else {
+        for (int t = 0; t < ntiles; t++)
+            SV_HIP(hipMemcpyAsync(&d->host_sum[t], d->tiles[d->local_of[t]].sum, sizeof(Summary),
+                                  hipMemcpyDeviceToHost, ctx->stream));
+    }
+    SV_HIP(hipStreamSynchronize(ctx->stream));
+}
+
+void fill_stats(const sv_domain *d, const SkipMap &skips, int nb, int sw, int count, sv_stats *stats) {
+    const int64_t V = (int64_t)d->Nt * d->Nx;
+    for (int k = 0; k < count; k++) {
+        sv_stats s{0, V, 0.0, 0};
+        for (const Summary &S : d->host_sum) {  // global tile order: identical on every rank
+            s.accepted += S.stats[k].accepted;
+            s.acceptance_sum += S.stats[k].acceptance_sum;
+        }
+        s.rejections = rejections_in(skips, sw + k, nb);
+        stats[sw + k] = s;
+    }
+}
+
+void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u128 inc, sv_stats *stats) {
+    sv_ctx *ctx = d->ctx;
+    const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
+    const int64_t V = (int64_t)d->Nt * d->Nx;
+    const int64_t counts[2] = {V / 2, V / 2};
+    const auto specs = villain_specs(V, 2, counts, P.k > 1);
+    const int nb = (int)specs.size();
+    constexpr int NWv = 4;
+    const int TH = fused_th();
+    const int nsx = (d->Wt + FW_MAX - 1) / FW_MAX;
+    const int nsy = (d->Ht + TH - 1) / TH;
+    const Affine adv[3] = {host_power(inc, (uint64_t)NWv * d->Nx), host_power(inc, (uint64_t)NWv * d->Nx / 2),
+                           host_power(inc, (uint64_t)NWv * d->Nx / 4)};
+    SkipMap skips;
+    std::vector<Block> blocks;
+    std::vector<uint32_t> skipvec;
+    int sw = 0;
+    while (sw < sweeps) {
+        const int count = std::min(DOMAIN_BATCH, sweeps - sw);
+        Cursor c = cur;
+        plan_sweeps(ctx, c, inc, specs, sw, count, skips, blocks, skipvec);
+        upload_plan(ctx, blocks, skipvec);
+        for (auto &Tl : d->tiles) SV_HIP(hipMemsetAsync(Tl.sum, 0, sizeof(Summary), ctx->stream));
+        const int cur0 = d->cur;
+        for (int k = 0; k < count; k++) {
+            exchange(d);
+            const int in = d->cur, out = (d->cur + 1) % d->R;
+            for (auto &Tl : d->tiles) {
+                FArgs A;
+                A.P = P;
+                A.G = FGeom{d->Nt, d->Nx, Tl.T0, Tl.X0, d->Ht, d->Wt, d->pitch, d->plane, d->org};
+                A.phi_in = Tl.phi[in];
+                A.n_in = Tl.n[in];
+                A.phi_out = Tl.phi[out];
+                A.n_out = Tl.n[out];
+                A.nsx = nsx;
+                A.TH = TH;
+                A.nsy = nsy;
+                A.blocks = ctx->d_blocks + (size_t)k * nb;
+                A.skips = ctx->d_skips;
+                A.T = T;
+                A.adv[0] = adv[0];
+                A.adv[1] = adv[1];
+                A.adv[2] = adv[2];
+                A.stat = &Tl.sum->stats[k];
+                A.S = DevScratch{&Tl.sum->abort, &Tl.sum->nreport, Tl.sum->reports};
+                A.sweep = (uint32_t)k;
+                hipEvent_t ev;
+                ctx->time_begin(&ev);
+                launch_fused_tile(A, nsx * nsy, ctx->stream);
+                ctx->time_end(ev, 1);
+            }
+            d->cur = out;
+        }
+        SV_HIP(hipGetLastError());
+        gather(d);
+        AbortInfo a{0, {}};
+        for (const Summary &S : d->host_sum) {
+            a.abort |= S.abort;
+            const uint32_t nr = std::min<uint32_t>(S.nreport, MAX_REPORTS);
+            a.reports.insert(a.reports.end(), S.reports, S.reports + nr);
+        }
+        if (a.abort) ctx->time_discard();
+        ctx->time_collect();
+        if (!a.abort) {
+            fill_stats(d, skips, nb, sw, count, stats);
+            cur = c;
+            sw += count;
+            continue;
+        }
+        for (const Report &r : a.reports)
+            if (r.block == OVERFLOW_BLOCK)
+                throw std::runtime_error("|n| exceeds the fused path's int32 LDS image (domain mode has no fallback)");
+        const int bad = absorb_reports(a, sw, skips);
+        if (bad > 0) {
+            Cursor c2 = cur;
+            std::vector<Block> b2;
+            std::vector<uint32_t> s2;
+            plan_sweeps(ctx, c2, inc, specs, sw, bad, skips, b2, s2);
+            fill_stats(d, skips, nb, sw, bad, stats);
+            cur = c2;
+        }
+        d->cur = (cur0 + bad) % d->R;
+        sw += bad;
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------- C-ABI
+extern "C" {
+
+int sv_domain_unique_id(uint8_t *id) {
+    if (!id) return -1;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return -2;
+    std::memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+    return 0;
+}
+
+int sv_domain_exchange_plan(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t rank, int64_t *out) {
+    try {
+        if (!out || tiles_t < 1 || tiles_x < 1 || rank < 0 || rank >= tiles_t * tiles_x) return -1;
+        sv_domain d;
+        d.Nt = Nt;
+        d.Nx = Nx;
+        d.ty = tiles_t;
+        d.tx = tiles_x;
+        geometry(&d);
+        const int iy = rank / tiles_x, ix = rank % tiles_x;
+        for (int s = 0; s < NDIR; s++) {
+            int dy, dx;
+            dir_of(s, dy, dx);
+            const Rect S = send_rect(s, d.Ht, d.Wt), Rr = recv_rect(s, d.Ht, d.Wt);
+            int64_t *o = out + 10 * s;
+            o[0] = dy;
+            o[1] = dx;
+            o[2] = tile_index(&d, iy + dy, ix + dx);  // send to
+            o[3] = S.r0;
+            o[4] = S.c0;
+            o[5] = S.rows;
+            o[6] = S.cols;
+            o[7] = tile_index(&d, iy - dy, ix - dx);  // receive the message of direction s from
+            o[8] = Rr.r0;
+            o[9] = Rr.c0;
+        }
+        return 0;
+    } catch (const std::exception &) {
+        return -2;
+    }
+}
+
+int sv_domain_create(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t nranks,
+                     int32_t rank, const uint8_t *unique_id, sv_domain **out) {
+    if (!ctx || !out) return -1;
+    *out = nullptr;
+    sv_domain *d = new sv_domain();
+    try {
+        SV_HIP(hipSetDevice(ctx->device));
+        d->ctx = ctx;
+        d->Nt = Nt;
+        d->Nx = Nx;
+        d->ty = tiles_t;
+        d->tx = tiles_x;
+        d->nranks = nranks;
+        d->rank = rank;
+        if (tiles_t < 1 || tiles_x < 1) throw std::invalid_argument("tile grid must be at least 1 x 1");
+        if (nranks < 1 || rank < 0 || rank >= nranks) throw std::invalid_argument("bad rank / nranks");
+        if (nranks > 1 && nranks != tiles_t * tiles_x)
+            throw std::invalid_argument("with several ranks, each rank owns exactly one tile (nranks == tiles_t * tiles_x)");
+        if (nranks > 1 && !unique_id) throw std::invalid_argument("a unique id (sv_domain_unique_id on rank 0) is required");
+        d->loopback = nranks == 1 && unique_id != nullptr;
+        if (d->loopback && tiles_t * tiles_x != 1) throw std::invalid_argument("RCCL loopback mode needs a 1 x 1 tile grid");
+        geometry(d);
+        const int ntiles = tiles_t * tiles_x;
+        d->local_of.assign(ntiles, -1);
+        for (int t = 0; t < ntiles; t++) {
+            if (nranks > 1 && t != rank) continue;
+            sv_domain_tile T;
+            T.iy = t / tiles_x;
+            T.ix = t % tiles_x;
+            T.T0 = T.iy * d->Ht;
+            T.X0 = T.ix * d->Wt;
+            for (int s = 0; s < NDIR; s++) {
+                int dy, dx;
+                dir_of(s, dy, dx);
+                T.nbr[s] = tile_index(d, T.iy + dy, T.ix + dx);
+            }
+            d->local_of[t] = (int)d->tiles.size();
+            d->tiles.push_back(T);
+        }
+        for (auto &T : d->tiles) {
+            T.phi.assign(d->R, nullptr);
+            T.n.assign(d->R, nullptr);
+            for (int i = 0; i < d->R; i++) {
+                SV_HIP(hipMalloc(&T.phi[i], d->plane * sizeof(double)));
+                SV_HIP(hipMalloc(&T.n[i], 2 * d->plane * sizeof(int64_t)));
+                SV_HIP(hipMemset(T.phi[i], 0, d->plane * sizeof(double)));
+                SV_HIP(hipMemset(T.n[i], 0, 2 * d->plane * sizeof(int64_t)));
+            }
+            SV_HIP(hipMalloc(&T.send, d->msg_words * sizeof(uint64_t)));
+            SV_HIP(hipMalloc(&T.recv, d->msg_words * sizeof(uint64_t)));
+            SV_HIP(hipMemset(T.recv, 0, d->msg_words * sizeof(uint64_t)));
+            SV_HIP(hipMalloc(&T.sum, sizeof(Summary)));
+            SV_HIP(hipMemset(T.sum, 0, sizeof(Summary)));
+        }
+        if (nranks > 1 || d->loopback) {
+            ncclUniqueId u;
+            std::memcpy(u.internal, unique_id, NCCL_UNIQUE_ID_BYTES);
+            check_nccl(ncclCommInitRank(&d->comm, nranks, u, rank), "ncclCommInitRank");
+            SV_HIP(hipMalloc(&d->gathered, (size_t)nranks * sizeof(Summary)));
+        }
+        SV_HIP(hipDeviceSynchronize());
+        *out = d;
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        sv_domain_destroy(d);
+        return -2;
+    }
+}
+
+int sv_domain_destroy(sv_domain *d) {
+    if (!d) return 0;
+    if (d->ctx) {
+        (void)hipSetDevice(d->ctx->device);
+        (void)hipStreamSynchronize(d->ctx->stream);
+    }
+    for (auto &T : d->tiles) {
+        for (auto p : T.phi) (void)hipFree(p);
+        for (auto p : T.n) (void)hipFree(p);
+        (void)hipFree(T.send);
+        (void)hipFree(T.recv);
+        (void)hipFree(T.sum);
+    }
+    if (d->comm) (void)ncclCommDestroy(d->comm);
+    (void)hipFree(d->gathered);
+    delete d;
+    return 0;
+}
+
+int sv_domain_upload(sv_domain *d, const double *phi, const int64_t *n) {
+    if (!d) return -1;
+    sv_ctx *ctx = d->ctx;
+    try {
+        SV_HIP(hipSetDevice(ctx->device));
+        const int64_t V = (int64_t)d->Nt * d->Nx;
+        for (auto &T : d->tiles) {
+            if (!phi || !n) {
+                SV_HIP(hipMemsetAsync(T.phi[d->cur], 0, d->plane * sizeof(double), ctx->stream));
+                SV_HIP(hipMemsetAsync(T.n[d->cur], 0, 2 * d->plane * sizeof(int64_t), ctx->stream));
+                continue;
+            }
+            const int64_t g0 = (int64_t)T.T0 * d->Nx + T.X0;
+            SV_HIP(hipMemcpy2DAsync(T.phi[d->cur] + d->org, d->pitch * sizeof(double), phi + g0, d->Nx * sizeof(double),
+                                    d->Wt * sizeof(double), d->Ht, hipMemcpyHostToDevice, ctx->stream));
+            for (int c = 0; c < 2; c++)
+                SV_HIP(hipMemcpy2DAsync(T.n[d->cur] + c * d->plane + d->org, d->pitch * sizeof(int64_t), n + c * V + g0,
+                                        d->Nx * sizeof(int64_t), d->Wt * sizeof(int64_t), d->Ht, hipMemcpyHostToDevice,
+                                        ctx->stream));
+        }
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_domain_download(sv_domain *d, double *phi, int64_t *n) {
+    if (!d || !phi || !n) return -1;
+    sv_ctx *ctx = d->ctx;
+    try {
+        SV_HIP(hipSetDevice(ctx->device));
+        const int64_t V = (int64_t)d->Nt * d->Nx;
+        for (auto &T : d->tiles) {
+            const int64_t g0 = (int64_t)T.T0 * d->Nx + T.X0;
+            SV_HIP(hipMemcpy2DAsync(phi + g0, d->Nx * sizeof(double), T.phi[d->cur] + d->org, d->pitch * sizeof(double),
+                                    d->Wt * sizeof(double), d->Ht, hipMemcpyDeviceToHost, ctx->stream));
+            for (int c = 0; c < 2; c++)
+                SV_HIP(hipMemcpy2DAsync(n + c * V + g0, d->Nx * sizeof(int64_t), T.n[d->cur] + c * d->plane + d->org,
+                                        d->pitch * sizeof(int64_t), d->Wt * sizeof(int64_t), d->Ht,
+                                        hipMemcpyDeviceToHost, ctx->stream));
+        }
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_domain_run(sv_domain *d, double kappa, int64_t W, double interval_phi, int64_t interval_n, int32_t sweeps,
+                  sv_rng *rng, sv_stats *stats) {
+    if (!d || !rng || (sweeps > 0 && !stats)) return -1;
+    sv_ctx *ctx = d->ctx;
+    try {
+        if (sweeps < 0) throw std::invalid_argument("sweeps must be >= 0");
+        if (interval_n < 0 || interval_n > (1 << 20)) throw std::invalid_argument("interval_n out of range");
+        if ((W < 0 ? -W : W) * interval_n >= (1LL << 28)) throw std::invalid_argument("|W * interval_n| too large");
+        SV_HIP(hipSetDevice(ctx->device));
+        VParams P = make_params(d->Nx, kappa, W, interval_phi, interval_n);
+        u128 inc{rng->inc_lo, rng->inc_hi};
+        Cursor cur{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
+        run_domain(d, P, sweeps, cur, inc, stats);
+        rng->state_hi = cur.s.hi;
+        rng->state_lo = cur.s.lo;
+        rng->has_uint32 = (int32_t)cur.has;
+        rng->uinteger = cur.buf;
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
+}  // extern "C"

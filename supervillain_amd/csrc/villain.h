@@ -1,0 +1,79 @@
+// villain.h -- declarations shared by villain.hip (single-lattice drivers) and domain.hip
+// (domain decomposition): the fused sweep kernel's arguments and the host planning helpers.
+#pragma once
+#include "common.h"
+
+namespace sv {
+
+struct VParams {
+    int32_t N;
+    double half_kappa;
+    int64_t W;
+    double lo_phi, range_phi;  // uniform(-interval_phi, +interval_phi): low, high - low
+    int64_t interval_n;
+    uint32_t k, thr;           // choice over 2*interval_n+1 values; Lemire threshold
+};
+
+static constexpr uint32_t OVERFLOW_BLOCK = 0xFFFFu;  // report tag: state not representable on this path
+static constexpr int FW_MAX = 123;     // colour-0 sites per region row <= 63, so lane 63 is always spare
+static constexpr int RW = FW_MAX + 5;  // 128 region columns: x0-2 .. x1+2
+static constexpr int SMALL_LDS = 128;  // small-offset maps cached in LDS (in-row offsets are <= w+4)
+
+// Geometry of one fused launch.  Periodic mode (TILE=false): the whole N x N lattice, rows and
+// columns wrap in memory.  Tile mode (TILE=true, domain decomposition): an Ht x Wt tile at global
+// origin (T0, X0) of an Nt x Nx lattice, stored with a ghost frame (rows -2..Ht+2, columns
+// -2..Wt+2 filled by the halo exchange) so memory never wraps; only the RNG addressing and the
+// colouring use global coordinates.
+struct FGeom {
+    int32_t Nt, Nx;   // global lattice
+    int32_t T0, X0;   // tile origin (0, 0 in periodic mode)
+    int32_t Ht, Wt;   // tile extent (Nt, Nx in periodic mode)
+    int64_t pitch;    // row pitch of phi/n buffers (elements)
+    int64_t plane;    // n component stride (elements)
+    int64_t org;      // element offset of tile site (0, 0)
+};
+
+struct FArgs {
+    VParams P;
+    FGeom G;
+    const double *phi_in;
+    const int64_t *n_in;
+    double *phi_out;
+    int64_t *n_out;
+    int32_t nsx, TH, nsy;  // column strips, rows per strip tile, row tiles
+    const Block *blocks;   // this sweep's 11 descriptors
+    const uint32_t *skips;
+    const JumpTables *T;
+    Affine adv[3];  // advance a row base by NW rows: [0] NW*Nx draws, [1] NW*Nx/2, [2] NW*Nx/4
+    sv_stats *stat;
+    DevScratch S;
+    uint32_t sweep;
+};
+
+}  // namespace sv
+
+namespace svh {
+using namespace sv;
+
+// Skip lists keyed by (sweep index within the call, block index)
+using SkipMap = std::map<std::pair<int, int>, std::vector<uint32_t>>;
+
+struct AbortInfo {
+    int32_t abort;
+    std::vector<Report> reports;
+};
+
+// One sweep's block sequence: metropolis uniform(V), then per colour
+// [dphi uniform(n_c)][4 bounded choice(n_c)].
+std::vector<BlockSpec> villain_specs(int64_t V, int ncol, const int64_t *count, bool has_bounded);
+void plan_sweeps(sv_ctx *ctx, Cursor &cur, u128 inc, const std::vector<BlockSpec> &specs, int first, int count,
+                 const SkipMap &skips, std::vector<Block> &blocks, std::vector<uint32_t> &skipvec);
+void upload_plan(sv_ctx *ctx, const std::vector<Block> &blocks, const std::vector<uint32_t> &skipvec);
+VParams make_params(int32_t N, double kappa, int64_t W, double interval_phi, int64_t interval_n);
+int absorb_reports(const AbortInfo &a, int first, SkipMap &skips);
+int64_t rejections_in(const SkipMap &skips, int sweep, int nblocks);
+int fused_th();
+// launch villain_sweep_fused<4, true> (tile mode) with `grid` workgroups
+void launch_fused_tile(const FArgs &A, int grid, hipStream_t stream);
+
+}  // namespace svh

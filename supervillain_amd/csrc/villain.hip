@@ -24,20 +24,12 @@
 #include <cstdio>
 #include <cstdlib>
 
-#include "common.h"
+#include "villain.h"
 
 namespace sv {
 
 #define TWO_PI 6.283185307179586
 
-struct VParams {
-    int32_t N;
-    double half_kappa;
-    int64_t W;
-    double lo_phi, range_phi;  // uniform(-interval_phi, +interval_phi): low, high - low
-    int64_t interval_n;
-    uint32_t k, thr;           // choice over 2*interval_n+1 values; Lemire threshold
-};
 
 // Block order inside one sweep's descriptor array:
 //   [0] metropolis (uniform V), then per colour c: [1+5c] dphi (uniform), [2+5c] fwd mu=0,
@@ -183,31 +175,13 @@ __global__ __launch_bounds__(256) void villain_pass_generic(VParams P, double *p
 // fused path (even N)
 // ================================================================================================
 
-static constexpr uint32_t OVERFLOW_BLOCK = 0xFFFFu;  // report tag: state not representable on this path
-static constexpr int FW_MAX = 123;     // colour-0 sites per region row <= 63, so lane 63 is always spare
-static constexpr int RW = FW_MAX + 5;  // 128 region columns: x0-2 .. x1+2
-static constexpr int SMALL_LDS = 128;  // small-offset maps cached in LDS (in-row offsets are <= w+4)
 
 template <int NW>
 struct FusedGeom {
     static constexpr int R = 2 * NW + 3;  // ring rows: outputs t.. up to prefetched rows t+2+2NW
 };
 
-struct FArgs {
-    VParams P;
-    const double *phi_in;
-    const int64_t *n_in;
-    double *phi_out;
-    int64_t *n_out;
-    int32_t nsx, TH, nsy;  // column strips, rows per strip tile, row tiles
-    const Block *blocks;   // this sweep's 11 descriptors
-    const uint32_t *skips;
-    const JumpTables *T;
-    Affine adv[3];  // advance a row base by NW rows: [0] NW*N draws, [1] NW*N/2, [2] NW*N/4
-    sv_stats *stat;
-    DevScratch S;
-    uint32_t sweep;
-};
+
 
 // v mod N for v in [-2N, 3N) without a division
 __device__ __forceinline__ int32_t wrapN(int32_t v, int32_t N) {
@@ -291,7 +265,7 @@ __device__ __forceinline__ int32_t choice_value(const FArgs &A, uint32_t word, u
 __device__ __forceinline__ Draws draws_general(const FArgs &A, int c, bool active, int64_t gq, int64_t gx, int64_t xb,
                                                const u128 *bases, const Affine *sm) {
     const JumpTables *T = A.T;
-    const int64_t N = A.P.N;
+    const int64_t N = A.G.Nx;  // row length of the global stream layout
     const int bb = 1 + 5 * c;
     const int64_t lin = gq * N + gx, rank = lin >> 1;
     Draws D;
@@ -372,7 +346,7 @@ __device__ __forceinline__ Draws draws_fast(const FArgs &A, int c, bool active, 
     return D;
 }
 
-template <int NW>
+template <int NW, bool TILE>
 __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
     constexpr int R = FusedGeom<NW>::R;
     constexpr int nthreads = NW * 64;
@@ -389,9 +363,15 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
 
     if (*(volatile const int32_t *)A.S.abort) return;
 
-    const int32_t N = A.P.N;
+    const FGeom &Gm = A.G;
+    const int32_t Nt = Gm.Nt, Nx = Gm.Nx;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t V = (int64_t)N * N;
+    const int64_t V = Gm.plane;
+    // global row of local row q; memory offset of local row q / local column c
+    auto grow = [&](int32_t q) { return wrapN(Gm.T0 + q, Nt); };
+    auto mrow = [&](int32_t q) -> int64_t { return TILE ? Gm.org + (int64_t)q * Gm.pitch : (int64_t)wrapN(q, Nt) * Nx; };
+    auto mcol = [&](int32_t c) -> int32_t { return TILE ? c : wrapN(c, Nx); };
+    const int32_t par0 = (Gm.T0 + Gm.X0) & 1;  // colour parity offset of local coordinates
 
     // XCD-aware tile order: blocks b, b+8, ... share an XCD; give each XCD a contiguous run of tiles
     const int G = A.nsx * A.nsy;
@@ -402,14 +382,15 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
         b = xcd * per + (xcd < rem ? xcd : rem) + k;
     }
     const int ix = b % A.nsx, iy = b / A.nsx;
-    const int32_t x0 = (int32_t)((int64_t)ix * N / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * N / A.nsx);
+    const int32_t x0 = (int32_t)((int64_t)ix * Gm.Wt / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * Gm.Wt / A.nsx);
     const int32_t w = x1 - x0;
     const int32_t t0 = iy * A.TH;
-    const int32_t t1 = t0 + A.TH < N ? t0 + A.TH : N;
+    const int32_t t1 = t0 + A.TH < Gm.Ht ? t0 + A.TH : Gm.Ht;
     const int32_t rbase = t0 - 2;  // local row 0
     const int32_t cols = w + 5;
-    const int32_t xb = x0 - 2 < 0 ? 0 : x0 - 2;  // row bases at the first non-wrapped region column
-    const bool interior = x0 >= 4 && x1 + 2 < N;
+    const int32_t gx0 = Gm.X0 + x0;                  // global column of the strip's first site
+    const int32_t xb = gx0 - 2 < 0 ? 0 : gx0 - 2;    // row bases at the first non-wrapped region column (global)
+    const bool interior = gx0 >= 4 && gx0 + w + 2 < Nx;
 
     for (int e = threadIdx.x; e < SMALL_LDS; e += nthreads) s_small[e] = A.T->small[e];
     if (threadIdx.x < 3) s_adv[threadIdx.x] = A.adv[threadIdx.x];
@@ -433,14 +414,14 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
         const int e = threadIdx.x + k * nthreads;
         pf_rr[k] = e / cols;
         pf_cc[k] = e - pf_rr[k] * cols;
-        pf_gx[k] = wrapN(x0 - 2 + pf_cc[k], N);
+        pf_gx[k] = mcol(x0 - 2 + pf_cc[k]);
     }
     auto prefetch = [&](int32_t ra) {
 #pragma unroll
         for (int k = 0; k < PF; k++) {
             const int32_t q = ra + pf_rr[k];
             if (pf_rr[k] < NW && q >= t0 - 2 && q <= t1 + 2) {
-                const int64_t g = (int64_t)wrapN(q, N) * N + pf_gx[k];
+                const int64_t g = mrow(q) + pf_gx[k];
                 pf_phi[k] = A.phi_in[g];
                 pf_n0[k] = A.n_in[g];
                 pf_n1[k] = A.n_in[V + g];
@@ -470,7 +451,7 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
     const int32_t tfirst = t0 - 3;
     int32_t brow = tfirst + 2 - bc + wave;  // D0 row t+2+wave, D1 row t+1+wave
     u128 bases{0, 0};
-    if (base_lane) bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)base_pos(bty, wrapN(brow, N), N, xb, bhas));
+    if (base_lane) bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)base_pos(bty, grow(brow), Nx, xb, bhas));
     __builtin_amdgcn_s_waitcnt(0);
     if (base_lane) s_base[wave][lane] = bases;
 
@@ -485,7 +466,7 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
             const int rr = e / w, cc = e - rr * w;
             const int32_t q = r0 + rr;
             const int slot = (q - rbase) % R, cx = cc + 2;
-            const int64_t g = (int64_t)q * N + x0 + cc;  // tile sites never wrap
+            const int64_t g = mrow(q) + x0 + cc;  // tile sites never wrap
             A.phi_out[g] = s_phi[slot][cx];
             A.n_out[g] = (int64_t)s_n0[slot][cx];
             A.n_out[V + g] = (int64_t)s_n1[slot][cx];
@@ -505,8 +486,8 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
         {
             const int32_t q = t + 2 + wave;
             const bool row_ok = (q >= t0 - 1) && (q <= t1 + 1);
-            const int32_t gq = wrapN(q, N);
-            const int32_t xs = (x0 - 1) + ((q + x0 - 1) & 1);  // (q + x) even
+            const int32_t gq = grow(q);
+            const int32_t xs = (x0 - 1) + ((par0 + q + x0 - 1) & 1);  // global (t + x) even
             const int32_t x = xs + 2 * lane;
             const bool active = row_ok && x <= x1 + 1;
             u128 bs[6];
@@ -514,10 +495,10 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
             for (int k = 0; k < 6; k++) bs[k] = s_base[wave][k];
             Draws D;
             if (fast[0])
-                D = draws_fast(A, 0, active, lane, (uint32_t)gq * (uint32_t)N, (uint32_t)xs, (uint32_t)x, (uint32_t)xb,
-                               bs, s_small);
+                D = draws_fast(A, 0, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
+                               (uint32_t)(Gm.X0 + x), (uint32_t)xb, bs, s_small);
             else
-                D = draws_general(A, 0, active, gq, wrapN(x, N), xb, bs, s_small);
+                D = draws_general(A, 0, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small);
             if (active) {
                 const int lr = q - rbase;
                 const int sm = (lr - 1) % R, s0 = lr % R, sp = (lr + 1) % R;
@@ -572,8 +553,8 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
         {
             const int32_t q = t + 1 + wave;
             const bool row_ok = (q >= t0) && (q <= t1);
-            const int32_t gq = wrapN(q, N);
-            const int32_t xs = x0 + ((q + x0 + 1) & 1);  // (q + x) odd
+            const int32_t gq = grow(q);
+            const int32_t xs = x0 + ((par0 + q + x0 + 1) & 1);  // global (t + x) odd
             const int32_t x = xs + 2 * lane;
             const bool active = row_ok && x <= x1;
             u128 bs[6];
@@ -581,10 +562,10 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
             for (int k = 0; k < 6; k++) bs[k] = s_base[wave][8 + k];
             Draws D;
             if (fast[1])
-                D = draws_fast(A, 1, active, lane, (uint32_t)gq * (uint32_t)N, (uint32_t)xs, (uint32_t)x, (uint32_t)xb,
-                               bs, s_small);
+                D = draws_fast(A, 1, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
+                               (uint32_t)(Gm.X0 + x), (uint32_t)xb, bs, s_small);
             else
-                D = draws_general(A, 1, active, gq, wrapN(x, N), xb, bs, s_small);
+                D = draws_general(A, 1, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small);
             if (active) {
                 const int lr = q - rbase;
                 const int sm = (lr - 1) % R, s0 = lr % R;
@@ -628,10 +609,10 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
         commit(t + 3 + NW);  // slots of rows [t-NW, t): not read in phase C
         // advance the row bases by NW rows (one affine map; a full jump where the row wraps)
         if (base_lane) {
-            const int64_t p_old = base_pos(bty, wrapN(brow, N), N, xb, bhas);
-            const int64_t p_new = base_pos(bty, wrapN(brow + NW, N), N, xb, bhas);
+            const int64_t p_old = base_pos(bty, grow(brow), Nx, xb, bhas);
+            const int64_t p_new = base_pos(bty, grow(brow + NW), Nx, xb, bhas);
             const int ai = bty == 0 ? 0 : (bty == 1 ? 1 : 2);
-            const int64_t step = bty == 0 ? (int64_t)NW * N : (bty == 1 ? (int64_t)NW * N / 2 : (int64_t)NW * N / 4);
+            const int64_t step = bty == 0 ? (int64_t)NW * Nx : (bty == 1 ? (int64_t)NW * Nx / 2 : (int64_t)NW * Nx / 4);
             if (p_new - p_old == step) bases = apply(s_adv[ai], bases);
             else bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)p_new);
             brow += NW;
@@ -652,9 +633,10 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
     flush_stats(A.stat, acc_count, psum);
 }
 
-template __global__ void villain_sweep_fused<2>(FArgs);
-template __global__ void villain_sweep_fused<4>(FArgs);
-template __global__ void villain_sweep_fused<6>(FArgs);
+template __global__ void villain_sweep_fused<2, false>(FArgs);
+template __global__ void villain_sweep_fused<4, false>(FArgs);
+template __global__ void villain_sweep_fused<6, false>(FArgs);
+template __global__ void villain_sweep_fused<4, true>(FArgs);
 
 // ================================================================================================
 // observables (fused reductions over the current state)
@@ -694,28 +676,35 @@ __global__ void villain_observables_kernel(int32_t N, double half_kappa, const d
 // ==================================================================================================
 // host drivers
 // ==================================================================================================
-using namespace sv;
+namespace svh {
 
-namespace {
-
-struct VillainPlan {
-    std::vector<BlockSpec> specs;  // per sweep
-};
-
-std::vector<BlockSpec> villain_specs(const sv_villain *st, bool has_bounded) {
+std::vector<BlockSpec> villain_specs(int64_t V, int ncol, const int64_t *count, bool has_bounded) {
     std::vector<BlockSpec> s;
-    int64_t V = (int64_t)st->N * st->N;
     s.push_back({UNIFORM, (uint32_t)V});
-    for (int c = 0; c < st->ncol; c++) {
-        uint32_t nc = (uint32_t)st->count[c];
+    for (int c = 0; c < ncol; c++) {
+        uint32_t nc = (uint32_t)count[c];
         s.push_back({UNIFORM, nc});
         for (int q = 0; q < 4; q++) s.push_back({BOUNDED, has_bounded ? nc : 0u});
     }
     return s;
 }
 
-// Skip lists keyed by (sweep index within the call, block index)
-using SkipMap = std::map<std::pair<int, int>, std::vector<uint32_t>>;
+std::vector<BlockSpec> villain_specs(const sv_villain *st, bool has_bounded) {
+    return villain_specs((int64_t)st->N * st->N, st->ncol, st->count, has_bounded);
+}
+
+int64_t rejections_in(const SkipMap &skips, int sweep, int nblocks) {
+    int64_t rj = 0;
+    for (int bi = 0; bi < nblocks; bi++) {
+        auto it = skips.find({sweep, bi});
+        if (it != skips.end()) rj += (int64_t)it->second.size();
+    }
+    return rj;
+}
+
+void launch_fused_tile(const FArgs &A, int grid, hipStream_t stream) {
+    villain_sweep_fused<4, true><<<grid, 4 * 64, 0, stream>>>(A);
+}
 
 // plan `count` sweeps starting at sweep `first`, writing descriptors to ctx host staging
 void plan_sweeps(sv_ctx *ctx, Cursor &cur, u128 inc, const std::vector<BlockSpec> &specs, int first, int count,
@@ -758,11 +747,6 @@ VParams make_params(int32_t N, double kappa, int64_t W, double interval_phi, int
 }
 
 DevScratch scratch(sv_ctx *ctx) { return DevScratch{ctx->d_abort, ctx->d_nreport, ctx->d_reports}; }
-
-struct AbortInfo {
-    int32_t abort;
-    std::vector<Report> reports;
-};
 
 AbortInfo read_abort(sv_ctx *ctx) {
     AbortInfo a;
@@ -910,6 +894,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         for (int k = 0; k < count; k++) {
             FArgs A;
             A.P = P;
+            A.G = FGeom{N, N, 0, 0, N, N, N, V, 0};
             A.phi_in = st->phi[st->cur];
             A.n_in = st->n[st->cur];
             A.phi_out = st->phi[st->cur ^ 1];
@@ -926,9 +911,9 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             A.stat = ctx->d_stats + k;
             A.S = scratch(ctx);
             A.sweep = (uint32_t)k;
-            if (NWv == 2) villain_sweep_fused<2><<<grid, 2 * 64, 0, ctx->stream>>>(A);
-            else if (NWv == 6) villain_sweep_fused<6><<<grid, 6 * 64, 0, ctx->stream>>>(A);
-            else villain_sweep_fused<4><<<grid, 4 * 64, 0, ctx->stream>>>(A);
+            if (NWv == 2) villain_sweep_fused<2, false><<<grid, 2 * 64, 0, ctx->stream>>>(A);
+            else if (NWv == 6) villain_sweep_fused<6, false><<<grid, 6 * 64, 0, ctx->stream>>>(A);
+            else villain_sweep_fused<4, false><<<grid, 4 * 64, 0, ctx->stream>>>(A);
             st->cur ^= 1;
         }
         ctx->time_end(ev, count);
@@ -1021,7 +1006,9 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     return true;
 }
 
-}  // namespace
+}  // namespace svh
+
+using namespace svh;
 
 // ---------------------------------------------------------------------------- C-ABI (Villain)
 extern "C" {

@@ -1,0 +1,119 @@
+"""Villain NeighborhoodUpdate on a domain-decomposed lattice (multi-GPU; SURVEY.md 8e, BASELINE config 4).
+
+The reference runs one lattice in one process (generator/villain/neighborhood.py:59-137); this is the
+same chain with the lattice cut into tiles (sv_domain_* in include/supervillain_amd.h).  One rank per
+GPU owns one tile; halos travel over RCCL inside libsvhip.so.  With a single rank every tile lives on
+one GPU -- the same code path minus RCCL, which is how the decomposition is checked bit-for-bit.
+
+    dom = VillainDomain(4096, 8192, tiles=(1, 2), kappa=0.5)            # one GPU, two tiles
+    dom = VillainDomain.distributed(8192, 16384, tiles=(2, 4), kappa=0.5)  # one rank per GPU
+    dom.upload(phi, n)      # or dom.cold()
+    stats = dom.run(100, rng)   # rng: numpy Generator(PCG64), advanced exactly as the reference would
+"""
+import ctypes
+
+import numpy as np
+
+from supervillain_amd import _native
+from supervillain_amd._abi import rng_from_numpy, rng_to_numpy
+
+UNIQUE_ID_BYTES = 128
+
+
+def tile_grid(nranks):
+    """Tile grid (tiles_t, tiles_x) for n ranks: 1x1, 1x2, 2x2, 2x4, ... (x gets the larger factor)."""
+    if nranks < 1:
+        raise ValueError('nranks must be >= 1')
+    t = int(np.floor(np.sqrt(nranks)))
+    while nranks % t:
+        t -= 1
+    return t, nranks // t
+
+
+def exchange_plan(Nt, Nx, tiles, rank):
+    """The halo messages of tile `rank` as computed by libsvhip.so (host-only; no GPU needed).
+
+    Returns a list of 8 dicts in send order: dy, dx, send_to, src (row0, col0), shape (rows, cols),
+    recv_from, dst (row0, col0) -- tile-local coordinates, ghosts outside [0, Ht) x [0, Wt)."""
+    out = (ctypes.c_int64 * 80)()
+    rc = _native.lib().sv_domain_exchange_plan(int(Nt), int(Nx), int(tiles[0]), int(tiles[1]), int(rank), out)
+    if rc != 0:
+        raise ValueError(f'invalid decomposition {Nt}x{Nx} into {tiles} (rank {rank})')
+    plan = []
+    for s in range(8):
+        o = [int(v) for v in out[10 * s:10 * s + 10]]
+        plan.append({'dy': o[0], 'dx': o[1], 'send_to': o[2], 'src': (o[3], o[4]), 'shape': (o[5], o[6]),
+                     'recv_from': o[7], 'dst': (o[8], o[9])})
+    return plan
+
+
+class VillainDomain:
+    """An Nt x Nx Villain (phi, n) state cut into tiles, resident in HBM."""
+
+    def __init__(self, Nt, Nx=None, tiles=(1, 1), kappa=0.5, W=1, interval_phi=np.pi, interval_n=1, *,
+                 device=None, nranks=1, rank=0, unique_id=None):
+        Nx = Nt if Nx is None else Nx
+        self.Nt, self.Nx, self.tiles = int(Nt), int(Nx), (int(tiles[0]), int(tiles[1]))
+        self.kappa, self.W, self.interval_phi, self.interval_n = float(kappa), int(W), float(interval_phi), int(interval_n)
+        self.nranks, self.rank = int(nranks), int(rank)
+        self.ctx = _native.context(_native.default_device() if device is None else device)
+        uid = None
+        if unique_id is not None:
+            uid = (ctypes.c_uint8 * UNIQUE_ID_BYTES).from_buffer_copy(bytes(unique_id))
+        h = ctypes.c_void_p()
+        self.ctx.check(_native.lib().sv_domain_create(self.ctx.handle, self.Nt, self.Nx, self.tiles[0], self.tiles[1],
+                                                      self.nranks, self.rank, uid, ctypes.byref(h)),
+                       'sv_domain_create')
+        self.handle = h
+
+    @classmethod
+    def distributed(cls, Nt, Nx=None, tiles=None, group=None, **kw):
+        """One tile per rank of the (already initialised) default torch.distributed group; any backend
+        (gloo is enough: it only carries the 128-byte RCCL id)."""
+        import torch.distributed as dist
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        tiles = tile_grid(world) if tiles is None else tiles
+        box = [unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0, group=group)
+        return cls(Nt, Nx, tiles, nranks=world, rank=rank, unique_id=box[0], **kw)
+
+    def close(self):
+        if getattr(self, 'handle', None) is not None and _native._LIB is not None:
+            _native._LIB.sv_domain_destroy(self.handle)
+            self.handle = None
+
+    __del__ = close
+
+    def cold(self):
+        self.ctx.check(_native.lib().sv_domain_upload(self.handle, None, None), 'sv_domain_upload')
+
+    def upload(self, phi, n):
+        phi = np.ascontiguousarray(phi, dtype=np.float64).reshape(self.Nt, self.Nx)
+        n = np.ascontiguousarray(n, dtype=np.int64).reshape(2, self.Nt, self.Nx)
+        self.ctx.check(_native.lib().sv_domain_upload(self.handle, _native.ptr(phi), _native.ptr(n)), 'sv_domain_upload')
+
+    def download(self, phi=None, n=None):
+        """Copy this rank's tiles into global (Nt, Nx) arrays (other ranks' regions are left as given)."""
+        phi = np.zeros((self.Nt, self.Nx)) if phi is None else phi
+        n = np.zeros((2, self.Nt, self.Nx), dtype=np.int64) if n is None else n
+        self.ctx.check(_native.lib().sv_domain_download(self.handle, _native.ptr(phi), _native.ptr(n)),
+                       'sv_domain_download')
+        return phi, n
+
+    def run(self, sweeps, rng):
+        """`sweeps` NeighborhoodUpdate sweeps; advances `rng` (NumPy Generator) like the reference.
+        Collective when nranks > 1.  Returns per-sweep global stats."""
+        r = rng_from_numpy(rng)
+        st = _native.stats_array(max(sweeps, 1))
+        self.ctx.check(_native.lib().sv_domain_run(self.handle, self.kappa, self.W, self.interval_phi, self.interval_n,
+                                                   int(sweeps), ctypes.byref(r), st), 'sv_domain_run')
+        rng_to_numpy(r, rng)
+        return [st[i] for i in range(sweeps)]
+
+
+def unique_id():
+    """A fresh RCCL unique id (bytes), to be created on rank 0 and shared with every rank."""
+    buf = (ctypes.c_uint8 * UNIQUE_ID_BYTES)()
+    if _native.lib().sv_domain_unique_id(buf) != 0:
+        raise _native.NativeError('ncclGetUniqueId failed')
+    return bytes(buf)

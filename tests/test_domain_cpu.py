@@ -1,0 +1,147 @@
+"""Domain decomposition host logic (CPU): the halo plan computed by libsvhip.so fills every ghost cell
+with the right periodic neighbour value, its send/receive order matches pairwise (the RCCL
+point-to-point matching rule), and a real 2-rank exchange over torch.distributed (gloo) executed
+from that plan reproduces the ghost frames.  The device kernels are covered by test_gpu_domain.py."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from supervillain_amd.domain import exchange_plan, tile_grid
+
+GT, GB, GL, GR = 2, 3, 2, 3  # ghost rows above / below, columns left / right
+
+
+def test_tile_grid():
+    assert [tile_grid(n) for n in (1, 2, 4, 8, 6, 3)] == [(1, 1), (1, 2), (2, 2), (2, 4), (2, 3), (1, 3)]
+
+
+def padded_tile(G, tiles, rank):
+    """Tile `rank` of global array G with an unfilled (NaN) ghost frame."""
+    Nt, Nx = G.shape
+    ty, tx = tiles
+    Ht, Wt = Nt // ty, Nx // tx
+    iy, ix = divmod(rank, tx)
+    P = np.full((Ht + GT + GB, Wt + GL + GR), np.nan)
+    P[GT:GT + Ht, GL:GL + Wt] = G[iy * Ht:(iy + 1) * Ht, ix * Wt:(ix + 1) * Wt]
+    return P
+
+
+def expected_frame(G, tiles, rank):
+    Nt, Nx = G.shape
+    ty, tx = tiles
+    Ht, Wt = Nt // ty, Nx // tx
+    iy, ix = divmod(rank, tx)
+    rows = (np.arange(-GT, Ht + GB) + iy * Ht) % Nt
+    cols = (np.arange(-GL, Wt + GR) + ix * Wt) % Nx
+    return G[np.ix_(rows, cols)]
+
+
+def message(P, m):
+    (r0, c0), (h, w) = m['src'], m['shape']
+    return P[GT + r0:GT + r0 + h, GL + c0:GL + c0 + w].copy()
+
+
+def place(P, m, block):
+    (r0, c0), (h, w) = m['dst'], m['shape']
+    P[GT + r0:GT + r0 + h, GL + c0:GL + c0 + w] = block
+
+
+GRIDS = [(1, 1), (1, 2), (2, 1), (2, 2), (2, 4), (3, 2), (1, 8), (4, 4)]
+
+
+@pytest.mark.parametrize('tiles', GRIDS)
+def test_plan_fills_every_ghost(tiles):
+    ty, tx = tiles
+    Nt, Nx = 8 * ty, 6 * tx
+    G = np.random.default_rng(0).normal(size=(Nt, Nx))
+    ntiles = ty * tx
+    plans = [exchange_plan(Nt, Nx, tiles, r) for r in range(ntiles)]
+    P = [padded_tile(G, tiles, r) for r in range(ntiles)]
+    sent = {}
+    for r in range(ntiles):
+        for s, m in enumerate(plans[r]):
+            sent[(r, m['send_to'], s)] = message(P[r], m)
+    for r in range(ntiles):
+        for s, m in enumerate(plans[r]):
+            place(P[r], m, sent[(m['recv_from'], r, s)])
+    for r in range(ntiles):
+        np.testing.assert_array_equal(P[r], expected_frame(G, tiles, r))
+
+
+@pytest.mark.parametrize('tiles', GRIDS)
+def test_plan_pairwise_order_matches(tiles):
+    """ncclSend/ncclRecv between one pair of ranks match in call order: rank a's sends to b (in send
+    order) must be b's receives from a (in receive order), message by message."""
+    ty, tx = tiles
+    Nt, Nx = 8 * ty, 6 * tx
+    ntiles = ty * tx
+    plans = [exchange_plan(Nt, Nx, tiles, r) for r in range(ntiles)]
+    for a in range(ntiles):
+        for b in range(ntiles):
+            if a == b:
+                continue
+            sends = [s for s, m in enumerate(plans[a]) if m['send_to'] == b]
+            recvs = [s for s, m in enumerate(plans[b]) if m['recv_from'] == a]
+            assert sends == recvs
+            for s in sends:
+                assert plans[a][s]['shape'] == plans[b][s]['shape']
+
+
+def test_plan_rejects_bad_decompositions():
+    with pytest.raises(ValueError):
+        exchange_plan(10, 12, (4, 1), 0)   # does not divide
+    with pytest.raises(ValueError):
+        exchange_plan(6, 12, (2, 2), 0)    # odd tile extent
+    with pytest.raises(ValueError):
+        exchange_plan(4, 4, (2, 2), 0)     # 2 x 2 tiles are too small
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _exchange_worker(rank, world, port, tiles, Nt, Nx, errfile):
+    import torch
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        G = np.random.default_rng(1).normal(size=(Nt, Nx))
+        plan = exchange_plan(Nt, Nx, tiles, rank)
+        P = padded_tile(G, tiles, rank)
+        ops, recv = [], {}
+        # the C++ RCCL loop: sends in direction order, then receives in direction order (self: local)
+        for s, m in enumerate(plan):
+            if m['send_to'] != rank:
+                ops.append(dist.P2POp(dist.isend, torch.from_numpy(message(P, m)), m['send_to']))
+        for s, m in enumerate(plan):
+            if m['recv_from'] != rank:
+                recv[s] = torch.empty(m['shape'], dtype=torch.float64)
+                ops.append(dist.P2POp(dist.irecv, recv[s], m['recv_from']))
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        for s, m in enumerate(plan):
+            block = recv[s].numpy() if s in recv else message(P, plan[s])
+            place(P, m, block)
+        np.testing.assert_array_equal(P, expected_frame(G, tiles, rank))
+    except Exception as e:  # report to the parent
+        with open(errfile, 'a') as f:
+            f.write(f'rank {rank}: {e!r}\n')
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('tiles', [(1, 2), (2, 1)])
+def test_two_rank_gloo_exchange(tiles, tmp_path):
+    import torch.multiprocessing as mp
+    errfile = str(tmp_path / 'err.txt')
+    Nt, Nx = 8 * tiles[0], 6 * tiles[1]
+    mp.start_processes(_exchange_worker, args=(2, _free_port(), tiles, Nt, Nx, errfile), nprocs=2, join=True,
+                       start_method='spawn')
+    assert not os.path.exists(errfile), open(errfile).read()
