@@ -139,6 +139,23 @@ int sv_domain_run(sv_domain *d, double kappa, int64_t W, double interval_phi, in
  * (tile-local coordinates; ghosts are negative or >= the tile extent). */
 int sv_domain_exchange_plan(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t rank, int64_t *out);
 
+
+/* ---- Villain replica batches (BASELINE config 5; SURVEY.md 8e: replicas need no collectives) ------- */
+/* R independent NeighborhoodUpdate chains of one even N >= 4 advanced together (one launch per sweep
+ * for all replicas); replica r follows rngs[r] exactly as a single sv_villain_run with that state
+ * would.  Arrays are (R, N, N) phi and (R, 2, N, N) n; phi == NULL uploads a cold start.  stats has
+ * R * sweeps entries ([r][sweep]); obs (optional, R * sweeps * 4 doubles) receives per sweep the
+ * sums over the new configuration of (d phi - 2 pi n)^2 (the Villain action is kappa/2 times it,
+ * villain.py:51-66), (dn)^2 (winding.py:30-37) and n_0, n_1 (wrapping.py:17-25), computed by the
+ * sweep kernel itself (observable/observable.py:50-54 "inline" measurement). */
+typedef struct sv_replicas sv_replicas;
+int sv_replicas_create(sv_ctx *ctx, int32_t R, int32_t N, sv_replicas **out);
+int sv_replicas_destroy(sv_replicas *b);
+int sv_replicas_upload(sv_replicas *b, const double *phi, const int64_t *n);
+int sv_replicas_download(sv_replicas *b, double *phi, int64_t *n);
+int sv_replicas_run(sv_replicas *b, double kappa, int64_t W, double interval_phi, int64_t interval_n, int32_t sweeps,
+                    sv_rng *rngs, sv_stats *stats, double *obs);
+
 #ifdef __cplusplus
 }
 #endif

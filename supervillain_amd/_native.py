@@ -64,6 +64,11 @@ def lib():
         L.sv_domain_download.argtypes = [vp, vp, vp]
         L.sv_domain_run.argtypes = [vp, f64, i64, f64, i64, i32, P(SvRng), P(SvStats)]
         L.sv_domain_exchange_plan.argtypes = [i32, i32, i32, i32, i32, vp]
+        L.sv_replicas_create.argtypes = [vp, i32, i32, P(vp)]
+        L.sv_replicas_destroy.argtypes = [vp]
+        L.sv_replicas_upload.argtypes = [vp, vp, vp]
+        L.sv_replicas_download.argtypes = [vp, vp, vp]
+        L.sv_replicas_run.argtypes = [vp, f64, i64, f64, i64, i32, vp, vp, vp]
         _LIB = L
         return L
 
@@ -76,7 +81,9 @@ EXPORTED = ('sv_ctx_create', 'sv_ctx_destroy', 'sv_last_error', 'sv_device_count
             'sv_worldline_coexact', 'sv_worldline_plaquette_ordered_run',
             'sv_worldline_plaquette_checkerboard_run', 'sv_worldline_plaquette',
             'sv_domain_unique_id', 'sv_domain_create', 'sv_domain_destroy', 'sv_domain_upload', 'sv_domain_download',
-            'sv_domain_run', 'sv_domain_exchange_plan')
+            'sv_domain_run', 'sv_domain_exchange_plan',
+            'sv_replicas_create', 'sv_replicas_destroy', 'sv_replicas_upload', 'sv_replicas_download',
+            'sv_replicas_run')
 
 
 def default_device():

@@ -320,6 +320,7 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
                 A.stat = &Tl.sum->stats[k];
                 A.S = DevScratch{&Tl.sum->abort, &Tl.sum->nreport, Tl.sum->reports};
                 A.sweep = (uint32_t)k;
+                farg_single(A, nsx, nsy);
                 hipEvent_t ev;
                 ctx->time_begin(&ev);
                 launch_fused_tile(A, nsx * nsy, ctx->stream);

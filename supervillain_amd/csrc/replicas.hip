@@ -1,0 +1,424 @@
+// replicas.hip -- a batch of independent Villain NeighborhoodUpdate chains (BASELINE config 5:
+// 1024 replicas of L=128 at W=2 with inline observables; SURVEY.md 8e "replicas shard trivially").
+//
+// R replicas of one even N share every launch: one fused sweep kernel per sweep covers all of them
+// (workgroup runs of tiles_per_rep serve one replica), each replica replaying its own NumPy PCG64
+// stream.  Small lattices cannot fill 256 CUs on their own; batched they do.
+//
+// Planning.  Without rejections a sweep consumes exactly 4V u64 of a replica's stream (V metropolis,
+// then per colour V/2 dphi and 4 x V/4 words of choices -- the buffered half-word parity `has` never
+// changes because every choice block has an even number of draws), so every block descriptor is a
+// closed-form jump from the replica's batch-start state: a device kernel writes all R x sweeps x 11
+// descriptors at once.  A replica that met a NumPy Lemire rejection is planned on the host for the
+// batches it affects (the shared skip machinery of villain.hip), and the batch is replayed from the
+// failing sweep exactly like the single-lattice driver.
+//
+// Inline observables (ActionDensity, InternalEnergyDensity, WindingSquared, TorusWrapping) are summed
+// by the sweep kernel while it writes the finished rows (0 extra HBM bytes).
+#include <algorithm>
+#include <cstring>
+
+#include "villain.h"
+
+namespace sv {
+
+struct PlanIn {
+    uint64_t s_lo, s_hi;  // cursor: state before the batch's first draw
+    uint32_t has, buf;
+};
+
+static constexpr int REP_BATCH = 64;
+static constexpr int NB = 11;  // blocks per sweep (even N: 2 colours)
+
+// u64 offset of block b inside a sweep (h = V/4 words per choice block)
+__device__ __forceinline__ uint64_t block_off(int b, uint64_t V) {
+    const uint64_t nc = V / 2, h = V / 4;
+    if (b == 0) return 0;
+    if (b == 1) return V;
+    if (b <= 5) return V + nc + (uint64_t)(b - 2) * h;
+    if (b == 6) return V + 3 * nc;
+    return V + 4 * nc + (uint64_t)(b - 7) * h;
+}
+
+__global__ void plan_replicas(const PlanIn *in, const JumpTables *const *Trep, Block *out, int R, int count,
+                              uint64_t V) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= (int64_t)R * count * NB) return;
+    const int b = (int)(i % NB);
+    const int k = (int)((i / NB) % count);
+    const int r = (int)(i / ((int64_t)NB * count));
+    const PlanIn P = in[r];
+    const JumpTables *T = Trep[r];
+    const u128 s0{P.s_lo, P.s_hi};
+    const uint64_t per = 4 * V;
+    const u128 base = jump(T, s0, (uint32_t)(k * per + block_off(b, V) + 1));
+    Block B;
+    B.base_lo = base.lo;
+    B.base_hi = base.hi;
+    B.nskip = 0;
+    B.skip0 = 0;
+    const bool bounded = b != 0 && b != 1 && b != 6;
+    if (!bounded) {
+        B.has = 0;
+        B.buf = 0;
+    } else {
+        B.has = P.has;
+        if (k == 0 && b == 2) {
+            B.buf = P.buf;
+        } else {
+            // high half of the last u64 of the previous choice block
+            const int kp = b == 2 ? k - 1 : k;
+            const int pb = b == 2 ? 10 : (b == 7 ? 5 : b - 1);
+            const uint64_t last = kp * per + block_off(pb, V) + V / 4;  // steps to the state of that u64
+            B.buf = (uint32_t)(xsl_rr(jump(T, s0, (uint32_t)last)) >> 32);
+        }
+    }
+    out[i] = B;
+}
+
+}  // namespace sv
+
+using namespace svh;
+
+struct sv_replicas {
+    sv_ctx *ctx = nullptr;
+    int32_t R = 0, N = 0;
+    int64_t V = 0;
+    double *phi[2] = {nullptr, nullptr};
+    int64_t *n[2] = {nullptr, nullptr};
+    int cur = 0;
+    std::map<std::pair<uint64_t, uint64_t>, JumpTables *> tables;  // device, per increment
+    const JumpTables **d_Trep = nullptr;
+    Affine *d_adv = nullptr;
+    PlanIn *d_plan = nullptr;
+    Block *d_blocks = nullptr;
+    sv_stats *d_stats = nullptr;
+    double *d_obs = nullptr;
+    std::vector<std::pair<uint64_t, uint64_t>> incs;  // current per-replica increments
+};
+
+namespace {
+
+const JumpTables *replica_tables(sv_replicas *b, u128 inc) {
+    auto key = std::make_pair(inc.hi, inc.lo);
+    auto it = b->tables.find(key);
+    if (it != b->tables.end()) return it->second;
+    JumpTables *h = new JumpTables(make_tables(inc));
+    JumpTables *d = nullptr;
+    SV_HIP(hipMalloc(&d, sizeof(JumpTables)));
+    SV_HIP(hipMemcpy(d, h, sizeof(JumpTables), hipMemcpyHostToDevice));
+    delete h;
+    b->tables[key] = d;
+    return d;
+}
+
+// (re)bind per-replica tables and row-advance maps when the increments change
+void bind_increments(sv_replicas *b, const sv_rng *rngs) {
+    std::vector<std::pair<uint64_t, uint64_t>> incs(b->R);
+    for (int r = 0; r < b->R; r++) incs[r] = {rngs[r].inc_hi, rngs[r].inc_lo};
+    if (incs == b->incs) return;
+    std::vector<const JumpTables *> T(b->R);
+    std::vector<Affine> adv(3 * (size_t)b->R);
+    constexpr int NWv = 4;
+    for (int r = 0; r < b->R; r++) {
+        const u128 inc{incs[r].second, incs[r].first};
+        T[r] = replica_tables(b, inc);
+        adv[3 * r + 0] = host_power(inc, (uint64_t)NWv * b->N);
+        adv[3 * r + 1] = host_power(inc, (uint64_t)NWv * b->N / 2);
+        adv[3 * r + 2] = host_power(inc, (uint64_t)NWv * b->N / 4);
+    }
+    SV_HIP(hipMemcpy(b->d_Trep, T.data(), b->R * sizeof(JumpTables *), hipMemcpyHostToDevice));
+    SV_HIP(hipMemcpy(b->d_adv, adv.data(), adv.size() * sizeof(Affine), hipMemcpyHostToDevice));
+    b->incs = incs;
+}
+
+bool has_skips(const SkipMap &m, int first, int count) {
+    auto it = m.lower_bound({first, -1});
+    return it != m.end() && it->first.first < first + count;
+}
+
+// advance a no-skip replica's cursor by `sweeps` sweeps (closed form, see the file header)
+void advance_closed(Cursor &c, u128 inc, uint64_t V, int sweeps) {
+    if (sweeps <= 0) return;
+    c.s = host_jump(c.s, inc, (uint64_t)sweeps * 4 * V);
+    c.buf = (uint32_t)(xsl_rr(c.s) >> 32);
+}
+
+void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs, sv_stats *stats, double *obs) {
+    sv_ctx *ctx = b->ctx;
+    const int R = b->R;
+    const int64_t V = b->V;
+    const int64_t counts[2] = {V / 2, V / 2};
+    const auto specs = villain_specs(V, 2, counts, P.k > 1);
+    if ((int)specs.size() != NB) throw std::logic_error("unexpected block count");
+    bind_increments(b, rngs);
+    std::vector<Cursor> cur(R);
+    std::vector<u128> inc(R);
+    for (int r = 0; r < R; r++) {
+        cur[r] = Cursor{u128{rngs[r].state_lo, rngs[r].state_hi}, (uint32_t)rngs[r].has_uint32, rngs[r].uinteger};
+        inc[r] = u128{rngs[r].inc_lo, rngs[r].inc_hi};
+    }
+    std::vector<SkipMap> skips(R);
+    const int TH = fused_th();
+    const int nsx = (b->N + FW_MAX - 1) / FW_MAX;
+    const int nsy = (b->N + TH - 1) / TH;
+    const int tiles = nsx * nsy;
+    std::vector<PlanIn> pin(R);
+    std::vector<std::vector<Block>> hb;  // host-planned descriptors, alive until the batch's stream sync
+    std::vector<uint32_t> hskip, sk;
+    std::vector<sv_stats> hst;
+    std::vector<double> hobs;
+    int sw = 0;
+    while (sw < sweeps) {
+        const int count = std::min(REP_BATCH, sweeps - sw);
+        // --- plan: device closed form for every replica, host planner for replicas with skips
+        for (int r = 0; r < R; r++) pin[r] = PlanIn{cur[r].s.lo, cur[r].s.hi, cur[r].has, cur[r].buf};
+        SV_HIP(hipMemcpyAsync(b->d_plan, pin.data(), R * sizeof(PlanIn), hipMemcpyHostToDevice, ctx->stream));
+        const int64_t nplan = (int64_t)R * count * NB;
+        plan_replicas<<<(unsigned)((nplan + 255) / 256), 256, 0, ctx->stream>>>(b->d_plan, b->d_Trep, b->d_blocks, R,
+                                                                                  count, (uint64_t)V);
+        hskip.clear();
+        hb.clear();
+        std::vector<Cursor> end_host(R);
+        std::vector<char> hosted(R, 0);
+        for (int r = 0; r < R; r++) {
+            if (!has_skips(skips[r], sw, count)) continue;
+            hosted[r] = 1;
+            Cursor c = cur[r];
+            hb.emplace_back();
+            std::vector<Block> &blk = hb.back();
+            plan_sweeps(ctx, c, inc[r], specs, sw, count, skips[r], blk, sk);
+            for (Block &x : blk) x.skip0 += (int32_t)hskip.size();
+            hskip.insert(hskip.end(), sk.begin(), sk.end());
+            end_host[r] = c;
+            SV_HIP(hipMemcpyAsync(b->d_blocks + (size_t)r * count * NB, blk.data(), blk.size() * sizeof(Block),
+                                  hipMemcpyHostToDevice, ctx->stream));
+        }
+        ctx->ensure_skips(hskip.size() + 1);
+        if (!hskip.empty())
+            SV_HIP(hipMemcpyAsync(ctx->d_skips, hskip.data(), hskip.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                  ctx->stream));
+        SV_HIP(hipMemsetAsync(ctx->d_abort, 0, sizeof(int32_t), ctx->stream));
+        SV_HIP(hipMemsetAsync(ctx->d_nreport, 0, sizeof(uint32_t), ctx->stream));
+        SV_HIP(hipMemsetAsync(b->d_stats, 0, (size_t)R * count * sizeof(sv_stats), ctx->stream));
+        if (obs) SV_HIP(hipMemsetAsync(b->d_obs, 0, (size_t)R * count * 4 * sizeof(double), ctx->stream));
+        // --- sweeps
+        const int cur0 = b->cur;
+        hipEvent_t ev;
+        ctx->time_begin(&ev);
+        for (int k = 0; k < count; k++) {
+            FArgs A;
+            A.P = P;
+            A.G = FGeom{b->N, b->N, 0, 0, b->N, b->N, b->N, V, 0};
+            A.phi_in = b->phi[b->cur];
+            A.n_in = b->n[b->cur];
+            A.phi_out = b->phi[b->cur ^ 1];
+            A.n_out = b->n[b->cur ^ 1];
+            A.nsx = nsx;
+            A.TH = TH;
+            A.nsy = nsy;
+            A.blocks = b->d_blocks + (size_t)k * NB;
+            A.skips = ctx->d_skips;
+            A.T = nullptr;
+            A.stat = b->d_stats + k;
+            A.S = DevScratch{ctx->d_abort, ctx->d_nreport, ctx->d_reports};
+            A.sweep = (uint32_t)k;
+            A.tiles_per_rep = tiles;
+            A.rep_blocks = count * NB;
+            A.rep_field = V;
+            A.rep_stat = count;
+            A.rep_obs = 4 * count;
+            A.Trep = b->d_Trep;
+            A.advrep = b->d_adv;
+            A.obs = obs ? b->d_obs + 4 * k : nullptr;
+            launch_fused_batch(A, R * tiles, obs != nullptr, ctx->stream);
+            b->cur ^= 1;
+        }
+        ctx->time_end(ev, count);
+        SV_HIP(hipGetLastError());
+        // --- outcome
+        int32_t ab = 0;
+        uint32_t nrep = 0;
+        SV_HIP(hipMemcpyAsync(&ab, ctx->d_abort, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipMemcpyAsync(&nrep, ctx->d_nreport, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+        int good = count;
+        if (ab) {
+            ctx->time_discard();
+            nrep = std::min<uint32_t>(nrep, MAX_REPORTS);
+            std::vector<Report> reps(nrep);
+            if (nrep)
+                SV_HIP(hipMemcpy(reps.data(), ctx->d_reports, nrep * sizeof(Report), hipMemcpyDeviceToHost));
+            if (reps.empty()) throw std::runtime_error("device aborted without a rejection report");
+            uint32_t bad = ~0u;
+            for (const Report &x : reps) {
+                if (x.block == OVERFLOW_BLOCK) throw std::runtime_error("|n| exceeds the fused path's int32 LDS image");
+                bad = std::min(bad, x.sweep);
+            }
+            // each replica that failed in sweep `bad`: absorb its earliest block's rejected positions
+            for (int r = 0; r < R; r++) {
+                AbortInfo a{1, {}};
+                for (const Report &x : reps)
+                    if ((int)x.pad == r && x.sweep == bad) a.reports.push_back(x);
+                if (!a.reports.empty()) absorb_reports(a, sw, skips[r]);
+            }
+            good = (int)bad;
+        }
+        ctx->time_collect();
+        // --- keep sweeps [sw, sw + good): stats, observables, cursors
+        if (good > 0) {
+            hst.resize((size_t)R * count);
+            SV_HIP(hipMemcpy(hst.data(), b->d_stats, hst.size() * sizeof(sv_stats), hipMemcpyDeviceToHost));
+            if (obs) {
+                hobs.resize((size_t)R * count * 4);
+                SV_HIP(hipMemcpy(hobs.data(), b->d_obs, hobs.size() * sizeof(double), hipMemcpyDeviceToHost));
+            }
+            for (int r = 0; r < R; r++)
+                for (int k = 0; k < good; k++) {
+                    sv_stats s = hst[(size_t)r * count + k];
+                    s.proposed = V;
+                    s.rejections = rejections_in(skips[r], sw + k, NB);
+                    stats[(size_t)r * sweeps + sw + k] = s;
+                    if (obs)
+                        std::memcpy(obs + ((size_t)r * sweeps + sw + k) * 4, &hobs[((size_t)r * count + k) * 4],
+                                    4 * sizeof(double));
+                }
+        }
+        for (int r = 0; r < R; r++) {
+            if (good == count && hosted[r]) {
+                cur[r] = end_host[r];
+            } else if (has_skips(skips[r], sw, good)) {
+                Cursor c = cur[r];
+                std::vector<Block> blk;
+                plan_sweeps(ctx, c, inc[r], specs, sw, good, skips[r], blk, sk);
+                cur[r] = c;
+            } else {
+                advance_closed(cur[r], inc[r], (uint64_t)V, good);
+            }
+        }
+        b->cur = cur0 ^ (good & 1);
+        sw += good;
+    }
+    for (int r = 0; r < R; r++) {
+        rngs[r].state_hi = cur[r].s.hi;
+        rngs[r].state_lo = cur[r].s.lo;
+        rngs[r].has_uint32 = (int32_t)cur[r].has;
+        rngs[r].uinteger = cur[r].buf;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int sv_replicas_create(sv_ctx *ctx, int32_t R, int32_t N, sv_replicas **out) {
+    if (!ctx || !out) return -1;
+    *out = nullptr;
+    sv_replicas *b = new sv_replicas();
+    try {
+        if (R < 1) throw std::invalid_argument("need at least one replica");
+        if (N < 4 || N % 2) throw std::invalid_argument("replica batches need an even N >= 4");
+        if ((int64_t)REP_BATCH * 4 * (int64_t)N * N >= (1LL << 32))
+            throw std::invalid_argument("N too large for replica batches (use sv_villain_* per lattice)");
+        SV_HIP(hipSetDevice(ctx->device));
+        b->ctx = ctx;
+        b->R = R;
+        b->N = N;
+        b->V = (int64_t)N * N;
+        const size_t V = (size_t)b->V;
+        for (int i = 0; i < 2; i++) {
+            SV_HIP(hipMalloc(&b->phi[i], R * V * sizeof(double)));
+            SV_HIP(hipMalloc(&b->n[i], 2 * R * V * sizeof(int64_t)));
+        }
+        SV_HIP(hipMalloc(&b->d_Trep, R * sizeof(JumpTables *)));
+        SV_HIP(hipMalloc(&b->d_adv, 3 * R * sizeof(Affine)));
+        SV_HIP(hipMalloc(&b->d_plan, R * sizeof(PlanIn)));
+        SV_HIP(hipMalloc(&b->d_blocks, (size_t)R * REP_BATCH * NB * sizeof(Block)));
+        SV_HIP(hipMalloc(&b->d_stats, (size_t)R * REP_BATCH * sizeof(sv_stats)));
+        SV_HIP(hipMalloc(&b->d_obs, (size_t)R * REP_BATCH * 4 * sizeof(double)));
+        *out = b;
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        sv_replicas_destroy(b);
+        return -2;
+    }
+}
+
+int sv_replicas_destroy(sv_replicas *b) {
+    if (!b) return 0;
+    if (b->ctx) {
+        (void)hipSetDevice(b->ctx->device);
+        (void)hipStreamSynchronize(b->ctx->stream);
+    }
+    for (int i = 0; i < 2; i++) {
+        (void)hipFree(b->phi[i]);
+        (void)hipFree(b->n[i]);
+    }
+    for (auto &kv : b->tables) (void)hipFree(kv.second);
+    (void)hipFree(b->d_Trep);
+    (void)hipFree(b->d_adv);
+    (void)hipFree(b->d_plan);
+    (void)hipFree(b->d_blocks);
+    (void)hipFree(b->d_stats);
+    (void)hipFree(b->d_obs);
+    delete b;
+    return 0;
+}
+
+int sv_replicas_upload(sv_replicas *b, const double *phi, const int64_t *n) {
+    if (!b) return -1;
+    sv_ctx *ctx = b->ctx;
+    try {
+        SV_HIP(hipSetDevice(ctx->device));
+        const size_t V = (size_t)b->V, R = (size_t)b->R;
+        if (!phi || !n) {
+            SV_HIP(hipMemsetAsync(b->phi[b->cur], 0, R * V * sizeof(double), ctx->stream));
+            SV_HIP(hipMemsetAsync(b->n[b->cur], 0, 2 * R * V * sizeof(int64_t), ctx->stream));
+        } else {
+            SV_HIP(hipMemcpyAsync(b->phi[b->cur], phi, R * V * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+            SV_HIP(hipMemcpyAsync(b->n[b->cur], n, 2 * R * V * sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
+        }
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_replicas_download(sv_replicas *b, double *phi, int64_t *n) {
+    if (!b || !phi || !n) return -1;
+    sv_ctx *ctx = b->ctx;
+    try {
+        SV_HIP(hipSetDevice(ctx->device));
+        const size_t V = (size_t)b->V, R = (size_t)b->R;
+        SV_HIP(hipMemcpyAsync(phi, b->phi[b->cur], R * V * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipMemcpyAsync(n, b->n[b->cur], 2 * R * V * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_replicas_run(sv_replicas *b, double kappa, int64_t W, double interval_phi, int64_t interval_n, int32_t sweeps,
+                    sv_rng *rngs, sv_stats *stats, double *obs) {
+    if (!b || !rngs || (sweeps > 0 && !stats)) return -1;
+    sv_ctx *ctx = b->ctx;
+    try {
+        if (sweeps < 0) throw std::invalid_argument("sweeps must be >= 0");
+        if (interval_n < 0 || interval_n > (1 << 20)) throw std::invalid_argument("interval_n out of range");
+        if ((W < 0 ? -W : W) * interval_n >= (1LL << 28)) throw std::invalid_argument("|W * interval_n| too large");
+        SV_HIP(hipSetDevice(ctx->device));
+        const VParams P = make_params(b->N, kappa, W, interval_phi, interval_n);
+        run_replicas(b, P, sweeps, rngs, stats, obs);
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
+}  // extern "C"

@@ -48,6 +48,15 @@ struct FArgs {
     sv_stats *stat;
     DevScratch S;
     uint32_t sweep;
+    // replica batch (periodic mode): consecutive runs of tiles_per_rep workgroups serve one replica
+    int32_t tiles_per_rep;          // nsx * nsy
+    int32_t rep_blocks;             // descriptors per replica (0: shared)
+    int64_t rep_field;              // phi elements per replica (n: twice that)
+    int32_t rep_stat;               // stats entries per replica
+    int32_t rep_obs;                // obs entries per replica
+    const JumpTables *const *Trep;  // per-replica tables, or nullptr (all use T)
+    const Affine *advrep;           // per-replica adv[3], or nullptr (all use adv)
+    double *obs;                    // OBS kernels: per replica {sum (d phi - 2 pi n)^2, sum (dn)^2, sum n0, sum n1}
 };
 
 }  // namespace sv
@@ -75,5 +84,9 @@ int64_t rejections_in(const SkipMap &skips, int sweep, int nblocks);
 int fused_th();
 // launch villain_sweep_fused<4, true> (tile mode) with `grid` workgroups
 void launch_fused_tile(const FArgs &A, int grid, hipStream_t stream);
+// launch villain_sweep_fused<4, false, obs> over a replica batch (grid = replicas * tiles_per_rep)
+void launch_fused_batch(const FArgs &A, int grid, bool obs, hipStream_t stream);
+// plain single-lattice FArgs defaults (one replica, no observables)
+void farg_single(FArgs &A, int nsx, int nsy);
 
 }  // namespace svh

@@ -36,9 +36,10 @@ namespace sv {
 //   [3+5c] bwd mu=0, [4+5c] fwd mu=1, [5+5c] bwd mu=1 (bounded choice).
 __device__ __forceinline__ u128 block_base(const Block &b) { return u128{b.base_lo, b.base_hi}; }
 
-__device__ __forceinline__ void report(const DevScratch &S, uint32_t sweep, uint32_t block, uint32_t pos) {
+__device__ __forceinline__ void report(const DevScratch &S, uint32_t sweep, uint32_t block, uint32_t pos,
+                                       uint32_t rep = 0) {
     uint32_t i = atomicAdd(S.nreport, 1u);
-    if (i < (uint32_t)MAX_REPORTS) S.reports[i] = Report{sweep, block, pos, 0};
+    if (i < (uint32_t)MAX_REPORTS) S.reports[i] = Report{sweep, block, pos, rep};
     __hip_atomic_store(S.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -193,7 +194,7 @@ __device__ __forceinline__ int32_t wrapN(int32_t v, int32_t N) {
 }
 
 #ifndef SV_ABLATE
-#define SV_ABLATE 0  // timing experiments only: 1 = no exp, 2 = no RNG compositions, 3 = both
+#define SV_ABLATE 0  // timing experiments only: 1 = no exp, 2 = no RNG compositions, 4 = no wrapped-column jumps
 #endif
 __device__ __forceinline__ double sv_exp(double x) {
 #if SV_ABLATE & 1
@@ -250,21 +251,36 @@ __device__ __forceinline__ u128 from_base(const JumpTables *T, const Block *blk,
     const int64_t off = pos - bpos;
     u128 st;
     if (off >= 0 && off < SMALL_LDS) st = apply(sm[off], base);
+#if SV_ABLATE & 4
+    else st = apply(sm[off & (SMALL_LDS - 1)], base);  // timing experiment: no full jumps at wrapped columns
+#else
     else st = full_jump(T, blk, (uint32_t)pos);
+#endif
     return st;
 }
 
-__device__ __forceinline__ int32_t choice_value(const FArgs &A, uint32_t word, uint32_t bidx, uint32_t spos) {
+// What one workgroup's replica reads: its sweep descriptors and its PCG64 jump tables.
+struct Rep {
+    const Block *blocks;
+    const JumpTables *T;
+    uint32_t id;
+};
+
+__device__ __forceinline__ int32_t choice_value(const FArgs &A, const Rep &RP, uint32_t word, uint32_t bidx,
+                                                uint32_t spos) {
     bool rej;
     const uint32_t idx = lemire(word, A.P.k, A.P.thr, &rej);
-    if (rej) report(A.S, A.sweep, bidx, spos);
+    if (rej) report(A.S, A.sweep, bidx, spos, RP.id);
     return (int32_t)A.P.W * ((int32_t)idx - (int32_t)A.P.interval_n);
 }
 
 // General draws: any strip (wrapped columns), skips, mismatched buffers.  6 compositions per site.
-__device__ __forceinline__ Draws draws_general(const FArgs &A, int c, bool active, int64_t gq, int64_t gx, int64_t xb,
-                                               const u128 *bases, const Affine *sm) {
-    const JumpTables *T = A.T;
+// Columns of an edge strip that wrap around the lattice (global columns outside [xb, xb + RW)) draw
+// from the wave's second set of row bases `wb`, kept at global column xw, so no lane needs a full jump.
+__device__ __forceinline__ Draws draws_general(const FArgs &A, const Rep &RP, int c, bool active, int64_t gq, int64_t gx,
+                                               int64_t xb, const u128 *bases, const Affine *sm, bool edge,
+                                               int64_t xw, const u128 *wb) {
+    const JumpTables *T = RP.T;
     const int64_t N = A.G.Nx;  // row length of the global stream layout
     const int bb = 1 + 5 * c;
     const int64_t lin = gq * N + gx, rank = lin >> 1;
@@ -273,17 +289,20 @@ __device__ __forceinline__ Draws draws_general(const FArgs &A, int c, bool activ
     D.dphi = 0.0;
     D.cn[0] = D.cn[1] = D.cn[2] = D.cn[3] = 0;
     if (!active) return D;
-    D.u = 0.0 + 1.0 * to_double(xsl_rr(from_base(T, &A.blocks[0], sm, bases[0], gq * N + xb, lin)));
-    D.dphi = A.P.lo_phi + A.P.range_phi * to_double(xsl_rr(from_base(T, &A.blocks[bb], sm, bases[1], (gq * N + xb) >> 1, rank)));
+    const bool wr = edge && (gx < xb || gx >= xb + RW);
+    const int64_t xr = wr ? xw : xb;
+    D.u = 0.0 + 1.0 * to_double(xsl_rr(from_base(T, &RP.blocks[0], sm, wr ? wb[0] : bases[0], gq * N + xr, lin)));
+    D.dphi = A.P.lo_phi + A.P.range_phi * to_double(xsl_rr(from_base(T, &RP.blocks[bb], sm, wr ? wb[1] : bases[1],
+                                                                     (gq * N + xr) >> 1, rank)));
     if (A.P.k > 1) {
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            const Block *B = &A.blocks[bb + 1 + q];
+            const Block *B = &RP.blocks[bb + 1 + q];
             uint32_t word, spos = (uint32_t)rank;
             if (B->nskip == 0) {
                 const int64_t qq = rank - (int64_t)B->has;
                 const int64_t wi = qq < 0 ? 0 : (qq >> 1);
-                const uint64_t X = xsl_rr(from_base(T, B, sm, bases[2 + q], base_pos(2, gq, N, xb, B->has), wi));
+                const uint64_t X = xsl_rr(from_base(T, B, sm, wr ? wb[2 + q] : bases[2 + q], base_pos(2, gq, N, xr, B->has), wi));
                 word = (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
                 if (qq < 0) word = B->buf;  // has && rank == 0: the buffered half-word
             } else {
@@ -291,7 +310,7 @@ __device__ __forceinline__ Draws draws_general(const FArgs &A, int c, bool activ
                 word = bounded_word(T, *B, spos);
                 __builtin_amdgcn_s_waitcnt(0);
             }
-            D.cn[q] = choice_value(A, word, (uint32_t)(bb + 1 + q), spos);
+            D.cn[q] = choice_value(A, RP, word, (uint32_t)(bb + 1 + q), spos);
         }
     }
     return D;
@@ -301,7 +320,7 @@ __device__ __forceinline__ Draws draws_general(const FArgs &A, int c, bool activ
 // forward/backward pair).  4 compositions per site: the fwd and bwd choice blocks of a direction
 // read the SAME u64 word for two adjacent lanes (its two 32-bit halves), so each lane of a pair
 // computes one block's word and swaps the other half with its partner.
-__device__ __forceinline__ Draws draws_fast(const FArgs &A, int c, bool active, int32_t lane, uint32_t rowlin,
+__device__ __forceinline__ Draws draws_fast(const FArgs &A, const Rep &RP, int c, bool active, int32_t lane, uint32_t rowlin,
                                             uint32_t xs, uint32_t gx, uint32_t xb, const u128 *bases,
                                             const Affine *sm) {
     const int bb = 1 + 5 * c;
@@ -321,7 +340,7 @@ __device__ __forceinline__ Draws draws_fast(const FArgs &A, int c, bool active, 
         const uint32_t R0 = (rowlin + xs) >> 1;  // rank of lane 0
 #pragma unroll
         for (int mu = 0; mu < 2; mu++) {
-            const Block &F = A.blocks[bb + 1 + 2 * mu];
+            const Block &F = RP.blocks[bb + 1 + 2 * mu];
             const uint32_t h = F.has;
             const uint32_t P = (R0 - h) & 1u;                        // pairing parity of this row
             const uint32_t PW = (PR - h) >> 1;                       // word index of the row base
@@ -338,16 +357,16 @@ __device__ __forceinline__ Draws draws_fast(const FArgs &A, int c, bool active, 
             const uint32_t wf = half ? got : (uint32_t)X;
             const uint32_t wb = half ? (uint32_t)(X >> 32) : got;
             if (active) {
-                D.cn[2 * mu] = choice_value(A, wf, (uint32_t)(bb + 1 + 2 * mu), rank);
-                D.cn[2 * mu + 1] = choice_value(A, wb, (uint32_t)(bb + 2 + 2 * mu), rank);
+                D.cn[2 * mu] = choice_value(A, RP, wf, (uint32_t)(bb + 1 + 2 * mu), rank);
+                D.cn[2 * mu + 1] = choice_value(A, RP, wb, (uint32_t)(bb + 2 + 2 * mu), rank);
             }
         }
     }
     return D;
 }
 
-template <int NW, bool TILE>
-__global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
+template <int NW, bool TILE, bool REPS, bool OBS>
+__device__ __forceinline__ void sweep_body(const FArgs &A) {
     constexpr int R = FusedGeom<NW>::R;
     constexpr int nthreads = NW * 64;
     constexpr int PF = (NW * RW + nthreads - 1) / nthreads;  // prefetched elements per thread
@@ -358,8 +377,9 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
     __shared__ int32_t s_n1[R][RW];
     __shared__ Affine s_small[SMALL_LDS];
     __shared__ Affine s_adv[3];
-    __shared__ u128 s_base[NW][16];  // per wave: [8c + ty] = block ty's base for the colour-c row
+    __shared__ u128 s_base[NW][32];  // per wave: [8c + ty] = block ty's base for the colour-c row; [16 + ..] at xw
     __shared__ int32_t s_bad;
+    __shared__ double s_obs[4];  // OBS: workgroup sums of the inline observables
 
     if (*(volatile const int32_t *)A.S.abort) return;
 
@@ -374,13 +394,21 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
     const int32_t par0 = (Gm.T0 + Gm.X0) & 1;  // colour parity offset of local coordinates
 
     // XCD-aware tile order: blocks b, b+8, ... share an XCD; give each XCD a contiguous run of tiles
-    const int G = A.nsx * A.nsy;
+    const int G = gridDim.x;
     int b = blockIdx.x;
     {
         const int per = G / 8, rem = G % 8;
         const int xcd = b & 7, k = b >> 3;
         b = xcd * per + (xcd < rem ? xcd : rem) + k;
     }
+    // replica of this workgroup (replica batches; 0 otherwise)
+    const int rep = REPS ? __builtin_amdgcn_readfirstlane(b / A.tiles_per_rep) : 0;  // uniform: keep it scalar
+    if (REPS) b = __builtin_amdgcn_readfirstlane(b - rep * A.tiles_per_rep);
+    const Rep RP{REPS ? A.blocks + (int64_t)rep * A.rep_blocks : A.blocks, REPS ? A.Trep[rep] : A.T, (uint32_t)rep};
+    const double *phi_in = REPS ? A.phi_in + rep * A.rep_field : A.phi_in;
+    const int64_t *n_in = REPS ? A.n_in + 2 * rep * A.rep_field : A.n_in;
+    double *phi_out = REPS ? A.phi_out + rep * A.rep_field : A.phi_out;
+    int64_t *n_out = REPS ? A.n_out + 2 * rep * A.rep_field : A.n_out;
     const int ix = b % A.nsx, iy = b / A.nsx;
     const int32_t x0 = (int32_t)((int64_t)ix * Gm.Wt / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * Gm.Wt / A.nsx);
     const int32_t w = x1 - x0;
@@ -389,18 +417,24 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
     const int32_t rbase = t0 - 2;  // local row 0
     const int32_t cols = w + 5;
     const int32_t gx0 = Gm.X0 + x0;                  // global column of the strip's first site
-    const int32_t xb = gx0 - 2 < 0 ? 0 : gx0 - 2;    // row bases at the first non-wrapped region column (global)
     const bool interior = gx0 >= 4 && gx0 + w + 2 < Nx;
+    // row bases at the first non-wrapped region column (global); on rows of <= 128 sites at the row
+    // start, so that every column -- wrapped halo columns included -- is a small-table offset away
+    const int32_t xb = ((Nx <= SMALL_LDS && !interior) || gx0 - 2 < 0) ? 0 : gx0 - 2;
+    // edge strips of longer rows: a second set of row bases at the first wrapped global column xw
+    const bool edge = !(Nx <= SMALL_LDS && !interior) && (gx0 - 2 < 0 || gx0 + w + 2 >= Nx);
+    const int32_t xw = gx0 - 2 < 0 ? Nx - 2 : 0;
 
-    for (int e = threadIdx.x; e < SMALL_LDS; e += nthreads) s_small[e] = A.T->small[e];
-    if (threadIdx.x < 3) s_adv[threadIdx.x] = A.adv[threadIdx.x];
+    for (int e = threadIdx.x; e < SMALL_LDS; e += nthreads) s_small[e] = RP.T->small[e];
+    if (threadIdx.x < 3) s_adv[threadIdx.x] = REPS ? A.advrep[3 * rep + threadIdx.x] : A.adv[threadIdx.x];
     if (threadIdx.x == 0) s_bad = 0;
+    if (OBS && threadIdx.x < 4) s_obs[threadIdx.x] = 0.0;
 
     // fast draws need, per colour, no skips and equal buffers within each fwd/bwd pair
     bool fast[2];
 #pragma unroll
     for (int c = 0; c < 2; c++) {
-        const Block *B = &A.blocks[2 + 5 * c];
+        const Block *B = &RP.blocks[2 + 5 * c];
         fast[c] = interior && B[0].nskip == 0 && B[1].nskip == 0 && B[2].nskip == 0 && B[3].nskip == 0 &&
                   B[0].has == B[1].has && B[2].has == B[3].has;
     }
@@ -422,9 +456,9 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
             const int32_t q = ra + pf_rr[k];
             if (pf_rr[k] < NW && q >= t0 - 2 && q <= t1 + 2) {
                 const int64_t g = mrow(q) + pf_gx[k];
-                pf_phi[k] = A.phi_in[g];
-                pf_n0[k] = A.n_in[g];
-                pf_n1[k] = A.n_in[V + g];
+                pf_phi[k] = phi_in[g];
+                pf_n0[k] = n_in[g];
+                pf_n1[k] = n_in[V + g];
             }
         }
     };
@@ -444,14 +478,16 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
     };
 
     // ---- per-wave running row bases: lane 8c+ty holds block ty's base for this wave's colour-c row
-    const bool base_lane = (lane & 7) < 6 && lane < 16;
-    const int bc = lane >> 3, bty = lane & 7;
+    // (at column xb); lanes 16 + 8c + ty the same at column xw (edge strips only)
+    const bool base_lane = (lane & 7) < 6 && (lane < 16 || (edge && lane < 32));
+    const int bc = (lane >> 3) & 1, bty = lane & 7;
+    const int32_t bx = lane >= 16 ? xw : xb;
     const int bblk = bty == 0 ? 0 : 1 + 5 * bc + bty - 1;
-    const uint32_t bhas = (base_lane && bty >= 2) ? A.blocks[bblk].has : 0u;
+    const uint32_t bhas = (base_lane && bty >= 2) ? RP.blocks[bblk].has : 0u;
     const int32_t tfirst = t0 - 3;
     int32_t brow = tfirst + 2 - bc + wave;  // D0 row t+2+wave, D1 row t+1+wave
     u128 bases{0, 0};
-    if (base_lane) bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)base_pos(bty, grow(brow), Nx, xb, bhas));
+    if (base_lane) bases = full_jump(RP.T, &RP.blocks[bblk], (uint32_t)base_pos(bty, grow(brow), Nx, bx, bhas));
     __builtin_amdgcn_s_waitcnt(0);
     if (base_lane) s_base[wave][lane] = bases;
 
@@ -462,14 +498,40 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
     auto store_rows = [&](int32_t ra) {
         const int32_t r0 = ra < t0 ? t0 : ra, r1 = ra + NW < t1 ? ra + NW : t1;
         const int total = r1 > r0 ? (r1 - r0) * w : 0;
+        double o_act = 0.0, o_w2 = 0.0, o_n0 = 0.0, o_n1 = 0.0;  // OBS partials (integers exact in f64)
         for (int e = threadIdx.x; e < total; e += nthreads) {
             const int rr = e / w, cc = e - rr * w;
             const int32_t q = r0 + rr;
             const int slot = (q - rbase) % R, cx = cc + 2;
             const int64_t g = mrow(q) + x0 + cc;  // tile sites never wrap
-            A.phi_out[g] = s_phi[slot][cx];
-            A.n_out[g] = (int64_t)s_n0[slot][cx];
-            A.n_out[V + g] = (int64_t)s_n1[slot][cx];
+            phi_out[g] = s_phi[slot][cx];
+            n_out[g] = (int64_t)s_n0[slot][cx];
+            n_out[V + g] = (int64_t)s_n1[slot][cx];
+            if (OBS) {
+                // rows <= q+1 and columns <= x+1 are final here (villain.py:51-66, winding.py:30-37,
+                // wrapping.py:17-25): link residuals, plaquette winding dn, holonomy sums
+                const int slot1 = (q + 1 - rbase) % R;
+                const double ph = s_phi[slot][cx];
+                const double l0 = (0.0 + (s_phi[slot1][cx] - ph)) - TWO_PI * (double)s_n0[slot][cx];
+                const double l1 = (0.0 + (s_phi[slot][cx + 1] - ph)) - TWO_PI * (double)s_n1[slot][cx];
+                o_act += l0 * l0 + l1 * l1;
+                const int64_t dn = ((int64_t)s_n1[slot1][cx] - s_n1[slot][cx]) - ((int64_t)s_n0[slot][cx + 1] - s_n0[slot][cx]);
+                o_w2 += (double)(dn * dn);
+                o_n0 += (double)s_n0[slot][cx];
+                o_n1 += (double)s_n1[slot][cx];
+            }
+        }
+        if (OBS) {
+            o_act = wave_sum(o_act);
+            o_w2 = wave_sum(o_w2);
+            o_n0 = wave_sum(o_n0);
+            o_n1 = wave_sum(o_n1);
+            if (lane == 0) {
+                atomicAdd(&s_obs[0], o_act);
+                atomicAdd(&s_obs[1], o_w2);
+                atomicAdd(&s_obs[2], o_n0);
+                atomicAdd(&s_obs[3], o_n1);
+            }
         }
     };
 
@@ -495,10 +557,11 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
             for (int k = 0; k < 6; k++) bs[k] = s_base[wave][k];
             Draws D;
             if (fast[0])
-                D = draws_fast(A, 0, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
+                D = draws_fast(A, RP, 0, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
                                (uint32_t)(Gm.X0 + x), (uint32_t)xb, bs, s_small);
             else
-                D = draws_general(A, 0, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small);
+                D = draws_general(A, RP, 0, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small, edge, xw,
+                                  &s_base[wave][16]);
             if (active) {
                 const int lr = q - rbase;
                 const int sm = (lr - 1) % R, s0 = lr % R, sp = (lr + 1) % R;
@@ -562,10 +625,11 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
             for (int k = 0; k < 6; k++) bs[k] = s_base[wave][8 + k];
             Draws D;
             if (fast[1])
-                D = draws_fast(A, 1, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
+                D = draws_fast(A, RP, 1, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
                                (uint32_t)(Gm.X0 + x), (uint32_t)xb, bs, s_small);
             else
-                D = draws_general(A, 1, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small);
+                D = draws_general(A, RP, 1, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small, edge, xw,
+                                  &s_base[wave][24]);
             if (active) {
                 const int lr = q - rbase;
                 const int sm = (lr - 1) % R, s0 = lr % R;
@@ -609,12 +673,12 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
         commit(t + 3 + NW);  // slots of rows [t-NW, t): not read in phase C
         // advance the row bases by NW rows (one affine map; a full jump where the row wraps)
         if (base_lane) {
-            const int64_t p_old = base_pos(bty, grow(brow), Nx, xb, bhas);
-            const int64_t p_new = base_pos(bty, grow(brow + NW), Nx, xb, bhas);
+            const int64_t p_old = base_pos(bty, grow(brow), Nx, bx, bhas);
+            const int64_t p_new = base_pos(bty, grow(brow + NW), Nx, bx, bhas);
             const int ai = bty == 0 ? 0 : (bty == 1 ? 1 : 2);
             const int64_t step = bty == 0 ? (int64_t)NW * Nx : (bty == 1 ? (int64_t)NW * Nx / 2 : (int64_t)NW * Nx / 4);
             if (p_new - p_old == step) bases = apply(s_adv[ai], bases);
-            else bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)p_new);
+            else bases = full_jump(RP.T, &RP.blocks[bblk], (uint32_t)p_new);
             brow += NW;
             s_base[wave][lane] = bases;  // read by this wave only, after the barrier below
         }
@@ -628,15 +692,29 @@ __global__ __launch_bounds__(NW * 64) void villain_sweep_fused(FArgs A) {
     }
     if (s_bad && threadIdx.x == 0) {
         // |n| too large for the int32 LDS image: the host falls back to the generic path
-        report(A.S, A.sweep, OVERFLOW_BLOCK, 0);
+        report(A.S, A.sweep, OVERFLOW_BLOCK, 0, (uint32_t)rep);
     }
-    flush_stats(A.stat, acc_count, psum);
+    flush_stats(REPS ? A.stat + (int64_t)rep * A.rep_stat : A.stat, acc_count, psum);
+    if (OBS) {
+        __syncthreads();
+        if (threadIdx.x < 4) atomicAdd(&A.obs[(int64_t)rep * A.rep_obs + threadIdx.x], s_obs[threadIdx.x]);
+    }
 }
 
-template __global__ void villain_sweep_fused<2, false>(FArgs);
-template __global__ void villain_sweep_fused<4, false>(FArgs);
-template __global__ void villain_sweep_fused<6, false>(FArgs);
-template __global__ void villain_sweep_fused<4, true>(FArgs);
+// 3 waves / SIMD (12 per CU, what the LDS ring allows): caps the kernel at 168 VGPRs
+template <int NW, bool TILE, bool REPS>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(3))) void villain_sweep_fused(FArgs A) {
+    sweep_body<NW, TILE, REPS, false>(A);
+}
+// replica batch with the inline observables fused into the row stores: held to 3 waves / SIMD
+__global__ __launch_bounds__(4 * 64) __attribute__((amdgpu_waves_per_eu(3))) void villain_sweep_fused_obs(FArgs A) {
+    sweep_body<4, false, true, true>(A);
+}
+
+template __global__ void villain_sweep_fused<4, false, false>(FArgs);
+template __global__ void villain_sweep_fused<6, false, false>(FArgs);
+template __global__ void villain_sweep_fused<4, true, false>(FArgs);
+template __global__ void villain_sweep_fused<4, false, true>(FArgs);
 
 // ================================================================================================
 // observables (fused reductions over the current state)
@@ -703,7 +781,23 @@ int64_t rejections_in(const SkipMap &skips, int sweep, int nblocks) {
 }
 
 void launch_fused_tile(const FArgs &A, int grid, hipStream_t stream) {
-    villain_sweep_fused<4, true><<<grid, 4 * 64, 0, stream>>>(A);
+    villain_sweep_fused<4, true, false><<<grid, 4 * 64, 0, stream>>>(A);
+}
+
+void launch_fused_batch(const FArgs &A, int grid, bool obs, hipStream_t stream) {
+    if (obs) villain_sweep_fused_obs<<<grid, 4 * 64, 0, stream>>>(A);
+    else villain_sweep_fused<4, false, true><<<grid, 4 * 64, 0, stream>>>(A);
+}
+
+void farg_single(FArgs &A, int nsx, int nsy) {
+    A.tiles_per_rep = nsx * nsy;
+    A.rep_blocks = 0;
+    A.rep_field = 0;
+    A.rep_stat = 0;
+    A.rep_obs = 0;
+    A.Trep = nullptr;
+    A.advrep = nullptr;
+    A.obs = nullptr;
 }
 
 // plan `count` sweeps starting at sweep `first`, writing descriptors to ctx host staging
@@ -784,11 +878,11 @@ int absorb_reports(const AbortInfo &a, int first, SkipMap &skips) {
     return (int)best.first;
 }
 
-// Tunables (overridable for experiments with SV_FUSED_NW in {2,4,6} and SV_FUSED_TH)
+// Tunables (overridable for experiments with SV_FUSED_NW in {4,6} and SV_FUSED_TH)
 int fused_nw() {
     const char *e = getenv("SV_FUSED_NW");
     int v = e ? atoi(e) : 4;
-    return (v == 2 || v == 4 || v == 6) ? v : 4;
+    return v == 6 ? 6 : 4;
 }
 int fused_th() {
     const char *e = getenv("SV_FUSED_TH");
@@ -911,9 +1005,9 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             A.stat = ctx->d_stats + k;
             A.S = scratch(ctx);
             A.sweep = (uint32_t)k;
-            if (NWv == 2) villain_sweep_fused<2, false><<<grid, 2 * 64, 0, ctx->stream>>>(A);
-            else if (NWv == 6) villain_sweep_fused<6, false><<<grid, 6 * 64, 0, ctx->stream>>>(A);
-            else villain_sweep_fused<4, false><<<grid, 4 * 64, 0, ctx->stream>>>(A);
+            farg_single(A, nsx, nsy);
+            if (NWv == 6) villain_sweep_fused<6, false, false><<<grid, 6 * 64, 0, ctx->stream>>>(A);
+            else villain_sweep_fused<4, false, false><<<grid, 4 * 64, 0, ctx->stream>>>(A);
             st->cur ^= 1;
         }
         ctx->time_end(ev, count);

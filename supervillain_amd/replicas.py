@@ -1,0 +1,87 @@
+"""A batch of independent Villain NeighborhoodUpdate chains on one GPU (BASELINE config 5).
+
+Replica r is exactly the chain the reference's NeighborhoodUpdate (generator/villain/neighborhood.py:
+59-137) produces with `G.rng = rngs[r]`; all replicas advance together, one kernel launch per sweep
+(sv_replicas_* in include/supervillain_amd.h).  With inline=True the sweep kernel also measures, for
+every replica and sweep, the observables the reference measures inline (observable/observable.py:
+50-54): ActionDensity (action.py:25-31), InternalEnergyDensity (energy.py:25-30), WindingSquared
+(winding.py:30-37) and TorusWrapping (wrapping.py:17-25).
+"""
+import ctypes
+
+import numpy as np
+
+from supervillain_amd import _native
+from supervillain_amd._abi import SvRng, SvStats, rng_from_numpy, rng_to_numpy
+
+
+class VillainReplicas:
+
+    def __init__(self, R, N, kappa=0.5, W=1, interval_phi=np.pi, interval_n=1, *, device=None):
+        self.R, self.N = int(R), int(N)
+        self.kappa, self.W, self.interval_phi, self.interval_n = float(kappa), int(W), float(interval_phi), int(interval_n)
+        self.ctx = _native.context(_native.default_device() if device is None else device)
+        h = ctypes.c_void_p()
+        self.ctx.check(_native.lib().sv_replicas_create(self.ctx.handle, self.R, self.N, ctypes.byref(h)),
+                       'sv_replicas_create')
+        self.handle = h
+
+    def close(self):
+        if getattr(self, 'handle', None) is not None and _native._LIB is not None:
+            _native._LIB.sv_replicas_destroy(self.handle)
+            self.handle = None
+
+    __del__ = close
+
+    def cold(self):
+        self.ctx.check(_native.lib().sv_replicas_upload(self.handle, None, None), 'sv_replicas_upload')
+
+    def upload(self, phi, n):
+        phi = np.ascontiguousarray(phi, dtype=np.float64).reshape(self.R, self.N, self.N)
+        n = np.ascontiguousarray(n, dtype=np.int64).reshape(self.R, 2, self.N, self.N)
+        self.ctx.check(_native.lib().sv_replicas_upload(self.handle, _native.ptr(phi), _native.ptr(n)),
+                       'sv_replicas_upload')
+
+    def download(self):
+        phi = np.empty((self.R, self.N, self.N))
+        n = np.empty((self.R, 2, self.N, self.N), dtype=np.int64)
+        self.ctx.check(_native.lib().sv_replicas_download(self.handle, _native.ptr(phi), _native.ptr(n)),
+                       'sv_replicas_download')
+        return phi, n
+
+    def run(self, sweeps, rngs, inline=False):
+        """`sweeps` sweeps of every replica; rngs: R NumPy Generators, advanced in place.
+
+        Returns (stats, observables): stats has (R, sweeps) arrays 'accepted', 'acceptance' (the
+        reference's per-sweep increment of G.acceptance) and 'rejections'; observables is None or a
+        dict of (R, sweeps) arrays (TorusWrapping: (R, sweeps, 2))."""
+        if len(rngs) != self.R:
+            raise ValueError(f'need {self.R} generators')
+        r = (SvRng * self.R)(*[rng_from_numpy(g) for g in rngs])
+        st = (SvStats * (self.R * max(sweeps, 1)))()
+        obs = np.zeros((self.R, max(sweeps, 1), 4)) if inline else None
+        self.ctx.check(_native.lib().sv_replicas_run(self.handle, self.kappa, self.W, self.interval_phi,
+                                                     self.interval_n, int(sweeps), r, st,
+                                                     _native.ptr(obs) if inline else None), 'sv_replicas_run')
+        for g, x in zip(rngs, r):
+            rng_to_numpy(x, g)
+        V = self.N * self.N
+        stats = {
+            'accepted': np.array([[s.accepted for s in row] for row in _rows(st, self.R, sweeps)], dtype=np.int64),
+            'acceptance': np.array([[s.acceptance_sum / V for s in row] for row in _rows(st, self.R, sweeps)]),
+            'rejections': np.array([[s.rejections for s in row] for row in _rows(st, self.R, sweeps)], dtype=np.int64),
+        }
+        if not inline:
+            return stats, None
+        obs = obs[:, :sweeps]
+        S = self.kappa / 2 * obs[..., 0]
+        return stats, {
+            'ActionDensity': S / V,
+            'InternalEnergyDensity': S / (V * self.kappa),
+            'WindingSquared': obs[..., 1] / V,
+            'TorusWrapping': np.rint(obs[..., 2:4]).astype(np.int64),
+        }
+
+
+def _rows(st, R, sweeps):
+    return [[st[r * sweeps + k] for k in range(sweeps)] for r in range(R)]
