@@ -41,6 +41,9 @@ __device__ __forceinline__ void report(const DevScratch &S, uint32_t sweep, uint
     uint32_t i = atomicAdd(S.nreport, 1u);
     if (i < (uint32_t)MAX_REPORTS) S.reports[i] = Report{sweep, block, pos, rep};
     __hip_atomic_store(S.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // drain here, on the rare path: a result still pending at the join would make the compiler wait
+    // for every outstanding load and store (the row prefetch, the finished-row stores) on the common path
+    __builtin_amdgcn_s_waitcnt(0);
 }
 
 // stream position of bounded draw d, accounting for known rejected positions (sorted)
@@ -194,7 +197,8 @@ __device__ __forceinline__ int32_t wrapN(int32_t v, int32_t N) {
 }
 
 #ifndef SV_ABLATE
-#define SV_ABLATE 0  // timing experiments only: 1 = no exp, 2 = no RNG compositions, 4 = no wrapped-column jumps
+#define SV_ABLATE 0  // timing experiments only: 1 = no exp, 2 = no RNG compositions, 4 = no wrapped-column jumps,
+                     // 8 = no HBM stores, 16 = no HBM loads, 64 = no choice draws
 #endif
 __device__ __forceinline__ double sv_exp(double x) {
 #if SV_ABLATE & 1
@@ -320,7 +324,8 @@ __device__ __forceinline__ Draws draws_general(const FArgs &A, const Rep &RP, in
 // forward/backward pair).  4 compositions per site: the fwd and bwd choice blocks of a direction
 // read the SAME u64 word for two adjacent lanes (its two 32-bit halves), so each lane of a pair
 // computes one block's word and swaps the other half with its partner.
-__device__ __forceinline__ Draws draws_fast(const FArgs &A, const Rep &RP, int c, bool active, int32_t lane, uint32_t rowlin,
+__device__ __forceinline__ Draws draws_fast(const FArgs &A, const Rep &RP, int c, const uint32_t *hasw, bool active,
+                                            int32_t lane, uint32_t rowlin,
                                             uint32_t xs, uint32_t gx, uint32_t xb, const u128 *bases,
                                             const Affine *sm) {
     const int bb = 1 + 5 * c;
@@ -336,12 +341,11 @@ __device__ __forceinline__ Draws draws_fast(const FArgs &A, const Rep &RP, int c
         D.dphi = A.P.lo_phi + A.P.range_phi * to_double(xsl_rr(st));
     }
     D.cn[0] = D.cn[1] = D.cn[2] = D.cn[3] = 0;
-    if (A.P.k > 1) {
+    if (!(SV_ABLATE & 64) && A.P.k > 1) {
         const uint32_t R0 = (rowlin + xs) >> 1;  // rank of lane 0
 #pragma unroll
         for (int mu = 0; mu < 2; mu++) {
-            const Block &F = RP.blocks[bb + 1 + 2 * mu];
-            const uint32_t h = F.has;
+            const uint32_t h = hasw[mu];  // has of this direction's fwd (= bwd) choice block, preloaded
             const uint32_t P = (R0 - h) & 1u;                        // pairing parity of this row
             const uint32_t PW = (PR - h) >> 1;                       // word index of the row base
             uint32_t qq = rank - h;
@@ -430,6 +434,12 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     if (threadIdx.x == 0) s_bad = 0;
     if (OBS && threadIdx.x < 4) s_obs[threadIdx.x] = 0.0;
 
+    // the buffered-half flags of the fwd choice blocks (mu = 0, 1) per colour, kept in SGPRs: reading
+    // them from the descriptors inside the loop would put a vmcnt(0) wait behind the row prefetch
+    const uint32_t has_c0[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(RP.blocks[2].has),
+                                (uint32_t)__builtin_amdgcn_readfirstlane(RP.blocks[4].has)};
+    const uint32_t has_c1[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(RP.blocks[7].has),
+                                (uint32_t)__builtin_amdgcn_readfirstlane(RP.blocks[9].has)};
     // fast draws need, per colour, no skips and equal buffers within each fwd/bwd pair
     bool fast[2];
 #pragma unroll
@@ -456,9 +466,15 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             const int32_t q = ra + pf_rr[k];
             if (pf_rr[k] < NW && q >= t0 - 2 && q <= t1 + 2) {
                 const int64_t g = mrow(q) + pf_gx[k];
+#if SV_ABLATE & 16
+                pf_phi[k] = (double)(g & 7);
+                pf_n0[k] = 0;
+                pf_n1[k] = 0;
+#else
                 pf_phi[k] = phi_in[g];
                 pf_n0[k] = n_in[g];
                 pf_n1[k] = n_in[V + g];
+#endif
             }
         }
     };
@@ -495,18 +511,23 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     double psum = 0.0;
 
     // coalesced stores of finished rows [ra, ra+NW) (clipped to the tile) from the ring
+    // e / w by multiply-shift: exact for e < 1024 and w <= 123 (checked exhaustively)
+    const uint32_t inv_w = ((1u << 20) + (uint32_t)w - 1) / (uint32_t)w;
+    static_assert(NW * FW_MAX < 1024, "store_rows reciprocal checked exact for e < 1024");
     auto store_rows = [&](int32_t ra) {
         const int32_t r0 = ra < t0 ? t0 : ra, r1 = ra + NW < t1 ? ra + NW : t1;
         const int total = r1 > r0 ? (r1 - r0) * w : 0;
         double o_act = 0.0, o_w2 = 0.0, o_n0 = 0.0, o_n1 = 0.0;  // OBS partials (integers exact in f64)
         for (int e = threadIdx.x; e < total; e += nthreads) {
-            const int rr = e / w, cc = e - rr * w;
+            const int rr = (int)(((uint32_t)e * inv_w) >> 20), cc = e - rr * w;  // e / w
             const int32_t q = r0 + rr;
             const int slot = (q - rbase) % R, cx = cc + 2;
             const int64_t g = mrow(q) + x0 + cc;  // tile sites never wrap
+#if !(SV_ABLATE & 8)
             phi_out[g] = s_phi[slot][cx];
             n_out[g] = (int64_t)s_n0[slot][cx];
             n_out[V + g] = (int64_t)s_n1[slot][cx];
+#endif
             if (OBS) {
                 // rows <= q+1 and columns <= x+1 are final here (villain.py:51-66, winding.py:30-37,
                 // wrapping.py:17-25): link residuals, plaquette winding dn, holonomy sums
@@ -557,7 +578,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             for (int k = 0; k < 6; k++) bs[k] = s_base[wave][k];
             Draws D;
             if (fast[0])
-                D = draws_fast(A, RP, 0, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
+                D = draws_fast(A, RP, 0, has_c0, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
                                (uint32_t)(Gm.X0 + x), (uint32_t)xb, bs, s_small);
             else
                 D = draws_general(A, RP, 0, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small, edge, xw,
@@ -625,7 +646,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             for (int k = 0; k < 6; k++) bs[k] = s_base[wave][8 + k];
             Draws D;
             if (fast[1])
-                D = draws_fast(A, RP, 1, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
+                D = draws_fast(A, RP, 1, has_c1, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
                                (uint32_t)(Gm.X0 + x), (uint32_t)xb, bs, s_small);
             else
                 D = draws_general(A, RP, 1, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small, edge, xw,
