@@ -384,6 +384,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     __shared__ u128 s_base[NW][32];  // per wave: [8c + ty] = block ty's base for the colour-c row; [16 + ..] at xw
     __shared__ int32_t s_bad;
     __shared__ double s_obs[4];  // OBS: workgroup sums of the inline observables
+    __shared__ Block s_blk[11];  // this sweep's descriptors (LDS: no vector-memory waits in the loop)
 
     if (*(volatile const int32_t *)A.S.abort) return;
 
@@ -430,6 +431,8 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     const int32_t xw = gx0 - 2 < 0 ? Nx - 2 : 0;
 
     for (int e = threadIdx.x; e < SMALL_LDS; e += nthreads) s_small[e] = RP.T->small[e];
+    if (threadIdx.x < 11) s_blk[threadIdx.x] = RP.blocks[threadIdx.x];
+    const Rep RL{s_blk, RP.T, RP.id};  // the loop's view (valid after the prologue barrier)
     if (threadIdx.x < 3) s_adv[threadIdx.x] = REPS ? A.advrep[3 * rep + threadIdx.x] : A.adv[threadIdx.x];
     if (threadIdx.x == 0) s_bad = 0;
     if (OBS && threadIdx.x < 4) s_obs[threadIdx.x] = 0.0;
@@ -578,10 +581,10 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             for (int k = 0; k < 6; k++) bs[k] = s_base[wave][k];
             Draws D;
             if (fast[0])
-                D = draws_fast(A, RP, 0, has_c0, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
+                D = draws_fast(A, RL, 0, has_c0, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
                                (uint32_t)(Gm.X0 + x), (uint32_t)xb, bs, s_small);
             else
-                D = draws_general(A, RP, 0, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small, edge, xw,
+                D = draws_general(A, RL, 0, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small, edge, xw,
                                   &s_base[wave][16]);
             if (active) {
                 const int lr = q - rbase;
@@ -646,10 +649,10 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             for (int k = 0; k < 6; k++) bs[k] = s_base[wave][8 + k];
             Draws D;
             if (fast[1])
-                D = draws_fast(A, RP, 1, has_c1, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
+                D = draws_fast(A, RL, 1, has_c1, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
                                (uint32_t)(Gm.X0 + x), (uint32_t)xb, bs, s_small);
             else
-                D = draws_general(A, RP, 1, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small, edge, xw,
+                D = draws_general(A, RL, 1, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small, edge, xw,
                                   &s_base[wave][24]);
             if (active) {
                 const int lr = q - rbase;
@@ -699,7 +702,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             const int ai = bty == 0 ? 0 : (bty == 1 ? 1 : 2);
             const int64_t step = bty == 0 ? (int64_t)NW * Nx : (bty == 1 ? (int64_t)NW * Nx / 2 : (int64_t)NW * Nx / 4);
             if (p_new - p_old == step) bases = apply(s_adv[ai], bases);
-            else bases = full_jump(RP.T, &RP.blocks[bblk], (uint32_t)p_new);
+            else bases = full_jump(RP.T, &s_blk[bblk], (uint32_t)p_new);
             brow += NW;
             s_base[wave][lane] = bases;  // read by this wave only, after the barrier below
         }
