@@ -159,8 +159,9 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         inc[r] = u128{rngs[r].inc_lo, rngs[r].inc_hi};
     }
     std::vector<SkipMap> skips(R);
-    const int TH = fused_th();
-    const int nsx = (b->N + FW_MAX - 1) / FW_MAX;
+    const int nsx = b->N <= RW ? 1 : (b->N + FW_MAX - 1) / FW_MAX;  // one full-row strip up to 128 columns
+    // 64-row tiles, or 32 when that leaves the chip short of workgroups (measured: R=128, N=128)
+    const int TH = getenv("SV_FUSED_TH") ? fused_th() : ((int64_t)R * nsx * ((b->N + 63) / 64) < 768 ? 32 : 64);
     const int nsy = (b->N + TH - 1) / TH;
     const int tiles = nsx * nsy;
     std::vector<PlanIn> pin(R);
@@ -277,7 +278,7 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
                 for (int k = 0; k < good; k++) {
                     sv_stats s = hst[(size_t)r * count + k];
                     s.proposed = V;
-                    s.rejections = rejections_in(skips[r], sw + k, NB);
+                    s.rejections = skips[r].empty() ? 0 : rejections_in(skips[r], sw + k, NB);
                     stats[(size_t)r * sweeps + sw + k] = s;
                     if (obs)
                         std::memcpy(obs + ((size_t)r * sweeps + sw + k) * 4, &hobs[((size_t)r * count + k) * 4],

@@ -369,8 +369,11 @@ __device__ __forceinline__ Draws draws_fast(const FArgs &A, const Rep &RP, int c
     return D;
 }
 
-template <int NW, bool TILE, bool REPS, bool OBS>
+// FR (full rows, periodic lattices of Nx <= 128): one strip spans the whole row, its LDS columns ARE
+// the lattice columns and neighbours wrap inside LDS -- no column halo, every lane busy at N = 128.
+template <int NW, bool TILE, bool REPS, bool OBS, bool FR>
 __device__ __forceinline__ void sweep_body(const FArgs &A) {
+    static_assert(!(FR && TILE), "full-row strips are for periodic lattices");
     constexpr int R = FusedGeom<NW>::R;
     constexpr int nthreads = NW * 64;
     constexpr int PF = (NW * RW + nthreads - 1) / nthreads;  // prefetched elements per thread
@@ -420,9 +423,13 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     const int32_t t0 = iy * A.TH;
     const int32_t t1 = t0 + A.TH < Gm.Ht ? t0 + A.TH : Gm.Ht;
     const int32_t rbase = t0 - 2;  // local row 0
-    const int32_t cols = w + 5;
+    const int32_t cols = FR ? w : w + 5;
+    const int32_t cofs = FR ? 0 : x0 - 2;  // LDS column of local column x is x - cofs
+    // LDS neighbour columns (full rows wrap inside the row)
+    auto cxp = [&](int cx) { return FR ? (cx + 1 == w ? 0 : cx + 1) : cx + 1; };
+    auto cxm = [&](int cx) { return FR ? (cx == 0 ? w - 1 : cx - 1) : cx - 1; };
     const int32_t gx0 = Gm.X0 + x0;                  // global column of the strip's first site
-    const bool interior = gx0 >= 4 && gx0 + w + 2 < Nx;
+    const bool interior = !FR && gx0 >= 4 && gx0 + w + 2 < Nx;
     // row bases at the first non-wrapped region column (global); on rows of <= 128 sites at the row
     // start, so that every column -- wrapped halo columns included -- is a small-table offset away
     const int32_t xb = ((Nx <= SMALL_LDS && !interior) || gx0 - 2 < 0) ? 0 : gx0 - 2;
@@ -461,7 +468,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
         const int e = threadIdx.x + k * nthreads;
         pf_rr[k] = e / cols;
         pf_cc[k] = e - pf_rr[k] * cols;
-        pf_gx[k] = mcol(x0 - 2 + pf_cc[k]);
+        pf_gx[k] = FR ? pf_cc[k] : mcol(x0 - 2 + pf_cc[k]);
     }
     auto prefetch = [&](int32_t ra) {
 #pragma unroll
@@ -524,7 +531,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
         for (int e = threadIdx.x; e < total; e += nthreads) {
             const int rr = (int)(((uint32_t)e * inv_w) >> 20), cc = e - rr * w;  // e / w
             const int32_t q = r0 + rr;
-            const int slot = (q - rbase) % R, cx = cc + 2;
+            const int slot = (q - rbase) % R, cx = FR ? cc : cc + 2;
             const int64_t g = mrow(q) + x0 + cc;  // tile sites never wrap
 #if !(SV_ABLATE & 8)
             phi_out[g] = s_phi[slot][cx];
@@ -537,9 +544,9 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
                 const int slot1 = (q + 1 - rbase) % R;
                 const double ph = s_phi[slot][cx];
                 const double l0 = (0.0 + (s_phi[slot1][cx] - ph)) - TWO_PI * (double)s_n0[slot][cx];
-                const double l1 = (0.0 + (s_phi[slot][cx + 1] - ph)) - TWO_PI * (double)s_n1[slot][cx];
+                const double l1 = (0.0 + (s_phi[slot][cxp(cx)] - ph)) - TWO_PI * (double)s_n1[slot][cx];
                 o_act += l0 * l0 + l1 * l1;
-                const int64_t dn = ((int64_t)s_n1[slot1][cx] - s_n1[slot][cx]) - ((int64_t)s_n0[slot][cx + 1] - s_n0[slot][cx]);
+                const int64_t dn = ((int64_t)s_n1[slot1][cx] - s_n1[slot][cx]) - ((int64_t)s_n0[slot][cxp(cx)] - s_n0[slot][cx]);
                 o_w2 += (double)(dn * dn);
                 o_n0 += (double)s_n0[slot][cx];
                 o_n1 += (double)s_n1[slot][cx];
@@ -573,9 +580,9 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             const int32_t q = t + 2 + wave;
             const bool row_ok = (q >= t0 - 1) && (q <= t1 + 1);
             const int32_t gq = grow(q);
-            const int32_t xs = (x0 - 1) + ((par0 + q + x0 - 1) & 1);  // global (t + x) even
+            const int32_t xs = FR ? ((par0 + q) & 1) : (x0 - 1) + ((par0 + q + x0 - 1) & 1);  // global (t + x) even
             const int32_t x = xs + 2 * lane;
-            const bool active = row_ok && x <= x1 + 1;
+            const bool active = row_ok && (FR ? x < w : x <= x1 + 1);
             u128 bs[6];
 #pragma unroll
             for (int k = 0; k < 6; k++) bs[k] = s_base[wave][k];
@@ -589,15 +596,15 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             if (active) {
                 const int lr = q - rbase;
                 const int sm = (lr - 1) % R, s0 = lr % R, sp = (lr + 1) % R;
-                const int cx = x - (x0 - 2);
+                const int cx = x - cofs, cp = cxp(cx), cm = cxm(cx);
                 const double ph = s_phi[s0][cx];
                 // r0 on the four links: f0=(0,q,x), b0=(0,q-1,x), f1=(1,q,x), b1=(1,q,x-1)
-                const int32_t n_f0 = s_n0[s0][cx], n_b0 = s_n0[sm][cx], n_f1 = s_n1[s0][cx], n_b1 = s_n1[s0][cx - 1];
+                const int32_t n_f0 = s_n0[s0][cx], n_b0 = s_n0[sm][cx], n_f1 = s_n1[s0][cx], n_b1 = s_n1[s0][cm];
                 double r0[4];
                 r0[0] = (0.0 + (s_phi[sp][cx] - ph)) - TWO_PI * (double)n_f0;
                 r0[1] = (0.0 + (ph - s_phi[sm][cx])) - TWO_PI * (double)n_b0;
-                r0[2] = (0.0 + (s_phi[s0][cx + 1] - ph)) - TWO_PI * (double)n_f1;
-                r0[3] = (0.0 + (ph - s_phi[s0][cx - 1])) - TWO_PI * (double)n_b1;
+                r0[2] = (0.0 + (s_phi[s0][cp] - ph)) - TWO_PI * (double)n_f1;
+                r0[3] = (0.0 + (ph - s_phi[s0][cm])) - TWO_PI * (double)n_b1;
                 double cr[4];
                 cr[0] = (0.0 + (0.0 - D.dphi)) - TWO_PI * (double)D.cn[0];
                 cr[1] = (0.0 + (D.dphi - 0.0)) - TWO_PI * (double)D.cn[1];
@@ -614,7 +621,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
                 p = p < 0.0 ? 0.0 : p;
                 p = p > 1.0 ? 1.0 : p;
                 const int acc = D.u < p;
-                const bool own = q >= t0 && q < t1 && x >= x0 && x < x1;
+                const bool own = q >= t0 && q < t1 && (FR || (x >= x0 && x < x1));
                 if (own) {  // count each site once; colour-0 phi is final after this pass
                     acc_count += acc;
                     psum += p;
@@ -628,11 +635,11 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
                 s_n0[s0][cx] = n_f0 + c0;
                 s_n0[sm][cx] = n_b0 + c1;
                 s_n1[s0][cx] = n_f1 + c2;
-                s_n1[s0][cx - 1] = n_b1 + c3;
+                s_n1[s0][cm] = n_b1 + c3;
                 s_r0[s0][cx] = (r0[0] + dcp_f) - TWO_PI * (double)c0;
                 s_r0[sm][cx] = (r0[1] + dcp_b) - TWO_PI * (double)c1;
                 s_r1[s0][cx] = (r0[2] + dcp_f) - TWO_PI * (double)c2;
-                s_r1[s0][cx - 1] = (r0[3] + dcp_b) - TWO_PI * (double)c3;
+                s_r1[s0][cm] = (r0[3] + dcp_b) - TWO_PI * (double)c3;
             }
         }
         __syncthreads();
@@ -641,9 +648,9 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             const int32_t q = t + 1 + wave;
             const bool row_ok = (q >= t0) && (q <= t1);
             const int32_t gq = grow(q);
-            const int32_t xs = x0 + ((par0 + q + x0 + 1) & 1);  // global (t + x) odd
+            const int32_t xs = FR ? ((par0 + q + 1) & 1) : x0 + ((par0 + q + x0 + 1) & 1);  // global (t + x) odd
             const int32_t x = xs + 2 * lane;
-            const bool active = row_ok && x <= x1;
+            const bool active = row_ok && (FR ? x < w : x <= x1);
             u128 bs[6];
 #pragma unroll
             for (int k = 0; k < 6; k++) bs[k] = s_base[wave][8 + k];
@@ -657,13 +664,13 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             if (active) {
                 const int lr = q - rbase;
                 const int sm = (lr - 1) % R, s0 = lr % R;
-                const int cx = x - (x0 - 2);
+                const int cx = x - cofs, cm = cxm(cx);
                 const double ph = s_phi[s0][cx];
                 double ri[4];
                 ri[0] = s_r0[s0][cx];
                 ri[1] = s_r0[sm][cx];
                 ri[2] = s_r1[s0][cx];
-                ri[3] = s_r1[s0][cx - 1];
+                ri[3] = s_r1[s0][cm];
                 double cr[4];
                 cr[0] = (0.0 + (0.0 - D.dphi)) - TWO_PI * (double)D.cn[0];
                 cr[1] = (0.0 + (D.dphi - 0.0)) - TWO_PI * (double)D.cn[1];
@@ -680,7 +687,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
                 p = p < 0.0 ? 0.0 : p;
                 p = p > 1.0 ? 1.0 : p;
                 const int acc = D.u < p;
-                if (q >= t0 && q < t1 && x >= x0 && x < x1) {
+                if (q >= t0 && q < t1 && (FR || (x >= x0 && x < x1))) {
                     acc_count += acc;
                     psum += p;
                 }
@@ -690,7 +697,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
                     s_n0[s0][cx] += D.cn[0];
                     s_n0[sm][cx] += D.cn[1];
                     s_n1[s0][cx] += D.cn[2];
-                    s_n1[s0][cx - 1] += D.cn[3];
+                    s_n1[s0][cm] += D.cn[3];
                 }
             }
         }
@@ -726,19 +733,23 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
 }
 
 // 3 waves / SIMD (12 per CU, what the LDS ring allows): caps the kernel at 168 VGPRs
-template <int NW, bool TILE, bool REPS>
+template <int NW, bool TILE, bool REPS, bool FR>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(3))) void villain_sweep_fused(FArgs A) {
-    sweep_body<NW, TILE, REPS, false>(A);
+    sweep_body<NW, TILE, REPS, false, FR>(A);
 }
 // replica batch with the inline observables fused into the row stores: held to 3 waves / SIMD
+template <bool FR>
 __global__ __launch_bounds__(4 * 64) __attribute__((amdgpu_waves_per_eu(3))) void villain_sweep_fused_obs(FArgs A) {
-    sweep_body<4, false, true, true>(A);
+    sweep_body<4, false, true, true, FR>(A);
 }
 
-template __global__ void villain_sweep_fused<4, false, false>(FArgs);
-template __global__ void villain_sweep_fused<6, false, false>(FArgs);
-template __global__ void villain_sweep_fused<4, true, false>(FArgs);
-template __global__ void villain_sweep_fused<4, false, true>(FArgs);
+template __global__ void villain_sweep_fused<4, false, false, false>(FArgs);
+template __global__ void villain_sweep_fused<6, false, false, false>(FArgs);
+template __global__ void villain_sweep_fused<4, true, false, false>(FArgs);
+template __global__ void villain_sweep_fused<4, false, true, false>(FArgs);
+template __global__ void villain_sweep_fused<4, false, true, true>(FArgs);
+template __global__ void villain_sweep_fused_obs<false>(FArgs);
+template __global__ void villain_sweep_fused_obs<true>(FArgs);
 
 // ================================================================================================
 // observables (fused reductions over the current state)
@@ -805,12 +816,15 @@ int64_t rejections_in(const SkipMap &skips, int sweep, int nblocks) {
 }
 
 void launch_fused_tile(const FArgs &A, int grid, hipStream_t stream) {
-    villain_sweep_fused<4, true, false><<<grid, 4 * 64, 0, stream>>>(A);
+    villain_sweep_fused<4, true, false, false><<<grid, 4 * 64, 0, stream>>>(A);
 }
 
 void launch_fused_batch(const FArgs &A, int grid, bool obs, hipStream_t stream) {
-    if (obs) villain_sweep_fused_obs<<<grid, 4 * 64, 0, stream>>>(A);
-    else villain_sweep_fused<4, false, true><<<grid, 4 * 64, 0, stream>>>(A);
+    const bool fr = A.nsx == 1 && A.G.Nx <= RW;  // full-row strips
+    if (obs && fr) villain_sweep_fused_obs<true><<<grid, 4 * 64, 0, stream>>>(A);
+    else if (obs) villain_sweep_fused_obs<false><<<grid, 4 * 64, 0, stream>>>(A);
+    else if (fr) villain_sweep_fused<4, false, true, true><<<grid, 4 * 64, 0, stream>>>(A);
+    else villain_sweep_fused<4, false, true, false><<<grid, 4 * 64, 0, stream>>>(A);
 }
 
 void farg_single(FArgs &A, int nsx, int nsy) {
@@ -1030,8 +1044,8 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             A.S = scratch(ctx);
             A.sweep = (uint32_t)k;
             farg_single(A, nsx, nsy);
-            if (NWv == 6) villain_sweep_fused<6, false, false><<<grid, 6 * 64, 0, ctx->stream>>>(A);
-            else villain_sweep_fused<4, false, false><<<grid, 4 * 64, 0, ctx->stream>>>(A);
+            if (NWv == 6) villain_sweep_fused<6, false, false, false><<<grid, 6 * 64, 0, ctx->stream>>>(A);
+            else villain_sweep_fused<4, false, false, false><<<grid, 4 * 64, 0, ctx->stream>>>(A);
             st->cur ^= 1;
         }
         ctx->time_end(ev, count);

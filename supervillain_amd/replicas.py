@@ -14,6 +14,10 @@ import numpy as np
 from supervillain_amd import _native
 from supervillain_amd._abi import SvRng, SvStats, rng_from_numpy, rng_to_numpy
 
+# numpy image of sv_stats (include/supervillain_amd.h)
+STATS_DTYPE = np.dtype([('accepted', '<i8'), ('proposed', '<i8'), ('acceptance_sum', '<f8'), ('rejections', '<i8')])
+assert STATS_DTYPE.itemsize == __import__('ctypes').sizeof(SvStats)
+
 
 class VillainReplicas:
 
@@ -58,19 +62,17 @@ class VillainReplicas:
         if len(rngs) != self.R:
             raise ValueError(f'need {self.R} generators')
         r = (SvRng * self.R)(*[rng_from_numpy(g) for g in rngs])
-        st = (SvStats * (self.R * max(sweeps, 1)))()
+        st = np.zeros((self.R, max(sweeps, 1)), dtype=STATS_DTYPE)  # sv_stats[R][sweeps]
         obs = np.zeros((self.R, max(sweeps, 1), 4)) if inline else None
         self.ctx.check(_native.lib().sv_replicas_run(self.handle, self.kappa, self.W, self.interval_phi,
-                                                     self.interval_n, int(sweeps), r, st,
+                                                     self.interval_n, int(sweeps), r, _native.ptr(st),
                                                      _native.ptr(obs) if inline else None), 'sv_replicas_run')
         for g, x in zip(rngs, r):
             rng_to_numpy(x, g)
         V = self.N * self.N
-        stats = {
-            'accepted': np.array([[s.accepted for s in row] for row in _rows(st, self.R, sweeps)], dtype=np.int64),
-            'acceptance': np.array([[s.acceptance_sum / V for s in row] for row in _rows(st, self.R, sweeps)]),
-            'rejections': np.array([[s.rejections for s in row] for row in _rows(st, self.R, sweeps)], dtype=np.int64),
-        }
+        st = st[:, :sweeps]
+        stats = {'accepted': st['accepted'].copy(), 'acceptance': st['acceptance_sum'] / V,
+                 'rejections': st['rejections'].copy()}
         if not inline:
             return stats, None
         obs = obs[:, :sweeps]
@@ -81,7 +83,3 @@ class VillainReplicas:
             'WindingSquared': obs[..., 1] / V,
             'TorusWrapping': np.rint(obs[..., 2:4]).astype(np.int64),
         }
-
-
-def _rows(st, R, sweeps):
-    return [[st[r * sweeps + k] for k in range(sweeps)] for r in range(R)]

@@ -36,7 +36,7 @@ def run_batch(R, N, kappa, W, phi0, n0, sweeps, gens, inline=False):
     return phi, n, stats, obs
 
 
-@pytest.mark.parametrize('N,sweeps', [(16, 5), (64, 70), (128, 3)])
+@pytest.mark.parametrize('N,sweeps', [(16, 5), (64, 70), (128, 3), (130, 2), (256, 2)])
 def test_each_replica_is_its_own_chain(N, sweeps, oracle_lib):
     R = 5
     phi0, n0 = hot(R, N, 2, N)
