@@ -12,6 +12,12 @@ with the fields resident in HBM.
          GPU, with an RCCL halo exchange every sweep (weak scaling: L x L sites per GPU).  The chain
          is bit-identical to running that lattice on one GPU.  --strong keeps the lattice at L x L.
 Rank 0 prints one JSON line.
+
+Secondary workloads (not the headline line; BASELINE.json configs 5 and 3):
+  --workload replicas   1024 independent L=128 Villain chains, W=2, inline observables, split over
+                        the N ranks (config 5; replicas need no collectives)
+  --workload worldline  L=1024 Worldline: one checkerboard PlaquetteUpdate + one CoexactUpdate sweep
+                        per step, W=1 (config 3); N > 1 runs independent replicas
 """
 import argparse
 import ctypes
@@ -27,6 +33,7 @@ sys.path.insert(0, ROOT)
 
 ALG_BYTES_PER_SITE = 48      # one read + one write of phi (f64) and n (2 x i64) per sweep
 SURVEY_BYTES_PER_SITE = 88   # two separate colour passes
+WORLDLINE_BYTES = 168        # Plaquette (88) + Coexact (80) per plaquette-step
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
@@ -44,7 +51,15 @@ def parse():
     ap.add_argument('--strong', action='store_true', help='N>1: decompose one L x L lattice (strong scaling)')
     ap.add_argument('--tiles', default=None, help='tile grid TYxTX (default from N); with N=1 emulates the '
                                                    'decomposition on one GPU')
-    return ap.parse_args()
+    ap.add_argument('--workload', default='villain', choices=['villain', 'replicas', 'worldline'])
+    ap.add_argument('--replicas', type=int, default=1024, help='replicas workload: total replica count')
+    args = ap.parse_args()
+    if args.workload == 'replicas':
+        args.L = 128 if args.L == 4096 else args.L
+        args.W = 2 if args.W == 1 else args.W
+    if args.workload == 'worldline':
+        args.L = 1024 if args.L == 4096 else args.L
+    return args
 
 
 def traffic_from_profiles(L):
@@ -92,12 +107,15 @@ def kernel_time(Lib, ctx):
     return ms.value / 1e3 / max(launches.value, 1)
 
 
-def report(args, world, sites_per_step, sites_per_launch, elapsed, acc, avg_launch_s, config, traffic_L):
-    achieved = ALG_BYTES_PER_SITE * sites_per_launch / avg_launch_s / 1e9
+def report(args, world, sites_per_step, sites_per_launch, elapsed, acc, avg_launch_s, config, traffic_L,
+           metric='lattice-site updates/sec (sweeps/s × L²), L=4096 Villain, 1→8 MI355X',
+           unit='lattice-site updates/s', kernel='villain_sweep_fused', alg_bytes=ALG_BYTES_PER_SITE,
+           survey_bytes=SURVEY_BYTES_PER_SITE, baseline=None):
+    achieved = alg_bytes * sites_per_launch / avg_launch_s / 1e9
     out = {
-        'metric': 'lattice-site updates/sec (sweeps/s × L²), L=4096 Villain, 1→8 MI355X',
+        'metric': metric,
         'value': args.steps * sites_per_step / elapsed,
-        'unit': 'lattice-site updates/s',
+        'unit': unit,
         'n_gpus': world,
         'steps': args.steps,
         'warmup': args.warmup,
@@ -109,15 +127,133 @@ def report(args, world, sites_per_step, sites_per_launch, elapsed, acc, avg_laun
         'data': 'synthetic (cold start, NumPy PCG64 seed 0)',
         'config': dict(config, kappa=args.kappa, W=args.W, acceptance_rate=acc),
         'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                     'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic_from_profiles(traffic_L),
-                     'kernel': 'villain_sweep_fused', 'avg_launch_us': avg_launch_s * 1e6,
-                     'alg_bytes_per_site': ALG_BYTES_PER_SITE,
-                     'survey_effective_GBps': SURVEY_BYTES_PER_SITE * sites_per_launch / avg_launch_s / 1e9},
+                     'frac': achieved / HBM_PEAK_GBS,
+                     'traffic': traffic_from_profiles(traffic_L) if kernel == 'villain_sweep_fused' else None,
+                     'kernel': kernel, 'avg_launch_us': avg_launch_s * 1e6,
+                     'alg_bytes_per_site': alg_bytes,
+                     'survey_effective_GBps': survey_bytes * sites_per_launch / avg_launch_s / 1e9},
         'cpu_baseline': None,
     }
     if world == 1 and not args.no_cpu_baseline:
-        out['cpu_baseline'] = cpu_baseline(args.L, args.kappa, args.W, args.cpu_sweeps)
+        out['cpu_baseline'] = (baseline or (lambda: cpu_baseline(args.L, args.kappa, args.W, args.cpu_sweeps)))()
     print(json.dumps(out), flush=True)
+
+
+def run_replicas(args, world, rank, dist):
+    """BASELINE config 5: independent L x L replica chains (seed = global replica index), W=2, inline
+    observables fused into the sweep kernel; the replicas are split over the ranks, no collective."""
+    from supervillain_amd import _native
+    from supervillain_amd.replicas import VillainReplicas
+    L, Rt = args.L, args.replicas
+    per = Rt // world
+    first = rank * per
+    B = VillainReplicas(per, L, args.kappa, args.W)
+    B.cold()
+    gens = [np.random.default_rng(first + r) for r in range(per)]
+    Lib = _native.lib()
+    if args.warmup:
+        B.run(args.warmup, gens, inline=True)
+    Lib.sv_ctx_set_timing(B.ctx.handle, 1)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    stats, obs = B.run(args.steps, gens, inline=True)
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = max_over_ranks(dist, t1 - t0)
+    launches_s = kernel_time(Lib, B.ctx)
+    acc = float(stats['accepted'].sum()) / (args.steps * per * L * L)
+
+    def baseline():
+        from oracle import oracle as O
+        sweeps, n = 20, 8
+        t = time.perf_counter()
+        for r in range(n):
+            phi, nn = np.zeros((L, L)), np.zeros((2, L, L), dtype=np.int64)
+            O.villain_neighborhood(L, args.kappa, args.W, phi, nn, sweeps, np.random.default_rng(r))
+        dt = time.perf_counter() - t
+        return {'value': n * sweeps * L * L / dt, 'unit': 'replica-site updates/s', 'cores': 1, 'kind': 'port',
+                'sample': f'{n} replicas x {sweeps} sweeps of L={L} Villain NeighborhoodUpdate (W={args.W}), '
+                          'oracle/sv_oracle.c single-threaded (no observables)'}
+
+    if rank == 0:
+        config = {'workload': f'{Rt} independent L={L} Villain NeighborhoodUpdate replica chains (W={args.W}), '
+                              'inline ActionDensity/InternalEnergyDensity/WindingSquared/TorusWrapping, '
+                              f'{per} replicas per GPU, one launch per sweep for all of them',
+                  'L': L, 'replicas': Rt, 'replicas_per_gpu': per, 'path': 'replicas',
+                  'parallelism': f'{world} GPU(s), replicas sharded, no collectives'}
+        report(args, world, Rt * L * L, per * L * L, elapsed, acc, launches_s, config, L,
+               metric=f'replica-site updates/sec, {Rt} x L={L} Villain replicas, W={args.W}, inline observables',
+               unit='replica-site updates/s', kernel='villain_sweep_fused_obs', baseline=baseline)
+    B.close()
+
+
+def run_worldline(args, world, rank, dist):
+    """BASELINE config 3: L x L Worldline, one checkerboard PlaquetteUpdate sweep + one CoexactUpdate
+    sweep per step, m = v = 0 cold start; N > 1 runs independent chains (seed = rank)."""
+    from supervillain_amd import _native
+    from supervillain_amd._abi import rng_from_numpy
+    L = args.L
+    Lib = _native.lib()
+    ctx = _native.context(_native.default_device())
+    h = ctypes.c_void_p()
+    ctx.check(Lib.sv_worldline_create(ctx.handle, L, 0, ctypes.byref(h)), 'sv_worldline_create')
+    m = np.zeros((2, L, L), dtype=np.int64)
+    v = np.zeros((L, L), dtype=np.int64)
+    ctx.check(Lib.sv_worldline_upload(h, _native.ptr(m), _native.ptr(v)), 'sv_worldline_upload')
+    r = rng_from_numpy(np.random.default_rng(rank))
+    Weff = float(args.W)
+
+    def step(k):
+        st = _native.stats_array(1)
+        acc = 0
+        for _ in range(k):
+            ctx.check(Lib.sv_worldline_plaquette_checkerboard_run(h, args.kappa, Weff, 1, ctypes.byref(r), st),
+                      'plaquette')
+            acc += st[0].accepted
+            ctx.check(Lib.sv_worldline_coexact_run(h, args.kappa, Weff, 1, 1, ctypes.byref(r), st), 'coexact')
+        return acc
+
+    if args.warmup:
+        step(args.warmup)
+    Lib.sv_ctx_set_timing(ctx.handle, 1)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    acc = step(args.steps)
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = max_over_ranks(dist, t1 - t0)
+    ms = ctypes.c_double()
+    launches = ctypes.c_int64()
+    Lib.sv_ctx_kernel_time(ctx.handle, ctypes.byref(ms), ctypes.byref(launches))
+    step_kernel_s = ms.value / 1e3 / args.steps  # both sweeps' kernels per step
+
+    def baseline():
+        from oracle import oracle as O
+        mm, vv = np.zeros((2, L, L), dtype=np.int64), np.zeros((L, L), dtype=np.int64)
+        g = np.random.default_rng(0)
+        k = 3
+        t = time.perf_counter()
+        for _ in range(k):
+            O.worldline_plaquette_cb(L, args.kappa, Weff, mm, vv, 1, g)
+            O.worldline_coexact(L, args.kappa, Weff, mm, vv, 1, g)
+        dt = time.perf_counter() - t
+        return {'value': k * L * L / dt, 'unit': 'plaquette-steps/s', 'cores': 1, 'kind': 'port',
+                'sample': f'{k} steps (checkerboard Plaquette + Coexact sweep) of L={L} Worldline, '
+                          'oracle/sv_oracle.c single-threaded'}
+
+    if rank == 0:
+        config = {'workload': f'L={L} Worldline: checkerboard PlaquetteUpdate + CoexactUpdate sweep per step, '
+                              f'W={args.W}, kappa={args.kappa}, bit-exact PCG64 replay (per-colour kernels)',
+                  'L': L, 'path': 'worldline', 'parallelism': f'{world} independent chain(s)'}
+        report(args, world, world * L * L, L * L, elapsed, acc / (args.steps * L * L), step_kernel_s, config, L,
+               metric=f'plaquette-steps/sec (Plaquette + Coexact sweep), L={L} Worldline, W={args.W}',
+               unit='plaquette-steps/s', kernel='plaquette_cb_pass+coexact_pass', alg_bytes=WORLDLINE_BYTES,
+               survey_bytes=WORLDLINE_BYTES, baseline=baseline)
+    Lib.sv_worldline_destroy(h)
 
 
 def run_domain(args, world, rank, local, dist):
@@ -172,6 +308,11 @@ def main():
         import torch.distributed as dist
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         dist.init_process_group('gloo', rank=rank, world_size=world)
+    if args.workload != 'villain':
+        (run_replicas if args.workload == 'replicas' else run_worldline)(args, world, rank, dist)
+        if dist:
+            dist.destroy_process_group()
+        return
     if world > 1 or args.tiles:
         run_domain(args, world, rank, local, dist)
         if dist:

@@ -362,12 +362,17 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
             wclear(ctx);
             ctx->ensure_stats(count);
             SV_HIP(hipMemsetAsync(ctx->d_stats, 0, count * sizeof(sv_stats), ctx->stream));
+            hipEvent_t ev;
+            ctx->time_begin(&ev);
             for (int k = 0; k < count; k++) launch(ctx->d_blocks + (size_t)k * nb, ctx->d_stats + k, (uint32_t)k);
+            ctx->time_end(ev, count);
             SV_HIP(hipGetLastError());
             if (!wcheck(ctx, reps)) {
+                ctx->time_collect();
                 cur = c;
                 break;
             }
+            ctx->time_discard();
             wabsorb(reps, sw, skips);
             snapshot(st, true);
         }
