@@ -130,6 +130,7 @@ struct sv_worldline {
     int32_t *order = nullptr;    // sequential plaquette: plaquettes grouped by dependency level
     int32_t *pos = nullptr;      // sequential plaquette: visit position of each plaquette
     int32_t *done = nullptr;     // (unused)
+    void *stripes = nullptr;     // striped per-sweep statistics (worldline.hip StatStripe[64][16])
     int32_t *sites = nullptr;
     int32_t ncol = 0;
     int64_t count[4] = {0, 0, 0, 0};

@@ -85,7 +85,7 @@ __device__ __forceinline__ void flush_stats(sv_stats *st, int64_t acc, double ps
     psum = wave_sum(psum);
     if ((threadIdx.x & 63) == 0) {
         atomicAdd((unsigned long long *)&st->accepted, a);
-        atomicAdd(&st->acceptance_sum, psum);
+        unsafeAtomicAdd(&st->acceptance_sum, psum);  // hardware f64 atomic (coarse-grained HBM)
     }
 }
 
@@ -728,7 +728,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     flush_stats(REPS ? A.stat + (int64_t)rep * A.rep_stat : A.stat, acc_count, psum);
     if (OBS) {
         __syncthreads();
-        if (threadIdx.x < 4) atomicAdd(&A.obs[(int64_t)rep * A.rep_obs + threadIdx.x], s_obs[threadIdx.x]);
+        if (threadIdx.x < 4) unsafeAtomicAdd(&A.obs[(int64_t)rep * A.rep_obs + threadIdx.x], s_obs[threadIdx.x]);
     }
 }
 
@@ -777,10 +777,10 @@ __global__ void villain_observables_kernel(int32_t N, double half_kappa, const d
     s_n0 = wave_sum(s_n0);
     s_n1 = wave_sum(s_n1);
     if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&out[0], half_kappa * s_act);
-        atomicAdd(&out[1], s_w2);
-        atomicAdd(&out[2], s_n0);
-        atomicAdd(&out[3], s_n1);
+        unsafeAtomicAdd(&out[0], half_kappa * s_act);
+        unsafeAtomicAdd(&out[1], s_w2);
+        unsafeAtomicAdd(&out[2], s_n0);
+        unsafeAtomicAdd(&out[3], s_n1);
     }
 }
 

@@ -53,21 +53,44 @@ __device__ __forceinline__ double wsum(double v) {
     return v;
 }
 
-__device__ __forceinline__ void wflush(sv_stats *st, int64_t acc, double psum) {
+// Per-sweep statistics are accumulated in NSTRIPE stripes (one 128-B line each) picked by workgroup:
+// thousands of short waves adding into ONE address serialize in one L2 channel (measured: ~200 us
+// per L=1024 colour pass).  fold_stripes sums them into the sweep's sv_stats in a fixed order.
+static constexpr int NSTRIPE = 16;
+struct StatStripe {
+    unsigned long long acc;
+    double psum;
+    uint64_t pad[14];
+};
+
+__device__ __forceinline__ void wflush(StatStripe *ss, int64_t acc, double psum) {
     unsigned long long a = (unsigned long long)acc;
     for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
     psum = wsum(psum);
     if ((threadIdx.x & 63) == 0) {
-        atomicAdd((unsigned long long *)&st->accepted, a);
-        atomicAdd(&st->acceptance_sum, psum);
+        StatStripe *st = ss + ((blockIdx.x + blockIdx.y * 7 + (threadIdx.x >> 6) * 3) & (NSTRIPE - 1));
+        atomicAdd(&st->acc, a);
+        unsafeAtomicAdd(&st->psum, psum);  // hardware f64 atomic (coarse-grained HBM)
     }
+}
+
+__global__ void fold_stripes(const StatStripe *ss, sv_stats *out, int count) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= count) return;
+    unsigned long long a = 0;
+    double p = 0.0;
+    for (int j = 0; j < NSTRIPE; j++) {
+        a += ss[k * NSTRIPE + j].acc;
+        p += ss[k * NSTRIPE + j].psum;
+    }
+    out[k].accepted = (int64_t)a;
+    out[k].acceptance_sum = p;
 }
 
 // delta(v)/W on link (mu, s) of a D=2 two-form v, exactly as reference_delta + coexact.py:80:
 //   dv0[s] = 0 - (-1)(v[s] - v[s-e1]),  dv1[s] = 0 - (+1)(v[s] - v[s-e0]);  then / W_eff
 template <bool VF>
-__device__ __forceinline__ double dvw_link(const void *v, int64_t N, int mu, int64_t s, double Weff) {
-    const int64_t t = s / N, x = s - t * N;
+__device__ __forceinline__ double dvw_at(const void *v, int64_t N, int mu, int64_t s, int64_t t, int64_t x, double Weff) {
     const int64_t nb = mu == 0 ? t * N + (x == 0 ? N - 1 : x - 1) : (t == 0 ? N - 1 : t - 1) * N + x;
     double d;
     if (VF) {
@@ -80,6 +103,11 @@ __device__ __forceinline__ double dvw_link(const void *v, int64_t N, int mu, int
         d = mu == 0 ? (double)(0 - (-diff)) : (double)(0 - diff);
     }
     return d / Weff;
+}
+template <bool VF>
+__device__ __forceinline__ double dvw_link(const void *v, int64_t N, int mu, int64_t s, double Weff) {
+    const int64_t t = s / N, x = s - t * N;
+    return dvw_at<VF>(v, N, mu, s, t, x, Weff);
 }
 
 struct WParams {
@@ -95,7 +123,7 @@ struct WParams {
 template <bool VF>
 __global__ __launch_bounds__(256) void coexact_pass(WParams P, int64_t *m, const void *v, const int32_t *sites,
                                                     int64_t nc, int color, const Block *blocks, const uint32_t *skips,
-                                                    const JumpTables *T, sv_stats *stat, DevScratch S,
+                                                    const JumpTables *T, StatStripe *stat, DevScratch S,
                                                     uint32_t sweep) {
     if (*(volatile const int32_t *)S.abort) return;
     const int64_t N = P.N, V = N * N;
@@ -145,7 +173,7 @@ __global__ __launch_bounds__(256) void coexact_pass(WParams P, int64_t *m, const
 template <bool VF>
 __global__ __launch_bounds__(256) void plaquette_cb_pass(WParams P, int64_t *m, void *v, const int32_t *sites,
                                                          int64_t nc, int color, const Block *blocks,
-                                                         const uint32_t *skips, const JumpTables *T, sv_stats *stat,
+                                                         const uint32_t *skips, const JumpTables *T, StatStripe *stat,
                                                          DevScratch S, uint32_t sweep) {
     if (*(volatile const int32_t *)S.abort) return;
     const int64_t N = P.N, V = N * N;
@@ -186,6 +214,158 @@ __global__ __launch_bounds__(256) void plaquette_cb_pass(WParams P, int64_t *m, 
 }
 
 // ------------------------------------------------------------------------------------------------
+// Row kernels (even N): a wave owns the colour-c sites of one row chunk of 128 columns.  Every draw of
+// the chunk is one small-table composition away from a per-row base state (one table jump per wave,
+// uniform), instead of a 4-level table jump per lane -- the same addressing as the Villain sweep.
+static constexpr int ROWW = 128;  // columns per wave
+
+__device__ __forceinline__ void row_small(Affine *sm, const JumpTables *T) {
+    for (int e = threadIdx.x; e < ROWW; e += blockDim.x) sm[e] = T->small[e];
+    __syncthreads();
+}
+
+// uniform(0, 1) draw at stream position pos of a uniform block; pos_b: the wave's base position
+__device__ __forceinline__ double row_uniform(const JumpTables *T, const Affine *sm, const Block &b, int64_t pos_b,
+                                              int64_t pos) {
+    const u128 base = jump(T, wbase(b), (uint32_t)pos_b);
+    return to_double(xsl_rr(apply(sm[pos - pos_b], base)));
+}
+
+// bounded draw d (= the colour rank) of a choice block; d_b: the wave's smallest rank.  Skip lists
+// (after a Lemire rejection) take the per-lane path.
+__device__ __forceinline__ uint32_t row_bounded(const JumpTables *T, const Affine *sm, const Block &b,
+                                                const uint32_t *skips, int64_t d, int64_t d_b, uint32_t k,
+                                                uint32_t thr, const DevScratch &S, uint32_t sweep, uint32_t bidx) {
+    if (b.nskip) return wbounded(T, b, skips, (uint32_t)d, k, thr, S, sweep, bidx);
+    const int64_t qq = d - (int64_t)b.has;
+    const int64_t wb = (d_b - (int64_t)b.has) < 0 ? 0 : ((d_b - (int64_t)b.has) >> 1);
+    const u128 base = jump(T, wbase(b), (uint32_t)wb);
+    uint32_t word;
+    if (qq < 0) {
+        word = b.buf;
+    } else {
+        const uint64_t X = xsl_rr(apply(sm[(qq >> 1) - wb], base));
+        word = (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
+    }
+    bool rej;
+    const uint32_t idx = lemire(word, k, thr, &rej);
+    if (rej) {
+        wreport(S, sweep, bidx, (uint32_t)d);
+        __builtin_amdgcn_s_waitcnt(0);
+    }
+    return idx;
+}
+
+template <bool VF>
+__global__ __launch_bounds__(256) void coexact_rows(WParams P, int64_t *m, const void *v, int color,
+                                                    const Block *blocks, const uint32_t *skips, const JumpTables *T,
+                                                    StatStripe *stat, DevScratch S, uint32_t sweep) {
+    __shared__ Affine sm[ROWW];
+    row_small(sm, T);
+    if (*(volatile const int32_t *)S.abort) return;
+    const int64_t N = P.N, V = N * N;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t tt = (int64_t)blockIdx.y * 4 + wave;
+    int64_t acc_count = 0;
+    double psum = 0.0;
+    if (tt < N) {
+        const int64_t x0 = (int64_t)blockIdx.x * ROWW;
+        const int64_t xs = x0 + ((tt + x0 + color) & 1);  // (t + x) % 2 == colour (even N)
+        const int64_t xx = xs + 2 * lane;
+        const int64_t lin_b = tt * N + xs;
+        if (xx < N && xx < x0 + ROWW) {
+            const int64_t x = tt * N + xx;
+            const int64_t tp = (tt + 1 == N) ? 0 : tt + 1, xp = (xx + 1 == N) ? 0 : xx + 1;
+            const int64_t xe0 = tp * N + xx;
+            const int64_t xe1 = tt * N + xp;
+            const double u = 0.0 + 1.0 * row_uniform(T, sm, blocks[0], lin_b, x);
+            const uint32_t j = row_bounded(T, sm, blocks[1 + color], skips, x >> 1, lin_b >> 1, P.k, P.thr, S, sweep,
+                                           1 + color);
+            const int64_t t = (int64_t)j < P.it ? (int64_t)j - P.it : (int64_t)j - P.it + 1;
+            const int mus[4] = {1, 1, 0, 0};
+            const int64_t ss[4] = {x, xe0, x, xe1};
+            const int64_t st_[4] = {tt, tp, tt, tt}, sx_[4] = {xx, xx, xx, xp};
+            const int64_t cm[4] = {-t, +t, +t, -t};
+            double dS = 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int64_t l = mus[q] * V + ss[q];
+                const double a = P.c * (double)cm[q];
+                const double f = (double)m[l] - dvw_at<VF>(v, N, mus[q], ss[q], st_[q], sx_[q], P.Weff);
+                const double b = (2.0 * f) + (double)cm[q];
+                dS += a * b;
+            }
+            double p = exp(-dS);
+            p = p < 0.0 ? 0.0 : p;
+            p = p > 1.0 ? 1.0 : p;
+            const int acc = u < p;
+            acc_count = acc;
+            psum = p;
+            if (acc) {
+                m[x] += t;
+                m[xe1] -= t;
+                m[V + x] -= t;
+                m[V + xe0] += t;
+            }
+        }
+    }
+    wflush(stat, acc_count, psum);
+}
+
+template <bool VF>
+__global__ __launch_bounds__(256) void plaquette_cb_rows(WParams P, int64_t *m, void *v, int color, const Block *blocks,
+                                                         const uint32_t *skips, const JumpTables *T, StatStripe *stat,
+                                                         DevScratch S, uint32_t sweep) {
+    __shared__ Affine sm[ROWW];
+    row_small(sm, T);
+    if (*(volatile const int32_t *)S.abort) return;
+    const int64_t N = P.N, V = N * N;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t tt = (int64_t)blockIdx.y * 4 + wave;
+    int64_t acc_count = 0;
+    double psum = 0.0;
+    if (tt < N) {
+        const int64_t x0 = (int64_t)blockIdx.x * ROWW;
+        const int64_t xs = x0 + ((tt + x0 + color) & 1);
+        const int64_t xx = xs + 2 * lane;
+        const int64_t lin_b = tt * N + xs;
+        if (xx < N && xx < x0 + ROWW) {
+            const int64_t x = tt * N + xx;
+            const int64_t tp = (tt + 1 == N) ? 0 : tt + 1, xp = (xx + 1 == N) ? 0 : xx + 1;
+            const int64_t xm = tp * N + xx;
+            const int64_t xn = tt * N + xp;
+            const double u = 0.0 + 1.0 * row_uniform(T, sm, blocks[0], lin_b, x);
+            const uint32_t jm = row_bounded(T, sm, blocks[1 + 2 * color], skips, x >> 1, lin_b >> 1, 2u, 0u, S, sweep,
+                                            1 + 2 * color);
+            const uint32_t jv = row_bounded(T, sm, blocks[2 + 2 * color], skips, x >> 1, lin_b >> 1, 3u, 1u, S, sweep,
+                                            2 + 2 * color);
+            const int64_t cm = jm ? 1 : -1, cv = (int64_t)jv - 1;
+            const double f1 = (double)m[x] - dvw_at<VF>(v, N, 0, x, tt, xx, P.Weff);
+            const double f2 = (double)m[V + xm] - dvw_at<VF>(v, N, 1, xm, tp, xx, P.Weff);
+            const double f3 = (double)m[xn] - dvw_at<VF>(v, N, 0, xn, tt, xp, P.Weff);
+            const double f4 = (double)m[V + x] - dvw_at<VF>(v, N, 1, x, tt, xx, P.Weff);
+            const double df = (double)cm - (double)cv / P.Weff;
+            const double dS = df / P.kappa * ((((f1 + f2) - f3) - f4) + 2.0 * df);
+            double p = exp(-dS);
+            p = p < 0.0 ? 0.0 : p;
+            p = p > 1.0 ? 1.0 : p;
+            const int acc = u < p;
+            acc_count = acc;
+            psum = p;
+            if (acc) {
+                m[x] += cm;
+                m[V + xm] += cm;
+                m[xn] -= cm;
+                m[V + x] -= cm;
+                if (VF) ((double *)v)[x] += (double)cv;
+                else ((int64_t *)v)[x] += cv;
+            }
+        }
+    }
+    wflush(stat, acc_count, psum);
+}
+
+// ------------------------------------------------------------------------------------------------
 // Reference-order PlaquetteUpdate: f = m - delta(v)/W once per sweep (plaquette.py:53), then one
 // launch per dependency level.  Blocks: [0] change_m (k=2, V), [1] change_v (k=3, V),
 // [2] metropolis (uniform V); the draw index of a plaquette is its visit position (plaquette.py:58-69).
@@ -203,7 +383,7 @@ __global__ void plaquette_f_init(WParams P, const int64_t *m, const void *v, dou
 template <bool VF>
 __global__ __launch_bounds__(256) void plaquette_level(WParams P, int64_t *m, void *v, double *f, const int32_t *list,
                                                        int32_t count, const int32_t *pos, const Block *blocks,
-                                                       const uint32_t *skips, const JumpTables *T, sv_stats *stat,
+                                                       const uint32_t *skips, const JumpTables *T, StatStripe *stat,
                                                        DevScratch S) {
     if (*(volatile const int32_t *)S.abort) return;
     const int64_t N = P.N, V = N * N;
@@ -362,10 +542,13 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
             wclear(ctx);
             ctx->ensure_stats(count);
             SV_HIP(hipMemsetAsync(ctx->d_stats, 0, count * sizeof(sv_stats), ctx->stream));
+            StatStripe *ss = (StatStripe *)st->stripes;
+            SV_HIP(hipMemsetAsync(ss, 0, (size_t)count * NSTRIPE * sizeof(StatStripe), ctx->stream));
             hipEvent_t ev;
             ctx->time_begin(&ev);
-            for (int k = 0; k < count; k++) launch(ctx->d_blocks + (size_t)k * nb, ctx->d_stats + k, (uint32_t)k);
+            for (int k = 0; k < count; k++) launch(ctx->d_blocks + (size_t)k * nb, ss + (size_t)k * NSTRIPE, (uint32_t)k);
             ctx->time_end(ev, count);
+            fold_stripes<<<1, 64, 0, ctx->stream>>>(ss, ctx->d_stats, count);
             SV_HIP(hipGetLastError());
             if (!wcheck(ctx, reps)) {
                 ctx->time_collect();
@@ -409,6 +592,7 @@ int sv_worldline_create(sv_ctx *ctx, int32_t N, int32_t v_is_float, sv_worldline
         SV_HIP(hipMalloc(&st->m, 2 * V * sizeof(int64_t)));
         SV_HIP(hipMalloc(&st->v, vb));
         SV_HIP(hipMalloc(&st->snap_m, 2 * V * sizeof(int64_t)));
+        SV_HIP(hipMalloc(&st->stripes, (size_t)64 * NSTRIPE * sizeof(StatStripe)));
         SV_HIP(hipMalloc(&st->snap_v, vb));
         std::vector<int32_t> sites;
         st->ncol = build_colors(N, sites, st->count, st->offset);
@@ -429,6 +613,7 @@ int sv_worldline_destroy(sv_worldline *st) {
     (void)hipFree(st->v);
     (void)hipFree(st->snap_m);
     (void)hipFree(st->snap_v);
+    (void)hipFree(st->stripes);
     (void)hipFree(st->sites);
     if (st->f) (void)hipFree(st->f);
     if (st->order) (void)hipFree(st->order);
@@ -482,7 +667,19 @@ int sv_worldline_coexact_run(sv_worldline *st, double kappa, double W_eff, int64
         std::vector<BlockSpec> specs;
         specs.push_back({UNIFORM, (uint32_t)((int64_t)st->N * st->N)});
         for (int c = 0; c < st->ncol; c++) specs.push_back({BOUNDED, (uint32_t)st->count[c]});
-        run_colour_sweeps(st, specs, sweeps, cur, inc, stats, [&](const Block *blocks, sv_stats *stat, uint32_t k) {
+        run_colour_sweeps(st, specs, sweeps, cur, inc, stats, [&](const Block *blocks, StatStripe *stat, uint32_t k) {
+            if (st->N % 2 == 0) {  // row kernels
+                const dim3 grid((unsigned)((st->N + ROWW - 1) / ROWW), (unsigned)((st->N + 3) / 4));
+                for (int c = 0; c < 2; c++) {
+                    if (st->v_is_float)
+                        coexact_rows<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips, T,
+                                                                          stat, wscratch(ctx), k);
+                    else
+                        coexact_rows<false><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips,
+                                                                           T, stat, wscratch(ctx), k);
+                }
+                return;
+            }
             for (int c = 0; c < st->ncol; c++) {
                 const int64_t nc = st->count[c];
                 if (!nc) continue;
@@ -536,7 +733,19 @@ int sv_worldline_plaquette_checkerboard_run(sv_worldline *st, double kappa, doub
             specs.push_back({BOUNDED, (uint32_t)st->count[c]});
             specs.push_back({BOUNDED, (uint32_t)st->count[c]});
         }
-        run_colour_sweeps(st, specs, sweeps, cur, inc, stats, [&](const Block *blocks, sv_stats *stat, uint32_t k) {
+        run_colour_sweeps(st, specs, sweeps, cur, inc, stats, [&](const Block *blocks, StatStripe *stat, uint32_t k) {
+            if (st->N % 2 == 0) {  // row kernels
+                const dim3 grid((unsigned)((st->N + ROWW - 1) / ROWW), (unsigned)((st->N + 3) / 4));
+                for (int c = 0; c < 2; c++) {
+                    if (st->v_is_float)
+                        plaquette_cb_rows<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks,
+                                                                               ctx->d_skips, T, stat, wscratch(ctx), k);
+                    else
+                        plaquette_cb_rows<false><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks,
+                                                                                ctx->d_skips, T, stat, wscratch(ctx), k);
+                }
+                return;
+            }
             for (int c = 0; c < st->ncol; c++) {
                 const int64_t nc = st->count[c];
                 if (!nc) continue;
@@ -625,6 +834,8 @@ int sv_worldline_plaquette_ordered_run(sv_worldline *st, double kappa, double W_
             wupload(ctx, blocks, skipvec);
             wclear(ctx);
             SV_HIP(hipMemsetAsync(ctx->d_stats, 0, sizeof(sv_stats), ctx->stream));
+            StatStripe *ss = (StatStripe *)st->stripes;
+            SV_HIP(hipMemsetAsync(ss, 0, NSTRIPE * sizeof(StatStripe), ctx->stream));
             if (st->v_is_float)
                 plaquette_f_init<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f);
             else
@@ -636,12 +847,13 @@ int sv_worldline_plaquette_ordered_run(sv_worldline *st, double kappa, double W_
                 if (st->v_is_float)
                     plaquette_level<true><<<g, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f, st->order + start[l], cnt,
                                                                       st->pos, ctx->d_blocks, ctx->d_skips, T,
-                                                                      ctx->d_stats, wscratch(ctx));
+                                                                      ss, wscratch(ctx));
                 else
                     plaquette_level<false><<<g, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f, st->order + start[l],
                                                                        cnt, st->pos, ctx->d_blocks, ctx->d_skips, T,
-                                                                       ctx->d_stats, wscratch(ctx));
+                                                                       ss, wscratch(ctx));
             }
+            fold_stripes<<<1, 64, 0, ctx->stream>>>(ss, ctx->d_stats, 1);
             SV_HIP(hipGetLastError());
             if (!wcheck(ctx, reps)) {
                 cur = c;
