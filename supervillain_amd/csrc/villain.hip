@@ -78,14 +78,28 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
+// One atomic pair per WORKGROUP (every thread must call this): same-address atomics from thousands
+// of waves serialize in one L2 channel.
 __device__ __forceinline__ void flush_stats(sv_stats *st, int64_t acc, double psum) {
-    // one atomic pair per wave
+    __shared__ unsigned long long s_acc[16];
+    __shared__ double s_ps[16];
     unsigned long long a = (unsigned long long)acc;
     for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
     psum = wave_sum(psum);
     if ((threadIdx.x & 63) == 0) {
-        atomicAdd((unsigned long long *)&st->accepted, a);
-        unsafeAtomicAdd(&st->acceptance_sum, psum);  // hardware f64 atomic (coarse-grained HBM)
+        s_acc[threadIdx.x >> 6] = a;
+        s_ps[threadIdx.x >> 6] = psum;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long ta = 0;
+        double tp = 0.0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); w++) {
+            ta += s_acc[w];
+            tp += s_ps[w];
+        }
+        atomicAdd((unsigned long long *)&st->accepted, ta);
+        unsafeAtomicAdd(&st->acceptance_sum, tp);  // hardware f64 atomic (coarse-grained HBM)
     }
 }
 
