@@ -390,7 +390,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     static_assert(!(FR && TILE), "full-row strips are for periodic lattices");
     constexpr int R = FusedGeom<NW>::R;
     constexpr int nthreads = NW * 64;
-    constexpr int PF = (NW * RW + nthreads - 1) / nthreads;  // prefetched elements per thread
+    constexpr int PF = RW / 64;  // region columns per lane (each wave moves whole rows)
     __shared__ double s_phi[R][RW];
     __shared__ double s_r0[R][RW];
     __shared__ double s_r1[R][RW];
@@ -473,46 +473,48 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
                   B[0].has == B[1].has && B[2].has == B[3].has;
     }
 
-    // ---- register prefetch of region rows [ra, ra+NW) (clipped to [t0-2, t1+2])
+    // ---- register prefetch of region rows [ra, ra+NW) (clipped to [t0-2, t1+2]): wave w moves row
+    // ra + w, lane l columns l and l + 64 (row index math is uniform per wave)
     double pf_phi[PF];
     int64_t pf_n0[PF], pf_n1[PF];
-    int pf_rr[PF], pf_cc[PF], pf_gx[PF];
+    int pf_gx[PF];
 #pragma unroll
-    for (int k = 0; k < PF; k++) {
-        const int e = threadIdx.x + k * nthreads;
-        pf_rr[k] = e / cols;
-        pf_cc[k] = e - pf_rr[k] * cols;
-        pf_gx[k] = FR ? pf_cc[k] : mcol(x0 - 2 + pf_cc[k]);
-    }
+    for (int k = 0; k < PF; k++) pf_gx[k] = FR ? lane + 64 * k : mcol(x0 - 2 + lane + 64 * k);
     auto prefetch = [&](int32_t ra) {
+        const int32_t q = ra + wave;
+        if (q >= t0 - 2 && q <= t1 + 2) {
+            const int64_t g0 = mrow(q);
 #pragma unroll
-        for (int k = 0; k < PF; k++) {
-            const int32_t q = ra + pf_rr[k];
-            if (pf_rr[k] < NW && q >= t0 - 2 && q <= t1 + 2) {
-                const int64_t g = mrow(q) + pf_gx[k];
+            for (int k = 0; k < PF; k++) {
+                if (lane + 64 * k < cols) {
+                    const int64_t g = g0 + pf_gx[k];
 #if SV_ABLATE & 16
-                pf_phi[k] = (double)(g & 7);
-                pf_n0[k] = 0;
-                pf_n1[k] = 0;
+                    pf_phi[k] = (double)(g & 7);
+                    pf_n0[k] = 0;
+                    pf_n1[k] = 0;
 #else
-                pf_phi[k] = phi_in[g];
-                pf_n0[k] = n_in[g];
-                pf_n1[k] = n_in[V + g];
+                    pf_phi[k] = phi_in[g];
+                    pf_n0[k] = n_in[g];
+                    pf_n1[k] = n_in[V + g];
 #endif
+                }
             }
         }
     };
     auto commit = [&](int32_t ra) {
+        const int32_t q = ra + wave;
+        if (q >= t0 - 2 && q <= t1 + 2) {
+            const int slot = (q - rbase) % R;
 #pragma unroll
-        for (int k = 0; k < PF; k++) {
-            const int32_t q = ra + pf_rr[k];
-            if (pf_rr[k] < NW && q >= t0 - 2 && q <= t1 + 2) {
-                const int slot = (q - rbase) % R, cc = pf_cc[k];
-                s_phi[slot][cc] = pf_phi[k];
-                const int64_t a = pf_n0[k], c = pf_n1[k];
-                if (a > (1LL << 30) || a < -(1LL << 30) || c > (1LL << 30) || c < -(1LL << 30)) s_bad = 1;
-                s_n0[slot][cc] = (int32_t)a;
-                s_n1[slot][cc] = (int32_t)c;
+            for (int k = 0; k < PF; k++) {
+                const int cc = lane + 64 * k;
+                if (cc < cols) {
+                    s_phi[slot][cc] = pf_phi[k];
+                    const int64_t a = pf_n0[k], c = pf_n1[k];
+                    if (a > (1LL << 30) || a < -(1LL << 30) || c > (1LL << 30) || c < -(1LL << 30)) s_bad = 1;
+                    s_n0[slot][cc] = (int32_t)a;
+                    s_n1[slot][cc] = (int32_t)c;
+                }
             }
         }
     };
@@ -534,36 +536,40 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     int64_t acc_count = 0;
     double psum = 0.0;
 
-    // coalesced stores of finished rows [ra, ra+NW) (clipped to the tile) from the ring
-    // e / w by multiply-shift: exact for e < 1024 and w <= 123 (checked exhaustively)
-    const uint32_t inv_w = ((1u << 20) + (uint32_t)w - 1) / (uint32_t)w;
-    static_assert(NW * FW_MAX < 1024, "store_rows reciprocal checked exact for e < 1024");
+    // coalesced stores of finished rows [ra, ra+NW) (clipped to the tile) from the ring: wave w
+    // stores row ra + w, lane l columns l and l + 64
     auto store_rows = [&](int32_t ra) {
-        const int32_t r0 = ra < t0 ? t0 : ra, r1 = ra + NW < t1 ? ra + NW : t1;
-        const int total = r1 > r0 ? (r1 - r0) * w : 0;
+        const int32_t q = ra + wave;
         double o_act = 0.0, o_w2 = 0.0, o_n0 = 0.0, o_n1 = 0.0;  // OBS partials (integers exact in f64)
-        for (int e = threadIdx.x; e < total; e += nthreads) {
-            const int rr = (int)(((uint32_t)e * inv_w) >> 20), cc = e - rr * w;  // e / w
-            const int32_t q = r0 + rr;
-            const int slot = (q - rbase) % R, cx = FR ? cc : cc + 2;
-            const int64_t g = mrow(q) + x0 + cc;  // tile sites never wrap
+        if (q >= t0 && q < t1) {
+            const int slot = (q - rbase) % R;
+            const int64_t g0 = mrow(q) + x0;  // tile sites never wrap
+#pragma unroll
+            for (int k = 0; k < PF; k++) {
+                const int cc = lane + 64 * k;
+                if (cc < w) {
+                    const int cx = FR ? cc : cc + 2;
+                    const int64_t g = g0 + cc;
 #if !(SV_ABLATE & 8)
-            phi_out[g] = s_phi[slot][cx];
-            n_out[g] = (int64_t)s_n0[slot][cx];
-            n_out[V + g] = (int64_t)s_n1[slot][cx];
+                    phi_out[g] = s_phi[slot][cx];
+                    n_out[g] = (int64_t)s_n0[slot][cx];
+                    n_out[V + g] = (int64_t)s_n1[slot][cx];
 #endif
-            if (OBS) {
-                // rows <= q+1 and columns <= x+1 are final here (villain.py:51-66, winding.py:30-37,
-                // wrapping.py:17-25): link residuals, plaquette winding dn, holonomy sums
-                const int slot1 = (q + 1 - rbase) % R;
-                const double ph = s_phi[slot][cx];
-                const double l0 = (0.0 + (s_phi[slot1][cx] - ph)) - TWO_PI * (double)s_n0[slot][cx];
-                const double l1 = (0.0 + (s_phi[slot][cxp(cx)] - ph)) - TWO_PI * (double)s_n1[slot][cx];
-                o_act += l0 * l0 + l1 * l1;
-                const int64_t dn = ((int64_t)s_n1[slot1][cx] - s_n1[slot][cx]) - ((int64_t)s_n0[slot][cxp(cx)] - s_n0[slot][cx]);
-                o_w2 += (double)(dn * dn);
-                o_n0 += (double)s_n0[slot][cx];
-                o_n1 += (double)s_n1[slot][cx];
+                    if (OBS) {
+                        // rows <= q+1 and columns <= x+1 are final here (villain.py:51-66, winding.py:30-37,
+                        // wrapping.py:17-25): link residuals, plaquette winding dn, holonomy sums
+                        const int slot1 = (q + 1 - rbase) % R;
+                        const double ph = s_phi[slot][cx];
+                        const double l0 = (0.0 + (s_phi[slot1][cx] - ph)) - TWO_PI * (double)s_n0[slot][cx];
+                        const double l1 = (0.0 + (s_phi[slot][cxp(cx)] - ph)) - TWO_PI * (double)s_n1[slot][cx];
+                        o_act += l0 * l0 + l1 * l1;
+                        const int64_t dn = ((int64_t)s_n1[slot1][cx] - s_n1[slot][cx]) -
+                                           ((int64_t)s_n0[slot][cxp(cx)] - s_n0[slot][cx]);
+                        o_w2 += (double)(dn * dn);
+                        o_n0 += (double)s_n0[slot][cx];
+                        o_n1 += (double)s_n1[slot][cx];
+                    }
+                }
             }
         }
         if (OBS) {
@@ -614,16 +620,20 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
                 const double ph = s_phi[s0][cx];
                 // r0 on the four links: f0=(0,q,x), b0=(0,q-1,x), f1=(1,q,x), b1=(1,q,x-1)
                 const int32_t n_f0 = s_n0[s0][cx], n_b0 = s_n0[sm][cx], n_f1 = s_n1[s0][cx], n_b1 = s_n1[s0][cm];
+                // r and change_r feed nothing but dS, and dS nothing but exp(-dS) (exp(+-0) = 1): the
+                // reference's `0.0 +` of d() (lattice/reference.py:9-24) only normalizes a -0.0, so it is
+                // dropped here; (0 - dphi) and dphi are never -0.0 (dphi = -pi + 2 pi u), so change_r is
+                // bit-identical anyway
                 double r0[4];
-                r0[0] = (0.0 + (s_phi[sp][cx] - ph)) - TWO_PI * (double)n_f0;
-                r0[1] = (0.0 + (ph - s_phi[sm][cx])) - TWO_PI * (double)n_b0;
-                r0[2] = (0.0 + (s_phi[s0][cp] - ph)) - TWO_PI * (double)n_f1;
-                r0[3] = (0.0 + (ph - s_phi[s0][cm])) - TWO_PI * (double)n_b1;
+                r0[0] = (s_phi[sp][cx] - ph) - TWO_PI * (double)n_f0;
+                r0[1] = (ph - s_phi[sm][cx]) - TWO_PI * (double)n_b0;
+                r0[2] = (s_phi[s0][cp] - ph) - TWO_PI * (double)n_f1;
+                r0[3] = (ph - s_phi[s0][cm]) - TWO_PI * (double)n_b1;
                 double cr[4];
-                cr[0] = (0.0 + (0.0 - D.dphi)) - TWO_PI * (double)D.cn[0];
-                cr[1] = (0.0 + (D.dphi - 0.0)) - TWO_PI * (double)D.cn[1];
-                cr[2] = (0.0 + (0.0 - D.dphi)) - TWO_PI * (double)D.cn[2];
-                cr[3] = (0.0 + (D.dphi - 0.0)) - TWO_PI * (double)D.cn[3];
+                cr[0] = (0.0 - D.dphi) - TWO_PI * (double)D.cn[0];
+                cr[1] = D.dphi - TWO_PI * (double)D.cn[1];
+                cr[2] = (0.0 - D.dphi) - TWO_PI * (double)D.cn[2];
+                cr[3] = D.dphi - TWO_PI * (double)D.cn[3];
                 double dS = 0.0;
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
@@ -642,8 +652,8 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
                 }
                 const double cphi = D.dphi * (double)acc;
                 s_phi[s0][cx] = (ph + cphi) + 0.0;  // final colour-0 phi (the colour-1 pass adds +0.0)
-                const double dcp_f = 0.0 + (0.0 - cphi);
-                const double dcp_b = 0.0 + (cphi - 0.0);
+                const double dcp_f = 0.0 - cphi;  // d(change_phi) up to the sign of a zero (see above)
+                const double dcp_b = cphi;
                 const int32_t c0 = acc ? D.cn[0] : 0, c1 = acc ? D.cn[1] : 0;
                 const int32_t c2 = acc ? D.cn[2] : 0, c3 = acc ? D.cn[3] : 0;
                 s_n0[s0][cx] = n_f0 + c0;
@@ -686,10 +696,10 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
                 ri[2] = s_r1[s0][cx];
                 ri[3] = s_r1[s0][cm];
                 double cr[4];
-                cr[0] = (0.0 + (0.0 - D.dphi)) - TWO_PI * (double)D.cn[0];
-                cr[1] = (0.0 + (D.dphi - 0.0)) - TWO_PI * (double)D.cn[1];
-                cr[2] = (0.0 + (0.0 - D.dphi)) - TWO_PI * (double)D.cn[2];
-                cr[3] = (0.0 + (D.dphi - 0.0)) - TWO_PI * (double)D.cn[3];
+                cr[0] = (0.0 - D.dphi) - TWO_PI * (double)D.cn[0];
+                cr[1] = D.dphi - TWO_PI * (double)D.cn[1];
+                cr[2] = (0.0 - D.dphi) - TWO_PI * (double)D.cn[2];
+                cr[3] = D.dphi - TWO_PI * (double)D.cn[3];
                 double dS = 0.0;
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
