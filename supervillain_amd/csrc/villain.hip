@@ -338,6 +338,64 @@ __device__ __forceinline__ Draws draws_general(const FArgs &A, const Rep &RP, in
 // forward/backward pair).  4 compositions per site: the fwd and bwd choice blocks of a direction
 // read the SAME u64 word for two adjacent lanes (its two 32-bit halves), so each lane of a pair
 // computes one block's word and swaps the other half with its partner.
+// Per-lane constants of the fast draws, packed in one register per colour: the small-table offsets of
+// the metropolis (bits 0-6), dphi (7-13) and the two choice words (14-20, 21-27) and which half of
+// each word pair the lane computes (28, 29).  They are the same for every row a wave visits (rows
+// advance NW = 4 at a time, so every parity involved is fixed), hence computed once per kernel.
+__device__ __forceinline__ uint32_t fast_pack(const uint32_t *hasw, int32_t lane, uint32_t rowlin, uint32_t xs,
+                                              uint32_t gx, uint32_t xb) {
+    const uint32_t lin = rowlin + gx, rank = lin >> 1;
+    const uint32_t PR = (rowlin + xb) >> 1;
+    uint32_t pk = ((gx - xb) & (SMALL_LDS - 1)) | (((rank - PR) & (SMALL_LDS - 1)) << 7);
+    const uint32_t R0 = (rowlin + xs) >> 1;  // rank of lane 0
+#pragma unroll
+    for (int mu = 0; mu < 2; mu++) {
+        const uint32_t h = hasw[mu];
+        const uint32_t P = (R0 - h) & 1u;   // pairing parity of the row
+        const uint32_t PW = (PR - h) >> 1;  // word index of the row base
+        uint32_t qq = rank - h;
+        if (lane == 63 && P) qq = R0 - h;  // lane 63 serves lane 0's word
+        const uint32_t half = (lane == 63 && P) ? 0u : (qq & 1u);
+        pk |= (((qq >> 1) - PW) & (SMALL_LDS - 1)) << (14 + 7 * mu);
+        pk |= half << (28 + mu);
+    }
+    return pk;
+}
+
+__device__ __forceinline__ Draws draws_fastp(const FArgs &A, const Rep &RP, int c, bool active, int32_t lane,
+                                             uint32_t pk, uint32_t rank, const u128 *bases, const Affine *sm) {
+    const int bb = 1 + 5 * c;
+    Draws D;
+    {
+        const u128 st = sv_apply(sm[pk & (SMALL_LDS - 1)], bases[0]);
+        D.u = 0.0 + 1.0 * to_double(xsl_rr(st));
+    }
+    {
+        const u128 st = sv_apply(sm[(pk >> 7) & (SMALL_LDS - 1)], bases[1]);
+        D.dphi = A.P.lo_phi + A.P.range_phi * to_double(xsl_rr(st));
+    }
+    D.cn[0] = D.cn[1] = D.cn[2] = D.cn[3] = 0;
+    if (!(SV_ABLATE & 64) && A.P.k > 1) {
+#pragma unroll
+        for (int mu = 0; mu < 2; mu++) {
+            const uint32_t half = (pk >> (28 + mu)) & 1u;
+            const u128 st = sv_apply(sm[(pk >> (14 + 7 * mu)) & (SMALL_LDS - 1)], half ? bases[3 + 2 * mu] : bases[2 + 2 * mu]);
+            const uint64_t X = xsl_rr(st);
+            // lo lanes computed the fwd word (send its high half), hi lanes the bwd word (send its low half)
+            const uint32_t send = half ? (uint32_t)X : (uint32_t)(X >> 32);
+            const int partner = half ? ((lane - 1) & 63) : lane + 1;
+            const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute(partner << 2, (int)send);
+            const uint32_t wf = half ? got : (uint32_t)X;
+            const uint32_t wb = half ? (uint32_t)(X >> 32) : got;
+            if (active) {
+                D.cn[2 * mu] = choice_value(A, RP, wf, (uint32_t)(bb + 1 + 2 * mu), rank);
+                D.cn[2 * mu + 1] = choice_value(A, RP, wb, (uint32_t)(bb + 2 + 2 * mu), rank);
+            }
+        }
+    }
+    return D;
+}
+
 __device__ __forceinline__ Draws draws_fast(const FArgs &A, const Rep &RP, int c, const uint32_t *hasw, bool active,
                                             int32_t lane, uint32_t rowlin,
                                             uint32_t xs, uint32_t gx, uint32_t xb, const u128 *bases,
@@ -533,6 +591,21 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     __builtin_amdgcn_s_waitcnt(0);
     if (base_lane) s_base[wave][lane] = bases;
 
+    // fast-draw lane constants per colour (valid for every row of this wave, see fast_pack)
+    uint32_t pk0 = 0, pk1 = 0;
+    if (fast[0]) {
+        const int32_t q = tfirst + 2 + wave;
+        const int32_t xs = (x0 - 1) + ((par0 + q + x0 - 1) & 1);
+        pk0 = fast_pack(has_c0, lane, (uint32_t)grow(q) * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
+                        (uint32_t)(Gm.X0 + xs + 2 * lane), (uint32_t)xb);
+    }
+    if (fast[1]) {
+        const int32_t q = tfirst + 1 + wave;
+        const int32_t xs = x0 + ((par0 + q + x0 + 1) & 1);
+        pk1 = fast_pack(has_c1, lane, (uint32_t)grow(q) * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
+                        (uint32_t)(Gm.X0 + xs + 2 * lane), (uint32_t)xb);
+    }
+
     int64_t acc_count = 0;
     double psum = 0.0;
 
@@ -608,8 +681,8 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             for (int k = 0; k < 6; k++) bs[k] = s_base[wave][k];
             Draws D;
             if (fast[0])
-                D = draws_fast(A, RL, 0, has_c0, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
-                               (uint32_t)(Gm.X0 + x), (uint32_t)xb, bs, s_small);
+                D = draws_fastp(A, RL, 0, active, lane, pk0, ((uint32_t)gq * (uint32_t)Nx + (uint32_t)(Gm.X0 + x)) >> 1,
+                                bs, s_small);
             else
                 D = draws_general(A, RL, 0, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small, edge, xw,
                                   &s_base[wave][16]);
@@ -680,8 +753,8 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             for (int k = 0; k < 6; k++) bs[k] = s_base[wave][8 + k];
             Draws D;
             if (fast[1])
-                D = draws_fast(A, RL, 1, has_c1, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
-                               (uint32_t)(Gm.X0 + x), (uint32_t)xb, bs, s_small);
+                D = draws_fastp(A, RL, 1, active, lane, pk1, ((uint32_t)gq * (uint32_t)Nx + (uint32_t)(Gm.X0 + x)) >> 1,
+                                bs, s_small);
             else
                 D = draws_general(A, RL, 1, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small, edge, xw,
                                   &s_base[wave][24]);
