@@ -52,6 +52,8 @@ def parse():
     ap.add_argument('--tiles', default=None, help='tile grid TYxTX (default from N); with N=1 emulates the '
                                                    'decomposition on one GPU')
     ap.add_argument('--workload', default='villain', choices=['villain', 'replicas', 'worldline'])
+    ap.add_argument('--event-timing', default='batch', choices=['launch', 'batch'],
+                    help='hipEvents around each batch of 64 fused launches (default) or around every launch')
     ap.add_argument('--replicas', type=int, default=1024, help='replicas workload: total replica count')
     args = ap.parse_args()
     if args.workload == 'replicas':
@@ -340,7 +342,7 @@ def main():
 
     if args.warmup:
         run(args.warmup)
-    Lib.sv_ctx_set_timing(ctx.handle, 1)
+    Lib.sv_ctx_set_timing(ctx.handle, 2 if args.event_timing == 'launch' else 1)
     t0 = time.perf_counter()
     st = run(args.steps)  # synchronous on return (stream synchronized)
     t1 = time.perf_counter()

@@ -55,9 +55,10 @@ int sv_ctx_create(int device, sv_ctx **out);
 int sv_ctx_destroy(sv_ctx *ctx);
 const char *sv_last_error(sv_ctx *ctx);
 int sv_device_count(void);
-/* Measurement hooks: when enabled, each batch of back-to-back sweep-kernel launches is bracketed by
- * hipEvents on the context's stream; sv_ctx_kernel_time returns the summed device time and the
- * number of launches since enable (batches that hit a Lemire rejection are not counted). */
+/* Measurement hooks: enable = 1 brackets each batch of back-to-back sweep-kernel launches with
+ * hipEvents on the context's stream, enable = 2 brackets every single-lattice fused launch;
+ * sv_ctx_kernel_time returns the summed device time and the number of launches since enable
+ * (batches that hit a Lemire rejection are not counted). */
 int sv_ctx_set_timing(sv_ctx *ctx, int32_t enable);
 int sv_ctx_kernel_time(sv_ctx *ctx, double *ms_total, int64_t *launches);
 const char *sv_build_info(void);

@@ -99,6 +99,7 @@ extern "C" {
 int sv_ctx_set_timing(sv_ctx *ctx, int32_t enable) {
     if (!ctx) return -1;
     ctx->timing = enable != 0;
+    ctx->timing_mode = enable;
     ctx->timed_ms = 0.0;
     ctx->timed_launches = 0;
     return 0;

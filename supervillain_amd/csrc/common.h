@@ -86,6 +86,7 @@ struct sv_ctx {
     size_t h_blocks_cap = 0;
     // optional per-launch timing of the sweep kernels (hipEvents on ctx->stream)
     bool timing = false;
+    int timing_mode = 0;  // 1: events around each batch of launches, 2: around every launch
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
     std::vector<int64_t> ev_launches;

@@ -1119,8 +1119,11 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         SV_HIP(hipMemsetAsync(ctx->d_stats, 0, count * sizeof(sv_stats), ctx->stream));
         const int cur0 = st->cur;
         hipEvent_t ev;
-        ctx->time_begin(&ev);
+        const bool per_launch = ctx->timing_mode == 2;  // events around every launch, else around the batch
+        if (!per_launch) ctx->time_begin(&ev);
         for (int k = 0; k < count; k++) {
+            hipEvent_t ev1;
+            if (per_launch) ctx->time_begin(&ev1);
             FArgs A;
             A.P = P;
             A.G = FGeom{N, N, 0, 0, N, N, N, V, 0};
@@ -1143,9 +1146,10 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             farg_single(A, nsx, nsy);
             if (NWv == 6) villain_sweep_fused<6, false, false, false><<<grid, 6 * 64, 0, ctx->stream>>>(A);
             else villain_sweep_fused<4, false, false, false><<<grid, 4 * 64, 0, ctx->stream>>>(A);
+            if (per_launch) ctx->time_end(ev1, 1);
             st->cur ^= 1;
         }
-        ctx->time_end(ev, count);
+        if (!per_launch) ctx->time_end(ev, count);
         SV_HIP(hipGetLastError());
         auto tp2 = std::chrono::steady_clock::now();
         AbortInfo a = read_abort(ctx);
