@@ -208,14 +208,10 @@ def run_worldline(args, world, rank, dist):
     Weff = float(args.W)
 
     def step(k):
-        st = _native.stats_array(1)
-        acc = 0
-        for _ in range(k):
-            ctx.check(Lib.sv_worldline_plaquette_checkerboard_run(h, args.kappa, Weff, 1, ctypes.byref(r), st),
-                      'plaquette')
-            acc += st[0].accepted
-            ctx.check(Lib.sv_worldline_coexact_run(h, args.kappa, Weff, 1, 1, ctypes.byref(r), st), 'coexact')
-        return acc
+        st = _native.stats_array(2 * k)  # one call: Sequentially(Plaquette, Coexact) x k on the device
+        ctx.check(Lib.sv_worldline_plaquette_coexact_run(h, args.kappa, Weff, 1, k, ctypes.byref(r), st),
+                  'sv_worldline_plaquette_coexact_run')
+        return sum(st[2 * i].accepted for i in range(k))  # Plaquette acceptances
 
     if args.warmup:
         step(args.warmup)

@@ -108,6 +108,11 @@ int sv_worldline_plaquette_ordered_run(sv_worldline *st, double kappa, double W_
  * random sequential order.  `sweeps` consecutive sweeps. */
 int sv_worldline_plaquette_checkerboard_run(sv_worldline *st, double kappa, double W_eff, int32_t sweeps, sv_rng *rng,
                                             sv_stats *stats);
+/* Sequentially(PlaquetteUpdate [checkerboard], CoexactUpdate) (combining.py:38-40) for `sweeps` steps in one
+ * call, both generators drawing from the same Generator (G1.rng is G2.rng); stats has 2 * sweeps entries:
+ * [2 s] the Plaquette sweep of step s, [2 s + 1] its Coexact sweep. */
+int sv_worldline_plaquette_coexact_run(sv_worldline *st, double kappa, double W_eff, int64_t interval_t, int32_t sweeps,
+                                       sv_rng *rng, sv_stats *stats);
 int sv_worldline_plaquette(sv_ctx *ctx, int32_t N, double kappa, double W_eff, int64_t *m, void *v,
                            int32_t v_is_float, const int64_t *order, sv_rng *rng, sv_stats *stats);
 

@@ -519,11 +519,14 @@ void snapshot(sv_worldline *st, bool restore) {
 }
 
 // Batched colour-pass runner with snapshot + replay on a rejection.
+// nstat statistics per sweep (a combined Plaquette + Coexact step has two); block b's rejections are
+// counted in statistic stat_of[b].
 template <typename Launch>
 void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, int32_t sweeps, Cursor &cur, u128 inc,
-                       sv_stats *stats, Launch launch) {
+                       sv_stats *stats, Launch launch, int nstat = 1, std::vector<int> stat_of = {}) {
     sv_ctx *ctx = st->ctx;
     const int nb = (int)specs.size();
+    if (stat_of.empty()) stat_of.assign(nb, 0);
     const int64_t V = (int64_t)st->N * st->N;
     const int BATCH = 64;
     SkipMap skips;
@@ -540,15 +543,16 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
             wplan(c, inc, specs, sw, count, skips, blocks, skipvec);
             wupload(ctx, blocks, skipvec);
             wclear(ctx);
-            ctx->ensure_stats(count);
-            SV_HIP(hipMemsetAsync(ctx->d_stats, 0, count * sizeof(sv_stats), ctx->stream));
+            ctx->ensure_stats((size_t)count * nstat);
+            SV_HIP(hipMemsetAsync(ctx->d_stats, 0, (size_t)count * nstat * sizeof(sv_stats), ctx->stream));
             StatStripe *ss = (StatStripe *)st->stripes;
-            SV_HIP(hipMemsetAsync(ss, 0, (size_t)count * NSTRIPE * sizeof(StatStripe), ctx->stream));
+            SV_HIP(hipMemsetAsync(ss, 0, (size_t)count * nstat * NSTRIPE * sizeof(StatStripe), ctx->stream));
             hipEvent_t ev;
             ctx->time_begin(&ev);
-            for (int k = 0; k < count; k++) launch(ctx->d_blocks + (size_t)k * nb, ss + (size_t)k * NSTRIPE, (uint32_t)k);
+            for (int k = 0; k < count; k++)
+                launch(ctx->d_blocks + (size_t)k * nb, ss + (size_t)k * nstat * NSTRIPE, (uint32_t)k);
             ctx->time_end(ev, count);
-            fold_stripes<<<1, 64, 0, ctx->stream>>>(ss, ctx->d_stats, count);
+            fold_stripes<<<(count * nstat + 63) / 64, 64, 0, ctx->stream>>>(ss, ctx->d_stats, count * nstat);
             SV_HIP(hipGetLastError());
             if (!wcheck(ctx, reps)) {
                 ctx->time_collect();
@@ -559,19 +563,96 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
             wabsorb(reps, sw, skips);
             snapshot(st, true);
         }
-        SV_HIP(hipMemcpyAsync(stats + sw, ctx->d_stats, count * sizeof(sv_stats), hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipMemcpyAsync(stats + (size_t)sw * nstat, ctx->d_stats, (size_t)count * nstat * sizeof(sv_stats),
+                              hipMemcpyDeviceToHost, ctx->stream));
         SV_HIP(hipStreamSynchronize(ctx->stream));
         for (int k = 0; k < count; k++) {
-            stats[sw + k].proposed = V;
-            int64_t rj = 0;
+            for (int j = 0; j < nstat; j++) {
+                stats[(size_t)(sw + k) * nstat + j].proposed = V;
+                stats[(size_t)(sw + k) * nstat + j].rejections = 0;
+            }
             for (int bi = 0; bi < nb; bi++) {
                 auto it = skips.find({sw + k, bi});
-                if (it != skips.end()) rj += (int64_t)it->second.size();
+                if (it != skips.end()) stats[(size_t)(sw + k) * nstat + stat_of[bi]].rejections += (int64_t)it->second.size();
             }
-            stats[sw + k].rejections = rj;
         }
         sw += count;
     }
+}
+
+// one CoexactUpdate sweep's colour passes (blocks: [0] metropolis, [1 + c] t of colour c)
+void launch_coexact(sv_worldline *st, const WParams &P, const Block *blocks, StatStripe *stat, uint32_t k,
+                    const JumpTables *T) {
+    sv_ctx *ctx = st->ctx;
+    if (st->N % 2 == 0) {  // row kernels
+        const dim3 grid((unsigned)((st->N + ROWW - 1) / ROWW), (unsigned)((st->N + 3) / 4));
+        for (int c = 0; c < 2; c++) {
+            if (st->v_is_float)
+                coexact_rows<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips, T, stat,
+                                                                  wscratch(ctx), k);
+            else
+                coexact_rows<false><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips, T, stat,
+                                                                   wscratch(ctx), k);
+        }
+        return;
+    }
+    for (int c = 0; c < st->ncol; c++) {
+        const int64_t nc = st->count[c];
+        if (!nc) continue;
+        const int grid = (int)((nc + 255) / 256);
+        if (st->v_is_float)
+            coexact_pass<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->sites + st->offset[c], nc, c, blocks,
+                                                              ctx->d_skips, T, stat, wscratch(ctx), k);
+        else
+            coexact_pass<false><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->sites + st->offset[c], nc, c, blocks,
+                                                               ctx->d_skips, T, stat, wscratch(ctx), k);
+    }
+}
+
+// one checkerboard PlaquetteUpdate sweep (blocks: [0] metropolis, [1 + 2c] change_m, [2 + 2c] change_v)
+void launch_plaquette_cb(sv_worldline *st, const WParams &P, const Block *blocks, StatStripe *stat, uint32_t k,
+                         const JumpTables *T) {
+    sv_ctx *ctx = st->ctx;
+    if (st->N % 2 == 0) {  // row kernels
+        const dim3 grid((unsigned)((st->N + ROWW - 1) / ROWW), (unsigned)((st->N + 3) / 4));
+        for (int c = 0; c < 2; c++) {
+            if (st->v_is_float)
+                plaquette_cb_rows<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips, T,
+                                                                       stat, wscratch(ctx), k);
+            else
+                plaquette_cb_rows<false><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips, T,
+                                                                        stat, wscratch(ctx), k);
+        }
+        return;
+    }
+    for (int c = 0; c < st->ncol; c++) {
+        const int64_t nc = st->count[c];
+        if (!nc) continue;
+        const int grid = (int)((nc + 255) / 256);
+        if (st->v_is_float)
+            plaquette_cb_pass<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->sites + st->offset[c], nc, c,
+                                                                   blocks, ctx->d_skips, T, stat, wscratch(ctx), k);
+        else
+            plaquette_cb_pass<false><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->sites + st->offset[c], nc, c,
+                                                                    blocks, ctx->d_skips, T, stat, wscratch(ctx), k);
+    }
+}
+
+std::vector<BlockSpec> coexact_specs(const sv_worldline *st) {
+    std::vector<BlockSpec> specs;
+    specs.push_back({UNIFORM, (uint32_t)((int64_t)st->N * st->N)});
+    for (int c = 0; c < st->ncol; c++) specs.push_back({BOUNDED, (uint32_t)st->count[c]});
+    return specs;
+}
+
+std::vector<BlockSpec> plaquette_cb_specs(const sv_worldline *st) {
+    std::vector<BlockSpec> specs;
+    specs.push_back({UNIFORM, (uint32_t)((int64_t)st->N * st->N)});
+    for (int c = 0; c < st->ncol; c++) {
+        specs.push_back({BOUNDED, (uint32_t)st->count[c]});
+        specs.push_back({BOUNDED, (uint32_t)st->count[c]});
+    }
+    return specs;
 }
 
 }  // namespace
@@ -592,7 +673,7 @@ int sv_worldline_create(sv_ctx *ctx, int32_t N, int32_t v_is_float, sv_worldline
         SV_HIP(hipMalloc(&st->m, 2 * V * sizeof(int64_t)));
         SV_HIP(hipMalloc(&st->v, vb));
         SV_HIP(hipMalloc(&st->snap_m, 2 * V * sizeof(int64_t)));
-        SV_HIP(hipMalloc(&st->stripes, (size_t)64 * NSTRIPE * sizeof(StatStripe)));
+        SV_HIP(hipMalloc(&st->stripes, (size_t)2 * 64 * NSTRIPE * sizeof(StatStripe)));  // batch x 2 stats
         SV_HIP(hipMalloc(&st->snap_v, vb));
         std::vector<int32_t> sites;
         st->ncol = build_colors(N, sites, st->count, st->offset);
@@ -664,36 +745,8 @@ int sv_worldline_coexact_run(sv_worldline *st, double kappa, double W_eff, int64
         u128 inc{rng->inc_lo, rng->inc_hi};
         Cursor cur{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
         const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
-        std::vector<BlockSpec> specs;
-        specs.push_back({UNIFORM, (uint32_t)((int64_t)st->N * st->N)});
-        for (int c = 0; c < st->ncol; c++) specs.push_back({BOUNDED, (uint32_t)st->count[c]});
-        run_colour_sweeps(st, specs, sweeps, cur, inc, stats, [&](const Block *blocks, StatStripe *stat, uint32_t k) {
-            if (st->N % 2 == 0) {  // row kernels
-                const dim3 grid((unsigned)((st->N + ROWW - 1) / ROWW), (unsigned)((st->N + 3) / 4));
-                for (int c = 0; c < 2; c++) {
-                    if (st->v_is_float)
-                        coexact_rows<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips, T,
-                                                                          stat, wscratch(ctx), k);
-                    else
-                        coexact_rows<false><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips,
-                                                                           T, stat, wscratch(ctx), k);
-                }
-                return;
-            }
-            for (int c = 0; c < st->ncol; c++) {
-                const int64_t nc = st->count[c];
-                if (!nc) continue;
-                const int grid = (int)((nc + 255) / 256);
-                if (st->v_is_float)
-                    coexact_pass<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->sites + st->offset[c], nc,
-                                                                      c, blocks, ctx->d_skips, T, stat,
-                                                                      wscratch(ctx), k);
-                else
-                    coexact_pass<false><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->sites + st->offset[c], nc,
-                                                                       c, blocks, ctx->d_skips, T, stat,
-                                                                       wscratch(ctx), k);
-            }
-        });
+        run_colour_sweeps(st, coexact_specs(st), sweeps, cur, inc, stats,
+                          [&](const Block *blocks, StatStripe *stat, uint32_t k) { launch_coexact(st, P, blocks, stat, k, T); });
         rng->state_hi = cur.s.hi;
         rng->state_lo = cur.s.lo;
         rng->has_uint32 = (int32_t)cur.has;
@@ -727,39 +780,46 @@ int sv_worldline_plaquette_checkerboard_run(sv_worldline *st, double kappa, doub
         u128 inc{rng->inc_lo, rng->inc_hi};
         Cursor cur{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
         const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
-        std::vector<BlockSpec> specs;
-        specs.push_back({UNIFORM, (uint32_t)((int64_t)st->N * st->N)});
-        for (int c = 0; c < st->ncol; c++) {
-            specs.push_back({BOUNDED, (uint32_t)st->count[c]});
-            specs.push_back({BOUNDED, (uint32_t)st->count[c]});
-        }
-        run_colour_sweeps(st, specs, sweeps, cur, inc, stats, [&](const Block *blocks, StatStripe *stat, uint32_t k) {
-            if (st->N % 2 == 0) {  // row kernels
-                const dim3 grid((unsigned)((st->N + ROWW - 1) / ROWW), (unsigned)((st->N + 3) / 4));
-                for (int c = 0; c < 2; c++) {
-                    if (st->v_is_float)
-                        plaquette_cb_rows<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks,
-                                                                               ctx->d_skips, T, stat, wscratch(ctx), k);
-                    else
-                        plaquette_cb_rows<false><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks,
-                                                                                ctx->d_skips, T, stat, wscratch(ctx), k);
-                }
-                return;
-            }
-            for (int c = 0; c < st->ncol; c++) {
-                const int64_t nc = st->count[c];
-                if (!nc) continue;
-                const int grid = (int)((nc + 255) / 256);
-                if (st->v_is_float)
-                    plaquette_cb_pass<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->sites + st->offset[c],
-                                                                           nc, c, blocks, ctx->d_skips, T, stat,
-                                                                           wscratch(ctx), k);
-                else
-                    plaquette_cb_pass<false><<<grid, 256, 0, ctx->stream>>>(
-                        P, st->m, st->v, st->sites + st->offset[c], nc, c, blocks, ctx->d_skips, T, stat,
-                        wscratch(ctx), k);
-            }
-        });
+        run_colour_sweeps(st, plaquette_cb_specs(st), sweeps, cur, inc, stats,
+                          [&](const Block *blocks, StatStripe *stat, uint32_t k) { launch_plaquette_cb(st, P, blocks, stat, k, T); });
+        rng->state_hi = cur.s.hi;
+        rng->state_lo = cur.s.lo;
+        rng->has_uint32 = (int32_t)cur.has;
+        rng->uinteger = cur.buf;
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
+// Sequentially(PlaquetteUpdate checkerboard, CoexactUpdate) for `sweeps` steps in one call, the two
+// generators drawing from ONE Generator (G1.rng is G2.rng) in the order Sequentially.step
+// (combining.py:38-40) calls them; stats[2 s] is the Plaquette sweep of step s, stats[2 s + 1] the
+// Coexact sweep.
+int sv_worldline_plaquette_coexact_run(sv_worldline *st, double kappa, double W_eff, int64_t interval_t, int32_t sweeps,
+                                       sv_rng *rng, sv_stats *stats) {
+    if (!st || !rng || (sweeps > 0 && !stats)) return -1;
+    sv_ctx *ctx = st->ctx;
+    try {
+        if (interval_t < 1 || interval_t > (1 << 20)) throw std::invalid_argument("interval_t must be in [1, 2^20]");
+        SV_HIP(hipSetDevice(ctx->device));
+        const WParams Pp = wparams(st->N, kappa, W_eff, 1), Pc = wparams(st->N, kappa, W_eff, interval_t);
+        u128 inc{rng->inc_lo, rng->inc_hi};
+        Cursor cur{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
+        const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
+        std::vector<BlockSpec> specs = plaquette_cb_specs(st);
+        const int np = (int)specs.size();
+        for (const BlockSpec &b : coexact_specs(st)) specs.push_back(b);
+        std::vector<int> stat_of(specs.size(), 0);
+        for (size_t b = np; b < specs.size(); b++) stat_of[b] = 1;
+        run_colour_sweeps(
+            st, specs, sweeps, cur, inc, stats,
+            [&](const Block *blocks, StatStripe *stat, uint32_t k) {
+                launch_plaquette_cb(st, Pp, blocks, stat, k, T);
+                launch_coexact(st, Pc, blocks + np, stat + NSTRIPE, k, T);
+            },
+            2, stat_of);
         rng->state_hi = cur.s.hi;
         rng->state_lo = cur.s.lo;
         rng->has_uint32 = (int32_t)cur.has;

@@ -154,3 +154,41 @@ def test_plaquette_checkerboard_oracle(N, W, oracle_lib):
     assert G.rng.bit_generator.state == g.bit_generator.state
     assert G.accepted == sum(s.accepted for s in st)
     assert S.valid(cfg)
+
+
+@pytest.mark.parametrize('N,W,sweeps', [(8, 1, 5), (9, 2, 4), (128, 1, 70), (64, float('inf'), 3)])
+def test_plaquette_coexact_steps_oracle(N, W, sweeps, oracle_lib):
+    """sv_worldline_plaquette_coexact_run: Sequentially(checkerboard Plaquette, Coexact) with one shared
+    Generator, `sweeps` steps in one device call (crossing the 64-sweep batch at N=128), against the
+    oracle run sweep by sweep in the same order."""
+    import ctypes
+    from supervillain_amd import _native
+    from supervillain_amd._abi import rng_from_numpy, rng_to_numpy
+    vf = W == float('inf')
+    Weff = 2 * np.pi if vf else float(W)
+    r0 = np.random.default_rng(N + 1)
+    v0 = (r0.uniform(-2, 2, (N, N)) if vf else r0.integers(-2, 3, (N, N))).astype(np.float64 if vf else np.int64)
+    m0 = np.zeros((2, N, N), dtype=np.int64)
+    Lib = _native.lib()
+    ctx = _native.context(_native.default_device())
+    h = ctypes.c_void_p()
+    ctx.check(Lib.sv_worldline_create(ctx.handle, N, int(vf), ctypes.byref(h)), 'create')
+    ctx.check(Lib.sv_worldline_upload(h, _native.ptr(m0), _native.ptr(v0)), 'upload')
+    gen = np.random.default_rng(7)
+    r = rng_from_numpy(gen)
+    st = _native.stats_array(2 * sweeps)
+    ctx.check(Lib.sv_worldline_plaquette_coexact_run(h, 0.5, Weff, 1, sweeps, ctypes.byref(r), st), 'run')
+    rng_to_numpy(r, gen)
+    m, v = np.empty_like(m0), np.empty_like(v0)
+    ctx.check(Lib.sv_worldline_download(h, _native.ptr(m), _native.ptr(v)), 'download')
+    Lib.sv_worldline_destroy(h)
+    g = np.random.default_rng(7)
+    mm, vv = m0.copy(), v0.copy()
+    for s in range(sweeps):
+        sp = oracle_lib.worldline_plaquette_cb(N, 0.5, Weff, mm, vv, 1, g)[0]
+        sc = oracle_lib.worldline_coexact(N, 0.5, Weff, mm, vv, 1, g)[0]
+        assert st[2 * s].accepted == sp.accepted and st[2 * s + 1].accepted == sc.accepted, s
+        np.testing.assert_allclose([st[2 * s].acceptance_sum, st[2 * s + 1].acceptance_sum],
+                                   [sp.acceptance_sum, sc.acceptance_sum], rtol=1e-12)
+    assert (m == mm).all() and (v == vv).all()
+    assert gen.bit_generator.state == g.bit_generator.state
