@@ -35,6 +35,10 @@ def lib():
         L.sv_o_worldline_coexact.argtypes = [i32, f64, f64, i64, vp, vp, i32, i32, P(SvRng), vp]
         L.sv_o_worldline_plaquette_seq.argtypes = [i32, f64, f64, vp, vp, i32, vp, P(SvRng), vp]
         L.sv_o_worldline_plaquette_cb.argtypes = [i32, f64, f64, vp, vp, i32, i32, P(SvRng), vp]
+        L.sv_o_villain_site.argtypes = [i32, f64, f64, vp, vp, i32, P(SvRng), vp]
+        L.sv_o_villain_link.argtypes = [i32, f64, i64, i64, vp, vp, i32, P(SvRng), vp]
+        L.sv_o_villain_exact.argtypes = [i32, f64, i64, vp, vp, i32, P(SvRng), vp]
+        L.sv_o_villain_cohomology.argtypes = [i32, f64, i64, vp, vp, i32, P(SvRng), vp]
         _LIB = L
     return _LIB
 
@@ -142,6 +146,33 @@ def worldline_plaquette_cb(N, kappa, W_eff, m, v, sweeps, gen):
     st = _stats_array(sweeps)
     rc = lib().sv_o_worldline_plaquette_cb(N, kappa, float(W_eff), _ptr(m), _ptr(v), v_is_float, sweeps,
                                            ctypes.byref(r), st)
+    if rc != 0:
+        raise ValueError('oracle rejected the arguments')
+    rng_to_numpy(r, gen)
+    return [st[i] for i in range(sweeps)]
+
+
+def villain_generator(kind, N, kappa, W, phi, n, sweeps, gen, interval=None):
+    """Run `sweeps` steps of a SURVEY.md 8(f) Villain generator ('SiteUpdate', 'LinkUpdate',
+    'ExactUpdate', 'CohomologyUpdate') in place on (phi (N,N) f64, n (2,N,N) i64)."""
+    assert phi.dtype == np.float64 and n.dtype == np.int64 and phi.flags.c_contiguous and n.flags.c_contiguous
+    r = rng_from_numpy(gen)
+    st = _stats_array(sweeps)
+    L = lib()
+    if kind == 'SiteUpdate':
+        rc = L.sv_o_villain_site(N, kappa, np.pi if interval is None else float(interval), _ptr(phi), _ptr(n), sweeps,
+                                 ctypes.byref(r), st)
+    elif kind == 'LinkUpdate':
+        rc = L.sv_o_villain_link(N, kappa, int(W), 1 if interval is None else int(interval), _ptr(phi), _ptr(n), sweeps,
+                                 ctypes.byref(r), st)
+    elif kind == 'ExactUpdate':
+        rc = L.sv_o_villain_exact(N, kappa, 1 if interval is None else int(interval), _ptr(phi), _ptr(n), sweeps,
+                                  ctypes.byref(r), st)
+    elif kind == 'CohomologyUpdate':
+        rc = L.sv_o_villain_cohomology(N, kappa, 1 if interval is None else int(interval), _ptr(phi), _ptr(n), sweeps,
+                                       ctypes.byref(r), st)
+    else:
+        raise ValueError(kind)
     if rc != 0:
         raise ValueError('oracle rejected the arguments')
     rng_to_numpy(r, gen)

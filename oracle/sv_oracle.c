@@ -570,3 +570,219 @@ int sv_o_worldline_plaquette_cb(int32_t N_, double kappa, double Weff, int64_t *
     colors_free(&C);
     return 0;
 }
+
+/* ================================================================ SURVEY.md 8(f) Villain generators */
+#define PI_D 3.141592653589793 /* np.pi */
+
+/* NumPy's float64 pairwise sum of a contiguous array (np.sum of a 1-D array; checked against
+ * numpy 2.2 for n = 1..299, 513, 1000, 4096 by tools/make_golden.py's author). */
+static double np_pairwise_sum(const double *a, int64_t n) {
+    if (n < 8) {
+        double res = 0.0;
+        for (int64_t i = 0; i < n; i++) res += a[i];
+        return res;
+    } else if (n <= 128) {
+        double r[8];
+        for (int j = 0; j < 8; j++) r[j] = a[j];
+        int64_t i;
+        for (i = 8; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; j++) r[j] += a[i + j];
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; i++) res += a[i];
+        return res;
+    } else {
+        int64_t n2 = n / 2;
+        n2 -= n2 % 8;
+        return np_pairwise_sum(a, n2) + np_pairwise_sum(a + n2, n - n2);
+    }
+}
+
+/* value of choice index j among (-iv..-1, 1..iv): link.py:44, exact.py:38, cohomology.py:60 */
+static inline int64_t nonzero_value(uint32_t j, int64_t iv) { return (int64_t)j < iv ? (int64_t)j - iv : (int64_t)j - iv + 1; }
+
+/* SiteUpdate.step, site.py:43-118: NeighborhoodUpdate's phi proposal, n untouched; d(phi) kept and
+ * updated incrementally between the colours. */
+int sv_o_villain_site(int32_t N, double kappa, double interval_phi, double *phi, const int64_t *n, int32_t sweeps,
+                      sv_rng *rng, sv_stats *stats) {
+    if (N < 2 || sweeps < 0) return -1;
+    const int64_t V = (int64_t)N * N;
+    colors_t C = colors_make(N);
+    double *metro = (double *)malloc(sizeof(double) * V), *dphi = (double *)malloc(sizeof(double) * 2 * V);
+    double *cphi = (double *)malloc(sizeof(double) * V), *dSl = (double *)malloc(sizeof(double) * 2 * V);
+    int64_t *acc = (int64_t *)malloc(sizeof(int64_t) * V);
+    const double range = interval_phi - (-interval_phi);
+    pcg g = pcg_load(rng);
+    for (int32_t sw = 0; sw < sweeps; sw++) {
+        sv_stats *st = &stats[sw];
+        memset(st, 0, sizeof(*st));
+        for (int64_t s = 0; s < V; s++) metro[s] = pcg_uniform(&g, 0.0, 1.0);                      /* :72 */
+        for (int mu = 0; mu < 2; mu++)                                                              /* :84 */
+            for (int64_t s = 0; s < V; s++) dphi[mu * V + s] = 0.0 + (phi[fwd(s, mu, N)] - phi[s]);
+        for (int c = 0; c < C.ncol; c++) {
+            const int64_t nc = C.count[c];
+            const int64_t *sites = C.sites[c];
+            for (int64_t s = 0; s < V; s++) cphi[s] = 0.0;
+            for (int64_t i = 0; i < nc; i++) cphi[sites[i]] = pcg_uniform(&g, -interval_phi, range);   /* :92 */
+            for (int mu = 0; mu < 2; mu++)                                                          /* :96-97 */
+                for (int64_t s = 0; s < V; s++) {
+                    const double cd = 0.0 + (cphi[fwd(s, mu, N)] - cphi[s]);
+                    dSl[mu * V + s] = ((kappa / 2) * cd) * ((2 * (dphi[mu * V + s] - TWO_PI * (double)n[mu * V + s])) + cd);
+                }
+            for (int64_t i = 0; i < nc; i++) {                                                      /* :101-108 */
+                const int64_t s = sites[i];
+                double dS = 0.0;
+                dS += dSl[s];
+                dS += dSl[bwd(s, 0, N)];
+                dS += dSl[V + s];
+                dS += dSl[V + bwd(s, 1, N)];
+                double p = exp(-dS);
+                p = p < 0.0 ? 0.0 : p;
+                p = p > 1.0 ? 1.0 : p;
+                acc[s] = metro[s] < p;
+                st->accepted += acc[s];
+                st->acceptance_sum += p;
+            }
+            for (int64_t i = 0; i < nc; i++) cphi[sites[i]] *= (double)acc[sites[i]];             /* :111 */
+            for (int64_t s = 0; s < V; s++) phi[s] = phi[s] + cphi[s];                              /* :112 */
+            for (int mu = 0; mu < 2; mu++)                                                          /* :113 */
+                for (int64_t s = 0; s < V; s++) dphi[mu * V + s] = dphi[mu * V + s] + (0.0 + (cphi[fwd(s, mu, N)] - cphi[s]));
+        }
+        st->proposed = V;
+    }
+    pcg_store(&g, rng);
+    free(metro), free(dphi), free(cphi), free(dSl), free(acc);
+    colors_free(&C);
+    return 0;
+}
+
+/* LinkUpdate.step, link.py:53-99: every link at once; change_n = W * choice(n_changes, (2,N,N)) is drawn
+ * BEFORE the metropolis uniforms.  stats.acceptance_sum = sum of the 2V probabilities. */
+int sv_o_villain_link(int32_t N, double kappa, int64_t W, int64_t interval_n, const double *phi, int64_t *n,
+                      int32_t sweeps, sv_rng *rng, sv_stats *stats) {
+    if (N < 2 || sweeps < 0 || interval_n < 1) return -1;
+    const int64_t V = (int64_t)N * N;
+    int64_t *cn = (int64_t *)malloc(sizeof(int64_t) * 2 * V);
+    double *p = (double *)malloc(sizeof(double) * 2 * V);
+    const uint32_t k = (uint32_t)(2 * interval_n);
+    pcg g = pcg_load(rng);
+    for (int32_t sw = 0; sw < sweeps; sw++) {
+        sv_stats *st = &stats[sw];
+        memset(st, 0, sizeof(*st));
+        for (int64_t l = 0; l < 2 * V; l++) cn[l] = W * nonzero_value(pcg_bounded(&g, k, &st->rejections), interval_n); /* :76 */
+        for (int mu = 0; mu < 2; mu++)
+            for (int64_t s = 0; s < V; s++) {                                                       /* :78-81 */
+                const int64_t l = mu * V + s;
+                const double dphi = 0.0 + (phi[fwd(s, mu, N)] - phi[s]);
+                const double dS = ((-TWO_PI * kappa) * (double)cn[l]) * ((dphi - TWO_PI * (double)n[l]) - PI_D * (double)cn[l]);
+                double q = exp(-dS);
+                q = q < 0.0 ? 0.0 : q;
+                p[l] = q > 1.0 ? 1.0 : q;
+            }
+        for (int64_t l = 0; l < 2 * V; l++) {                                                       /* :83-91 */
+            const double u = pcg_uniform(&g, 0.0, 1.0);
+            const int a = u < p[l];
+            st->accepted += a;
+            st->acceptance_sum += p[l];
+            if (a) n[l] += cn[l];
+        }
+        st->proposed = 2 * V;
+    }
+    pcg_store(&g, rng);
+    free(cn), free(p);
+    return 0;
+}
+
+/* ExactUpdate.step, exact.py:50-129: n += d(z) for a colour's worth of integer zero-forms z. */
+int sv_o_villain_exact(int32_t N, double kappa, int64_t interval_z, const double *phi, int64_t *n, int32_t sweeps,
+                       sv_rng *rng, sv_stats *stats) {
+    if (N < 2 || sweeps < 0 || interval_z < 1) return -1;
+    const int64_t V = (int64_t)N * N;
+    colors_t C = colors_make(N);
+    double *metro = (double *)malloc(sizeof(double) * V), *dphi = (double *)malloc(sizeof(double) * 2 * V);
+    double *dSl = (double *)malloc(sizeof(double) * 2 * V);
+    int64_t *z = (int64_t *)malloc(sizeof(int64_t) * V), *acc = (int64_t *)malloc(sizeof(int64_t) * V);
+    const uint32_t k = (uint32_t)(2 * interval_z);
+    pcg g = pcg_load(rng);
+    for (int mu = 0; mu < 2; mu++)
+        for (int64_t s = 0; s < V; s++) dphi[mu * V + s] = 0.0 + (phi[fwd(s, mu, N)] - phi[s]);      /* :71 */
+    for (int32_t sw = 0; sw < sweeps; sw++) {
+        sv_stats *st = &stats[sw];
+        memset(st, 0, sizeof(*st));
+        for (int64_t s = 0; s < V; s++) metro[s] = pcg_uniform(&g, 0.0, 1.0);                      /* :73 */
+        for (int c = 0; c < C.ncol; c++) {
+            const int64_t nc = C.count[c];
+            const int64_t *sites = C.sites[c];
+            for (int64_t s = 0; s < V; s++) z[s] = 0;
+            for (int64_t i = 0; i < nc; i++) z[sites[i]] = nonzero_value(pcg_bounded(&g, k, &st->rejections), interval_z); /* :91 */
+            for (int mu = 0; mu < 2; mu++)                                                          /* :94-99 */
+                for (int64_t s = 0; s < V; s++) {
+                    const int64_t l = mu * V + s;
+                    const int64_t cnl = 0 + (z[fwd(s, mu, N)] - z[s]);
+                    dSl[l] = ((-TWO_PI * kappa) * (double)cnl) * ((dphi[l] - TWO_PI * (double)n[l]) - PI_D * (double)cnl);
+                }
+            for (int64_t i = 0; i < nc; i++) {                                                      /* :103-111 */
+                const int64_t s = sites[i];
+                double dS = 0.0;
+                dS += dSl[s];
+                dS += dSl[bwd(s, 0, N)];
+                dS += dSl[V + s];
+                dS += dSl[V + bwd(s, 1, N)];
+                double p = exp(-dS);
+                p = p < 0.0 ? 0.0 : p;
+                p = p > 1.0 ? 1.0 : p;
+                acc[s] = metro[s] < p;
+                st->accepted += acc[s];
+                st->acceptance_sum += p;
+            }
+            for (int64_t i = 0; i < nc; i++) z[sites[i]] *= acc[sites[i]];                         /* :114 */
+            for (int mu = 0; mu < 2; mu++)                                                          /* :115 */
+                for (int64_t s = 0; s < V; s++) n[mu * V + s] += 0 + (z[fwd(s, mu, N)] - z[s]);
+        }
+        st->proposed = V;
+    }
+    pcg_store(&g, rng);
+    free(metro), free(dphi), free(dSl), free(z), free(acc);
+    colors_free(&C);
+    return 0;
+}
+
+/* CohomologyUpdate.step, cohomology.py:64-117: per direction one h (choice) then one uniform; the
+ * change in action on the slice x_mu = 0 is a NumPy float64 sum (pairwise).  stats.accepted counts
+ * accepted directions, acceptance_sum sums the D probabilities, proposed = D = 2. */
+int sv_o_villain_cohomology(int32_t N, double kappa, int64_t interval_h, const double *phi, int64_t *n, int32_t sweeps,
+                            sv_rng *rng, sv_stats *stats) {
+    if (N < 2 || sweeps < 0 || interval_h < 1) return -1;
+    const int64_t V = (int64_t)N * N;
+    double *terms = (double *)malloc(sizeof(double) * N);
+    const uint32_t k = (uint32_t)(2 * interval_h);
+    pcg g = pcg_load(rng);
+    for (int32_t sw = 0; sw < sweeps; sw++) {
+        sv_stats *st = &stats[sw];
+        memset(st, 0, sizeof(*st));
+        for (int mu = 0; mu < 2; mu++) {
+            const int64_t h = nonzero_value(pcg_bounded(&g, k, &st->rejections), interval_h);       /* :89 */
+            const double change_r = -TWO_PI * (double)h;                                            /* :94 */
+            for (int64_t i = 0; i < N; i++) {
+                const int64_t s = mu == 0 ? i : i * N;  /* slice x_mu = 0: (0, 0, i) or (1, i, 0) */
+                const int64_t l = mu * V + s;
+                /* r = d(phi) - 2 pi n, fresh each step (:82); D = 2 slices are disjoint links */
+                const double r = (0.0 + (phi[fwd(s, mu, N)] - phi[s])) - TWO_PI * (double)n[l];
+                terms[i] = ((kappa / 2) * change_r) * ((2 * r) + change_r);                           /* :97 */
+            }
+            const double dS = np_pairwise_sum(terms, N);
+            double p = exp(-dS);
+            p = p < 0.0 ? 0.0 : p;
+            p = p > 1.0 ? 1.0 : p;
+            const double u = pcg_uniform(&g, 0.0, 1.0);                                            /* :100 */
+            if (u < p) {
+                for (int64_t i = 0; i < N; i++) n[mu * V + (mu == 0 ? i : i * N)] += h;
+                st->accepted += 1;
+            }
+            st->acceptance_sum += p;
+        }
+        st->proposed = 2;
+    }
+    pcg_store(&g, rng);
+    free(terms);
+    return 0;
+}

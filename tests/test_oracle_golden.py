@@ -89,3 +89,31 @@ def test_worldline_plaquette_sequential(oracle_lib):
             np.testing.assert_allclose(tot, c['acceptance'][k], rtol=1e-12)
         assert (m == c['m']).all() and (v == c['v']).all()
         assert (state_of(g) == c['rng1']).all()
+
+
+ACCEPTANCE_DENOMINATOR = {'SiteUpdate': lambda N: N * N, 'ExactUpdate': lambda N: N * N,
+                          'LinkUpdate': lambda N: 2 * N * N, 'CohomologyUpdate': lambda N: 2}
+
+
+def generator_interval(c):
+    if c['kw_interval'] == -1:
+        return None
+    return 0.7 if c['kind'] == 'SiteUpdate' else c['kw_interval']
+
+
+def test_villain_generators_golden(oracle_lib):
+    """SiteUpdate, LinkUpdate, ExactUpdate, CohomologyUpdate chains from the reference
+    (including forced NumPy Lemire rejections) reproduced bit-for-bit by the oracle."""
+    kinds = set()
+    for c in cases('villain_generators.npz'):
+        N, kind = c['N'], c['kind']
+        phi, n = c['phi0'].reshape(N, N).copy(), c['n0'].reshape(2, N, N).copy()
+        g = generator_from(c['rng0'])
+        st = oracle_lib.villain_generator(kind, N, c['kappa'], c['W'], phi, n, c['sweeps'], g, generator_interval(c))
+        assert (phi == c['phi'].reshape(N, N)).all() and (n == c['n'].reshape(2, N, N)).all(), (kind, N)
+        assert (state_of(g) == c['rng1']).all()
+        assert list(np.cumsum([s.accepted for s in st])) == list(c['accepted'])
+        d = ACCEPTANCE_DENOMINATOR[kind](N)
+        np.testing.assert_allclose(np.cumsum([s.acceptance_sum / d for s in st]), c['acceptance'], rtol=1e-12)
+        kinds.add(kind)
+    assert kinds == set(ACCEPTANCE_DENOMINATOR)

@@ -7,6 +7,10 @@ travels to the GPU box; these fixtures are the only form in which its behaviour 
 
 Sources exercised (all /root/reference paths):
   NeighborhoodUpdate.step   supervillain/generator/villain/neighborhood.py:59-137
+  SiteUpdate.step           supervillain/generator/villain/site.py:43-118
+  LinkUpdate.step           supervillain/generator/villain/link.py:53-99
+  ExactUpdate.step          supervillain/generator/villain/exact.py:50-129
+  CohomologyUpdate.step     supervillain/generator/villain/cohomology.py:64-117
   CoexactUpdate.step        supervillain/generator/worldline/coexact.py:53-128
   PlaquetteUpdate.step      supervillain/generator/worldline/plaquette.py:35-104
   Lattice.checkerboarding   supervillain/lattice/compact.py:191-239
@@ -80,6 +84,30 @@ def villain_chain(sv, N, kappa, W, sweeps, gen, hot_seed=None, interval_phi=np.p
                 phi0=phi0, n0=n0, rng0=rng0, phi=np.asarray(cfg['phi'])[0].copy(), n=np.asarray(cfg['n']).copy(),
                 accepted=np.array(accepted), acceptance=np.array(acceptance), rng1=rng_state(G.rng),
                 action=float(S(cfg['phi'], cfg['n'])))
+
+
+def villain_generator_chain(sv, kind, kw, N, kappa, W, sweeps, gen, hot_seed=None):
+    """A chain of one of the SURVEY.md 8(f) Villain generators (Site, Link, Exact, Cohomology)."""
+    L = sv.lattice.Lattice2D(N)
+    S = sv.action.Villain(L, kappa, W)
+    G = getattr(sv.generator.villain, kind)(S, **kw)
+    G.rng = gen
+    cfg = S.configurations(1)[0]
+    if hot_seed is not None:
+        r = np.random.default_rng(hot_seed)
+        cfg = {'phi': sv.lattice.Form(r.uniform(-np.pi, np.pi, (1, N, N)), degree=0, lattice=L),
+               'n': sv.lattice.Form(W * r.integers(-2, 3, (2, N, N)), degree=1, lattice=L)}
+    phi0, n0 = np.asarray(cfg['phi'])[0].copy(), np.asarray(cfg['n']).copy()
+    rng0 = rng_state(G.rng)
+    accepted, acceptance = [], []
+    for _ in range(sweeps):
+        cfg = G.step(cfg)
+        accepted.append(G.accepted)
+        acceptance.append(G.acceptance)
+    return dict(kind=kind, kw_interval=int(list(kw.values())[0]) if kw else -1, N=N, kappa=kappa, W=W,
+                sweeps=sweeps, phi0=phi0, n0=n0, rng0=rng0, phi=np.asarray(cfg['phi'])[0].copy(),
+                n=np.asarray(cfg['n']).copy(), accepted=np.array(accepted), acceptance=np.array(acceptance),
+                rng1=rng_state(G.rng), report=np.array(G.report()))
 
 
 def coexact_chain(sv, N, kappa, W, sweeps, seed, vseed, interval_t=1):
@@ -204,6 +232,25 @@ def main():
     for pos, half, hot in [(25 + 7 + 3, 0, 191), (25 + 7 + 4 + 4 + 4 + 4 + 6 + 2, 1, 192)]:
         rej.append(villain_chain(sv, 5, 0.1, 1, 3, crafted_generator(pos, pos, half), hot))
     save('villain_rejections.npz', rej)
+
+    # --- SiteUpdate, LinkUpdate, ExactUpdate, CohomologyUpdate chains
+    more = []
+    seed = 300
+    for kind, kws in [('SiteUpdate', [{}, {'interval_phi': 0.7}]), ('LinkUpdate', [{}, {'interval_n': 3}]),
+                      ('ExactUpdate', [{}, {'interval_z': 2}]), ('CohomologyUpdate', [{}, {'interval_h': 2}])]:
+        for kw in kws:
+            for N, kappa, W, sweeps, hot in [(4, 0.5, 1, 12, None), (5, 0.3, 1, 10, 1), (8, 0.2, 2, 10, 2),
+                                             (16, 0.4, 1, 6, 3), (9, 0.15, 1, 6, 4)]:
+                seed += 1
+                more.append(villain_generator_chain(sv, kind, kw, N, kappa, W, sweeps, np.random.default_rng(seed),
+                                                    None if hot is None else seed * 7 + hot))
+    # forced Lemire rejections in LinkUpdate (interval_n=3: 6 choices, threshold 4) and ExactUpdate
+    for kind, kw, pos in [('LinkUpdate', {'interval_n': 3}, 5), ('LinkUpdate', {'interval_n': 3}, 40),
+                          ('ExactUpdate', {'interval_z': 3}, 64 + 9)]:
+        for half in (0, 1):
+            more.append(villain_generator_chain(sv, kind, kw, 8, 0.3, 1, 3, crafted_generator(pos, pos, half),
+                                                pos * 3 + half))
+    save('villain_generators.npz', more)
 
     # --- CoexactUpdate chains
     co = []
