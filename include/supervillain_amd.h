@@ -84,6 +84,28 @@ int sv_villain_run(sv_villain *st, double kappa, int64_t W, double interval_phi,
  * winding.py:30-37, wrapping.py:17-25): out[0]=S (villain.py:51-66), out[1]=sum (dn)^2, out[2..3]=sum n_mu */
 int sv_villain_observables(sv_villain *st, double kappa, double *out);
 
+/* ---- Villain (phi, n): the other local updates of the Villain Hammer ----------- */
+/* Each runs `sweeps` consecutive steps of one generator on the device-resident state of
+ * sv_villain_create (upload/download as above), advancing rng exactly as the reference's NumPy calls
+ * would; stats has `sweeps` entries, folded by the caller like the reference generator does. */
+/* Replaces SiteUpdate.step, supervillain/generator/villain/site.py:43-120 (interval_phi: site.py:23).
+ * stats.proposed = V; acceptance_sum = sum of the V Metropolis probabilities. */
+int sv_villain_site_run(sv_villain *st, double kappa, double interval_phi, int32_t sweeps, sv_rng *rng,
+                        sv_stats *stats);
+/* Replaces LinkUpdate.step, supervillain/generator/villain/link.py:53-101 (interval_n: link.py:32; W from
+ * the Villain action).  stats.proposed = 2 V; acceptance_sum = sum of the 2 V probabilities (the
+ * reference adds their mean, link.py:94). */
+int sv_villain_link_run(sv_villain *st, double kappa, int64_t W, int64_t interval_n, int32_t sweeps, sv_rng *rng,
+                        sv_stats *stats);
+/* Replaces ExactUpdate.step, supervillain/generator/villain/exact.py:50-129 (interval_z: exact.py:29).
+ * stats.proposed = V. */
+int sv_villain_exact_run(sv_villain *st, double kappa, int64_t interval_z, int32_t sweeps, sv_rng *rng,
+                         sv_stats *stats);
+/* Replaces CohomologyUpdate.step, supervillain/generator/villain/cohomology.py:64-117 (interval_h:
+ * cohomology.py:45).  stats.proposed = D = 2; accepted counts accepted directions. */
+int sv_villain_cohomology_run(sv_villain *st, double kappa, int64_t interval_h, int32_t sweeps, sv_rng *rng,
+                              sv_stats *stats);
+
 /* ---- Worldline (m, v): CoexactUpdate, PlaquetteUpdate ------------------------------------- */
 /* W_eff is Worldline._W (worldline.py:49): W, or 2*pi when W is infinite; v_is_float selects the
  * float64 v layout used at W = infinity. */

@@ -117,6 +117,9 @@ struct sv_villain {
     int64_t count[4] = {0, 0, 0, 0};
     int64_t offset[4] = {0, 0, 0, 0};
     std::vector<int64_t> partial;  // host scratch
+    char *d_aux = nullptr;         // small per-call device block (CohomologyUpdate: rng | stats | plan)
+    char *h_aux = nullptr;         // its pinned host image
+    size_t aux_cap = 0;
 };
 
 struct sv_worldline {

@@ -80,6 +80,9 @@ void plan_sweeps(sv_ctx *ctx, Cursor &cur, u128 inc, const std::vector<BlockSpec
 void upload_plan(sv_ctx *ctx, const std::vector<Block> &blocks, const std::vector<uint32_t> &skipvec);
 VParams make_params(int32_t N, double kappa, int64_t W, double interval_phi, int64_t interval_n);
 int absorb_reports(const AbortInfo &a, int first, SkipMap &skips);
+DevScratch scratch(sv_ctx *ctx);
+AbortInfo read_abort(sv_ctx *ctx);  // synchronizes the stream
+void clear_abort(sv_ctx *ctx);
 int64_t rejections_in(const SkipMap &skips, int sweep, int nblocks);
 int fused_th();
 // launch villain_sweep_fused<4, true> (tile mode) with `grid` workgroups

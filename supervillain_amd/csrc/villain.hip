@@ -1285,6 +1285,8 @@ int sv_villain_destroy(sv_villain *st) {
     (void)hipFree(st->snap_phi);
     (void)hipFree(st->snap_n);
     (void)hipFree(st->sites);
+    if (st->d_aux) (void)hipFree(st->d_aux);
+    if (st->h_aux) (void)hipHostFree(st->h_aux);
     delete st;
     return 0;
 }

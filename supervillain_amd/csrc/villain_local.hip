@@ -1,0 +1,745 @@
+// villain_local.hip -- the remaining local Villain updates of SURVEY.md 8(f) on gfx950, each a
+// bit-exact replay of the reference chain under a fixed NumPy seed:
+//
+//   SiteUpdate        supervillain/generator/villain/site.py:43-120        phi only, checkerboard
+//   LinkUpdate        supervillain/generator/villain/link.py:53-101        every link at once
+//   ExactUpdate       supervillain/generator/villain/exact.py:50-129       n += d(z), checkerboard
+//   CohomologyUpdate  supervillain/generator/villain/cohomology.py:64-117  one slice per direction
+//
+// Site/Exact/Link are colour (or whole-lattice) passes in which a lane owns one colour site (one
+// link) per iteration of a grid-stride loop.  The grid stride S is chosen so that every draw a lane
+// consumes sits at an arithmetic sequence of NumPy stream positions: the lane jumps once (4-level
+// table) to its first draw of a block and then advances by ONE precomputed affine map per
+// iteration (S, 2S or S/2 PCG64 steps).  Blocks holding known Lemire rejections (rare: only for
+// interval counts that are not powers of two) take the per-element full-jump path instead.
+//
+// Floating point follows the reference op by op (-ffp-contract=off):
+//   d(x) on link (mu,s):  0.0 + (x[s+e] - x[s])                            (lattice/reference.py:9-24)
+//   Site dS_link:         ((kappa/2) * cd) * ((2 * (dphi - (2pi)*n)) + cd)  (site.py:94)
+//   Site dphi update:     dphi + (0.0 + (cphi[s+e] - cphi[s]))             (site.py:111)
+//   Exact/Link dS_link:   ((-2pi*kappa) * cn) * ((dphi - (2pi)*n) - pi*cn)  (exact.py:95-98, link.py:78-81)
+//   face_sum:             (((0 + f0[x]) + f0[x-e0]) + f1[x]) + f1[x-e1]    (reference.py:48-64)
+//   Cohomology dS:        NumPy pairwise float64 sum over the slice        (cohomology.py:97)
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+
+#include "villain.h"
+
+namespace sv {
+
+#define LTWO_PI 6.283185307179586  // 2 * np.pi
+#define LPI 3.141592653589793      // np.pi
+
+struct LParams {
+    int32_t N;
+    int64_t V;
+    double half_kappa;   // Site: kappa / 2
+    double m2pik;        // Exact/Link: -2 * np.pi * kappa
+    double lo, range;    // Site: uniform(-interval_phi, +interval_phi) as low, high - low
+    int64_t W;           // Link: change_n = W * choice(...)
+    int64_t iv;          // Link/Exact: values (-iv .. -1, 1 .. iv)
+    uint32_t k, thr;     // choice over 2 iv values: Lemire bound and threshold
+};
+
+namespace {
+
+__device__ __forceinline__ u128 lbase(const Block &b) { return u128{b.base_lo, b.base_hi}; }
+
+__device__ __forceinline__ void lreport(const DevScratch &S, uint32_t sweep, uint32_t block, uint32_t pos) {
+    uint32_t i = atomicAdd(S.nreport, 1u);
+    if (i < (uint32_t)MAX_REPORTS) S.reports[i] = Report{sweep, block, pos, 0};
+    __hip_atomic_store(S.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// stream position of bounded draw d, accounting for known rejected positions (sorted)
+__device__ __forceinline__ uint32_t lskip_pos(const Block &b, const uint32_t *skips, uint32_t d) {
+    uint32_t q = d;
+    for (int i = 0; i < b.nskip; i++)
+        if (skips[b.skip0 + i] <= q) q++;
+    return q;
+}
+
+// value of choice index j among (-iv .. -1, 1 .. iv): link.py:43, exact.py:38, cohomology.py:60
+__device__ __forceinline__ int64_t nonzero_value(uint32_t j, int64_t iv) {
+    return (int64_t)j < iv ? (int64_t)j - iv : (int64_t)j - iv + 1;
+}
+
+// Uniform block draws at positions p0, p0 + stride, ...: one table jump, then one affine map each.
+struct UniLane {
+    u128 s;
+    bool init;
+    __device__ __forceinline__ uint64_t next(const JumpTables *T, const Block &b, uint32_t p, const Affine &adv) {
+        s = init ? apply(adv, s) : jump(T, lbase(b), p);
+        init = true;
+        return xsl_rr(s);
+    }
+};
+
+// Bounded block uint32 words at draw positions q0, q0 + stride, ... (stride even, no skips): NumPy's
+// buffered half-word first, then the low and high halves of consecutive u64s.
+struct BndLane {
+    u128 s;
+    bool init;
+    __device__ __forceinline__ uint32_t next(const JumpTables *T, const Block &b, uint32_t q, const Affine &adv_half) {
+        if (b.has && q == 0) return b.buf;
+        const uint32_t qq = q - b.has;
+        s = init ? apply(adv_half, s) : jump(T, lbase(b), qq >> 1);
+        init = true;
+        const uint64_t X = xsl_rr(s);
+        return (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
+    }
+};
+
+// uint32 of bounded draw d by a full jump (blocks with known rejections)
+__device__ __forceinline__ uint32_t bnd_word_slow(const JumpTables *T, const Block &b, const uint32_t *skips,
+                                                  uint32_t d, uint32_t *qout) {
+    const uint32_t q = lskip_pos(b, skips, d);
+    *qout = q;
+    if (b.has && q == 0) return b.buf;
+    const uint32_t qq = q - b.has;
+    const uint64_t X = xsl_rr(jump(T, lbase(b), qq >> 1));
+    return (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
+}
+
+__device__ __forceinline__ double lwave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// One atomic pair per workgroup (all threads call it).
+__device__ __forceinline__ void lflush(sv_stats *st, int64_t acc, double psum) {
+    __shared__ unsigned long long s_acc[16];
+    __shared__ double s_ps[16];
+    unsigned long long a = (unsigned long long)acc;
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+    psum = lwave_sum(psum);
+    if ((threadIdx.x & 63) == 0) {
+        s_acc[threadIdx.x >> 6] = a;
+        s_ps[threadIdx.x >> 6] = psum;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long ta = 0;
+        double tp = 0.0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); w++) {
+            ta += s_acc[w];
+            tp += s_ps[w];
+        }
+        atomicAdd((unsigned long long *)&st->accepted, ta);
+        unsafeAtomicAdd(&st->acceptance_sum, tp);
+    }
+}
+
+__device__ __forceinline__ double clip01(double p) {
+    p = p < 0.0 ? 0.0 : p;
+    return p > 1.0 ? 1.0 : p;
+}
+
+// colour-index e -> site (even N: row-major parity colouring, e = s >> 1)
+__device__ __forceinline__ int64_t even_site(int64_t e, int64_t N, int color) {
+    const int64_t half = N >> 1;
+    const int64_t t = e / half, j = e - t * half;
+    return t * N + 2 * j + ((color + t) & 1);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// d(phi) into D (2, N, N) at the start of a Site sweep (site.py:81) or an Exact call (exact.py:71);
+// `normalize` also stores phi + 0.0 (every site receives phi + change_phi with change_phi = +0.0 in
+// some colour pass of the reference, which maps -0.0 to +0.0).
+__global__ void local_dphi_init(int32_t N, double *phi, double *D, int normalize, const int32_t *abort) {
+    if (*(volatile const int32_t *)abort) return;
+    const int64_t V = (int64_t)N * N;
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < V; s += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = s / N, x = s - t * N;
+        const double p = phi[s];
+        D[s] = 0.0 + (phi[((t + 1 == N) ? 0 : t + 1) * N + x] - p);
+        D[V + s] = 0.0 + (phi[t * N + ((x + 1 == N) ? 0 : x + 1)] - p);
+        if (normalize) phi[s] = p + 0.0;
+    }
+}
+
+// One colour pass of SiteUpdate (site.py:83-111).  Blocks: [0] metropolis uniform(V), [1 + c] the
+// colour's uniform(-interval_phi, interval_phi, n_c).  EVEN: colour sites computed from e, stride
+// S = grid threads (a multiple of N, so metropolis positions advance by exactly 2S).
+template <bool EVEN>
+__global__ __launch_bounds__(256) void site_pass(LParams P, double *phi, const int64_t *n, double *D,
+                                                 const int32_t *sites, int64_t nc, int color, const Block *blocks,
+                                                 const JumpTables *T, Affine adv_m, Affine adv_e, sv_stats *stat,
+                                                 const int32_t *abort) {
+    if (*(volatile const int32_t *)abort) return;
+    const int64_t N = P.N, V = P.V;
+    const int64_t S = (int64_t)gridDim.x * blockDim.x;
+    const Block BM = blocks[0], BD = blocks[1 + color];
+    UniLane um{u128{0, 0}, false}, ud{u128{0, 0}, false};
+    int64_t acc_count = 0;
+    double psum = 0.0;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nc; e += S) {
+        const int64_t s = EVEN ? even_site(e, N, color) : sites[e];
+        if (!EVEN) um.init = ud.init = false;
+        const double u = 0.0 + 1.0 * to_double(um.next(T, BM, (uint32_t)s, adv_m));
+        const double dph = P.lo + P.range * to_double(ud.next(T, BD, (uint32_t)e, adv_e));
+        const int64_t t = s / N, x = s - t * N;
+        const int64_t L[4] = {s, ((t == 0) ? N - 1 : t - 1) * N + x, V + s, V + t * N + ((x == 0) ? N - 1 : x - 1)};
+        const double cd_f = 0.0 + (0.0 - dph), cd_b = 0.0 + (dph - 0.0);
+        double dv[4];
+        int64_t nv[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            dv[q] = D[L[q]];
+            nv[q] = n[L[q]];
+        }
+        double dS = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const double cd = (q & 1) ? cd_b : cd_f;
+            dS += (P.half_kappa * cd) * ((2.0 * (dv[q] - LTWO_PI * (double)nv[q])) + cd);
+        }
+        const double p = clip01(exp(-dS));
+        const int acc = u < p;
+        acc_count += acc;
+        psum += p;
+        const double cphi = dph * (double)acc;
+        phi[s] = phi[s] + cphi;
+        const double dcf = 0.0 + (0.0 - cphi), dcb = 0.0 + (cphi - 0.0);
+#pragma unroll
+        for (int q = 0; q < 4; q++) D[L[q]] = dv[q] + ((q & 1) ? dcb : dcf);
+    }
+    lflush(stat, acc_count, psum);
+}
+
+// One colour pass of ExactUpdate (exact.py:85-115).  Blocks: [0] metropolis uniform(V), [1 + c] the
+// colour's choice(zs, n_c).  D = d(phi) is fixed for the call.
+template <bool EVEN>
+__global__ __launch_bounds__(256) void exact_pass(LParams P, int64_t *n, const double *D, const int32_t *sites,
+                                                  int64_t nc, int color, const Block *blocks, const uint32_t *skips,
+                                                  const JumpTables *T, Affine adv_m, Affine adv_half, sv_stats *stat,
+                                                  DevScratch Sx, uint32_t sweep) {
+    if (*(volatile const int32_t *)Sx.abort) return;
+    const int64_t N = P.N, V = P.V;
+    const int64_t S = (int64_t)gridDim.x * blockDim.x;
+    const Block BM = blocks[0], BZ = blocks[1 + color];
+    const bool slow = BZ.nskip > 0;
+    UniLane um{u128{0, 0}, false};
+    BndLane uz{u128{0, 0}, false};
+    int64_t acc_count = 0;
+    double psum = 0.0;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nc; e += S) {
+        const int64_t s = EVEN ? even_site(e, N, color) : sites[e];
+        if (!EVEN) um.init = uz.init = false;
+        const double u = 0.0 + 1.0 * to_double(um.next(T, BM, (uint32_t)s, adv_m));
+        uint32_t q = (uint32_t)e, w;
+        if (slow) w = bnd_word_slow(T, BZ, skips, (uint32_t)e, &q);
+        else w = uz.next(T, BZ, (uint32_t)e, adv_half);
+        bool rej;
+        const uint32_t idx = lemire(w, P.k, P.thr, &rej);
+        if (rej) lreport(Sx, sweep, 1u + (uint32_t)color, q);
+        const int64_t z = nonzero_value(idx, P.iv);
+        const int64_t t = s / N, x = s - t * N;
+        const int64_t L[4] = {s, ((t == 0) ? N - 1 : t - 1) * N + x, V + s, V + t * N + ((x == 0) ? N - 1 : x - 1)};
+        const int64_t cn_f = 0 + (0 - z), cn_b = 0 + (z - 0);
+        int64_t nv[4];
+        double dS = 0.0;
+#pragma unroll
+        for (int q4 = 0; q4 < 4; q4++) {
+            nv[q4] = n[L[q4]];
+            const double cn = (double)((q4 & 1) ? cn_b : cn_f);
+            dS += (P.m2pik * cn) * ((D[L[q4]] - LTWO_PI * (double)nv[q4]) - LPI * cn);
+        }
+        const double p = clip01(exp(-dS));
+        const int acc = u < p;
+        acc_count += acc;
+        psum += p;
+        if (acc) {
+#pragma unroll
+            for (int q4 = 0; q4 < 4; q4++) n[L[q4]] = nv[q4] + ((q4 & 1) ? cn_b : cn_f);
+        }
+    }
+    lflush(stat, acc_count, psum);
+}
+
+// One LinkUpdate sweep (link.py:66-99).  Blocks: [0] choice(n_changes, (2,N,N)), [1] uniform(0,1,(2,N,N)).
+// Link l = mu V + s; grid stride S is even, so bounded words advance by S/2 and uniforms by S.
+__global__ __launch_bounds__(256) void link_sweep(LParams P, const double *phi, int64_t *n, const Block *blocks,
+                                                  const uint32_t *skips, const JumpTables *T, Affine adv_u,
+                                                  Affine adv_half, sv_stats *stat, DevScratch Sx, uint32_t sweep) {
+    if (*(volatile const int32_t *)Sx.abort) return;
+    const int64_t N = P.N, V = P.V;
+    const int64_t S = (int64_t)gridDim.x * blockDim.x;
+    const Block BC = blocks[0], BU = blocks[1];
+    const bool slow = BC.nskip > 0;
+    UniLane uu{u128{0, 0}, false};
+    BndLane uc{u128{0, 0}, false};
+    int64_t acc_count = 0;
+    double psum = 0.0;
+    for (int64_t l = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; l < 2 * V; l += S) {
+        uint32_t q = (uint32_t)l, w;
+        if (slow) w = bnd_word_slow(T, BC, skips, (uint32_t)l, &q);
+        else w = uc.next(T, BC, (uint32_t)l, adv_half);
+        bool rej;
+        const uint32_t idx = lemire(w, P.k, P.thr, &rej);
+        if (rej) lreport(Sx, sweep, 0u, q);
+        const int64_t cn = P.W * nonzero_value(idx, P.iv);
+        const int mu = l >= V;
+        const int64_t s = l - (mu ? V : 0);
+        const int64_t t = s / N, x = s - t * N;
+        const int64_t f = mu ? t * N + ((x + 1 == N) ? 0 : x + 1) : ((t + 1 == N) ? 0 : t + 1) * N + x;
+        const double dphi = 0.0 + (phi[f] - phi[s]);
+        const int64_t nl = n[l];
+        const double dS = (P.m2pik * (double)cn) * ((dphi - LTWO_PI * (double)nl) - LPI * (double)cn);
+        const double p = clip01(exp(-dS));
+        const double u = 0.0 + 1.0 * to_double(uu.next(T, BU, (uint32_t)l, adv_u));
+        const int acc = u < p;
+        acc_count += acc;
+        psum += p;
+        if (acc) n[l] = nl + cn;
+    }
+    lflush(stat, acc_count, psum);
+}
+
+// ------------------------------------------------------------------------------------------------
+// CohomologyUpdate (cohomology.py:79-117), every sweep of a call in one workgroup.  Per sweep and
+// direction mu: h = choice(h) (one bounded uint32), dS = pairwise sum over the N links of the slice
+// x_mu = 0 of ((kappa/2) change_r) (2 r + change_r), then one uniform(0,1); on acceptance n += h on
+// the slice.  The few draws are made serially by thread 0 on the live PCG64 state.
+struct CohoRng {
+    uint64_t s_lo, s_hi, inc_lo, inc_hi;
+    uint32_t has, buf;
+};
+
+// NumPy pairwise_sum plan for one length: leaves (start, len <= 128) in recursion order and a
+// postfix program (0 = push next leaf, 1 = add the top two).
+struct PairwisePlan {
+    int32_t nleaf, nprog;
+};
+static constexpr int MAX_LEAVES = 2048;
+
+__device__ __forceinline__ uint64_t coho_u64(u128 &s, const u128 &inc) {
+    s = add(mul(s, mult()), inc);
+    return xsl_rr(s);
+}
+
+__global__ __launch_bounds__(256) void cohomology_run(int32_t N, double half_kappa, int64_t ih, uint32_t k,
+                                                      uint32_t thr, const double *phi, int64_t *n,
+                                                      int32_t sweeps, CohoRng *rng, sv_stats *stats,
+                                                      const int32_t *leaves /* 2 per leaf */,
+                                                      const uint8_t *prog, PairwisePlan plan) {
+    __shared__ double leafv[MAX_LEAVES];
+    __shared__ double s_dS;
+    __shared__ int64_t s_h;
+    __shared__ int s_acc;
+    const int64_t V = (int64_t)N * N;
+    u128 st{rng->s_lo, rng->s_hi}, inc{rng->inc_lo, rng->inc_hi};
+    uint32_t has = rng->has, buf = rng->buf;
+    for (int32_t sw = 0; sw < sweeps; sw++) {
+        int64_t accepted = 0, rejections = 0;
+        double psum = 0.0;
+        for (int mu = 0; mu < 2; mu++) {
+            if (threadIdx.x == 0) {
+                uint32_t idx;
+                for (;;) {  // buffered 32-bit Lemire (NumPy), rejections draw again
+                    uint32_t x;
+                    if (has) {
+                        x = buf;
+                        has = 0;
+                    } else {
+                        const uint64_t X = coho_u64(st, inc);
+                        x = (uint32_t)X;
+                        buf = (uint32_t)(X >> 32);
+                        has = 1;
+                    }
+                    bool rej;
+                    idx = lemire(x, k, thr, &rej);
+                    if (!rej) break;
+                    rejections++;
+                }
+                s_h = nonzero_value(idx, ih);
+            }
+            __syncthreads();
+            const int64_t h = s_h;
+            const double change_r = -LTWO_PI * (double)h;  // cohomology.py:94
+            const double a = half_kappa * change_r;
+            // leaves: slice x_mu = 0 is n[0, 0, i] (mu = 0) or n[1, i, 0] (mu = 1)
+            for (int j = threadIdx.x; j < plan.nleaf; j += blockDim.x) {
+                const int32_t i0 = leaves[2 * j], len = leaves[2 * j + 1];
+                auto term = [&](int64_t i) {
+                    const int64_t s = mu == 0 ? i : i * N;
+                    const int64_t fs = mu == 0 ? N + i : i * N + 1;  // s + e_mu (N >= 2: no wrap)
+                    const double r = (0.0 + (phi[fs] - phi[s])) - LTWO_PI * (double)n[(int64_t)mu * V + s];
+                    return a * ((2.0 * r) + change_r);
+                };
+                double res;
+                if (len < 8) {
+                    res = 0.0;
+                    for (int i = 0; i < len; i++) res += term(i0 + i);
+                } else {
+                    double r8[8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) r8[q] = term(i0 + q);
+                    int i = 8;
+                    for (; i < len - (len % 8); i += 8)
+#pragma unroll
+                        for (int q = 0; q < 8; q++) r8[q] += term(i0 + i + q);
+                    res = ((r8[0] + r8[1]) + (r8[2] + r8[3])) + ((r8[4] + r8[5]) + (r8[6] + r8[7]));
+                    for (; i < len; i++) res += term(i0 + i);
+                }
+                leafv[j] = res;
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                double stk[40];
+                int top = 0, nl = 0;
+                for (int pc = 0; pc < plan.nprog; pc++) {
+                    if (prog[pc] == 0) stk[top++] = leafv[nl++];
+                    else {
+                        const double b = stk[--top];
+                        stk[top - 1] = stk[top - 1] + b;
+                    }
+                }
+                const double dS = stk[0];
+                const double p = clip01(exp(-dS));
+                const double u = 0.0 + 1.0 * to_double(coho_u64(st, inc));  // cohomology.py:100
+                s_acc = u < p;
+                s_dS = p;
+            }
+            __syncthreads();
+            if (s_acc) {
+                for (int64_t i = threadIdx.x; i < N; i += blockDim.x) {
+                    const int64_t s = mu == 0 ? i : i * N;
+                    n[(int64_t)mu * V + s] += h;
+                }
+            }
+            accepted += s_acc;
+            psum += s_dS;
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            stats[sw].accepted = accepted;
+            stats[sw].proposed = 2;
+            stats[sw].acceptance_sum = psum;
+            stats[sw].rejections = rejections;
+        }
+    }
+    if (threadIdx.x == 0) {
+        rng->s_lo = st.lo;
+        rng->s_hi = st.hi;
+        rng->has = has;
+        rng->buf = buf;
+    }
+}
+
+}  // namespace sv
+
+// ==================================================================================================
+// host drivers
+// ==================================================================================================
+namespace svh {
+
+static LParams lparams(int32_t N) {
+    LParams P{};
+    P.N = N;
+    P.V = (int64_t)N * N;
+    return P;
+}
+
+static void set_bounded(LParams &P, int64_t iv) {
+    if (iv < 1) throw std::invalid_argument("the interval must be >= 1");
+    if (iv > (1 << 20)) throw std::invalid_argument("interval too large");
+    P.iv = iv;
+    P.k = (uint32_t)(2 * iv);
+    P.thr = (uint32_t)((0u - P.k) % P.k);
+}
+
+static int gcd_i(int64_t a, int64_t b) { return (int)std::gcd(a, b); }
+
+// Grid for a pass over `count` elements whose lanes advance by the whole grid: the stride is a
+// multiple of `mult` (and of 256) so that per-lane stream positions stay arithmetic.
+static int grid_for(int64_t count, int64_t mult) {
+    const int64_t target = 256 * 2048;  // 8 waves per CU on 256 CUs
+    if (count <= target) return (int)std::max<int64_t>(1, (count + 255) / 256);
+    const int64_t l = mult / gcd_i(mult, 256) * 256;  // lcm(mult, 256)
+    int64_t S = std::max<int64_t>(1, target / l) * l;
+    return (int)(S / 256);
+}
+
+// Run `sweeps` sweeps of a local update in batches of up to 64: plan every draw block of the batch,
+// launch every pass, then read the abort flag once.  A Lemire rejection (known only on the device)
+// restores the batch-start snapshot and replays the batch with the rejected stream position skipped.
+template <class LaunchSweep>
+static void run_local(sv_villain *st, const std::vector<BlockSpec> &specs, int32_t sweeps, Cursor &cur, u128 inc,
+                      sv_stats *stats, bool touches_phi, bool touches_n, LaunchSweep launch_sweep) {
+    sv_ctx *ctx = st->ctx;
+    const int64_t V = (int64_t)st->N * st->N;
+    const int nb = (int)specs.size();
+    SkipMap skips;
+    std::vector<Block> blocks;
+    std::vector<uint32_t> skipvec;
+    const int BATCH = 64;
+    double *phi = st->phi[st->cur];
+    int64_t *n = st->n[st->cur];
+    for (int sw = 0; sw < sweeps;) {
+        const int count = std::min(BATCH, sweeps - sw);
+        if (touches_phi)
+            SV_HIP(hipMemcpyAsync(st->snap_phi, phi, V * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+        if (touches_n)
+            SV_HIP(hipMemcpyAsync(st->snap_n, n, 2 * V * sizeof(int64_t), hipMemcpyDeviceToDevice, ctx->stream));
+        for (int attempt = 0;; attempt++) {
+            if (attempt > 256) throw std::runtime_error("rejection replay did not converge");
+            Cursor c = cur;
+            plan_sweeps(ctx, c, inc, specs, sw, count, skips, blocks, skipvec);
+            upload_plan(ctx, blocks, skipvec);
+            clear_abort(ctx);
+            ctx->ensure_stats(count);
+            SV_HIP(hipMemsetAsync(ctx->d_stats, 0, count * sizeof(sv_stats), ctx->stream));
+            hipEvent_t ev;
+            ctx->time_begin(&ev);
+            for (int k = 0; k < count; k++) launch_sweep(k, ctx->d_blocks + (size_t)k * nb, ctx->d_stats + k);
+            ctx->time_end(ev, count);
+            SV_HIP(hipGetLastError());
+            AbortInfo a = read_abort(ctx);
+            if (a.abort) ctx->time_discard();
+            ctx->time_collect();
+            if (!a.abort) {
+                cur = c;
+                break;
+            }
+            absorb_reports(a, sw, skips);
+            if (touches_phi)
+                SV_HIP(hipMemcpyAsync(phi, st->snap_phi, V * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+            if (touches_n)
+                SV_HIP(hipMemcpyAsync(n, st->snap_n, 2 * V * sizeof(int64_t), hipMemcpyDeviceToDevice, ctx->stream));
+        }
+        SV_HIP(hipMemcpyAsync(stats + sw, ctx->d_stats, count * sizeof(sv_stats), hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+        for (int k = 0; k < count; k++) stats[sw + k].rejections = rejections_in(skips, sw + k, nb);
+        sw += count;
+    }
+}
+
+static Cursor cursor_of(const sv_rng *rng) {
+    return Cursor{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
+}
+
+static void store_cursor(const Cursor &c, sv_rng *rng) {
+    rng->state_hi = c.s.hi;
+    rng->state_lo = c.s.lo;
+    rng->has_uint32 = (int32_t)c.has;
+    rng->uinteger = c.buf;
+}
+
+// Pairwise-sum plan of NumPy's pairwise_sum (numpy/_core/src/umath/loops_utils.h.src) for length n.
+static void pairwise_plan(int64_t i0, int64_t n, std::vector<int32_t> &leaves, std::vector<uint8_t> &prog) {
+    if (n <= 128) {
+        leaves.push_back((int32_t)i0);
+        leaves.push_back((int32_t)n);
+        prog.push_back(0);
+        return;
+    }
+    int64_t n2 = n / 2;
+    n2 -= n2 % 8;
+    pairwise_plan(i0, n2, leaves, prog);
+    pairwise_plan(i0 + n2, n - n2, leaves, prog);
+    prog.push_back(1);
+}
+
+}  // namespace svh
+
+using namespace svh;
+
+extern "C" {
+
+int sv_villain_site_run(sv_villain *st, double kappa, double interval_phi, int32_t sweeps, sv_rng *rng,
+                        sv_stats *stats) {
+    if (!st || !rng || (sweeps > 0 && !stats)) return -1;
+    sv_ctx *ctx = st->ctx;
+    try {
+        if (sweeps < 0) throw std::invalid_argument("sweeps must be >= 0");
+        SV_HIP(hipSetDevice(ctx->device));
+        const int32_t N = st->N;
+        const int64_t V = (int64_t)N * N;
+        LParams P = lparams(N);
+        P.half_kappa = kappa / 2.0;
+        P.lo = -interval_phi;
+        P.range = interval_phi - (-interval_phi);
+        u128 inc{rng->inc_lo, rng->inc_hi};
+        Cursor cur = cursor_of(rng);
+        const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
+        std::vector<BlockSpec> specs{{UNIFORM, (uint32_t)V}};
+        for (int c = 0; c < st->ncol; c++) specs.push_back({UNIFORM, (uint32_t)st->count[c]});
+        const bool even = N % 2 == 0;
+        const int grid = grid_for(V / 2 + 1, N);
+        const int64_t Sl = (int64_t)grid * 256;
+        const Affine adv_m = host_power(inc, 2 * Sl), adv_e = host_power(inc, Sl);
+        const int gi = (int)std::min<int64_t>((V + 255) / 256, 4096);
+        double *phi = st->phi[st->cur];
+        const int64_t *n = st->n[st->cur];
+        run_local(st, specs, sweeps, cur, inc, stats, true, false, [&](int k, const Block *B, sv_stats *ds) {
+            (void)k;
+            local_dphi_init<<<gi, 256, 0, ctx->stream>>>(N, phi, st->r, 1, ctx->d_abort);
+            for (int c = 0; c < st->ncol; c++) {
+                const int64_t nc = st->count[c];
+                if (!nc) continue;
+                if (even)
+                    site_pass<true><<<grid, 256, 0, ctx->stream>>>(P, phi, n, st->r, nullptr, nc, c, B, T, adv_m,
+                                                                   adv_e, ds, ctx->d_abort);
+                else
+                    site_pass<false><<<(int)((nc + 255) / 256), 256, 0, ctx->stream>>>(
+                        P, phi, n, st->r, st->sites + st->offset[c], nc, c, B, T, adv_m, adv_e, ds, ctx->d_abort);
+            }
+        });
+        for (int k = 0; k < sweeps; k++) stats[k].proposed = V;
+        store_cursor(cur, rng);
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_villain_exact_run(sv_villain *st, double kappa, int64_t interval_z, int32_t sweeps, sv_rng *rng,
+                         sv_stats *stats) {
+    if (!st || !rng || (sweeps > 0 && !stats)) return -1;
+    sv_ctx *ctx = st->ctx;
+    try {
+        if (sweeps < 0) throw std::invalid_argument("sweeps must be >= 0");
+        SV_HIP(hipSetDevice(ctx->device));
+        const int32_t N = st->N;
+        const int64_t V = (int64_t)N * N;
+        LParams P = lparams(N);
+        P.m2pik = -LTWO_PI * kappa;
+        set_bounded(P, interval_z);
+        u128 inc{rng->inc_lo, rng->inc_hi};
+        Cursor cur = cursor_of(rng);
+        const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
+        std::vector<BlockSpec> specs{{UNIFORM, (uint32_t)V}};
+        for (int c = 0; c < st->ncol; c++) specs.push_back({BOUNDED, (uint32_t)st->count[c]});
+        const bool even = N % 2 == 0;
+        const int grid = grid_for(V / 2 + 1, N);
+        const int64_t Sl = (int64_t)grid * 256;
+        const Affine adv_m = host_power(inc, 2 * Sl), adv_half = host_power(inc, Sl / 2);
+        const int gi = (int)std::min<int64_t>((V + 255) / 256, 4096);
+        double *phi = st->phi[st->cur];
+        int64_t *n = st->n[st->cur];
+        clear_abort(ctx);
+        local_dphi_init<<<gi, 256, 0, ctx->stream>>>(N, phi, st->r, 0, ctx->d_abort);  // exact.py:71 (phi fixed)
+        run_local(st, specs, sweeps, cur, inc, stats, false, true, [&](int k, const Block *B, sv_stats *ds) {
+            for (int c = 0; c < st->ncol; c++) {
+                const int64_t nc = st->count[c];
+                if (!nc) continue;
+                if (even)
+                    exact_pass<true><<<grid, 256, 0, ctx->stream>>>(P, n, st->r, nullptr, nc, c, B, ctx->d_skips, T,
+                                                                    adv_m, adv_half, ds, scratch(ctx), (uint32_t)k);
+                else
+                    exact_pass<false><<<(int)((nc + 255) / 256), 256, 0, ctx->stream>>>(
+                        P, n, st->r, st->sites + st->offset[c], nc, c, B, ctx->d_skips, T, adv_m, adv_half, ds,
+                        scratch(ctx), (uint32_t)k);
+            }
+        });
+        for (int k = 0; k < sweeps; k++) stats[k].proposed = V;
+        store_cursor(cur, rng);
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_villain_link_run(sv_villain *st, double kappa, int64_t W, int64_t interval_n, int32_t sweeps, sv_rng *rng,
+                        sv_stats *stats) {
+    if (!st || !rng || (sweeps > 0 && !stats)) return -1;
+    sv_ctx *ctx = st->ctx;
+    try {
+        if (sweeps < 0) throw std::invalid_argument("sweeps must be >= 0");
+        SV_HIP(hipSetDevice(ctx->device));
+        const int32_t N = st->N;
+        const int64_t V = (int64_t)N * N;
+        LParams P = lparams(N);
+        P.m2pik = -LTWO_PI * kappa;
+        P.W = W;
+        set_bounded(P, interval_n);
+        u128 inc{rng->inc_lo, rng->inc_hi};
+        Cursor cur = cursor_of(rng);
+        const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
+        const std::vector<BlockSpec> specs{{BOUNDED, (uint32_t)(2 * V)}, {UNIFORM, (uint32_t)(2 * V)}};
+        const int grid = grid_for(2 * V, 2);
+        const int64_t Sl = (int64_t)grid * 256;
+        const Affine adv_u = host_power(inc, Sl), adv_half = host_power(inc, Sl / 2);
+        const double *phi = st->phi[st->cur];
+        int64_t *n = st->n[st->cur];
+        run_local(st, specs, sweeps, cur, inc, stats, false, true, [&](int k, const Block *B, sv_stats *ds) {
+            link_sweep<<<grid, 256, 0, ctx->stream>>>(P, phi, n, B, ctx->d_skips, T, adv_u, adv_half, ds,
+                                                      scratch(ctx), (uint32_t)k);
+        });
+        for (int k = 0; k < sweeps; k++) stats[k].proposed = 2 * V;
+        store_cursor(cur, rng);
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_villain_cohomology_run(sv_villain *st, double kappa, int64_t interval_h, int32_t sweeps, sv_rng *rng,
+                              sv_stats *stats) {
+    if (!st || !rng || (sweeps > 0 && !stats)) return -1;
+    sv_ctx *ctx = st->ctx;
+    try {
+        if (sweeps < 0) throw std::invalid_argument("sweeps must be >= 0");
+        if (sweeps == 0) return 0;
+        SV_HIP(hipSetDevice(ctx->device));
+        LParams P = lparams(st->N);
+        set_bounded(P, interval_h);
+        std::vector<int32_t> leaves;
+        std::vector<uint8_t> prog;
+        pairwise_plan(0, st->N, leaves, prog);
+        if ((int)leaves.size() / 2 > MAX_LEAVES) throw std::invalid_argument("lattice too large for the slice sum");
+        // one device buffer (rng | stats | leaves | prog) and one pinned host image of it, kept by the
+        // state: every transfer is a stream-ordered DMA on ctx->stream
+        const size_t o_st = 64, o_lv = o_st + ((sizeof(sv_stats) * sweeps + 63) / 64) * 64;
+        const size_t o_pg = o_lv + leaves.size() * sizeof(int32_t), total = o_pg + prog.size();
+        if (total > st->aux_cap) {
+            SV_HIP(hipStreamSynchronize(ctx->stream));
+            if (st->d_aux) SV_HIP(hipFree(st->d_aux));
+            if (st->h_aux) SV_HIP(hipHostFree(st->h_aux));
+            st->d_aux = st->h_aux = nullptr;
+            st->aux_cap = 0;
+            SV_HIP(hipMalloc((void **)&st->d_aux, total));
+            SV_HIP(hipHostMalloc((void **)&st->h_aux, total, hipHostMallocDefault));
+            st->aux_cap = total;
+        }
+        char *hb = st->h_aux;
+        CohoRng h{rng->state_lo, rng->state_hi, rng->inc_lo, rng->inc_hi, (uint32_t)rng->has_uint32, rng->uinteger};
+        memcpy(hb, &h, sizeof(h));
+        memcpy(hb + o_lv, leaves.data(), leaves.size() * sizeof(int32_t));
+        memcpy(hb + o_pg, prog.data(), prog.size());
+        char *d = st->d_aux;
+        SV_HIP(hipMemcpyAsync(d, hb, total, hipMemcpyHostToDevice, ctx->stream));
+        const PairwisePlan plan{(int32_t)(leaves.size() / 2), (int32_t)prog.size()};
+        hipEvent_t ev;
+        ctx->time_begin(&ev);
+        cohomology_run<<<1, 256, 0, ctx->stream>>>(st->N, kappa / 2.0, P.iv, P.k, P.thr, st->phi[st->cur],
+                                                   st->n[st->cur], sweeps, (CohoRng *)d, (sv_stats *)(d + o_st),
+                                                   (const int32_t *)(d + o_lv), (const uint8_t *)(d + o_pg), plan);
+        ctx->time_end(ev, 1);
+        SV_HIP(hipGetLastError());
+        SV_HIP(hipMemcpyAsync(hb, d, o_lv, hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+        ctx->time_collect();
+        memcpy(&h, hb, sizeof(h));
+        memcpy(stats, hb + o_st, sizeof(sv_stats) * sweeps);
+        rng->state_lo = h.s_lo;
+        rng->state_hi = h.s_hi;
+        rng->has_uint32 = (int32_t)h.has;
+        rng->uinteger = h.buf;
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
+}  // extern "C"

@@ -154,3 +154,193 @@ class NeighborhoodUpdate(DeviceState, Generator):
             + '\n' +
             f'    {self.acceptance / self.sweeps:.6f} average Metropolis acceptance probability.'
         )
+
+
+# ------------------------------------------------------------------------------------------------
+# The rest of the Villain Hammer's local updates: SiteUpdate, LinkUpdate, ExactUpdate,
+# CohomologyUpdate.  Same constructors, attributes, `step` contract and `report()` text as the
+# reference; each sweep runs in libsvhip.so on a device-resident (phi, n).
+
+class _VillainLocal(DeviceState, Generator):
+    """Shared plumbing: device state, host<->device copies and the reference's counter folding."""
+
+    NAME = None
+    NOUN = None                 # report() wording
+    RETURNS = ('phi', 'n')      # fields the step changes (the rest of cfg passes through)
+
+    def _init_common(self, action, device):
+        if not _is_villain(action):
+            raise ValueError('Need a Villain action')
+        self.Action = action
+        self.Lattice = action.Lattice
+        self.kappa = action.kappa
+        self.rng = np.random.default_rng()
+        self.accepted = 0
+        self.proposed = 0
+        self.acceptance = 0.
+        self.sweeps = 0
+        self.device = device
+
+    def __str__(self):
+        return self.NAME
+
+    def _state(self):
+        L = self.Lattice
+        if L.D != 2:
+            raise NotImplementedError(f'the MI355X {self.NAME} is implemented for D=2 lattices')
+        dev = self.__dict__.get('_dev')
+        if dev is None or dev[1] != L.N:
+            ctx = self._device_context()
+            h = ctypes.c_void_p()
+            ctx.check(_native.lib().sv_villain_create(ctx.handle, L.N, ctypes.byref(h)), 'sv_villain_create')
+            dev = (ctx, L.N, h)
+            self._dev = dev
+        return dev
+
+    def __del__(self):
+        dev = self.__dict__.get('_dev')
+        if dev is not None and _native._LIB is not None:
+            try:
+                _native._LIB.sv_villain_destroy(dev[2])
+            except Exception:
+                pass
+
+    def _proposals(self):
+        return self.Lattice.sites
+
+    def _advance(self, phi, n, sweeps):
+        ctx, N, h = self._state()
+        L = _native.lib()
+        st = _native.stats_array(sweeps)
+        r = rng_from_numpy(self.rng)
+        ctx.check(L.sv_villain_upload(h, _native.ptr(phi), _native.ptr(n)), 'sv_villain_upload')
+        ctx.check(self._run(L, h, sweeps, r, st), f'{self.NAME} run')
+        ctx.check(L.sv_villain_download(h, _native.ptr(phi), _native.ptr(n)), 'sv_villain_download')
+        rng_to_numpy(r, self.rng)
+        P = self._proposals()
+        for k in range(sweeps):
+            self.sweeps += 1
+            self.proposed += P
+            self.acceptance += st[k].acceptance_sum / P
+            self.accepted += int(st[k].accepted)
+
+    def _fields(self, cfg):
+        N = self.Lattice.N
+        phi = np.array(cfg['phi'], dtype=np.float64, order='C', copy=True).reshape(1, N, N)
+        n = np.array(cfg['n'], dtype=np.int64, order='C', copy=True).reshape(2, N, N)
+        return phi, n
+
+    def _result(self, cfg, phi, n):
+        L = self.Lattice
+        new = {'phi': wrap_like(cfg['phi'], phi, 0, L), 'n': wrap_like(cfg['n'], n, 1, L)}
+        return cfg | {k: new[k] for k in self.RETURNS}
+
+    def step(self, cfg):
+        phi, n = self._fields(cfg)
+        self._advance(phi, n, 1)
+        return self._result(cfg, phi, n)
+
+    def _steps(self, cfg, count):
+        """`count` consecutive steps in one device call (used by KeepEvery)."""
+        phi, n = self._fields(cfg)
+        self._advance(phi, n, count)
+        return self._result(cfg, phi, n)
+
+    def inline_observables(self, steps):
+        return {}
+
+    def report(self):
+        return (
+            f'There were {self.accepted} {self.NOUN} proposals accepted of {self.proposed} proposed updates.'
+            + '\n' +
+            f'    {self.accepted/self.proposed:.6f} acceptance rate'
+            + '\n' +
+            f'    {self.acceptance / self.sweeps:.6f} average Metropolis acceptance probability.'
+        )
+
+
+class SiteUpdate(_VillainLocal):
+    r'''Checkerboard Metropolis update of phi alone, n untouched (supervillain/generator/villain/site.py:12-135):
+    Δφ_x ~ U(-interval_phi, +interval_phi) on one colour at a time.'''
+
+    NAME = 'SiteUpdate'
+    NOUN = 'single-phi'
+    RETURNS = ('phi',)
+
+    def __init__(self, action, interval_phi=np.pi, *, device=None):
+        self._init_common(action, device)
+        self.interval_phi = interval_phi
+
+    def _run(self, L, h, sweeps, r, st):
+        return L.sv_villain_site_run(h, float(self.kappa), float(self.interval_phi), sweeps, ctypes.byref(r), st)
+
+
+class LinkUpdate(_VillainLocal):
+    r'''Independent Metropolis updates of every link, Δn ~ W × {-interval_n..-1, 1..interval_n}
+    (supervillain/generator/villain/link.py:12-109).'''
+
+    NAME = 'LinkUpdate'
+    NOUN = 'single-link'
+    RETURNS = ('n',)
+
+    def __init__(self, action, interval_n=1, *, device=None):
+        self._init_common(action, device)
+        W = action.W
+        if not (np.isfinite(W) and float(W) == int(W)):
+            raise NotImplementedError('LinkUpdate needs a finite integer W (W * choice(...) is an integer change)')
+        self.interval_n = interval_n
+        self.n_changes = tuple(n for n in range(-interval_n, 0)) + tuple(n for n in range(1, interval_n + 1))
+
+    def _proposals(self):
+        return 2 * self.Lattice.sites  # int(np.prod(n.shape)), link.py:95
+
+    def _run(self, L, h, sweeps, r, st):
+        return L.sv_villain_link_run(h, float(self.kappa), int(self.Action.W), int(self.interval_n), sweeps,
+                                     ctypes.byref(r), st)
+
+
+class ExactUpdate(_VillainLocal):
+    r'''Checkerboard Metropolis update n -> n + dz with an integer zero-form z_x ~ {-interval_z..-1, 1..interval_z},
+    which keeps dn unchanged (supervillain/generator/villain/exact.py:12-137).'''
+
+    NAME = 'ExactUpdate'
+    NOUN = 'exact'
+    RETURNS = ('n',)
+
+    def __init__(self, action, interval_z=1, *, device=None):
+        self._init_common(action, device)
+        self.interval_z = interval_z
+        self.zs = tuple(z for z in range(-interval_z, 0)) + tuple(z for z in range(1, interval_z + 1))
+
+    def _run(self, L, h, sweeps, r, st):
+        return L.sv_villain_exact_run(h, float(self.kappa), int(self.interval_z), sweeps, ctypes.byref(r), st)
+
+
+class CohomologyUpdate(_VillainLocal):
+    r'''Winding-sector update: per direction mu, n_mu += h_mu on the slice x_mu = 0, h_mu ~ {-interval_h..-1,
+    1..interval_h}, Metropolized as one proposal (supervillain/generator/villain/cohomology.py:12-125).'''
+
+    NAME = 'CohomologyUpdate'
+    NOUN = 'cohomology'
+    RETURNS = ('n',)
+
+    def __init__(self, action, interval_h=1, *, device=None):
+        self._init_common(action, device)
+        self.interval_h = interval_h
+        self.h = tuple(h for h in range(-interval_h, 0)) + tuple(h for h in range(1, interval_h + 1))
+
+    def _proposals(self):
+        return self.Lattice.D
+
+    def _run(self, L, h, sweeps, r, st):
+        return L.sv_villain_cohomology_run(h, float(self.kappa), int(self.interval_h), sweeps, ctypes.byref(r), st)
+
+
+def Hammer(S, worms=1):
+    r'''The reference's Villain Hammer (supervillain/generator/villain/__init__.py:11-67) without its worm
+    (ClassicWorm is outside this build's hot path, SURVEY.md 2): Sequentially(Site, Link, Exact, Cohomology),
+    LinkUpdate omitted at W = infinity.'''
+    from supervillain_amd.generator.combining import Sequentially
+    if S.W < float('inf'):
+        return Sequentially((SiteUpdate(S), LinkUpdate(S), ExactUpdate(S), CohomologyUpdate(S)))
+    return Sequentially((SiteUpdate(S), ExactUpdate(S), CohomologyUpdate(S)))
