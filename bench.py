@@ -18,6 +18,11 @@ Secondary workloads (not the headline line; BASELINE.json configs 5 and 3):
                         the N ranks (config 5; replicas need no collectives)
   --workload worldline  L=1024 Worldline: one checkerboard PlaquetteUpdate + one CoexactUpdate sweep
                         per step, W=1 (config 3); N > 1 runs independent replicas
+  --workload site|link|exact|cohomology|hammer
+                        SURVEY.md 8(f) rows at L=4096: one sweep of SiteUpdate / LinkUpdate / ExactUpdate /
+                        CohomologyUpdate per step, or one Villain Hammer step (Site, Link, Exact, Cohomology,
+                        each with its own stream, as the reference's Hammer minus its worm); device-resident
+                        fields; N > 1 runs independent chains
 """
 import argparse
 import ctypes
@@ -34,6 +39,10 @@ sys.path.insert(0, ROOT)
 ALG_BYTES_PER_SITE = 48      # one read + one write of phi (f64) and n (2 x i64) per sweep
 SURVEY_BYTES_PER_SITE = 88   # two separate colour passes
 WORLDLINE_BYTES = 168        # Plaquette (88) + Coexact (80) per plaquette-step
+# SURVEY.md 8(f) rows, compulsory HBM bytes per site and sweep: Site reads phi and n and
+# writes phi (8 + 16 + 8); Exact reads phi and n and writes n (8 + 16 + 16); Link the same per site
+# (2 links); Cohomology touches 2 N links (reported per site of the slice sum, not a roofline workload)
+LOCAL_BYTES = {'site': 32, 'exact': 40, 'link': 40, 'hammer': 32 + 40 + 40}
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
@@ -51,7 +60,7 @@ def parse():
     ap.add_argument('--strong', action='store_true', help='N>1: decompose one L x L lattice (strong scaling)')
     ap.add_argument('--tiles', default=None, help='tile grid TYxTX (default from N); with N=1 emulates the '
                                                    'decomposition on one GPU')
-    ap.add_argument('--workload', default='villain', choices=['villain', 'replicas', 'worldline'])
+    ap.add_argument('--workload', default='villain', choices=['villain', 'replicas', 'worldline', 'site', 'link', 'exact', 'cohomology', 'hammer'])
     ap.add_argument('--event-timing', default='batch', choices=['launch', 'batch'],
                     help='hipEvents around each batch of 64 fused launches (default) or around every launch')
     ap.add_argument('--replicas', type=int, default=1024, help='replicas workload: total replica count')
@@ -254,6 +263,83 @@ def run_worldline(args, world, rank, dist):
     Lib.sv_worldline_destroy(h)
 
 
+def run_local(args, world, rank, dist):
+    """the Villain Hammer's local updates on a device-resident L x L state, cold start."""
+    from supervillain_amd import _native
+    from supervillain_amd._abi import rng_from_numpy
+    L, kind = args.L, args.workload
+    Lib = _native.lib()
+    ctx = _native.context(_native.default_device())
+    h = ctypes.c_void_p()
+    ctx.check(Lib.sv_villain_create(ctx.handle, L, ctypes.byref(h)), 'sv_villain_create')
+    phi = np.zeros((L, L))
+    n = np.zeros((2, L, L), dtype=np.int64)
+    ctx.check(Lib.sv_villain_upload(h, _native.ptr(phi), _native.ptr(n)), 'upload')
+    kinds = ['site', 'link', 'exact', 'cohomology'] if kind == 'hammer' else [kind]
+    rngs = {k: rng_from_numpy(np.random.default_rng(100 * rank + i)) for i, k in enumerate(kinds)}
+    calls = {
+        'site': lambda k, st: Lib.sv_villain_site_run(h, args.kappa, float(np.pi), k, ctypes.byref(rngs['site']), st),
+        'link': lambda k, st: Lib.sv_villain_link_run(h, args.kappa, args.W, 1, k, ctypes.byref(rngs['link']), st),
+        'exact': lambda k, st: Lib.sv_villain_exact_run(h, args.kappa, 1, k, ctypes.byref(rngs['exact']), st),
+        'cohomology': lambda k, st: Lib.sv_villain_cohomology_run(h, args.kappa, 1, k,
+                                                                 ctypes.byref(rngs['cohomology']), st),
+    }
+
+    def run(k):
+        acc = 0
+        if kind == 'hammer':  # Sequentially: one step of each generator in turn
+            for _ in range(k):
+                for g in kinds:
+                    st = _native.stats_array(1)
+                    ctx.check(calls[g](1, st), g)
+                    acc += st[0].accepted if g == 'site' else 0
+        else:
+            st = _native.stats_array(k)
+            ctx.check(calls[kind](k, st), kind)
+            acc = sum(st[i].accepted for i in range(k))
+        return acc
+
+    if args.warmup:
+        run(args.warmup)
+    Lib.sv_ctx_set_timing(ctx.handle, 1)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    acc = run(args.steps)
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = max_over_ranks(dist, t1 - t0)
+    ms = ctypes.c_double()
+    launches = ctypes.c_int64()
+    Lib.sv_ctx_kernel_time(ctx.handle, ctypes.byref(ms), ctypes.byref(launches))
+    step_kernel_s = ms.value / 1e3 / args.steps  # all kernels of one step (sweep)
+
+    def baseline():
+        from oracle import oracle as O
+        names = {'site': 'SiteUpdate', 'link': 'LinkUpdate', 'exact': 'ExactUpdate', 'cohomology': 'CohomologyUpdate'}
+        pp, nn = np.zeros((L, L)), np.zeros((2, L, L), dtype=np.int64)
+        k = 2 if kind != 'cohomology' else 2000
+        t = time.perf_counter()
+        for _ in range(k):
+            for g in kinds:
+                O.villain_generator(names[g], L, args.kappa, args.W, pp, nn, 1, np.random.default_rng(1))
+        dt = time.perf_counter() - t
+        return {'value': k * L * L / dt, 'unit': 'lattice-site updates/s', 'cores': 1, 'kind': 'port',
+                'sample': f'{k} steps of L={L} {kind}, oracle/sv_oracle.c single-threaded'}
+
+    if rank == 0:
+        what = {'site': 'SiteUpdate', 'link': 'LinkUpdate', 'exact': 'ExactUpdate', 'cohomology': 'CohomologyUpdate',
+                'hammer': 'Villain Hammer minus worm: SiteUpdate, LinkUpdate, ExactUpdate, CohomologyUpdate'}[kind]
+        config = {'workload': f'L={L} Villain {what} sweep per step, kappa={args.kappa}, W={args.W}, bit-exact '
+                              'reference chain (PCG64 replay), device-resident fields',
+                  'L': L, 'path': kind, 'parallelism': f'{world} independent chain(s)'}
+        report(args, world, world * L * L, L * L, elapsed, acc / (args.steps * L * L), step_kernel_s, config, L,
+               metric=f'lattice-site updates/sec ({what}), L={L} Villain', kernel=f'{kind} (all kernels of a step)',
+               alg_bytes=LOCAL_BYTES.get(kind, 0), survey_bytes=LOCAL_BYTES.get(kind, 0), baseline=baseline)
+    Lib.sv_villain_destroy(h)
+
+
 def run_domain(args, world, rank, local, dist):
     """N > 1 (or --tiles on one GPU): one lattice, domain-decomposed, RCCL halos."""
     from supervillain_amd import _native
@@ -307,7 +393,8 @@ def main():
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         dist.init_process_group('gloo', rank=rank, world_size=world)
     if args.workload != 'villain':
-        (run_replicas if args.workload == 'replicas' else run_worldline)(args, world, rank, dist)
+        fn = {'replicas': run_replicas, 'worldline': run_worldline}.get(args.workload, run_local)
+        fn(args, world, rank, dist)
         if dist:
             dist.destroy_process_group()
         return

@@ -159,7 +159,7 @@ __global__ void local_dphi_init(int32_t N, double *phi, double *D, int normalize
         const double p = phi[s];
         D[s] = 0.0 + (phi[((t + 1 == N) ? 0 : t + 1) * N + x] - p);
         D[V + s] = 0.0 + (phi[t * N + ((x + 1 == N) ? 0 : x + 1)] - p);
-        if (normalize) phi[s] = p + 0.0;
+        if (normalize && p == 0.0 && __signbit(p)) phi[s] = p + 0.0;  // only -0.0 changes
     }
 }
 
