@@ -39,6 +39,8 @@ def lib():
         L.sv_o_villain_link.argtypes = [i32, f64, i64, i64, vp, vp, i32, P(SvRng), vp]
         L.sv_o_villain_exact.argtypes = [i32, f64, i64, vp, vp, i32, P(SvRng), vp]
         L.sv_o_villain_cohomology.argtypes = [i32, f64, i64, vp, vp, i32, P(SvRng), vp]
+        L.sv_o_worldline_vortex.argtypes = [i32, f64, f64, i64, vp, vp, i32, i32, P(SvRng), vp]
+        L.sv_o_worldline_wrapping.argtypes = [i32, f64, f64, i64, vp, vp, i32, i32, P(SvRng), vp]
         _LIB = L
     return _LIB
 
@@ -173,6 +175,22 @@ def villain_generator(kind, N, kappa, W, phi, n, sweeps, gen, interval=None):
                                        ctypes.byref(r), st)
     else:
         raise ValueError(kind)
+    if rc != 0:
+        raise ValueError('oracle rejected the arguments')
+    rng_to_numpy(r, gen)
+    return [st[i] for i in range(sweeps)]
+
+
+def worldline_generator(kind, N, kappa, W_eff, m, v, sweeps, gen, interval=None):
+    """Run `sweeps` steps of a SURVEY.md 8(f) Worldline generator ('VortexUpdate' changes v, 'WrappingUpdate'
+    changes m) in place on (m (2,N,N) i64, v (N,N) i64, or f64 at W = infinity)."""
+    assert m.dtype == np.int64 and m.flags.c_contiguous and v.flags.c_contiguous
+    v_is_float = int(v.dtype == np.float64)
+    r = rng_from_numpy(gen)
+    st = _stats_array(sweeps)
+    iv = 1 if interval is None else int(interval)
+    fn = {'VortexUpdate': lib().sv_o_worldline_vortex, 'WrappingUpdate': lib().sv_o_worldline_wrapping}[kind]
+    rc = fn(N, kappa, float(W_eff), iv, _ptr(m), _ptr(v), v_is_float, sweeps, ctypes.byref(r), st)
     if rc != 0:
         raise ValueError('oracle rejected the arguments')
     rng_to_numpy(r, gen)

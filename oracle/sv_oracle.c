@@ -786,3 +786,157 @@ int sv_o_villain_cohomology(int32_t N, double kappa, int64_t interval_h, const d
     free(terms);
     return 0;
 }
+
+/* ================================================================ SURVEY.md 8(f) Worldline generators */
+/* raw dense delta(v) for a D=2 two-form (reference.py:27-45, rows ('delta',2) = (0,0,1,-1),(1,0,0,+1)):
+ * dv0[x] = 0 - (-1)(v[x] - v[x-e1]), dv1[x] = 0 - (+1)(v[x] - v[x-e0]); float64 for either v dtype. */
+static void delta_v_raw(int64_t N, const void *v, int v_is_float, double *dv) {
+    const int64_t V = N * N;
+    for (int64_t s = 0; s < V; s++) {
+        const int64_t b1 = bwd(s, 1, N), b0 = bwd(s, 0, N);
+        if (v_is_float) {
+            const double *vf = (const double *)v;
+            dv[s] = 0.0 - (-(vf[s] - vf[b1]));
+            dv[V + s] = 0.0 - (vf[s] - vf[b0]);
+        } else {
+            const int64_t *vi = (const int64_t *)v;
+            dv[s] = (double)(0 - (-(vi[s] - vi[b1])));
+            dv[V + s] = (double)(0 - (vi[s] - vi[b0]));
+        }
+    }
+}
+
+/* VortexUpdate.step, vortex.py:51-136 (D=2: one 2-form component).  metropolis = uniform(V) first (:92);
+ * per colour the proposals (choice(vs) for finite W, uniform(-iv, iv) at W = inf, :105-108); delta_v kept
+ * incrementally (:98, :130) -- for integer v it stays exact, for float v the patch order is the spec.
+ * dS_link = ((0.5/kappa) * (-cdv/W)) * ((2 * (m - delta_v/W)) - cdv/W)   (:112-115)
+ * dS      = (((0 + dSl1[x]) + dSl1[x+e0]) + dSl0[x]) + dSl0[x+e1]   (coface_sum_at, compact.py:1185-1247) */
+int sv_o_worldline_vortex(int32_t N, double kappa, double Weff, int64_t interval_v, const int64_t *m, void *v,
+                          int32_t v_is_float, int32_t sweeps, sv_rng *rng, sv_stats *stats) {
+    if (N < 2 || sweeps < 0 || interval_v < 1) return -1;
+    const int64_t V = (int64_t)N * N;
+    colors_t C = colors_make(N);
+    double *metro = (double *)malloc(sizeof(double) * V), *dv = (double *)malloc(sizeof(double) * 2 * V);
+    double *vals = (double *)malloc(sizeof(double) * V);
+    const uint32_t k = (uint32_t)(2 * interval_v);
+    const double lo = -(double)interval_v, range = (double)interval_v - (-(double)interval_v);
+    pcg g = pcg_load(rng);
+    for (int32_t sw = 0; sw < sweeps; sw++) {
+        sv_stats *st = &stats[sw];
+        memset(st, 0, sizeof(*st));
+        for (int64_t s = 0; s < V; s++) metro[s] = pcg_uniform(&g, 0.0, 1.0);
+        delta_v_raw(N, v, v_is_float, dv);                                                      /* :98 */
+        for (int c = 0; c < C.ncol; c++) {
+            const int64_t nc = C.count[c];
+            const int64_t *sites = C.sites[c];
+            for (int64_t i = 0; i < nc; i++)
+                vals[i] = v_is_float ? pcg_uniform(&g, lo, range)
+                                     : (double)nonzero_value(pcg_bounded(&g, k, &st->rejections), interval_v);
+            for (int64_t i = 0; i < nc; i++) {
+                const int64_t s = sites[i];
+                const int64_t L0 = s, L0f = fwd(s, 1, N), L1 = V + s, L1f = V + fwd(s, 0, N);
+                const double a = vals[i];
+                /* cdv / W on the four boundary links (delta_sparse, compact.py:1042-1116) */
+                const double c0 = v_is_float ? (0.0 - (-a)) / Weff : (double)(0 - (-(int64_t)a)) / Weff;
+                const double c0f = v_is_float ? (0.0 + (-a)) / Weff : (double)(0 + (-(int64_t)a)) / Weff;
+                const double c1 = v_is_float ? (0.0 - a) / Weff : (double)(0 - (int64_t)a) / Weff;
+                const double c1f = v_is_float ? (0.0 + a) / Weff : (double)(0 + (int64_t)a) / Weff;
+                const double hk = 0.5 / kappa;
+#define DSL(L, c) ((hk * (-(c))) * ((2 * ((double)m[L] - dv[L] / Weff)) - (c)))
+                double dS = 0.0;
+                dS += DSL(L1, c1);
+                dS += DSL(L1f, c1f);
+                dS += DSL(L0, c0);
+                dS += DSL(L0f, c0f);
+#undef DSL
+                double p = exp(-dS);
+                p = p < 0.0 ? 0.0 : p;
+                p = p > 1.0 ? 1.0 : p;
+                const int acc = metro[s] < p;
+                st->accepted += acc;
+                st->acceptance_sum += p;
+                /* v[x] += vals * accepted; delta_v patched with the same sparse delta (:129-131) */
+                if (v_is_float) {
+                    const double ap = a * (double)acc;
+                    ((double *)v)[s] = ((double *)v)[s] + ap;
+                    dv[L0] = dv[L0] - (-ap);
+                    dv[L0f] = dv[L0f] + (-ap);
+                    dv[L1] = dv[L1] - ap;
+                    dv[L1f] = dv[L1f] + ap;
+                } else {
+                    const int64_t ap = (int64_t)a * acc;
+                    ((int64_t *)v)[s] += ap;
+                    dv[L0] = (double)((int64_t)dv[L0] + ap);
+                    dv[L0f] = (double)((int64_t)dv[L0f] - ap);
+                    dv[L1] = (double)((int64_t)dv[L1] - ap);
+                    dv[L1f] = (double)((int64_t)dv[L1f] + ap);
+                }
+            }
+        }
+        st->proposed = V;
+    }
+    pcg_store(&g, rng);
+    free(metro), free(dv), free(vals);
+    colors_free(&C);
+    return 0;
+}
+
+/* WrappingUpdate.step, wrapping.py:43-90 (D=2).  Draws: choice(w, N) for the mu = 0 cycles (one per x,
+ * constant along t), choice(w, N) for mu = 1 (one per t), then per mu uniform(0, 1, N) (:76).
+ * dS_link = ((0.5/kappa) * cm) * ((2 * (m - delta(v)/W)) + cm)           (:69)
+ * mu = 0: dS[x] = dS_link[0].sum(axis=0) -- NumPy reduces the outer axis sequentially from row 0;
+ * mu = 1: dS[t] = dS_link[1].sum(axis=1) -- NumPy pairwise sum of each contiguous row. */
+int sv_o_worldline_wrapping(int32_t N, double kappa, double Weff, int64_t interval_w, int64_t *m, const void *v,
+                            int32_t v_is_float, int32_t sweeps, sv_rng *rng, sv_stats *stats) {
+    if (N < 2 || sweeps < 0 || interval_w < 1) return -1;
+    const int64_t V = (int64_t)N * N;
+    double *dvw = (double *)malloc(sizeof(double) * 2 * V), *row = (double *)malloc(sizeof(double) * N);
+    double *prob = (double *)malloc(sizeof(double) * 2 * N);
+    int64_t *cm = (int64_t *)malloc(sizeof(int64_t) * 2 * N);
+    const uint32_t k = (uint32_t)(2 * interval_w);
+    const double hk = 0.5 / kappa;
+    delta_v_by_W(N, v, v_is_float, Weff, dvw);
+    pcg g = pcg_load(rng);
+    for (int32_t sw = 0; sw < sweeps; sw++) {
+        sv_stats *st = &stats[sw];
+        memset(st, 0, sizeof(*st));
+        for (int64_t i = 0; i < 2 * N; i++) cm[i] = nonzero_value(pcg_bounded(&g, k, &st->rejections), interval_w);
+#define DSL(mu, t, x, c) \
+    ((hk * (double)(c)) * ((2 * ((double)m[(mu) * V + (t) * N + (x)] - dvw[(mu) * V + (t) * N + (x)])) + (double)(c)))
+        for (int mu = 0; mu < 2; mu++)
+            for (int64_t j = 0; j < N; j++) { /* cycle j: column x = j (mu = 0) or row t = j (mu = 1) */
+                const int64_t c = cm[mu * N + j];
+                double dS;
+                if (mu == 0) {
+                    dS = DSL(0, 0, j, c);
+                    for (int64_t t = 1; t < N; t++) dS = dS + DSL(0, t, j, c);
+                } else {
+                    for (int64_t x = 0; x < N; x++) row[x] = DSL(1, j, x, c);
+                    dS = np_pairwise_sum(row, N);
+                }
+                double p = exp(-dS);
+                p = p < 0.0 ? 0.0 : p;
+                prob[mu * N + j] = p > 1.0 ? 1.0 : p;
+            }
+#undef DSL
+        for (int mu = 0; mu < 2; mu++)
+            for (int64_t j = 0; j < N; j++) {
+                const double u = pcg_uniform(&g, 0.0, 1.0);
+                const double p = prob[mu * N + j];
+                const int acc = u < p;
+                st->accepted += acc;
+                st->acceptance_sum += p;
+                if (acc) {
+                    const int64_t c = cm[mu * N + j];
+                    if (mu == 0)
+                        for (int64_t t = 0; t < N; t++) m[t * N + j] += c;
+                    else
+                        for (int64_t x = 0; x < N; x++) m[V + j * N + x] += c;
+                }
+            }
+        st->proposed = 2 * N;
+    }
+    pcg_store(&g, rng);
+    free(dvw), free(row), free(prob), free(cm);
+    return 0;
+}

@@ -117,3 +117,26 @@ def test_villain_generators_golden(oracle_lib):
         np.testing.assert_allclose(np.cumsum([s.acceptance_sum / d for s in st]), c['acceptance'], rtol=1e-12)
         kinds.add(kind)
     assert kinds == set(ACCEPTANCE_DENOMINATOR)
+
+
+WORLDLINE_DENOMINATOR = {'VortexUpdate': lambda N: N * N, 'WrappingUpdate': lambda N: 2 * N}
+
+
+def test_worldline_generators_golden(oracle_lib):
+    """VortexUpdate and WrappingUpdate chains from the reference (finite and infinite W,
+    forced NumPy Lemire rejections) reproduced bit-for-bit by the oracle."""
+    kinds = set()
+    for c in cases('worldline_generators.npz'):
+        N, kind = c['N'], c['kind']
+        m, v = c['m0'].copy(), np.ascontiguousarray(c['v0'])
+        g = generator_from(c['rng0'])
+        iv = None if c['kw_interval'] == -1 else c['kw_interval']
+        st = oracle_lib.worldline_generator(kind, N, c['kappa'], c['W_eff'], m, v, c['sweeps'], g, iv)
+        assert (m == c['m']).all() and (v == c['v']).all(), (kind, N, c['W'])
+        assert (state_of(g) == c['rng1']).all(), (kind, N)
+        assert list(np.cumsum([s.accepted for s in st])) == list(c['accepted']), (kind, N)
+        d = WORLDLINE_DENOMINATOR[kind](N)
+        np.testing.assert_allclose(np.cumsum([s.acceptance_sum / d for s in st]), c['acceptance'], rtol=1e-12)
+        kinds.add(kind)
+    assert kinds == set(WORLDLINE_DENOMINATOR)
+    assert sum(1 for c in cases('worldline_generators.npz') if c['kw_interval'] == 3) >= 4  # rejection cases
