@@ -138,6 +138,16 @@ int sv_worldline_plaquette_coexact_run(sv_worldline *st, double kappa, double W_
 int sv_worldline_plaquette(sv_ctx *ctx, int32_t N, double kappa, double W_eff, int64_t *m, void *v,
                            int32_t v_is_float, const int64_t *order, sv_rng *rng, sv_stats *stats);
 
+/* ---- Worldline (m, v): the other updates of the Worldline Hammer -------------- */
+/* Replaces VortexUpdate.step, supervillain/generator/worldline/vortex.py:51-136 (interval_v: vortex.py:33):
+ * checkerboard Metropolis on v alone, m read only.  stats.proposed = V. */
+int sv_worldline_vortex_run(sv_worldline *st, double kappa, double W_eff, int64_t interval_v, int32_t sweeps,
+                            sv_rng *rng, sv_stats *stats);
+/* Replaces WrappingUpdate.step, supervillain/generator/worldline/wrapping.py:43-90 (interval_w: wrapping.py:26):
+ * 2N torus-cycle proposals on m, v read only.  stats.proposed = 2N. */
+int sv_worldline_wrapping_run(sv_worldline *st, double kappa, double W_eff, int64_t interval_w, int32_t sweeps,
+                              sv_rng *rng, sv_stats *stats);
+
 
 /* ---- Villain on a domain-decomposed lattice (multi-GPU; SURVEY.md 8e, BASELINE config 4) -------- */
 /* The same chain as sv_villain_* (NeighborhoodUpdate, neighborhood.py:59-137) on an Nt x Nx lattice

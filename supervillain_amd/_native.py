@@ -62,6 +62,8 @@ def lib():
         L.sv_worldline_plaquette_checkerboard_run.argtypes = [vp, f64, f64, i32, P(SvRng), P(SvStats)]
         L.sv_worldline_plaquette.argtypes = [vp, i32, f64, f64, vp, vp, i32, vp, P(SvRng), P(SvStats)]
         L.sv_worldline_plaquette_coexact_run.argtypes = [vp, f64, f64, i64, i32, P(SvRng), P(SvStats)]
+        L.sv_worldline_vortex_run.argtypes = [vp, f64, f64, i64, i32, P(SvRng), P(SvStats)]
+        L.sv_worldline_wrapping_run.argtypes = [vp, f64, f64, i64, i32, P(SvRng), P(SvStats)]
         L.sv_domain_unique_id.argtypes = [vp]
         L.sv_domain_create.argtypes = [vp, i32, i32, i32, i32, i32, i32, vp, P(vp)]
         L.sv_domain_destroy.argtypes = [vp]
@@ -86,6 +88,7 @@ EXPORTED = ('sv_ctx_create', 'sv_ctx_destroy', 'sv_last_error', 'sv_device_count
             'sv_worldline_destroy', 'sv_worldline_upload', 'sv_worldline_download', 'sv_worldline_coexact_run',
             'sv_worldline_coexact', 'sv_worldline_plaquette_ordered_run',
             'sv_worldline_plaquette_checkerboard_run', 'sv_worldline_plaquette', 'sv_worldline_plaquette_coexact_run',
+            'sv_worldline_vortex_run', 'sv_worldline_wrapping_run',
             'sv_domain_unique_id', 'sv_domain_create', 'sv_domain_destroy', 'sv_domain_upload', 'sv_domain_download',
             'sv_domain_run', 'sv_domain_exchange_plan',
             'sv_replicas_create', 'sv_replicas_destroy', 'sv_replicas_upload', 'sv_replicas_download',

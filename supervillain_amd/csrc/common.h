@@ -139,6 +139,8 @@ struct sv_worldline {
     int32_t ncol = 0;
     int64_t count[4] = {0, 0, 0, 0};
     int64_t offset[4] = {0, 0, 0, 0};
+    char *d_aux = nullptr;  // WrappingUpdate scratch (cycle proposals, dS, flags, pairwise plan)
+    size_t aux_cap = 0;
 };
 
 #define SV_HIP(call)                                                                                   \

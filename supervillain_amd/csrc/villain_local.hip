@@ -20,12 +20,9 @@
 //   Exact/Link dS_link:   ((-2pi*kappa) * cn) * ((dphi - (2pi)*n) - pi*cn)  (exact.py:95-98, link.py:78-81)
 //   face_sum:             (((0 + f0[x]) + f0[x-e0]) + f1[x]) + f1[x-e1]    (reference.py:48-64)
 //   Cohomology dS:        NumPy pairwise float64 sum over the slice        (cohomology.py:97)
-#include <algorithm>
 #include <cstdio>
-#include <cstring>
-#include <numeric>
 
-#include "villain.h"
+#include "local.h"
 
 namespace sv {
 
@@ -43,109 +40,7 @@ struct LParams {
     uint32_t k, thr;     // choice over 2 iv values: Lemire bound and threshold
 };
 
-namespace {
-
-__device__ __forceinline__ u128 lbase(const Block &b) { return u128{b.base_lo, b.base_hi}; }
-
-__device__ __forceinline__ void lreport(const DevScratch &S, uint32_t sweep, uint32_t block, uint32_t pos) {
-    uint32_t i = atomicAdd(S.nreport, 1u);
-    if (i < (uint32_t)MAX_REPORTS) S.reports[i] = Report{sweep, block, pos, 0};
-    __hip_atomic_store(S.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// stream position of bounded draw d, accounting for known rejected positions (sorted)
-__device__ __forceinline__ uint32_t lskip_pos(const Block &b, const uint32_t *skips, uint32_t d) {
-    uint32_t q = d;
-    for (int i = 0; i < b.nskip; i++)
-        if (skips[b.skip0 + i] <= q) q++;
-    return q;
-}
-
-// value of choice index j among (-iv .. -1, 1 .. iv): link.py:43, exact.py:38, cohomology.py:60
-__device__ __forceinline__ int64_t nonzero_value(uint32_t j, int64_t iv) {
-    return (int64_t)j < iv ? (int64_t)j - iv : (int64_t)j - iv + 1;
-}
-
-// Uniform block draws at positions p0, p0 + stride, ...: one table jump, then one affine map each.
-struct UniLane {
-    u128 s;
-    bool init;
-    __device__ __forceinline__ uint64_t next(const JumpTables *T, const Block &b, uint32_t p, const Affine &adv) {
-        s = init ? apply(adv, s) : jump(T, lbase(b), p);
-        init = true;
-        return xsl_rr(s);
-    }
-};
-
-// Bounded block uint32 words at draw positions q0, q0 + stride, ... (stride even, no skips): NumPy's
-// buffered half-word first, then the low and high halves of consecutive u64s.
-struct BndLane {
-    u128 s;
-    bool init;
-    __device__ __forceinline__ uint32_t next(const JumpTables *T, const Block &b, uint32_t q, const Affine &adv_half) {
-        if (b.has && q == 0) return b.buf;
-        const uint32_t qq = q - b.has;
-        s = init ? apply(adv_half, s) : jump(T, lbase(b), qq >> 1);
-        init = true;
-        const uint64_t X = xsl_rr(s);
-        return (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
-    }
-};
-
-// uint32 of bounded draw d by a full jump (blocks with known rejections)
-__device__ __forceinline__ uint32_t bnd_word_slow(const JumpTables *T, const Block &b, const uint32_t *skips,
-                                                  uint32_t d, uint32_t *qout) {
-    const uint32_t q = lskip_pos(b, skips, d);
-    *qout = q;
-    if (b.has && q == 0) return b.buf;
-    const uint32_t qq = q - b.has;
-    const uint64_t X = xsl_rr(jump(T, lbase(b), qq >> 1));
-    return (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
-}
-
-__device__ __forceinline__ double lwave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
-// One atomic pair per workgroup (all threads call it).
-__device__ __forceinline__ void lflush(sv_stats *st, int64_t acc, double psum) {
-    __shared__ unsigned long long s_acc[16];
-    __shared__ double s_ps[16];
-    unsigned long long a = (unsigned long long)acc;
-    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
-    psum = lwave_sum(psum);
-    if ((threadIdx.x & 63) == 0) {
-        s_acc[threadIdx.x >> 6] = a;
-        s_ps[threadIdx.x >> 6] = psum;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long ta = 0;
-        double tp = 0.0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); w++) {
-            ta += s_acc[w];
-            tp += s_ps[w];
-        }
-        atomicAdd((unsigned long long *)&st->accepted, ta);
-        unsafeAtomicAdd(&st->acceptance_sum, tp);
-    }
-}
-
-__device__ __forceinline__ double clip01(double p) {
-    p = p < 0.0 ? 0.0 : p;
-    return p > 1.0 ? 1.0 : p;
-}
-
-// colour-index e -> site (even N: row-major parity colouring, e = s >> 1)
-__device__ __forceinline__ int64_t even_site(int64_t e, int64_t N, int color) {
-    const int64_t half = N >> 1;
-    const int64_t t = e / half, j = e - t * half;
-    return t * N + 2 * j + ((color + t) & 1);
-}
-
-}  // namespace
+using namespace loc;
 
 // ------------------------------------------------------------------------------------------------
 // d(phi) into D (2, N, N) at the start of a Site sweep (site.py:81) or an Exact call (exact.py:71);
@@ -454,96 +349,25 @@ static void set_bounded(LParams &P, int64_t iv) {
     P.thr = (uint32_t)((0u - P.k) % P.k);
 }
 
-static int gcd_i(int64_t a, int64_t b) { return (int)std::gcd(a, b); }
+using namespace loc;
 
-// Grid for a pass over `count` elements whose lanes advance by the whole grid: the stride is a
-// multiple of `mult` (and of 256) so that per-lane stream positions stay arithmetic.
-static int grid_for(int64_t count, int64_t mult) {
-    const int64_t target = 256 * 2048;  // 8 waves per CU on 256 CUs
-    if (count <= target) return (int)std::max<int64_t>(1, (count + 255) / 256);
-    const int64_t l = mult / gcd_i(mult, 256) * 256;  // lcm(mult, 256)
-    int64_t S = std::max<int64_t>(1, target / l) * l;
-    return (int)(S / 256);
-}
-
-// Run `sweeps` sweeps of a local update in batches of up to 64: plan every draw block of the batch,
-// launch every pass, then read the abort flag once.  A Lemire rejection (known only on the device)
-// restores the batch-start snapshot and replays the batch with the rejected stream position skipped.
+// Villain state: the snapshot is (phi, n) as the update touches them
 template <class LaunchSweep>
 static void run_local(sv_villain *st, const std::vector<BlockSpec> &specs, int32_t sweeps, Cursor &cur, u128 inc,
                       sv_stats *stats, bool touches_phi, bool touches_n, LaunchSweep launch_sweep) {
     sv_ctx *ctx = st->ctx;
     const int64_t V = (int64_t)st->N * st->N;
-    const int nb = (int)specs.size();
-    SkipMap skips;
-    std::vector<Block> blocks;
-    std::vector<uint32_t> skipvec;
-    const int BATCH = 64;
     double *phi = st->phi[st->cur];
     int64_t *n = st->n[st->cur];
-    for (int sw = 0; sw < sweeps;) {
-        const int count = std::min(BATCH, sweeps - sw);
+    auto copy = [&](bool to_snap) {
         if (touches_phi)
-            SV_HIP(hipMemcpyAsync(st->snap_phi, phi, V * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+            SV_HIP(hipMemcpyAsync(to_snap ? st->snap_phi : phi, to_snap ? phi : st->snap_phi, V * sizeof(double),
+                                  hipMemcpyDeviceToDevice, ctx->stream));
         if (touches_n)
-            SV_HIP(hipMemcpyAsync(st->snap_n, n, 2 * V * sizeof(int64_t), hipMemcpyDeviceToDevice, ctx->stream));
-        for (int attempt = 0;; attempt++) {
-            if (attempt > 256) throw std::runtime_error("rejection replay did not converge");
-            Cursor c = cur;
-            plan_sweeps(ctx, c, inc, specs, sw, count, skips, blocks, skipvec);
-            upload_plan(ctx, blocks, skipvec);
-            clear_abort(ctx);
-            ctx->ensure_stats(count);
-            SV_HIP(hipMemsetAsync(ctx->d_stats, 0, count * sizeof(sv_stats), ctx->stream));
-            hipEvent_t ev;
-            ctx->time_begin(&ev);
-            for (int k = 0; k < count; k++) launch_sweep(k, ctx->d_blocks + (size_t)k * nb, ctx->d_stats + k);
-            ctx->time_end(ev, count);
-            SV_HIP(hipGetLastError());
-            AbortInfo a = read_abort(ctx);
-            if (a.abort) ctx->time_discard();
-            ctx->time_collect();
-            if (!a.abort) {
-                cur = c;
-                break;
-            }
-            absorb_reports(a, sw, skips);
-            if (touches_phi)
-                SV_HIP(hipMemcpyAsync(phi, st->snap_phi, V * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
-            if (touches_n)
-                SV_HIP(hipMemcpyAsync(n, st->snap_n, 2 * V * sizeof(int64_t), hipMemcpyDeviceToDevice, ctx->stream));
-        }
-        SV_HIP(hipMemcpyAsync(stats + sw, ctx->d_stats, count * sizeof(sv_stats), hipMemcpyDeviceToHost, ctx->stream));
-        SV_HIP(hipStreamSynchronize(ctx->stream));
-        for (int k = 0; k < count; k++) stats[sw + k].rejections = rejections_in(skips, sw + k, nb);
-        sw += count;
-    }
-}
-
-static Cursor cursor_of(const sv_rng *rng) {
-    return Cursor{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
-}
-
-static void store_cursor(const Cursor &c, sv_rng *rng) {
-    rng->state_hi = c.s.hi;
-    rng->state_lo = c.s.lo;
-    rng->has_uint32 = (int32_t)c.has;
-    rng->uinteger = c.buf;
-}
-
-// Pairwise-sum plan of NumPy's pairwise_sum (numpy/_core/src/umath/loops_utils.h.src) for length n.
-static void pairwise_plan(int64_t i0, int64_t n, std::vector<int32_t> &leaves, std::vector<uint8_t> &prog) {
-    if (n <= 128) {
-        leaves.push_back((int32_t)i0);
-        leaves.push_back((int32_t)n);
-        prog.push_back(0);
-        return;
-    }
-    int64_t n2 = n / 2;
-    n2 -= n2 % 8;
-    pairwise_plan(i0, n2, leaves, prog);
-    pairwise_plan(i0 + n2, n - n2, leaves, prog);
-    prog.push_back(1);
+            SV_HIP(hipMemcpyAsync(to_snap ? st->snap_n : n, to_snap ? n : st->snap_n, 2 * V * sizeof(int64_t),
+                                  hipMemcpyDeviceToDevice, ctx->stream));
+    };
+    run_batches(ctx, specs, sweeps, cur, inc, stats, [&] { copy(true); }, [&] { copy(false); }, launch_sweep);
 }
 
 }  // namespace svh

@@ -697,6 +697,7 @@ int sv_worldline_destroy(sv_worldline *st) {
     (void)hipFree(st->stripes);
     (void)hipFree(st->sites);
     if (st->f) (void)hipFree(st->f);
+    if (st->d_aux) (void)hipFree(st->d_aux);
     if (st->order) (void)hipFree(st->order);
     if (st->pos) (void)hipFree(st->pos);
     if (st->done) (void)hipFree(st->done);

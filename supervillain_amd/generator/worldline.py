@@ -178,3 +178,116 @@ class PlaquetteUpdate(_WorldlineDevice, Generator):
             + '\n' +
             f'    {self.acceptance / self.proposed :.6f} average Metropolis acceptance probability.'
         )
+
+
+# ------------------------------------------------------------------------------------------------
+# The rest of the Worldline Hammer: VortexUpdate (v only) and WrappingUpdate (m on whole
+# torus cycles).  Same constructors, attributes, `step` contracts and `report()` text as the reference.
+
+class _WorldlineLocal(_WorldlineDevice, Generator):
+    NAME = None
+    NOUN = None
+    FIELD = None  # 'm' or 'v': what the step returns
+
+    def _init_common(self, action, device, message):
+        if not _is_worldline(action):
+            raise ValueError(message)
+        self.Action = action
+        self.accepted = 0
+        self.proposed = 0
+        self.acceptance = 0.
+        self.sweeps = 0
+        self.rng = np.random.default_rng()
+        self.device = device
+
+    def __str__(self):
+        return self.NAME
+
+    def _advance(self, cfg, sweeps):
+        ctx, _, h = self._state()
+        m, v = self._fields(cfg)
+        L = _native.lib()
+        st = _native.stats_array(sweeps)
+        r = rng_from_numpy(self.rng)
+        ctx.check(L.sv_worldline_upload(h, _native.ptr(m), _native.ptr(v)), 'sv_worldline_upload')
+        ctx.check(self._run(L, h, sweeps, r, st), f'{self.NAME} run')
+        ctx.check(L.sv_worldline_download(h, _native.ptr(m), _native.ptr(v)), 'sv_worldline_download')
+        rng_to_numpy(r, self.rng)
+        P = self._proposals()
+        for k in range(sweeps):
+            self.sweeps += 1
+            self.proposed += P
+            self.acceptance += st[k].acceptance_sum / P
+            self.accepted += int(st[k].accepted)
+        Lat = self.Action.Lattice
+        if self.FIELD == 'm':
+            return cfg | {'m': wrap_like(cfg['m'], m, 1, Lat)}
+        return cfg | {'v': wrap_like(cfg['v'], v, 2, Lat)}
+
+    def step(self, cfg):
+        return self._advance(cfg, 1)
+
+    def _steps(self, cfg, count):
+        return self._advance(cfg, count)
+
+    def inline_observables(self, steps):
+        return {}
+
+    def report(self):
+        return (
+            f'There were {self.accepted} {self.NOUN} proposals accepted of {self.proposed} proposed updates.'
+            + '\n' +
+            f'    {self.accepted/self.proposed:.6f} acceptance rate'
+            + '\n' +
+            f'    {self.acceptance / self.sweeps:.6f} average Metropolis acceptance probability.'
+        )
+
+
+class VortexUpdate(_WorldlineLocal):
+    r'''Checkerboard Metropolis update of v alone, m untouched (supervillain/generator/worldline/vortex.py:12-190):
+    Δv ~ {-interval_v..-1, 1..interval_v} (finite W) or uniform(-interval_v, interval_v) (W = ∞).'''
+
+    NAME = 'VortexUpdate'
+    NOUN = 'vortex'
+    FIELD = 'v'
+
+    def __init__(self, action, interval_v=1, *, device=None):
+        self._init_common(action, device, 'Need a Worldline action')
+        self.interval_v = interval_v
+        self.vs = tuple(v for v in range(-interval_v, 0)) + tuple(v for v in range(1, interval_v + 1))
+
+    def _proposals(self):
+        return self.Action.Lattice.cells_of_degree[2]
+
+    def _run(self, L, h, sweeps, r, st):
+        return L.sv_worldline_vortex_run(h, float(self.Action.kappa), float(self.Action._W), int(self.interval_v),
+                                         sweeps, ctypes.byref(r), st)
+
+
+class WrappingUpdate(_WorldlineLocal):
+    r'''Coordinated changes of m on whole torus cycles, Δm ~ {-interval_w..-1, 1..interval_w} on every link of the
+    cycle (supervillain/generator/worldline/wrapping.py:9-98).'''
+
+    NAME = 'WrappingUpdate'
+    NOUN = 'single-wrapping'
+    FIELD = 'm'
+
+    def __init__(self, action, interval_w=1, *, device=None):
+        self._init_common(action, device, 'The WrappingUpdate requires the Worldline action.')
+        self.interval_w = interval_w
+        self.w = tuple(h for h in range(-interval_w, 0)) + tuple(h for h in range(1, interval_w + 1))
+
+    def _proposals(self):
+        L = self.Action.Lattice
+        return L.D * L.N ** (L.D - 1)  # n_cycles, wrapping.py:86
+
+    def _run(self, L, h, sweeps, r, st):
+        return L.sv_worldline_wrapping_run(h, float(self.Action.kappa), float(self.Action._W), int(self.interval_w),
+                                           sweeps, ctypes.byref(r), st)
+
+
+def Hammer(S, worms=1):
+    r'''The reference's Worldline Hammer (supervillain/generator/worldline/__init__.py:10-40) without its worm
+    (ClassicWorm is outside this build's hot path): Sequentially(Vortex, Coexact, Wrapping).'''
+    from supervillain_amd.generator.combining import Sequentially
+    return Sequentially((VortexUpdate(S), CoexactUpdate(S), WrappingUpdate(S)))
