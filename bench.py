@@ -23,6 +23,9 @@ Secondary workloads (not the headline line; BASELINE.json configs 5 and 3):
                         CohomologyUpdate per step, or one Villain Hammer step (Site, Link, Exact, Cohomology,
                         each with its own stream, as the reference's Hammer minus its worm); device-resident
                         fields; N > 1 runs independent chains
+  --workload vortex|wrapping|wlhammer
+                        the same for the Worldline rows: VortexUpdate, WrappingUpdate, or one Worldline
+                        Hammer step (Vortex, Coexact, Wrapping) at L=4096, W=1
 """
 import argparse
 import ctypes
@@ -42,7 +45,11 @@ WORLDLINE_BYTES = 168        # Plaquette (88) + Coexact (80) per
 # SURVEY.md 8(f) rows, compulsory HBM bytes per site and sweep: Site reads phi and n and
 # writes phi (8 + 16 + 8); Exact reads phi and n and writes n (8 + 16 + 16); Link the same per site
 # (2 links); Cohomology touches 2 N links (reported per site of the slice sum, not a roofline workload)
-LOCAL_BYTES = {'site': 32, 'exact': 40, 'link': 40, 'hammer': 32 + 40 + 40}
+LOCAL_BYTES = {'site': 32, 'exact': 40, 'link': 40, 'hammer': 32 + 40 + 40,
+               # Worldline: Vortex reads m and v and writes v (16 + 8 + 8); Wrapping reads m and v (16 + 8);
+               # the Worldline Hammer adds Coexact's 80
+               'vortex': 32, 'wrapping': 24, 'wlhammer': 32 + 80 + 24}
+WORLDLINE_KINDS = ('vortex', 'wrapping', 'wlhammer')
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
@@ -60,7 +67,8 @@ def parse():
     ap.add_argument('--strong', action='store_true', help='N>1: decompose one L x L lattice (strong scaling)')
     ap.add_argument('--tiles', default=None, help='tile grid TYxTX (default from N); with N=1 emulates the '
                                                    'decomposition on one GPU')
-    ap.add_argument('--workload', default='villain', choices=['villain', 'replicas', 'worldline', 'site', 'link', 'exact', 'cohomology', 'hammer'])
+    ap.add_argument('--workload', default='villain', choices=['villain', 'replicas', 'worldline', 'site', 'link', 'exact', 'cohomology', 'hammer', 'vortex',
+                             'wrapping', 'wlhammer'])
     ap.add_argument('--event-timing', default='batch', choices=['launch', 'batch'],
                     help='hipEvents around each batch of 64 fused launches (default) or around every launch')
     ap.add_argument('--replicas', type=int, default=1024, help='replicas workload: total replica count')
@@ -264,35 +272,47 @@ def run_worldline(args, world, rank, dist):
 
 
 def run_local(args, world, rank, dist):
-    """the Villain Hammer's local updates on a device-resident L x L state, cold start."""
+    """the Villain and Worldline Hammers' local updates on a device-resident L x L state,
+    cold start (Worldline: m = 0, v = 0)."""
     from supervillain_amd import _native
     from supervillain_amd._abi import rng_from_numpy
     L, kind = args.L, args.workload
     Lib = _native.lib()
     ctx = _native.context(_native.default_device())
     h = ctypes.c_void_p()
-    ctx.check(Lib.sv_villain_create(ctx.handle, L, ctypes.byref(h)), 'sv_villain_create')
-    phi = np.zeros((L, L))
-    n = np.zeros((2, L, L), dtype=np.int64)
-    ctx.check(Lib.sv_villain_upload(h, _native.ptr(phi), _native.ptr(n)), 'upload')
-    kinds = ['site', 'link', 'exact', 'cohomology'] if kind == 'hammer' else [kind]
+    worldline = kind in WORLDLINE_KINDS
+    if worldline:
+        ctx.check(Lib.sv_worldline_create(ctx.handle, L, 0, ctypes.byref(h)), 'sv_worldline_create')
+        m, v = np.zeros((2, L, L), dtype=np.int64), np.zeros((L, L), dtype=np.int64)
+        ctx.check(Lib.sv_worldline_upload(h, _native.ptr(m), _native.ptr(v)), 'upload')
+        kinds = ['vortex', 'coexact', 'wrapping'] if kind == 'wlhammer' else [kind]
+    else:
+        ctx.check(Lib.sv_villain_create(ctx.handle, L, ctypes.byref(h)), 'sv_villain_create')
+        phi, n = np.zeros((L, L)), np.zeros((2, L, L), dtype=np.int64)
+        ctx.check(Lib.sv_villain_upload(h, _native.ptr(phi), _native.ptr(n)), 'upload')
+        kinds = ['site', 'link', 'exact', 'cohomology'] if kind == 'hammer' else [kind]
     rngs = {k: rng_from_numpy(np.random.default_rng(100 * rank + i)) for i, k in enumerate(kinds)}
+    kp, W = args.kappa, args.W
     calls = {
-        'site': lambda k, st: Lib.sv_villain_site_run(h, args.kappa, float(np.pi), k, ctypes.byref(rngs['site']), st),
-        'link': lambda k, st: Lib.sv_villain_link_run(h, args.kappa, args.W, 1, k, ctypes.byref(rngs['link']), st),
-        'exact': lambda k, st: Lib.sv_villain_exact_run(h, args.kappa, 1, k, ctypes.byref(rngs['exact']), st),
-        'cohomology': lambda k, st: Lib.sv_villain_cohomology_run(h, args.kappa, 1, k,
-                                                                 ctypes.byref(rngs['cohomology']), st),
+        'site': lambda k, st: Lib.sv_villain_site_run(h, kp, float(np.pi), k, ctypes.byref(rngs['site']), st),
+        'link': lambda k, st: Lib.sv_villain_link_run(h, kp, W, 1, k, ctypes.byref(rngs['link']), st),
+        'exact': lambda k, st: Lib.sv_villain_exact_run(h, kp, 1, k, ctypes.byref(rngs['exact']), st),
+        'cohomology': lambda k, st: Lib.sv_villain_cohomology_run(h, kp, 1, k, ctypes.byref(rngs['cohomology']), st),
+        'vortex': lambda k, st: Lib.sv_worldline_vortex_run(h, kp, float(W), 1, k, ctypes.byref(rngs['vortex']), st),
+        'coexact': lambda k, st: Lib.sv_worldline_coexact_run(h, kp, float(W), 1, k, ctypes.byref(rngs['coexact']),
+                                                              st),
+        'wrapping': lambda k, st: Lib.sv_worldline_wrapping_run(h, kp, float(W), 1, k, ctypes.byref(rngs['wrapping']),
+                                                                st),
     }
 
     def run(k):
         acc = 0
-        if kind == 'hammer':  # Sequentially: one step of each generator in turn
+        if len(kinds) > 1:  # a Hammer: Sequentially, one step of each generator in turn
             for _ in range(k):
                 for g in kinds:
                     st = _native.stats_array(1)
                     ctx.check(calls[g](1, st), g)
-                    acc += st[0].accepted if g == 'site' else 0
+                    acc += st[0].accepted if g == kinds[0] else 0
         else:
             st = _native.stats_array(k)
             ctx.check(calls[kind](k, st), kind)
@@ -317,27 +337,43 @@ def run_local(args, world, rank, dist):
 
     def baseline():
         from oracle import oracle as O
-        names = {'site': 'SiteUpdate', 'link': 'LinkUpdate', 'exact': 'ExactUpdate', 'cohomology': 'CohomologyUpdate'}
-        pp, nn = np.zeros((L, L)), np.zeros((2, L, L), dtype=np.int64)
+        names = {'site': 'SiteUpdate', 'link': 'LinkUpdate', 'exact': 'ExactUpdate', 'cohomology': 'CohomologyUpdate',
+                 'vortex': 'VortexUpdate', 'wrapping': 'WrappingUpdate'}
         k = 2 if kind != 'cohomology' else 2000
         t = time.perf_counter()
-        for _ in range(k):
-            for g in kinds:
-                O.villain_generator(names[g], L, args.kappa, args.W, pp, nn, 1, np.random.default_rng(1))
+        if worldline:
+            mm, vv = np.zeros((2, L, L), dtype=np.int64), np.zeros((L, L), dtype=np.int64)
+            for _ in range(k):
+                for g in kinds:
+                    if g == 'coexact':
+                        O.worldline_coexact(L, kp, float(W), mm, vv, 1, np.random.default_rng(1))
+                    else:
+                        O.worldline_generator(names[g], L, kp, float(W), mm, vv, 1, np.random.default_rng(1))
+        else:
+            pp, nn = np.zeros((L, L)), np.zeros((2, L, L), dtype=np.int64)
+            for _ in range(k):
+                for g in kinds:
+                    O.villain_generator(names[g], L, kp, W, pp, nn, 1, np.random.default_rng(1))
         dt = time.perf_counter() - t
-        return {'value': k * L * L / dt, 'unit': 'lattice-site updates/s', 'cores': 1, 'kind': 'port',
+        unit = 'plaquette-updates/s' if worldline else 'lattice-site updates/s'
+        return {'value': k * L * L / dt, 'unit': unit, 'cores': 1, 'kind': 'port',
                 'sample': f'{k} steps of L={L} {kind}, oracle/sv_oracle.c single-threaded'}
 
     if rank == 0:
         what = {'site': 'SiteUpdate', 'link': 'LinkUpdate', 'exact': 'ExactUpdate', 'cohomology': 'CohomologyUpdate',
-                'hammer': 'Villain Hammer minus worm: SiteUpdate, LinkUpdate, ExactUpdate, CohomologyUpdate'}[kind]
-        config = {'workload': f'L={L} Villain {what} sweep per step, kappa={args.kappa}, W={args.W}, bit-exact '
-                              'reference chain (PCG64 replay), device-resident fields',
+                'hammer': 'Villain Hammer minus worm: SiteUpdate, LinkUpdate, ExactUpdate, CohomologyUpdate',
+                'vortex': 'VortexUpdate', 'wrapping': 'WrappingUpdate',
+                'wlhammer': 'Worldline Hammer minus worm: VortexUpdate, CoexactUpdate, WrappingUpdate'}[kind]
+        model = 'Worldline' if worldline else 'Villain'
+        config = {'workload': f'L={L} {model} {what} sweep per step, kappa={kp}, W={W}, bit-exact reference chain '
+                              '(PCG64 replay), device-resident fields',
                   'L': L, 'path': kind, 'parallelism': f'{world} independent chain(s)'}
+        unit = 'plaquette-updates/s' if worldline else 'lattice-site updates/s'
         report(args, world, world * L * L, L * L, elapsed, acc / (args.steps * L * L), step_kernel_s, config, L,
-               metric=f'lattice-site updates/sec ({what}), L={L} Villain', kernel=f'{kind} (all kernels of a step)',
-               alg_bytes=LOCAL_BYTES.get(kind, 0), survey_bytes=LOCAL_BYTES.get(kind, 0), baseline=baseline)
-    Lib.sv_villain_destroy(h)
+               metric=f'{unit[:-2]}/sec ({what}), L={L} {model}', unit=unit,
+               kernel=f'{kind} (all kernels of a step)', alg_bytes=LOCAL_BYTES.get(kind, 0),
+               survey_bytes=LOCAL_BYTES.get(kind, 0), baseline=baseline)
+    (Lib.sv_worldline_destroy if worldline else Lib.sv_villain_destroy)(h)
 
 
 def run_domain(args, world, rank, local, dist):

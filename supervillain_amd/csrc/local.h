@@ -3,6 +3,7 @@
 // arithmetic position sequences, stats flush, small math.  Host: batch driver with rejection replay.
 #pragma once
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 
@@ -119,23 +120,30 @@ namespace svh {
 namespace loc {
 using namespace sv;
 
-static int gcd_i(int64_t a, int64_t b) { return (int)std::gcd(a, b); }
+static inline int gcd_i(int64_t a, int64_t b) { return (int)std::gcd(a, b); }
 
 // Grid for a pass over `count` elements whose lanes advance by the whole grid: the stride is a
-// multiple of `mult` (and of 256) so that per-lane stream positions stay arithmetic.
-static int grid_for(int64_t count, int64_t mult) {
-    const int64_t target = 256 * 2048;  // 8 waves per CU on 256 CUs
+// multiple of `mult` (and of 256) so that per-lane stream positions stay arithmetic.  Lanes take
+// about `iters` (default 2; measured flat from 1 to 16 at L=4096) elements each (one 4-level table jump amortized over them), the grid staying between
+// 2^17 lanes (2 waves per SIMD) and 2^19; SV_GS_ITERS overrides `iters` for experiments.
+static inline int grid_for(int64_t count, int64_t mult) {
+    static const int64_t iters = [] {
+        const char *e = getenv("SV_GS_ITERS");
+        const int64_t v = e ? atoll(e) : 2;
+        return v >= 1 ? v : 2;
+    }();
+    const int64_t target = std::min<int64_t>(1 << 19, std::max<int64_t>(1 << 17, count / iters));
     if (count <= target) return (int)std::max<int64_t>(1, (count + 255) / 256);
     const int64_t l = mult / gcd_i(mult, 256) * 256;  // lcm(mult, 256)
     int64_t S = std::max<int64_t>(1, target / l) * l;
     return (int)(S / 256);
 }
 
-static Cursor cursor_of(const sv_rng *rng) {
+static inline Cursor cursor_of(const sv_rng *rng) {
     return Cursor{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
 }
 
-static void store_cursor(const Cursor &c, sv_rng *rng) {
+static inline void store_cursor(const Cursor &c, sv_rng *rng) {
     rng->state_hi = c.s.hi;
     rng->state_lo = c.s.lo;
     rng->has_uint32 = (int32_t)c.has;
@@ -143,7 +151,7 @@ static void store_cursor(const Cursor &c, sv_rng *rng) {
 }
 
 // Pairwise-sum plan of NumPy's pairwise_sum (numpy/_core/src/umath/loops_utils.h.src) for length n.
-static void pairwise_plan(int64_t i0, int64_t n, std::vector<int32_t> &leaves, std::vector<uint8_t> &prog) {
+static inline void pairwise_plan(int64_t i0, int64_t n, std::vector<int32_t> &leaves, std::vector<uint8_t> &prog) {
     if (n <= 128) {
         leaves.push_back((int32_t)i0);
         leaves.push_back((int32_t)n);
@@ -160,10 +168,12 @@ static void pairwise_plan(int64_t i0, int64_t n, std::vector<int32_t> &leaves, s
 // Run `sweeps` sweeps of a local update in batches of up to 64: plan every draw block of the batch,
 // launch every pass, then read the abort flag once.  A Lemire rejection (known only on the device)
 // restores the batch-start snapshot and replays the batch with the rejected stream position skipped.
-// snapshot()/restore() save and put back the fields the update changes.
+// snapshot()/restore() save and put back the fields the update changes; with may_reject == false (no
+// bounded draws, or a Lemire threshold of 0: power-of-two choice counts never reject) no snapshot is taken.
 template <class Snapshot, class Restore, class LaunchSweep>
-static void run_batches(sv_ctx *ctx, const std::vector<BlockSpec> &specs, int32_t sweeps, Cursor &cur, u128 inc,
-                        sv_stats *stats, Snapshot snapshot, Restore restore, LaunchSweep launch_sweep) {
+static inline void run_batches(sv_ctx *ctx, const std::vector<BlockSpec> &specs, int32_t sweeps, Cursor &cur, u128 inc,
+                        sv_stats *stats, bool may_reject, Snapshot snapshot, Restore restore,
+                        LaunchSweep launch_sweep) {
     const int nb = (int)specs.size();
     SkipMap skips;
     std::vector<Block> blocks;
@@ -171,7 +181,7 @@ static void run_batches(sv_ctx *ctx, const std::vector<BlockSpec> &specs, int32_
     const int BATCH = 64;
     for (int sw = 0; sw < sweeps;) {
         const int count = std::min(BATCH, sweeps - sw);
-        snapshot();
+        if (may_reject) snapshot();
         for (int attempt = 0;; attempt++) {
             if (attempt > 256) throw std::runtime_error("rejection replay did not converge");
             Cursor c = cur;
@@ -192,6 +202,7 @@ static void run_batches(sv_ctx *ctx, const std::vector<BlockSpec> &specs, int32_
                 cur = c;
                 break;
             }
+            if (!may_reject) throw std::runtime_error("unexpected NumPy Lemire rejection report");
             absorb_reports(a, sw, skips);
             restore();
         }

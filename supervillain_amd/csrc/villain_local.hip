@@ -107,10 +107,66 @@ __global__ __launch_bounds__(256) void site_pass(LParams P, double *phi, const i
     lflush(stat, acc_count, psum);
 }
 
+// SiteUpdate for even N without a dphi array: pass 0 forms dphi = d(phi) from the sweep-start phi on the
+// fly, decides colour 0 and keeps its accepted changes cphi0 (compact, colour index); pass 1 rebuilds the
+// reference's incrementally updated dphi on its links as d(phi_start) + d(cphi0) (site.py:111) from the
+// same sweep-start phi and cphi0.  phi is ping-ponged (phi_in stays the sweep-start field):
+//   colour 0: (phi + cphi0) + 0.0,  colour 1: (phi + 0.0) + cphi1   (site.py:110, both colour passes)
+template <int PASS>
+__global__ __launch_bounds__(256) void site_pp(LParams P, const double *phi_in, double *phi_out, const int64_t *n,
+                                               double *cbuf, const Block *blocks, const JumpTables *T, Affine adv_m,
+                                               Affine adv_e, sv_stats *stat, const int32_t *abort) {
+    if (*(volatile const int32_t *)abort) return;
+    const int64_t N = P.N, V = P.V, nc = P.V >> 1;
+    const int64_t S = (int64_t)gridDim.x * blockDim.x;
+    const Block BM = blocks[0], BD = blocks[1 + PASS];
+    UniLane um{u128{0, 0}, false}, ud{u128{0, 0}, false};
+    int64_t acc_count = 0;
+    double psum = 0.0;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nc; e += S) {
+        const int64_t s = even_site(e, N, PASS);
+        const double u = 0.0 + 1.0 * to_double(um.next(T, BM, (uint32_t)s, adv_m));
+        const double dph = P.lo + P.range * to_double(ud.next(T, BD, (uint32_t)e, adv_e));
+        const int64_t t = s / N, x = s - t * N;
+        const int64_t f0 = ((t + 1 == N) ? 0 : t + 1) * N + x, b0 = ((t == 0) ? N - 1 : t - 1) * N + x;
+        const int64_t f1 = t * N + ((x + 1 == N) ? 0 : x + 1), b1 = t * N + ((x == 0) ? N - 1 : x - 1);
+        const double ps = phi_in[s];
+        double D[4] = {0.0 + (phi_in[f0] - ps), 0.0 + (ps - phi_in[b0]), 0.0 + (phi_in[f1] - ps),
+                       0.0 + (ps - phi_in[b1])};
+        if (PASS == 1) {
+            D[0] = D[0] + (0.0 + (cbuf[f0 >> 1] - 0.0));
+            D[1] = D[1] + (0.0 + (0.0 - cbuf[b0 >> 1]));
+            D[2] = D[2] + (0.0 + (cbuf[f1 >> 1] - 0.0));
+            D[3] = D[3] + (0.0 + (0.0 - cbuf[b1 >> 1]));
+        }
+        const int64_t L[4] = {s, b0, V + s, V + b1};
+        const double cd_f = 0.0 + (0.0 - dph), cd_b = 0.0 + (dph - 0.0);
+        double dS = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const double cd = (q & 1) ? cd_b : cd_f;
+            dS += (P.half_kappa * cd) * ((2.0 * (D[q] - LTWO_PI * (double)n[L[q]])) + cd);
+        }
+        const double p = clip01(exp(-dS));
+        const int acc = u < p;
+        acc_count += acc;
+        psum += p;
+        const double cphi = dph * (double)acc;
+        if (PASS == 0) {
+            phi_out[s] = (ps + cphi) + 0.0;
+            cbuf[e] = cphi;
+        } else {
+            phi_out[s] = (ps + 0.0) + cphi;
+        }
+    }
+    lflush(stat, acc_count, psum);
+}
+
 // One colour pass of ExactUpdate (exact.py:85-115).  Blocks: [0] metropolis uniform(V), [1 + c] the
-// colour's choice(zs, n_c).  D = d(phi) is fixed for the call.
+// colour's choice(zs, n_c).  dphi = d(phi) is fixed for the call, so it is formed on the fly from phi
+// (bit-identical to the reference's array, and 16 B/site less traffic than keeping it in HBM).
 template <bool EVEN>
-__global__ __launch_bounds__(256) void exact_pass(LParams P, int64_t *n, const double *D, const int32_t *sites,
+__global__ __launch_bounds__(256) void exact_pass(LParams P, int64_t *n, const double *phi, const int32_t *sites,
                                                   int64_t nc, int color, const Block *blocks, const uint32_t *skips,
                                                   const JumpTables *T, Affine adv_m, Affine adv_half, sv_stats *stat,
                                                   DevScratch Sx, uint32_t sweep) {
@@ -137,13 +193,17 @@ __global__ __launch_bounds__(256) void exact_pass(LParams P, int64_t *n, const d
         const int64_t t = s / N, x = s - t * N;
         const int64_t L[4] = {s, ((t == 0) ? N - 1 : t - 1) * N + x, V + s, V + t * N + ((x == 0) ? N - 1 : x - 1)};
         const int64_t cn_f = 0 + (0 - z), cn_b = 0 + (z - 0);
+        // d(phi) on the four links, exactly as d() forms it (phi is fixed during the update, exact.py:71)
+        const double ps = phi[s];
+        const double D[4] = {0.0 + (phi[((t + 1 == N) ? 0 : t + 1) * N + x] - ps), 0.0 + (ps - phi[L[1]]),
+                             0.0 + (phi[t * N + ((x + 1 == N) ? 0 : x + 1)] - ps), 0.0 + (ps - phi[L[3] - V])};
         int64_t nv[4];
         double dS = 0.0;
 #pragma unroll
         for (int q4 = 0; q4 < 4; q4++) {
             nv[q4] = n[L[q4]];
             const double cn = (double)((q4 & 1) ? cn_b : cn_f);
-            dS += (P.m2pik * cn) * ((D[L[q4]] - LTWO_PI * (double)nv[q4]) - LPI * cn);
+            dS += (P.m2pik * cn) * ((D[q4] - LTWO_PI * (double)nv[q4]) - LPI * cn);
         }
         const double p = clip01(exp(-dS));
         const int acc = u < p;
@@ -354,7 +414,7 @@ using namespace loc;
 // Villain state: the snapshot is (phi, n) as the update touches them
 template <class LaunchSweep>
 static void run_local(sv_villain *st, const std::vector<BlockSpec> &specs, int32_t sweeps, Cursor &cur, u128 inc,
-                      sv_stats *stats, bool touches_phi, bool touches_n, LaunchSweep launch_sweep) {
+                      sv_stats *stats, bool may_reject, bool touches_phi, bool touches_n, LaunchSweep launch_sweep) {
     sv_ctx *ctx = st->ctx;
     const int64_t V = (int64_t)st->N * st->N;
     double *phi = st->phi[st->cur];
@@ -367,7 +427,7 @@ static void run_local(sv_villain *st, const std::vector<BlockSpec> &specs, int32
             SV_HIP(hipMemcpyAsync(to_snap ? st->snap_n : n, to_snap ? n : st->snap_n, 2 * V * sizeof(int64_t),
                                   hipMemcpyDeviceToDevice, ctx->stream));
     };
-    run_batches(ctx, specs, sweeps, cur, inc, stats, [&] { copy(true); }, [&] { copy(false); }, launch_sweep);
+    run_batches(ctx, specs, sweeps, cur, inc, stats, may_reject, [&] { copy(true); }, [&] { copy(false); }, launch_sweep);
 }
 
 }  // namespace svh
@@ -401,7 +461,21 @@ int sv_villain_site_run(sv_villain *st, double kappa, double interval_phi, int32
         const int gi = (int)std::min<int64_t>((V + 255) / 256, 4096);
         double *phi = st->phi[st->cur];
         const int64_t *n = st->n[st->cur];
-        run_local(st, specs, sweeps, cur, inc, stats, true, false, [&](int k, const Block *B, sv_stats *ds) {
+        if (even) {
+            // two launches per sweep; the new phi goes to the snapshot buffer, then the pointers swap
+            // (SiteUpdate never replays: it makes no bounded draws)
+            run_local(st, specs, sweeps, cur, inc, stats, false, false, false, [&](int k, const Block *B, sv_stats *ds) {
+                (void)k;
+                double *in = st->phi[st->cur], *out = st->snap_phi;
+                site_pp<0><<<grid, 256, 0, ctx->stream>>>(P, in, out, n, st->r, B, T, adv_m, adv_e, ds, ctx->d_abort);
+                site_pp<1><<<grid, 256, 0, ctx->stream>>>(P, in, out, n, st->r, B, T, adv_m, adv_e, ds, ctx->d_abort);
+                std::swap(st->phi[st->cur], st->snap_phi);
+            });
+            for (int k = 0; k < sweeps; k++) stats[k].proposed = V;
+            store_cursor(cur, rng);
+            return 0;
+        }
+        run_local(st, specs, sweeps, cur, inc, stats, false, true, false, [&](int k, const Block *B, sv_stats *ds) {
             (void)k;
             local_dphi_init<<<gi, 256, 0, ctx->stream>>>(N, phi, st->r, 1, ctx->d_abort);
             for (int c = 0; c < st->ncol; c++) {
@@ -445,21 +519,18 @@ int sv_villain_exact_run(sv_villain *st, double kappa, int64_t interval_z, int32
         const int grid = grid_for(V / 2 + 1, N);
         const int64_t Sl = (int64_t)grid * 256;
         const Affine adv_m = host_power(inc, 2 * Sl), adv_half = host_power(inc, Sl / 2);
-        const int gi = (int)std::min<int64_t>((V + 255) / 256, 4096);
         double *phi = st->phi[st->cur];
         int64_t *n = st->n[st->cur];
-        clear_abort(ctx);
-        local_dphi_init<<<gi, 256, 0, ctx->stream>>>(N, phi, st->r, 0, ctx->d_abort);  // exact.py:71 (phi fixed)
-        run_local(st, specs, sweeps, cur, inc, stats, false, true, [&](int k, const Block *B, sv_stats *ds) {
+        run_local(st, specs, sweeps, cur, inc, stats, P.thr != 0, false, true, [&](int k, const Block *B, sv_stats *ds) {
             for (int c = 0; c < st->ncol; c++) {
                 const int64_t nc = st->count[c];
                 if (!nc) continue;
                 if (even)
-                    exact_pass<true><<<grid, 256, 0, ctx->stream>>>(P, n, st->r, nullptr, nc, c, B, ctx->d_skips, T,
+                    exact_pass<true><<<grid, 256, 0, ctx->stream>>>(P, n, phi, nullptr, nc, c, B, ctx->d_skips, T,
                                                                     adv_m, adv_half, ds, scratch(ctx), (uint32_t)k);
                 else
                     exact_pass<false><<<(int)((nc + 255) / 256), 256, 0, ctx->stream>>>(
-                        P, n, st->r, st->sites + st->offset[c], nc, c, B, ctx->d_skips, T, adv_m, adv_half, ds,
+                        P, n, phi, st->sites + st->offset[c], nc, c, B, ctx->d_skips, T, adv_m, adv_half, ds,
                         scratch(ctx), (uint32_t)k);
             }
         });
@@ -494,7 +565,7 @@ int sv_villain_link_run(sv_villain *st, double kappa, int64_t W, int64_t interva
         const Affine adv_u = host_power(inc, Sl), adv_half = host_power(inc, Sl / 2);
         const double *phi = st->phi[st->cur];
         int64_t *n = st->n[st->cur];
-        run_local(st, specs, sweeps, cur, inc, stats, false, true, [&](int k, const Block *B, sv_stats *ds) {
+        run_local(st, specs, sweeps, cur, inc, stats, P.thr != 0, false, true, [&](int k, const Block *B, sv_stats *ds) {
             link_sweep<<<grid, 256, 0, ctx->stream>>>(P, phi, n, B, ctx->d_skips, T, adv_u, adv_half, ds,
                                                       scratch(ctx), (uint32_t)k);
         });

@@ -12,8 +12,9 @@
 //  * PlaquetteUpdate, checkerboard: this build's GPU-native chain: colour passes with f
 //    evaluated fresh.  Oracle: oracle/sv_oracle.c sv_o_worldline_plaquette_cb.
 #include <algorithm>
+#include <cmath>
 
-#include "common.h"
+#include "local.h"
 
 namespace sv {
 
@@ -116,7 +117,30 @@ struct WParams {
     double c;  // 0.5 / kappa
     int64_t it;
     uint32_t k, thr;
+    double Winv;     // 1 / W when W is a power of two (x * Winv == x / W exactly)
+    int32_t wpow2;
+    int32_t grid;    // grid-stride colour passes (even N): workgroups, stride S = 256 grid
+    Affine adv_m;    // metropolis positions advance by 2S per lane iteration
+    Affine adv_half; // bounded-draw words advance by S/2
 };
+
+// delta(v)/W on link (mu, s) = (t, x), the division as dvw_at does it (exact reciprocal for power-of-two W)
+template <bool VF>
+__device__ __forceinline__ double dvw_p(const void *v, int64_t N, int mu, int64_t s, int64_t t, int64_t x,
+                                        const WParams &P) {
+    const int64_t nb = mu == 0 ? t * N + (x == 0 ? N - 1 : x - 1) : (t == 0 ? N - 1 : t - 1) * N + x;
+    double d;
+    if (VF) {
+        const double *vf = (const double *)v;
+        const double diff = vf[s] - vf[nb];
+        d = mu == 0 ? 0.0 - (-diff) : 0.0 - diff;
+    } else {
+        const int64_t *vi = (const int64_t *)v;
+        const int64_t diff = vi[s] - vi[nb];
+        d = mu == 0 ? (double)(0 - (-diff)) : (double)(0 - diff);
+    }
+    return P.wpow2 ? d * P.Winv : d / P.Weff;
+}
 
 // ------------------------------------------------------------------------------------------------
 // CoexactUpdate colour pass.  Blocks per sweep: [0] metropolis (uniform V), [1+c] t for colour c.
@@ -214,152 +238,113 @@ __global__ __launch_bounds__(256) void plaquette_cb_pass(WParams P, int64_t *m, 
 }
 
 // ------------------------------------------------------------------------------------------------
-// Row kernels (even N): a wave owns the colour-c sites of one row chunk of 128 columns.  Every draw of
-// the chunk is one small-table composition away from a per-row base state (one table jump per wave,
-// uniform), instead of a 4-level table jump per lane -- the same addressing as the Villain sweep.
-static constexpr int ROWW = 128;  // columns per wave
-
-__device__ __forceinline__ void row_small(Affine *sm, const JumpTables *T) {
-    for (int e = threadIdx.x; e < ROWW; e += blockDim.x) sm[e] = T->small[e];
-    __syncthreads();
-}
-
-// uniform(0, 1) draw at stream position pos of a uniform block; pos_b: the wave's base position
-__device__ __forceinline__ double row_uniform(const JumpTables *T, const Affine *sm, const Block &b, int64_t pos_b,
-                                              int64_t pos) {
-    const u128 base = jump(T, wbase(b), (uint32_t)pos_b);
-    return to_double(xsl_rr(apply(sm[pos - pos_b], base)));
-}
-
-// bounded draw d (= the colour rank) of a choice block; d_b: the wave's smallest rank.  Skip lists
-// (after a Lemire rejection) take the per-lane path.
-__device__ __forceinline__ uint32_t row_bounded(const JumpTables *T, const Affine *sm, const Block &b,
-                                                const uint32_t *skips, int64_t d, int64_t d_b, uint32_t k,
-                                                uint32_t thr, const DevScratch &S, uint32_t sweep, uint32_t bidx) {
-    if (b.nskip) return wbounded(T, b, skips, (uint32_t)d, k, thr, S, sweep, bidx);
-    const int64_t qq = d - (int64_t)b.has;
-    const int64_t wb = (d_b - (int64_t)b.has) < 0 ? 0 : ((d_b - (int64_t)b.has) >> 1);
-    const u128 base = jump(T, wbase(b), (uint32_t)wb);
-    uint32_t word;
-    if (qq < 0) {
-        word = b.buf;
-    } else {
-        const uint64_t X = xsl_rr(apply(sm[(qq >> 1) - wb], base));
-        word = (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
-    }
-    bool rej;
-    const uint32_t idx = lemire(word, k, thr, &rej);
-    if (rej) {
-        wreport(S, sweep, bidx, (uint32_t)d);
-        __builtin_amdgcn_s_waitcnt(0);
-    }
-    return idx;
-}
-
+// Grid-stride colour passes (even N; local.h stream addressing): a lane owns colour site e, e + S, ...;
+// its metropolis and bounded-draw stream states advance by one precomputed affine map per iteration.
+// CoexactUpdate, coexact.py:85-120: t = choice(ts) on the colour, m += delta(t accepted).
 template <bool VF>
-__global__ __launch_bounds__(256) void coexact_rows(WParams P, int64_t *m, const void *v, int color,
-                                                    const Block *blocks, const uint32_t *skips, const JumpTables *T,
-                                                    StatStripe *stat, DevScratch S, uint32_t sweep) {
-    __shared__ Affine sm[ROWW];
-    row_small(sm, T);
+__global__ __launch_bounds__(256) void coexact_gs(WParams P, int64_t *m, const void *v, int color,
+                                                  const Block *blocks, const uint32_t *skips, const JumpTables *T,
+                                                  StatStripe *stat, DevScratch S, uint32_t sweep) {
     if (*(volatile const int32_t *)S.abort) return;
-    const int64_t N = P.N, V = N * N;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t tt = (int64_t)blockIdx.y * 4 + wave;
+    const int64_t N = P.N, V = N * N, nc = V >> 1;
+    const int64_t G = (int64_t)gridDim.x * blockDim.x;
+    const Block BM = blocks[0], BT = blocks[1 + color];
+    const bool slow = BT.nskip > 0;
+    loc::UniLane um{u128{0, 0}, false};
+    loc::BndLane bt{u128{0, 0}, false};
     int64_t acc_count = 0;
     double psum = 0.0;
-    if (tt < N) {
-        const int64_t x0 = (int64_t)blockIdx.x * ROWW;
-        const int64_t xs = x0 + ((tt + x0 + color) & 1);  // (t + x) % 2 == colour (even N)
-        const int64_t xx = xs + 2 * lane;
-        const int64_t lin_b = tt * N + xs;
-        if (xx < N && xx < x0 + ROWW) {
-            const int64_t x = tt * N + xx;
-            const int64_t tp = (tt + 1 == N) ? 0 : tt + 1, xp = (xx + 1 == N) ? 0 : xx + 1;
-            const int64_t xe0 = tp * N + xx;
-            const int64_t xe1 = tt * N + xp;
-            const double u = 0.0 + 1.0 * row_uniform(T, sm, blocks[0], lin_b, x);
-            const uint32_t j = row_bounded(T, sm, blocks[1 + color], skips, x >> 1, lin_b >> 1, P.k, P.thr, S, sweep,
-                                           1 + color);
-            const int64_t t = (int64_t)j < P.it ? (int64_t)j - P.it : (int64_t)j - P.it + 1;
-            const int mus[4] = {1, 1, 0, 0};
-            const int64_t ss[4] = {x, xe0, x, xe1};
-            const int64_t st_[4] = {tt, tp, tt, tt}, sx_[4] = {xx, xx, xx, xp};
-            const int64_t cm[4] = {-t, +t, +t, -t};
-            double dS = 0.0;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nc; e += G) {
+        const int64_t x = loc::even_site(e, N, color);
+        const int64_t tt = x / N, xx = x - tt * N;
+        const double u = 0.0 + 1.0 * to_double(um.next(T, BM, (uint32_t)x, P.adv_m));
+        uint32_t q = (uint32_t)e, w;
+        if (slow) w = loc::bnd_word_slow(T, BT, skips, (uint32_t)e, &q);
+        else w = bt.next(T, BT, (uint32_t)e, P.adv_half);
+        bool rej;
+        const uint32_t j = lemire(w, P.k, P.thr, &rej);
+        if (rej) wreport(S, sweep, 1u + (uint32_t)color, q);
+        const int64_t t = (int64_t)j < P.it ? (int64_t)j - P.it : (int64_t)j - P.it + 1;
+        const int64_t tp = (tt + 1 == N) ? 0 : tt + 1, xp = (xx + 1 == N) ? 0 : xx + 1;
+        const int64_t xe0 = tp * N + xx, xe1 = tt * N + xp;
+        const int mus[4] = {1, 1, 0, 0};
+        const int64_t ss[4] = {x, xe0, x, xe1};
+        const int64_t st_[4] = {tt, tp, tt, tt}, sx_[4] = {xx, xx, xx, xp};
+        const int64_t cm[4] = {-t, +t, +t, -t};
+        double dS = 0.0;
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int64_t l = mus[q] * V + ss[q];
-                const double a = P.c * (double)cm[q];
-                const double f = (double)m[l] - dvw_at<VF>(v, N, mus[q], ss[q], st_[q], sx_[q], P.Weff);
-                const double b = (2.0 * f) + (double)cm[q];
-                dS += a * b;
-            }
-            double p = exp(-dS);
-            p = p < 0.0 ? 0.0 : p;
-            p = p > 1.0 ? 1.0 : p;
-            const int acc = u < p;
-            acc_count = acc;
-            psum = p;
-            if (acc) {
-                m[x] += t;
-                m[xe1] -= t;
-                m[V + x] -= t;
-                m[V + xe0] += t;
-            }
+        for (int q4 = 0; q4 < 4; q4++) {
+            const int64_t l = mus[q4] * V + ss[q4];
+            const double a = P.c * (double)cm[q4];
+            const double f = (double)m[l] - dvw_p<VF>(v, N, mus[q4], ss[q4], st_[q4], sx_[q4], P);
+            const double b = (2.0 * f) + (double)cm[q4];
+            dS += a * b;
+        }
+        const double p = loc::clip01(exp(-dS));
+        const int acc = u < p;
+        acc_count += acc;
+        psum += p;
+        if (acc) {
+            m[x] += t;
+            m[xe1] -= t;
+            m[V + x] -= t;
+            m[V + xe0] += t;
         }
     }
     wflush(stat, acc_count, psum);
 }
 
+// Checkerboard PlaquetteUpdate colour pass (the GPU-native chain): blocks [0] metropolis,
+// [1 + 2c] change_m = choice((-1, 1)), [2 + 2c] change_v = choice((-1, 0, 1)) of colour c.
 template <bool VF>
-__global__ __launch_bounds__(256) void plaquette_cb_rows(WParams P, int64_t *m, void *v, int color, const Block *blocks,
-                                                         const uint32_t *skips, const JumpTables *T, StatStripe *stat,
-                                                         DevScratch S, uint32_t sweep) {
-    __shared__ Affine sm[ROWW];
-    row_small(sm, T);
+__global__ __launch_bounds__(256) void plaquette_cb_gs(WParams P, int64_t *m, void *v, int color, const Block *blocks,
+                                                       const uint32_t *skips, const JumpTables *T, StatStripe *stat,
+                                                       DevScratch S, uint32_t sweep) {
     if (*(volatile const int32_t *)S.abort) return;
-    const int64_t N = P.N, V = N * N;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t tt = (int64_t)blockIdx.y * 4 + wave;
+    const int64_t N = P.N, V = N * N, nc = V >> 1;
+    const int64_t G = (int64_t)gridDim.x * blockDim.x;
+    const Block BM = blocks[0], BCM = blocks[1 + 2 * color], BCV = blocks[2 + 2 * color];
+    const bool slow = BCM.nskip > 0 || BCV.nskip > 0;
+    loc::UniLane um{u128{0, 0}, false};
+    loc::BndLane bm{u128{0, 0}, false}, bv{u128{0, 0}, false};
     int64_t acc_count = 0;
     double psum = 0.0;
-    if (tt < N) {
-        const int64_t x0 = (int64_t)blockIdx.x * ROWW;
-        const int64_t xs = x0 + ((tt + x0 + color) & 1);
-        const int64_t xx = xs + 2 * lane;
-        const int64_t lin_b = tt * N + xs;
-        if (xx < N && xx < x0 + ROWW) {
-            const int64_t x = tt * N + xx;
-            const int64_t tp = (tt + 1 == N) ? 0 : tt + 1, xp = (xx + 1 == N) ? 0 : xx + 1;
-            const int64_t xm = tp * N + xx;
-            const int64_t xn = tt * N + xp;
-            const double u = 0.0 + 1.0 * row_uniform(T, sm, blocks[0], lin_b, x);
-            const uint32_t jm = row_bounded(T, sm, blocks[1 + 2 * color], skips, x >> 1, lin_b >> 1, 2u, 0u, S, sweep,
-                                            1 + 2 * color);
-            const uint32_t jv = row_bounded(T, sm, blocks[2 + 2 * color], skips, x >> 1, lin_b >> 1, 3u, 1u, S, sweep,
-                                            2 + 2 * color);
-            const int64_t cm = jm ? 1 : -1, cv = (int64_t)jv - 1;
-            const double f1 = (double)m[x] - dvw_at<VF>(v, N, 0, x, tt, xx, P.Weff);
-            const double f2 = (double)m[V + xm] - dvw_at<VF>(v, N, 1, xm, tp, xx, P.Weff);
-            const double f3 = (double)m[xn] - dvw_at<VF>(v, N, 0, xn, tt, xp, P.Weff);
-            const double f4 = (double)m[V + x] - dvw_at<VF>(v, N, 1, x, tt, xx, P.Weff);
-            const double df = (double)cm - (double)cv / P.Weff;
-            const double dS = df / P.kappa * ((((f1 + f2) - f3) - f4) + 2.0 * df);
-            double p = exp(-dS);
-            p = p < 0.0 ? 0.0 : p;
-            p = p > 1.0 ? 1.0 : p;
-            const int acc = u < p;
-            acc_count = acc;
-            psum = p;
-            if (acc) {
-                m[x] += cm;
-                m[V + xm] += cm;
-                m[xn] -= cm;
-                m[V + x] -= cm;
-                if (VF) ((double *)v)[x] += (double)cv;
-                else ((int64_t *)v)[x] += cv;
-            }
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nc; e += G) {
+        const int64_t x = loc::even_site(e, N, color);
+        const int64_t tt = x / N, xx = x - tt * N;
+        const double u = 0.0 + 1.0 * to_double(um.next(T, BM, (uint32_t)x, P.adv_m));
+        uint32_t qm = (uint32_t)e, qv = (uint32_t)e, wm, wv;
+        if (slow) {
+            wm = loc::bnd_word_slow(T, BCM, skips, (uint32_t)e, &qm);
+            wv = loc::bnd_word_slow(T, BCV, skips, (uint32_t)e, &qv);
+        } else {
+            wm = bm.next(T, BCM, (uint32_t)e, P.adv_half);
+            wv = bv.next(T, BCV, (uint32_t)e, P.adv_half);
+        }
+        bool rej;
+        const uint32_t jm = lemire(wm, 2u, 0u, &rej);
+        const uint32_t jv = lemire(wv, 3u, 1u, &rej);
+        if (rej) wreport(S, sweep, 2u + 2u * (uint32_t)color, qv);
+        const int64_t cm = jm ? 1 : -1, cv = (int64_t)jv - 1;
+        const int64_t tp = (tt + 1 == N) ? 0 : tt + 1, xp = (xx + 1 == N) ? 0 : xx + 1;
+        const int64_t xm = tp * N + xx, xn = tt * N + xp;
+        const double f1 = (double)m[x] - dvw_p<VF>(v, N, 0, x, tt, xx, P);
+        const double f2 = (double)m[V + xm] - dvw_p<VF>(v, N, 1, xm, tp, xx, P);
+        const double f3 = (double)m[xn] - dvw_p<VF>(v, N, 0, xn, tt, xp, P);
+        const double f4 = (double)m[V + x] - dvw_p<VF>(v, N, 1, x, tt, xx, P);
+        const double df = (double)cm - (P.wpow2 ? (double)cv * P.Winv : (double)cv / P.Weff);
+        const double dS = df / P.kappa * ((((f1 + f2) - f3) - f4) + 2.0 * df);
+        const double p = loc::clip01(exp(-dS));
+        const int acc = u < p;
+        acc_count += acc;
+        psum += p;
+        if (acc) {
+            m[x] += cm;
+            m[V + xm] += cm;
+            m[xn] -= cm;
+            m[V + x] -= cm;
+            if (VF) ((double *)v)[x] += (double)cv;
+            else ((int64_t *)v)[x] += cv;
         }
     }
     wflush(stat, acc_count, psum);
@@ -491,8 +476,8 @@ int wabsorb(const std::vector<Report> &reps, int first, SkipMap &skips) {
     return (int)best.first;
 }
 
-WParams wparams(int32_t N, double kappa, double Weff, int64_t it) {
-    WParams P;
+WParams wparams(int32_t N, double kappa, double Weff, int64_t it, u128 inc) {
+    WParams P{};
     P.N = N;
     P.kappa = kappa;
     P.Weff = Weff;
@@ -500,6 +485,16 @@ WParams wparams(int32_t N, double kappa, double Weff, int64_t it) {
     P.it = it;
     P.k = (uint32_t)(2 * it);
     P.thr = (uint32_t)((0u - P.k) % P.k);
+    int ex = 0;
+    P.wpow2 = std::isfinite(Weff) && Weff > 0 && std::frexp(Weff, &ex) == 0.5;
+    P.Winv = P.wpow2 ? 1.0 / Weff : 0.0;
+    if (N % 2 == 0) {
+        const int64_t V = (int64_t)N * N;
+        P.grid = svh::loc::grid_for(V / 2 + 1, N);
+        const int64_t G = (int64_t)P.grid * 256;
+        P.adv_m = host_power(inc, 2 * G);
+        P.adv_half = host_power(inc, G / 2);
+    }
     return P;
 }
 
@@ -523,7 +518,8 @@ void snapshot(sv_worldline *st, bool restore) {
 // counted in statistic stat_of[b].
 template <typename Launch>
 void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, int32_t sweeps, Cursor &cur, u128 inc,
-                       sv_stats *stats, Launch launch, int nstat = 1, std::vector<int> stat_of = {}) {
+                       sv_stats *stats, Launch launch, int nstat = 1, std::vector<int> stat_of = {},
+                       bool may_reject = true) {
     sv_ctx *ctx = st->ctx;
     const int nb = (int)specs.size();
     if (stat_of.empty()) stat_of.assign(nb, 0);
@@ -536,7 +532,7 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
     int sw = 0;
     while (sw < sweeps) {
         const int count = std::min(BATCH, sweeps - sw);
-        snapshot(st, false);
+        if (may_reject) snapshot(st, false);  // no bounded draw that can reject: nothing to replay
         for (int attempt = 0;; attempt++) {
             if (attempt > 256) throw std::runtime_error("rejection replay did not converge");
             Cursor c = cur;
@@ -560,6 +556,7 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
                 break;
             }
             ctx->time_discard();
+            if (!may_reject) throw std::runtime_error("unexpected NumPy Lemire rejection report");
             wabsorb(reps, sw, skips);
             snapshot(st, true);
         }
@@ -584,14 +581,13 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
 void launch_coexact(sv_worldline *st, const WParams &P, const Block *blocks, StatStripe *stat, uint32_t k,
                     const JumpTables *T) {
     sv_ctx *ctx = st->ctx;
-    if (st->N % 2 == 0) {  // row kernels
-        const dim3 grid((unsigned)((st->N + ROWW - 1) / ROWW), (unsigned)((st->N + 3) / 4));
+    if (st->N % 2 == 0) {  // grid-stride colour passes
         for (int c = 0; c < 2; c++) {
             if (st->v_is_float)
-                coexact_rows<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips, T, stat,
+                coexact_gs<true><<<P.grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips, T, stat,
                                                                   wscratch(ctx), k);
             else
-                coexact_rows<false><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips, T, stat,
+                coexact_gs<false><<<P.grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips, T, stat,
                                                                    wscratch(ctx), k);
         }
         return;
@@ -613,14 +609,13 @@ void launch_coexact(sv_worldline *st, const WParams &P, const Block *blocks, Sta
 void launch_plaquette_cb(sv_worldline *st, const WParams &P, const Block *blocks, StatStripe *stat, uint32_t k,
                          const JumpTables *T) {
     sv_ctx *ctx = st->ctx;
-    if (st->N % 2 == 0) {  // row kernels
-        const dim3 grid((unsigned)((st->N + ROWW - 1) / ROWW), (unsigned)((st->N + 3) / 4));
+    if (st->N % 2 == 0) {  // grid-stride colour passes
         for (int c = 0; c < 2; c++) {
             if (st->v_is_float)
-                plaquette_cb_rows<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips, T,
+                plaquette_cb_gs<true><<<P.grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips, T,
                                                                        stat, wscratch(ctx), k);
             else
-                plaquette_cb_rows<false><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips, T,
+                plaquette_cb_gs<false><<<P.grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips, T,
                                                                         stat, wscratch(ctx), k);
         }
         return;
@@ -742,12 +737,14 @@ int sv_worldline_coexact_run(sv_worldline *st, double kappa, double W_eff, int64
     try {
         if (interval_t < 1 || interval_t > (1 << 20)) throw std::invalid_argument("interval_t must be in [1, 2^20]");
         SV_HIP(hipSetDevice(ctx->device));
-        WParams P = wparams(st->N, kappa, W_eff, interval_t);
+        WParams P = wparams(st->N, kappa, W_eff, interval_t, u128{rng->inc_lo, rng->inc_hi});
         u128 inc{rng->inc_lo, rng->inc_hi};
         Cursor cur{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
         const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
-        run_colour_sweeps(st, coexact_specs(st), sweeps, cur, inc, stats,
-                          [&](const Block *blocks, StatStripe *stat, uint32_t k) { launch_coexact(st, P, blocks, stat, k, T); });
+        run_colour_sweeps(
+            st, coexact_specs(st), sweeps, cur, inc, stats,
+            [&](const Block *blocks, StatStripe *stat, uint32_t k) { launch_coexact(st, P, blocks, stat, k, T); }, 1, {},
+            P.thr != 0);
         rng->state_hi = cur.s.hi;
         rng->state_lo = cur.s.lo;
         rng->has_uint32 = (int32_t)cur.has;
@@ -777,7 +774,7 @@ int sv_worldline_plaquette_checkerboard_run(sv_worldline *st, double kappa, doub
     sv_ctx *ctx = st->ctx;
     try {
         SV_HIP(hipSetDevice(ctx->device));
-        WParams P = wparams(st->N, kappa, W_eff, 1);
+        WParams P = wparams(st->N, kappa, W_eff, 1, u128{rng->inc_lo, rng->inc_hi});
         u128 inc{rng->inc_lo, rng->inc_hi};
         Cursor cur{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
         const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
@@ -805,7 +802,8 @@ int sv_worldline_plaquette_coexact_run(sv_worldline *st, double kappa, double W_
     try {
         if (interval_t < 1 || interval_t > (1 << 20)) throw std::invalid_argument("interval_t must be in [1, 2^20]");
         SV_HIP(hipSetDevice(ctx->device));
-        const WParams Pp = wparams(st->N, kappa, W_eff, 1), Pc = wparams(st->N, kappa, W_eff, interval_t);
+        const u128 inc0{rng->inc_lo, rng->inc_hi};
+        const WParams Pp = wparams(st->N, kappa, W_eff, 1, inc0), Pc = wparams(st->N, kappa, W_eff, interval_t, inc0);
         u128 inc{rng->inc_lo, rng->inc_hi};
         Cursor cur{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
         const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
@@ -839,7 +837,7 @@ int sv_worldline_plaquette_ordered_run(sv_worldline *st, double kappa, double W_
     try {
         SV_HIP(hipSetDevice(ctx->device));
         const int64_t N = st->N, V = N * N;
-        WParams P = wparams(st->N, kappa, W_eff, 1);
+        WParams P = wparams(st->N, kappa, W_eff, 1, u128{rng->inc_lo, rng->inc_hi});
         u128 inc{rng->inc_lo, rng->inc_hi};
         Cursor cur{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
         const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);

@@ -13,6 +13,7 @@
 // sequential chain over t per column -- done by one wave per 16 columns while three waves stage the
 // link terms through LDS; the mu = 1 cycles (rows) are NumPy's pairwise sum of a contiguous row, one
 // workgroup per row (8 lanes per <=128-element leaf, one per pairwise accumulator).
+#include <cmath>
 #include <cstdio>
 
 #include "local.h"
@@ -21,11 +22,19 @@ namespace sv {
 
 #define WTWO_PI 6.283185307179586
 
+// x / W.  For W a power of two (W = 1, 2, 4, ...) x * (1/W) is the same correctly rounded value and
+// avoids the FP64 division sequence.
+__device__ __forceinline__ double div_w(double x, double Weff, double Winv, int wpow2) {
+    return wpow2 ? x * Winv : x / Weff;
+}
+
 struct VxParams {
     int32_t N;
     int64_t V;
     double hk;          // 0.5 / kappa
     double Weff;        // Worldline._W
+    double Winv;        // 1 / W when W is a power of two
+    int32_t wpow2;
     double lo, range;   // W = inf: uniform(-interval_v, +interval_v)
     int64_t iv;         // finite W: choice over (-iv .. -1, 1 .. iv)
     uint32_t k, thr;
@@ -78,10 +87,10 @@ __global__ __launch_bounds__(256) void vortex_pass(VxParams P, const int64_t *m,
         int64_t ai = 0;
         if (VF) {
             a = P.lo + P.range * to_double(up.next(T, BP, (uint32_t)e, adv_p));
-            c0 = (0.0 - (-a)) / P.Weff;
-            c0f = (0.0 + (-a)) / P.Weff;
-            c1 = (0.0 - a) / P.Weff;
-            c1f = (0.0 + a) / P.Weff;
+            c0 = div_w(0.0 - (-a), P.Weff, P.Winv, P.wpow2);
+            c0f = div_w(0.0 + (-a), P.Weff, P.Winv, P.wpow2);
+            c1 = div_w(0.0 - a, P.Weff, P.Winv, P.wpow2);
+            c1f = div_w(0.0 + a, P.Weff, P.Winv, P.wpow2);
             d0 = dv[L0];
             d0f = dv[L0f];
             d1 = dv[L1];
@@ -95,10 +104,10 @@ __global__ __launch_bounds__(256) void vortex_pass(VxParams P, const int64_t *m,
             if (rej) lreport(Sx, sweep, 1u + (uint32_t)color, q);
             ai = nonzero_value(idx, P.iv);
             a = (double)ai;
-            c0 = (double)(0 - (-ai)) / P.Weff;
-            c0f = (double)(0 + (-ai)) / P.Weff;
-            c1 = (double)(0 - ai) / P.Weff;
-            c1f = (double)(0 + ai) / P.Weff;
+            c0 = div_w((double)(0 - (-ai)), P.Weff, P.Winv, P.wpow2);
+            c0f = div_w((double)(0 + (-ai)), P.Weff, P.Winv, P.wpow2);
+            c1 = div_w((double)(0 - ai), P.Weff, P.Winv, P.wpow2);
+            c1f = div_w((double)(0 + ai), P.Weff, P.Winv, P.wpow2);
             // delta(v) of the current integer v (exact; equals the reference's incremental delta_v)
             const int64_t *vi = (const int64_t *)vv;
             const int64_t vs = vi[s];
@@ -108,10 +117,10 @@ __global__ __launch_bounds__(256) void vortex_pass(VxParams P, const int64_t *m,
             d1f = (double)(0 - (vi[f0] - vs));
         }
         double dS = 0.0;  // coface_sum_at order: l1[x], l1[x+e0], l0[x], l0[x+e1]
-        dS += (P.hk * (-c1)) * ((2.0 * ((double)m[L1] - d1 / P.Weff)) - c1);
-        dS += (P.hk * (-c1f)) * ((2.0 * ((double)m[L1f] - d1f / P.Weff)) - c1f);
-        dS += (P.hk * (-c0)) * ((2.0 * ((double)m[L0] - d0 / P.Weff)) - c0);
-        dS += (P.hk * (-c0f)) * ((2.0 * ((double)m[L0f] - d0f / P.Weff)) - c0f);
+        dS += (P.hk * (-c1)) * ((2.0 * ((double)m[L1] - div_w(d1, P.Weff, P.Winv, P.wpow2))) - c1);
+        dS += (P.hk * (-c1f)) * ((2.0 * ((double)m[L1f] - div_w(d1f, P.Weff, P.Winv, P.wpow2))) - c1f);
+        dS += (P.hk * (-c0)) * ((2.0 * ((double)m[L0] - div_w(d0, P.Weff, P.Winv, P.wpow2))) - c0);
+        dS += (P.hk * (-c0f)) * ((2.0 * ((double)m[L0f] - div_w(d0f, P.Weff, P.Winv, P.wpow2))) - c0f);
         const double p = clip01(exp(-dS));
         const int acc = u < p;
         acc_count += acc;
@@ -139,13 +148,15 @@ struct WrParams {
     int64_t V;
     double hk;    // 0.5 / kappa
     double Weff;
+    double Winv;
+    int32_t wpow2;
     int64_t iw;
     uint32_t k, thr;
 };
 
 // delta(v)/W on link (mu, t, x) (reference.py:27-45 then / _W, wrapping.py:69)
 template <bool VF>
-__device__ __forceinline__ double wr_dvw(const void *v, int64_t N, int mu, int64_t t, int64_t x, double Weff) {
+__device__ __forceinline__ double wr_dvw(const void *v, int64_t N, int mu, int64_t t, int64_t x, const WrParams &P) {
     const int64_t s = t * N + x;
     const int64_t nb = mu == 0 ? t * N + (x == 0 ? N - 1 : x - 1) : (t == 0 ? N - 1 : t - 1) * N + x;
     double d;
@@ -158,14 +169,14 @@ __device__ __forceinline__ double wr_dvw(const void *v, int64_t N, int mu, int64
         const int64_t diff = vi[s] - vi[nb];
         d = mu == 0 ? (double)(0 - (-diff)) : (double)(0 - diff);
     }
-    return d / Weff;
+    return div_w(d, P.Weff, P.Winv, P.wpow2);
 }
 
 // dS_link = ((0.5/kappa) * cm) * ((2 * (m - delta(v)/W)) + cm)   (wrapping.py:69)
 template <bool VF>
 __device__ __forceinline__ double wr_term(const WrParams &P, const int64_t *m, const void *v, int mu, int64_t t,
                                           int64_t x, int64_t c) {
-    const double dvw = wr_dvw<VF>(v, P.N, mu, t, x, P.Weff);
+    const double dvw = wr_dvw<VF>(v, P.N, mu, t, x, P);
     return (P.hk * (double)c) * ((2.0 * ((double)m[mu * P.V + t * P.N + x] - dvw)) + (double)c);
 }
 
@@ -185,7 +196,7 @@ __global__ void wrap_draw(WrParams P, const Block *blocks, const uint32_t *skips
 // mu = 0 cycles: dS[x] = sum over t of dS_link[0][t, x], sequentially from t = 0 (NumPy axis-0 reduce).
 // Workgroup = 16 columns; waves 1..3 stage RC rows x 16 columns of link terms in LDS (double buffered),
 // wave 0 lanes 0..15 add them in order.
-static constexpr int WR_CW = 16, WR_RC = 96;
+static constexpr int WR_CW = 8, WR_RC = 192, WR_LOADERS = 192;
 template <bool VF>
 __global__ __launch_bounds__(256) void wrap_cols(WrParams P, const int64_t *m, const void *v, const int64_t *cprop,
                                                  double *dS, const int32_t *abort) {
@@ -195,12 +206,17 @@ __global__ __launch_bounds__(256) void wrap_cols(WrParams P, const int64_t *m, c
     const int64_t x0 = (int64_t)blockIdx.x * WR_CW;
     const int tid = threadIdx.x;
     const int nch = (int)((N + WR_RC - 1) / WR_RC);
+    // loader thread lt (waves 1..3) owns column lt % WR_CW and rows lt / WR_CW + 24 k of each chunk
+    const int lt = tid - 64, col = lt & (WR_CW - 1), r0 = lt / WR_CW;
+    const int64_t xl = x0 + col;
+    const int64_t cl = (tid >= 64 && xl < N) ? cprop[xl] : 0;
     auto fill = [&](int ch) {
-        const int lt = tid - 64;
-        for (int e = lt; e < WR_RC * WR_CW; e += 192) {
-            const int r = e / WR_CW, col = e - r * WR_CW;
-            const int64_t t = (int64_t)ch * WR_RC + r, x = x0 + col;
-            if (t < N && x < N) tile[ch & 1][r][col] = wr_term<VF>(P, m, v, 0, t, x, cprop[x]);
+        if (xl >= N) return;
+#pragma unroll
+        for (int k = 0; k < WR_RC / (WR_LOADERS / WR_CW); k++) {
+            const int r = r0 + k * (WR_LOADERS / WR_CW);
+            const int64_t t = (int64_t)ch * WR_RC + r;
+            if (t < N) tile[ch & 1][r][col] = wr_term<VF>(P, m, v, 0, t, xl, cl);
         }
     };
     if (tid >= 64) fill(0);
@@ -312,6 +328,12 @@ __global__ void wrap_apply(WrParams P, int64_t *m, const int64_t *cprop, const i
 namespace svh {
 using namespace loc;
 
+static void set_winv(double W, double &Winv, int32_t &pow2) {
+    int e = 0;
+    pow2 = std::isfinite(W) && W > 0 && std::frexp(W, &e) == 0.5;
+    Winv = pow2 ? 1.0 / W : 0.0;
+}
+
 static void wl_bounded(int64_t iv, uint32_t &k, uint32_t &thr) {
     if (iv < 1) throw std::invalid_argument("the interval must be >= 1");
     if (iv > (1 << 20)) throw std::invalid_argument("interval too large");
@@ -353,6 +375,7 @@ int sv_worldline_vortex_run(sv_worldline *st, double kappa, double W_eff, int64_
         P.V = V;
         P.hk = 0.5 / kappa;
         P.Weff = W_eff;
+        set_winv(W_eff, P.Winv, P.wpow2);
         if (vf) {
             if (interval_v < 1) throw std::invalid_argument("the interval must be >= 1");
             P.lo = -(double)interval_v;
@@ -373,7 +396,7 @@ int sv_worldline_vortex_run(sv_worldline *st, double kappa, double W_eff, int64_
         if (vf && !st->f) SV_HIP(hipMalloc(&st->f, 2 * V * sizeof(double)));  // delta_v (vortex.py:98)
         const int gi = (int)std::min<int64_t>((V + 255) / 256, 4096);
         run_batches(
-            ctx, specs, sweeps, cur, inc, stats, [&] { wl_copy(st, true, false, true); },
+            ctx, specs, sweeps, cur, inc, stats, !vf && P.thr != 0, [&] { wl_copy(st, true, false, true); },
             [&] { wl_copy(st, false, false, true); },
             [&](int k, const Block *B, sv_stats *ds) {
                 if (vf) vortex_dv_init<<<gi, 256, 0, ctx->stream>>>(N, (const double *)st->v, st->f, ctx->d_abort);
@@ -423,6 +446,7 @@ int sv_worldline_wrapping_run(sv_worldline *st, double kappa, double W_eff, int6
         P.V = V;
         P.hk = 0.5 / kappa;
         P.Weff = W_eff;
+        set_winv(W_eff, P.Winv, P.wpow2);
         P.iw = interval_w;
         wl_bounded(interval_w, P.k, P.thr);
         u128 inc{rng->inc_lo, rng->inc_hi};
@@ -460,7 +484,7 @@ int sv_worldline_wrapping_run(sv_worldline *st, double kappa, double W_eff, int6
         const int gcols = (int)((N + WR_CW - 1) / WR_CW);
         const int gapp = (int)std::min<int64_t>((2 * V + 255) / 256, 8192);
         run_batches(
-            ctx, specs, sweeps, cur, inc, stats, [&] { wl_copy(st, true, true, false); },
+            ctx, specs, sweeps, cur, inc, stats, P.thr != 0, [&] { wl_copy(st, true, true, false); },
             [&] { wl_copy(st, false, true, false); },
             [&](int k, const Block *B, sv_stats *ds) {
                 wrap_draw<<<g2n, 256, 0, ctx->stream>>>(P, B, ctx->d_skips, T, cprop, scratch(ctx), (uint32_t)k);
