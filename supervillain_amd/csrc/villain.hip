@@ -210,6 +210,9 @@ __device__ __forceinline__ int32_t wrapN(int32_t v, int32_t N) {
     return v;
 }
 
+#ifndef SV_SCALAR_WAVE
+#define SV_SCALAR_WAVE 1
+#endif
 #ifndef SV_ABLATE
 #define SV_ABLATE 0  // timing experiments only: 1 = no exp, 2 = no RNG compositions, 4 = no wrapped-column jumps,
                      // 8 = no HBM stores, 16 = no HBM loads, 64 = no choice draws
@@ -465,7 +468,12 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
 
     const FGeom &Gm = A.G;
     const int32_t Nt = Gm.Nt, Nx = Gm.Nx;
+    // the wave index is uniform: keep it (and all row / ring-slot arithmetic derived from it) scalar
+#if SV_SCALAR_WAVE
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+#else
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#endif
     const int64_t V = Gm.plane;
     // global row of local row q; memory offset of local row q / local column c
     auto grow = [&](int32_t q) { return wrapN(Gm.T0 + q, Nt); };
