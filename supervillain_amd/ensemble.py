@@ -10,6 +10,7 @@ import numpy as np
 
 from supervillain_amd.batch import Batch
 from supervillain_amd.generator.combining import KeepEvery
+from supervillain_amd.pipeline import DeviceChain, device_program
 
 logger = logging.getLogger(__name__)
 
@@ -26,7 +27,12 @@ class Ensemble:
         self.configuration = configurations
         return self
 
-    def generate(self, steps, generator, start='cold', progress=_no_op, starting_index=0, index_stride=1):
+    def generate(self, steps, generator, start='cold', progress=_no_op, starting_index=0, index_stride=1,
+                 device_resident=True):
+        '''As the reference (ensemble.py:47-100).  With device_resident (default) and a generator built from this
+        package's device generators (alone, Sequentially, KeepEvery), the fields stay in HBM for the whole run and
+        only each kept configuration is copied back (supervillain_amd.pipeline) -- the same
+        chain, counters and rng states as the per-step loop.'''
         self.configuration = self.Action.configurations(steps)
         self.configuration |= generator.inline_observables(steps)
         self.index_stride = index_stride
@@ -39,15 +45,31 @@ class Ensemble:
         else:
             raise ValueError(f'Not sure how to transform a {type(start)} into a starting configuration.')
         t0 = time.perf_counter()
-        self.configuration[0] = generator.step(seed)
-        for i in progress(range(1, steps), desc='Generation'):
-            self.configuration[i] = generator.step(self.configuration[i - 1])
+        program = device_program(generator) if device_resident and steps > 0 else None
+        if program is not None:
+            chain = DeviceChain(self.Action, program)
+            try:
+                chain.upload(seed)
+                self.configuration[0] = self._emit(chain)
+                for i in progress(range(1, steps), desc='Generation'):
+                    self.configuration[i] = self._emit(chain)
+            finally:
+                chain.close()
+        else:
+            self.configuration[0] = generator.step(seed)
+            for i in progress(range(1, steps), desc='Generation'):
+                self.configuration[i] = generator.step(self.configuration[i - 1])
         self.start = start
         self.generator = generator
         logger.info(f'Generation of {steps} configurations: {time.perf_counter() - t0:.3f} s')
         for line in generator.report().split('\n'):
             logger.info(line)
         return self
+
+    @staticmethod
+    def _emit(chain):
+        obs = chain.advance()
+        return chain.download() | obs
 
     @classmethod
     def continue_from(cls, ensemble, steps, progress=_no_op):

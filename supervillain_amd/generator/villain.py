@@ -77,43 +77,55 @@ class NeighborhoodUpdate(DeviceState, Generator):
             except Exception:
                 pass
 
-    def _advance(self, phi, n, sweeps):
-        """Run `sweeps` sweeps on host arrays phi (1,N,N) f64 and n (2,N,N) i64, in place."""
-        ctx, N, h = self._state()
+    DEVICE_KIND = 'villain'
+
+    def _run_on(self, ctx, h, sweeps):
+        """`sweeps` sweeps on the device-resident state h (sv_villain); folds the counters like
+        neighborhood.py:131-135 and returns the inline observables of the new state (or None)."""
         L = _native.lib()
         st = _native.stats_array(sweeps)
         r = rng_from_numpy(self.rng)
-        ctx.check(L.sv_villain_upload(h, _native.ptr(phi), _native.ptr(n)), 'sv_villain_upload')
         ctx.check(L.sv_villain_run(h, float(self.kappa), int(self.Action.W), float(self.interval_phi),
                                    int(self.interval_n), sweeps, ctypes.byref(r), st, int(self.path)),
                   'sv_villain_run')
-        inline = None
-        if self.inline:
-            out = np.zeros(4)
-            ctx.check(L.sv_villain_observables(h, float(self.kappa), _native.ptr(out)), 'sv_villain_observables')
-            inline = out
-        ctx.check(L.sv_villain_download(h, _native.ptr(phi), _native.ptr(n)), 'sv_villain_download')
         rng_to_numpy(r, self.rng)
         V = self.Lattice.sites
-        for k in range(sweeps):  # fold exactly like neighborhood.py:131-135
+        for k in range(sweeps):
             self.sweeps += 1
             self.proposed += V
             self.acceptance += st[k].acceptance_sum / V
             self.accepted += int(st[k].accepted)
+        if self.inline:
+            out = np.zeros(4)
+            ctx.check(L.sv_villain_observables(h, float(self.kappa), _native.ptr(out)), 'sv_villain_observables')
+            return out
+        return None
+
+    def _advance(self, phi, n, sweeps):
+        """Run `sweeps` sweeps on host arrays phi (1,N,N) f64 and n (2,N,N) i64, in place."""
+        ctx, N, h = self._state()
+        L = _native.lib()
+        ctx.check(L.sv_villain_upload(h, _native.ptr(phi), _native.ptr(n)), 'sv_villain_upload')
+        inline = self._run_on(ctx, h, sweeps)
+        ctx.check(L.sv_villain_download(h, _native.ptr(phi), _native.ptr(n)), 'sv_villain_download')
         return inline
+
+    def _inline_dict(self, inline):
+        L = self.Lattice
+        V, kappa = L.sites, self.kappa
+        S = inline[0]
+        return {
+            'ActionDensity': S / V,                                   # observable/action.py:25-31
+            'InternalEnergyDensity': S / (V * kappa),                 # observable/energy.py:25-30
+            'WindingSquared': inline[1] / L.cells_of_degree[2],       # observable/winding.py:30-37
+            'TorusWrapping': np.array([int(round(inline[2])), int(round(inline[3]))], dtype=np.int64),
+        }
 
     def _result(self, cfg, phi, n, inline):
         L = self.Lattice
         out = cfg | {'phi': wrap_like(cfg['phi'], phi, 0, L), 'n': wrap_like(cfg['n'], n, 1, L)}
         if inline is not None:
-            V, kappa = L.sites, self.kappa
-            S = inline[0]
-            out |= {
-                'ActionDensity': S / V,                                   # observable/action.py:25-31
-                'InternalEnergyDensity': S / (V * kappa),                 # observable/energy.py:25-30
-                'WindingSquared': inline[1] / L.cells_of_degree[2],       # observable/winding.py:30-37
-                'TorusWrapping': np.array([int(round(inline[2])), int(round(inline[3]))], dtype=np.int64),
-            }
+            out |= self._inline_dict(inline)
         return out
 
     def _fields(self, cfg):
@@ -208,14 +220,14 @@ class _VillainLocal(DeviceState, Generator):
     def _proposals(self):
         return self.Lattice.sites
 
-    def _advance(self, phi, n, sweeps):
-        ctx, N, h = self._state()
+    DEVICE_KIND = 'villain'
+
+    def _run_on(self, ctx, h, sweeps):
+        """`sweeps` steps on the device-resident state h (sv_villain), counters folded like the reference."""
         L = _native.lib()
         st = _native.stats_array(sweeps)
         r = rng_from_numpy(self.rng)
-        ctx.check(L.sv_villain_upload(h, _native.ptr(phi), _native.ptr(n)), 'sv_villain_upload')
         ctx.check(self._run(L, h, sweeps, r, st), f'{self.NAME} run')
-        ctx.check(L.sv_villain_download(h, _native.ptr(phi), _native.ptr(n)), 'sv_villain_download')
         rng_to_numpy(r, self.rng)
         P = self._proposals()
         for k in range(sweeps):
@@ -223,6 +235,14 @@ class _VillainLocal(DeviceState, Generator):
             self.proposed += P
             self.acceptance += st[k].acceptance_sum / P
             self.accepted += int(st[k].accepted)
+        return None
+
+    def _advance(self, phi, n, sweeps):
+        ctx, N, h = self._state()
+        L = _native.lib()
+        ctx.check(L.sv_villain_upload(h, _native.ptr(phi), _native.ptr(n)), 'sv_villain_upload')
+        self._run_on(ctx, h, sweeps)
+        ctx.check(L.sv_villain_download(h, _native.ptr(phi), _native.ptr(n)), 'sv_villain_download')
 
     def _fields(self, cfg):
         N = self.Lattice.N

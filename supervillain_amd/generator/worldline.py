@@ -72,16 +72,14 @@ class CoexactUpdate(_WorldlineDevice, Generator):
     def __str__(self):
         return 'SiteUpdate'  # sic: the reference's CoexactUpdate.__str__ (coexact.py:50-51)
 
-    def _advance(self, cfg, sweeps):
-        ctx, _, h = self._state()
-        m, v = self._fields(cfg)
+    DEVICE_KIND = 'worldline'
+
+    def _run_on(self, ctx, h, sweeps):
         L = _native.lib()
         st = _native.stats_array(sweeps)
         r = rng_from_numpy(self.rng)
-        ctx.check(L.sv_worldline_upload(h, _native.ptr(m), _native.ptr(v)), 'sv_worldline_upload')
         ctx.check(L.sv_worldline_coexact_run(h, float(self.kappa), float(self.Action._W), int(self.interval_t),
                                              sweeps, ctypes.byref(r), st), 'sv_worldline_coexact_run')
-        ctx.check(L.sv_worldline_download(h, _native.ptr(m), None), 'sv_worldline_download')
         rng_to_numpy(r, self.rng)
         P = self.Lattice.cells_of_degree[2]
         for k in range(sweeps):  # coexact.py:122-124
@@ -89,6 +87,15 @@ class CoexactUpdate(_WorldlineDevice, Generator):
             self.proposed += P
             self.acceptance += st[k].acceptance_sum / P
             self.accepted += int(st[k].accepted)
+        return None
+
+    def _advance(self, cfg, sweeps):
+        ctx, _, h = self._state()
+        m, v = self._fields(cfg)
+        L = _native.lib()
+        ctx.check(L.sv_worldline_upload(h, _native.ptr(m), _native.ptr(v)), 'sv_worldline_upload')
+        self._run_on(ctx, h, sweeps)
+        ctx.check(L.sv_worldline_download(h, _native.ptr(m), None), 'sv_worldline_download')
         return cfg | {'m': wrap_like(cfg['m'], m, 1, self.Lattice)}
 
     def step(self, cfg):
@@ -133,13 +140,12 @@ class PlaquetteUpdate(_WorldlineDevice, Generator):
     def __str__(self):
         return 'PlaquetteUpdate'
 
-    def _advance(self, cfg, sweeps):
-        ctx, _, h = self._state()
-        m, v = self._fields(cfg)
+    DEVICE_KIND = 'worldline'
+
+    def _run_on(self, ctx, h, sweeps):
         Lib = _native.lib()
         L = self.Action.Lattice
         r = rng_from_numpy(self.rng)
-        ctx.check(Lib.sv_worldline_upload(h, _native.ptr(m), _native.ptr(v)), 'sv_worldline_upload')
         kappa, W = float(self.Action.kappa), float(self.Action._W)
         if self.mode == 'reference':
             st = _native.stats_array(1)
@@ -155,13 +161,22 @@ class PlaquetteUpdate(_WorldlineDevice, Generator):
             ctx.check(Lib.sv_worldline_plaquette_checkerboard_run(h, kappa, W, sweeps, ctypes.byref(r), st),
                       'sv_worldline_plaquette_checkerboard_run')
             stats = [(int(st[k].accepted), st[k].acceptance_sum) for k in range(sweeps)]
-        ctx.check(Lib.sv_worldline_download(h, _native.ptr(m), _native.ptr(v)), 'sv_worldline_download')
         rng_to_numpy(r, self.rng)
         P = L.sites * len(L.components[2])
         for acc, psum in stats:  # plaquette.py:73, 101-103
             self.acceptance += psum
             self.accepted += acc
             self.proposed += P
+        return None
+
+    def _advance(self, cfg, sweeps):
+        ctx, _, h = self._state()
+        m, v = self._fields(cfg)
+        Lib = _native.lib()
+        L = self.Action.Lattice
+        ctx.check(Lib.sv_worldline_upload(h, _native.ptr(m), _native.ptr(v)), 'sv_worldline_upload')
+        self._run_on(ctx, h, sweeps)
+        ctx.check(Lib.sv_worldline_download(h, _native.ptr(m), _native.ptr(v)), 'sv_worldline_download')
         return cfg | {'m': wrap_like(cfg['m'], m, 1, L), 'v': wrap_like(cfg['v'], v, 2, L)}
 
     def step(self, cfg):
@@ -203,15 +218,13 @@ class _WorldlineLocal(_WorldlineDevice, Generator):
     def __str__(self):
         return self.NAME
 
-    def _advance(self, cfg, sweeps):
-        ctx, _, h = self._state()
-        m, v = self._fields(cfg)
+    DEVICE_KIND = 'worldline'
+
+    def _run_on(self, ctx, h, sweeps):
         L = _native.lib()
         st = _native.stats_array(sweeps)
         r = rng_from_numpy(self.rng)
-        ctx.check(L.sv_worldline_upload(h, _native.ptr(m), _native.ptr(v)), 'sv_worldline_upload')
         ctx.check(self._run(L, h, sweeps, r, st), f'{self.NAME} run')
-        ctx.check(L.sv_worldline_download(h, _native.ptr(m), _native.ptr(v)), 'sv_worldline_download')
         rng_to_numpy(r, self.rng)
         P = self._proposals()
         for k in range(sweeps):
@@ -219,6 +232,15 @@ class _WorldlineLocal(_WorldlineDevice, Generator):
             self.proposed += P
             self.acceptance += st[k].acceptance_sum / P
             self.accepted += int(st[k].accepted)
+        return None
+
+    def _advance(self, cfg, sweeps):
+        ctx, _, h = self._state()
+        m, v = self._fields(cfg)
+        L = _native.lib()
+        ctx.check(L.sv_worldline_upload(h, _native.ptr(m), _native.ptr(v)), 'sv_worldline_upload')
+        self._run_on(ctx, h, sweeps)
+        ctx.check(L.sv_worldline_download(h, _native.ptr(m), _native.ptr(v)), 'sv_worldline_download')
         Lat = self.Action.Lattice
         if self.FIELD == 'm':
             return cfg | {'m': wrap_like(cfg['m'], m, 1, Lat)}
