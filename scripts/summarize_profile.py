@@ -46,7 +46,8 @@ summary = {
         'fetch_bytes_raw': fetch, 'fetch_bytes_x2': 2 * fetch, 'write_bytes': write,
         'hbm_bytes_per_launch': 2 * fetch + write,
         'hbm_bytes_per_launch_raw': fetch + write,
-        'algorithmic_bytes_per_launch': 48 * L * L,
+        'algorithmic_bytes_per_launch': 88 * L * L,          # SURVEY.md 8(d), what bench.py's roofline uses
+        'fused_min_bytes_per_launch': 48 * L * L,            # one read + one write of (phi, n) per sweep
         'counters_per_dispatch': pmc,
     }
 }
