@@ -41,6 +41,8 @@ def lib():
         L.sv_o_villain_cohomology.argtypes = [i32, f64, i64, vp, vp, i32, P(SvRng), vp]
         L.sv_o_worldline_vortex.argtypes = [i32, f64, f64, i64, vp, vp, i32, i32, P(SvRng), vp]
         L.sv_o_worldline_wrapping.argtypes = [i32, f64, f64, i64, vp, vp, i32, i32, P(SvRng), vp]
+        L.sv_o_villain_worm.argtypes = [i32, f64, i64, vp, vp, i32, P(SvRng), vp, vp]
+        L.sv_o_worldline_worm.argtypes = [i32, f64, f64, vp, vp, i32, i32, P(SvRng), vp, vp]
         _LIB = L
     return _LIB
 
@@ -195,3 +197,32 @@ def worldline_generator(kind, N, kappa, W_eff, m, v, sweeps, gen, interval=None)
         raise ValueError('oracle rejected the arguments')
     rng_to_numpy(r, gen)
     return [st[i] for i in range(sweeps)]
+
+
+def villain_worm(N, kappa, W, phi, n, worms, gen):
+    """`worms` Villain ClassicWorm steps in place on n (2,N,N) i64 given phi (N,N) f64.
+    Returns (Vortex_Vortex of the last worm (N,N) i64, Worm_Length per worm (worms,) i64)."""
+    assert n.dtype == np.int64 and n.flags.c_contiguous
+    phi = np.ascontiguousarray(phi, dtype=np.float64)
+    r = rng_from_numpy(gen)
+    hist = np.zeros((N, N), dtype=np.int64)
+    lengths = np.zeros(max(worms, 1), dtype=np.int64)
+    W = 0 if W == float('inf') else int(W)  # only W == 1 changes the algorithm
+    if lib().sv_o_villain_worm(N, kappa, W, _ptr(phi), _ptr(n), worms, ctypes.byref(r), _ptr(hist), _ptr(lengths)):
+        raise ValueError('oracle rejected the arguments')
+    rng_to_numpy(r, gen)
+    return hist, lengths[:worms]
+
+
+def worldline_worm(N, kappa, W_eff, m, v, worms, gen):
+    """`worms` Worldline ClassicWorm steps in place on m (2,N,N) i64 given v (N,N) (i64, or f64 at W = inf).
+    Returns (Spin_Spin of the last worm (N,N) i64, Worm_Length per worm (worms,) i64)."""
+    assert m.dtype == np.int64 and m.flags.c_contiguous and v.flags.c_contiguous
+    r = rng_from_numpy(gen)
+    hist = np.zeros((N, N), dtype=np.int64)
+    lengths = np.zeros(max(worms, 1), dtype=np.int64)
+    if lib().sv_o_worldline_worm(N, kappa, float(W_eff), _ptr(m), _ptr(v), int(v.dtype == np.float64), worms,
+                                 ctypes.byref(r), _ptr(hist), _ptr(lengths)):
+        raise ValueError('oracle rejected the arguments')
+    rng_to_numpy(r, gen)
+    return hist, lengths[:worms]

@@ -940,3 +940,122 @@ int sv_o_worldline_wrapping(int32_t N, double kappa, double Weff, int64_t interv
     free(dvw), free(row), free(prob), free(cm);
     return 0;
 }
+
+/* ---------------------------------------------------------------- worms */
+/* Villain ClassicWorm.step, supervillain/generator/villain/worm.py:96-131 (per-worm draws) and
+ * worm_kernel :133-183, D=2, `worms` consecutive steps on one (phi, n).  Coordinates are kept mod N:
+ * the reference's FFT-convention values (lattice/two_dimensional.py:221-249) only ever index arrays,
+ * where NumPy's negative indexing makes them equal to their value mod N.
+ *   orientation = choice([-1,+1])                 :114  -> integers(0, 2)
+ *   tail = choice(L.coordinates)                  :119  -> row integers(0, V) of the 'ij' meshgrid
+ *   head = tail if W != 1 else choice(coordinates) :123
+ *   loop: exit test (head==tail or W==1) and uniform >= 0.8      :143
+ *         choice = integers(0, 4)                                 :148
+ *         next plaquette / crossed link (two_dimensional.py:255-300): east (t,x-1) via link (0,t,x),
+ *         north (t+1,x) via (1,t+1,x), west (t,x+1) via (0,t,x+1), south (t-1,x) via (1,t,x)
+ *         dS = ((kappa/2)(-2 pi dn))(2 (dphi - 2 pi n) - 2 pi dn), accept on uniform < min(1, e^-dS)
+ *         histogram of head - tail after every move                :181-182
+ * hist (N*N, may be NULL): the LAST worm's Vortex_Vortex; lengths[w] = that worm's Worm_Length. */
+int sv_o_villain_worm(int32_t N_, double kappa, int64_t W, const double *phi, int64_t *n, int32_t worms, sv_rng *rng,
+                      int64_t *hist, int64_t *lengths) {
+    const int64_t N = N_, V = N * N;
+    if (N < 2 || worms < 0) return -1;
+    double *dphi = (double *)malloc(sizeof(double) * 2 * V);
+    int64_t *h = (int64_t *)malloc(sizeof(int64_t) * V);
+    for (int mu = 0; mu < 2; mu++) /* d(phi), worm.py:104 */
+        for (int64_t s = 0; s < V; s++) dphi[mu * V + s] = 0.0 + (phi[fwd(s, mu, N)] - phi[s]);
+    static const int64_t plaq[4] = {+1, +1, -1, -1}; /* east, north, west, south, worm.py:68 */
+    pcg g = pcg_load(rng);
+    for (int32_t w = 0; w < worms; w++) {
+        const int64_t orientation = pcg_bounded(&g, 2, NULL) ? +1 : -1;
+        const int64_t ti = pcg_bounded(&g, (uint32_t)V, NULL);
+        const int64_t tt = ti / N, tx = ti % N;
+        int64_t ht = tt, hx = tx;
+        if (W == 1) {
+            const int64_t hi = pcg_bounded(&g, (uint32_t)V, NULL);
+            ht = hi / N, hx = hi % N;
+        }
+        memset(h, 0, sizeof(int64_t) * V);
+        int64_t len = 0;
+        for (;;) {
+            if ((ht == tt && hx == tx) || W == 1)
+                if (pcg_uniform(&g, 0.0, 1.0) >= 0.8) break;
+            const uint32_t c = pcg_bounded(&g, 4, NULL);
+            int64_t nt = ht, nx = hx, lmu, lt = ht, lx = hx;
+            switch (c) {
+                case 0: nx = wrap(hx - 1, N); lmu = 0; break;                 /* east */
+                case 1: nt = wrap(ht + 1, N); lmu = 1; lt = nt; break;        /* north */
+                case 2: nx = wrap(hx + 1, N); lmu = 0; lx = nx; break;        /* west */
+                default: nt = wrap(ht - 1, N); lmu = 1; break;                /* south */
+            }
+            const int64_t l = lmu * V + lt * N + lx;
+            const double change_link = dphi[l] - TWO_PI * (double)n[l];
+            const int64_t dn = orientation * plaq[c];
+            const double dS = ((kappa / 2) * ((-TWO_PI) * (double)dn)) * (2 * change_link - TWO_PI * (double)dn);
+            double A = exp(-dS);
+            A = A < 1.0 ? A : 1.0;
+            if (pcg_uniform(&g, 0.0, 1.0) < A) {
+                ht = nt, hx = nx;
+                n[l] += dn;
+            }
+            h[wrap(ht - tt, N) * N + wrap(hx - tx, N)] += 1;
+            len++;
+        }
+        if (lengths) lengths[w] = len;
+    }
+    if (hist) memcpy(hist, h, sizeof(int64_t) * V);
+    pcg_store(&g, rng);
+    free(dphi), free(h);
+    return 0;
+}
+
+/* Worldline ClassicWorm.step, supervillain/generator/worldline/worm.py:146-193 (draws) and worm_kernel
+ * :26-94, D=2.  change_m = orientation * (+1,+1,-1,-1); moves +e0,+e1,-e0,-e1 (choice % 2 = axis,
+ * choice < 2 = forward); forward crosses the link at head, backward the link at next_head;
+ * dS = ((1/(2 kappa)) dm)(2 (m - delta(v)/W) + dm); exit when head == tail and uniform < 1/5.
+ * hist: the last worm's Spin_Spin histogram; lengths[w] = Worm_Length. */
+int sv_o_worldline_worm(int32_t N_, double kappa, double Weff, int64_t *m, const void *v, int32_t v_is_float,
+                        int32_t worms, sv_rng *rng, int64_t *hist, int64_t *lengths) {
+    const int64_t N = N_, V = N * N;
+    if (N < 2 || worms < 0) return -1;
+    double *dvw = (double *)malloc(sizeof(double) * 2 * V);
+    int64_t *h = (int64_t *)malloc(sizeof(int64_t) * V);
+    delta_v_by_W(N, v, v_is_float, Weff, dvw); /* worm.py:164 */
+    static const int64_t div[4] = {+1, +1, -1, -1};
+    pcg g = pcg_load(rng);
+    for (int32_t w = 0; w < worms; w++) {
+        const int64_t orientation = pcg_bounded(&g, 2, NULL) ? +1 : -1;
+        const int64_t ti = pcg_bounded(&g, (uint32_t)V, NULL);
+        const int64_t tail[2] = {ti / N, ti % N};
+        int64_t head[2] = {tail[0], tail[1]};
+        memset(h, 0, sizeof(int64_t) * V);
+        int64_t len = 0;
+        for (;;) {
+            if (head[0] == tail[0] && head[1] == tail[1])
+                if (pcg_uniform(&g, 0.0, 1.0) < 1.0 / 5) break;
+            const uint32_t c = pcg_bounded(&g, 4, NULL);
+            const int k = (int)(c % 2);
+            const int forward = c < 2;
+            int64_t next[2] = {head[0], head[1]};
+            next[k] = wrap(head[k] + (forward ? 1 : -1), N);
+            const int64_t *at = forward ? head : next;
+            const int64_t l = k * V + at[0] * N + at[1];
+            const double change_link = (double)m[l] - dvw[l];
+            const int64_t dm = orientation * div[c];
+            const double dS = ((1.0 / (2.0 * kappa)) * (double)dm) * (2.0 * change_link + (double)dm);
+            double A = exp(-dS);
+            A = 1.0 < A ? 1.0 : A;
+            if (pcg_uniform(&g, 0.0, 1.0) < A) {
+                head[0] = next[0], head[1] = next[1];
+                m[l] += dm;
+            }
+            h[wrap(head[0] - tail[0], N) * N + wrap(head[1] - tail[1], N)] += 1;
+            len++;
+        }
+        if (lengths) lengths[w] = len;
+    }
+    if (hist) memcpy(hist, h, sizeof(int64_t) * V);
+    pcg_store(&g, rng);
+    free(dvw), free(h);
+    return 0;
+}

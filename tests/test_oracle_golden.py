@@ -140,3 +140,21 @@ def test_worldline_generators_golden(oracle_lib):
         kinds.add(kind)
     assert kinds == set(WORLDLINE_DENOMINATOR)
     assert sum(1 for c in cases('worldline_generators.npz') if c['kw_interval'] == 3) >= 4  # rejection cases
+
+
+def test_worms_golden(oracle_lib):
+    """both ClassicWorms, step by step (every step's histogram and length)."""
+    O = oracle_lib
+    for c in cases('worms.npz'):
+        N, g = c['N'], generator_from(c['rng0'])
+        for k in range(c['steps']):
+            if c['action'] == 'villain':
+                n = c['n0'].copy() if k == 0 else n
+                hist, lengths = O.villain_worm(N, c['kappa'], c['W'], c['phi0'], n, 1, g)
+            else:
+                m = c['m0'].copy() if k == 0 else m
+                hist, lengths = O.worldline_worm(N, c['kappa'], c['W_eff'], m, np.ascontiguousarray(c['v0']), 1, g)
+            assert (hist == c['hist'][k]).all(), (c['action'], N, k)
+            assert lengths[0] == c['lengths'][k] == hist.sum()
+        assert ((n if c['action'] == 'villain' else m) == (c['n'] if c['action'] == 'villain' else c['m'])).all()
+        assert (state_of(g) == c['rng1']).all()
