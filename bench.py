@@ -23,6 +23,9 @@ Secondary workloads (not the headline line; BASELINE.json configs 5 and 3):
                         CohomologyUpdate per step, or one Villain Hammer step (Site, Link, Exact, Cohomology,
                         each with its own stream, as the reference's Hammer minus its worm); device-resident
                         fields; N > 1 runs independent chains
+  --workload worms      SURVEY.md 8(f) row 4: 1024 independent L=128 Villain chains (W=2, config-5 shape),
+                        thermalized by 100 NeighborhoodUpdate sweeps, then one ClassicWorm per chain per
+                        step (one GPU lane per chain); reported as worm moves/s over all chains
   --workload vortex|wrapping|wlhammer
                         the same for the Worldline rows: VortexUpdate, WrappingUpdate, or one Worldline
                         Hammer step (Vortex, Coexact, Wrapping) at L=4096, W=1
@@ -71,12 +74,12 @@ def parse():
     ap.add_argument('--tiles', default=None, help='tile grid TYxTX (default from N); with N=1 emulates the '
                                                    'decomposition on one GPU')
     ap.add_argument('--workload', default='villain', choices=['villain', 'replicas', 'worldline', 'site', 'link', 'exact', 'cohomology', 'hammer', 'vortex',
-                             'wrapping', 'wlhammer'])
+                             'wrapping', 'wlhammer', 'worms'])
     ap.add_argument('--event-timing', default='batch', choices=['launch', 'batch'],
                     help='hipEvents around each batch of 64 fused launches (default) or around every launch')
     ap.add_argument('--replicas', type=int, default=1024, help='replicas workload: total replica count')
     args = ap.parse_args()
-    if args.workload == 'replicas':
+    if args.workload in ('replicas', 'worms'):
         args.L = 128 if args.L == 4096 else args.L
         args.W = 2 if args.W == 1 else args.W
     if args.workload == 'worldline':
@@ -210,6 +213,69 @@ def run_replicas(args, world, rank, dist):
         report(args, world, Rt * L * L, per * L * L, elapsed, acc, launches_s, config, L,
                metric=f'replica-site updates/sec, {Rt} x L={L} Villain replicas, W={args.W}, inline observables',
                unit='replica-site updates/s', kernel='villain_sweep_fused_obs', baseline=baseline)
+    B.close()
+
+
+def run_worms(args, world, rank, dist):
+    """batched Villain ClassicWorms (supervillain/generator/villain/worm.py:85-183) on
+    config-5-shaped replicas; a step is one worm of every chain, the unit one worm move."""
+    from supervillain_amd import _native
+    from supervillain_amd.replicas import VillainReplicas
+    L, Rt = args.L, args.replicas
+    per = Rt // world
+    first = rank * per
+    B = VillainReplicas(per, L, args.kappa, args.W)
+    B.cold()
+    gens = [np.random.default_rng(first + r) for r in range(per)]
+    B.run(100, gens)  # thermalize: worms on a cold start are short
+    wgens = [np.random.default_rng(10 ** 6 + first + r) for r in range(per)]
+    Lib = _native.lib()
+    if args.warmup:
+        B.worm(wgens, worms=args.warmup)
+    Lib.sv_ctx_set_timing(B.ctx.handle, 1)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    _, lengths = B.worm(wgens, worms=args.steps)
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = max_over_ranks(dist, t1 - t0)
+    launch_s = kernel_time(Lib, B.ctx)
+    moves = float(lengths.sum())
+    if dist:
+        import torch
+        t = torch.tensor([moves], dtype=torch.float64)
+        dist.all_reduce(t)
+        moves = float(t.item())
+    phi, n = B.download() if rank == 0 else (None, None)
+
+    def baseline():
+        from oracle import oracle as O
+        t, done, k = time.perf_counter(), 0, 0
+        while time.perf_counter() - t < 10 and k < per:
+            nn = n[k].copy()
+            _, l = O.villain_worm(L, args.kappa, args.W, phi[k], nn, 20, np.random.default_rng(7 + k))
+            done += int(l.sum())
+            k += 1
+        dt = time.perf_counter() - t
+        return {'value': done / dt, 'unit': 'worm moves/s', 'cores': 1, 'kind': 'port',
+                'sample': f'20 worms on each of {k} thermalized L={L} chains (W={args.W}), oracle/sv_oracle.c '
+                          'single-threaded'}
+
+    if rank == 0:
+        mean_len = moves / (args.steps * Rt)
+        config = {'workload': f'{Rt} independent L={L} Villain chains (W={args.W}), one ClassicWorm per chain per '
+                              f'step, one GPU lane per chain ({per} per GPU), Vortex_Vortex histogram of the last '
+                              'worm, thermalized by 100 NeighborhoodUpdate sweeps',
+                  'L': L, 'replicas': Rt, 'replicas_per_gpu': per, 'path': 'worms', 'mean_worm_length': mean_len,
+                  'parallelism': f'{world} GPU(s), chains sharded, no collectives'}
+        # bytes per move: n of the crossed link + the two phi of d(phi) on it (8 + 16), the conditional n store
+        # and the histogram increment (8 + 8); a latency-bound walk, the roofline fraction is informational
+        out_moves = moves / max(args.steps, 1) * args.steps
+        report(args, world, out_moves / args.steps, out_moves / world, elapsed, 0.0, launch_s, config, L,
+               metric=f'worm moves/sec, {Rt} x L={L} Villain ClassicWorm chains, W={args.W}', unit='worm moves/s',
+               kernel='villain_worm', alg_bytes=40, min_bytes=40, baseline=baseline)
     B.close()
 
 
@@ -434,7 +500,7 @@ def main():
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         dist.init_process_group('gloo', rank=rank, world_size=world)
     if args.workload != 'villain':
-        fn = {'replicas': run_replicas, 'worldline': run_worldline}.get(args.workload, run_local)
+        fn = {'replicas': run_replicas, 'worldline': run_worldline, 'worms': run_worms}.get(args.workload, run_local)
         fn(args, world, rank, dist)
         if dist:
             dist.destroy_process_group()

@@ -194,6 +194,28 @@ int sv_replicas_download(sv_replicas *b, double *phi, int64_t *n);
 int sv_replicas_run(sv_replicas *b, double kappa, int64_t W, double interval_phi, int64_t interval_n, int32_t sweeps,
                     sv_rng *rngs, sv_stats *stats, double *obs);
 
+/* ---- ClassicWorm ---------------------------------------------------------
+ * `worms` consecutive worm steps of every chain, one GPU lane per chain (a worm is sequential).
+ *   Villain:   replaces ClassicWorm.step, supervillain/generator/villain/worm.py:85-131 + worm_kernel
+ *              :133-183 (W: the action's W; only W == 1 changes the algorithm, pass 0 for infinity).
+ *   Worldline: replaces ClassicWorm.step, supervillain/generator/worldline/worm.py:137-193 + worm_kernel
+ *              :26-94 (W_eff = Worldline._W).
+ * rng / rngs: one NumPy PCG64 state per chain, in/out.  hist (may be NULL): per chain the N*N int64
+ * displacement histogram of the LAST worm (Vortex_Vortex / Spin_Spin).  lengths (may be NULL): per
+ * chain `worms` int64 Worm_Length values.  max_moves (<= 0: unbounded) caps one worm; exceeding it is
+ * an error that leaves the chain mid-worm.  The fields are the state's device-resident ones. */
+int sv_villain_worm_run(sv_villain *st, double kappa, int64_t W, int32_t worms, int64_t max_moves, sv_rng *rng,
+                        int64_t *hist, int64_t *lengths);
+int sv_replicas_worm_run(sv_replicas *b, double kappa, int64_t W, int32_t worms, int64_t max_moves, sv_rng *rngs,
+                         int64_t *hist, int64_t *lengths);
+int sv_worldline_worm_run(sv_worldline *st, double kappa, double W_eff, int32_t worms, int64_t max_moves, sv_rng *rng,
+                          int64_t *hist, int64_t *lengths);
+/* R independent Worldline chains from host arrays: m (R, 2, N, N) int64 in/out, v (R, N, N) int64 or
+ * float64 (v_is_float), rngs[R]. */
+int sv_worldline_worm_batch(sv_ctx *ctx, int32_t R, int32_t N, double kappa, double W_eff, int64_t *m, const void *v,
+                            int32_t v_is_float, int32_t worms, int64_t max_moves, sv_rng *rngs, int64_t *hist,
+                            int64_t *lengths);
+
 #ifdef __cplusplus
 }
 #endif

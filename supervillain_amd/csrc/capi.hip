@@ -172,6 +172,7 @@ int sv_ctx_destroy(sv_ctx *ctx) {
     (void)hipFree(ctx->d_blocks);
     (void)hipFree(ctx->d_skips);
     (void)hipFree(ctx->d_stats);
+    sv::worm_release(ctx);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return 0;

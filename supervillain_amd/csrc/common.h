@@ -120,7 +120,16 @@ struct sv_villain {
     char *d_aux = nullptr;         // small per-call device block (CohomologyUpdate: rng | stats | plan)
     char *h_aux = nullptr;         // its pinned host image
     size_t aux_cap = 0;
+    double *d_obs = nullptr;       // inline observables: 4 device sums (coarse-grained hipMalloc)
+    double *h_obs = nullptr;       // and their pinned host image
 };
+
+namespace sv {
+// worm.hip: Villain worms over R chains stored (R, N, N) phi / (R, 2, N, N) n on the device
+void villain_worms_device(sv_ctx *ctx, int32_t R, int32_t N, const double *phi, int64_t *n, double kappa, int64_t W,
+                          int32_t worms, int64_t max_moves, sv_rng *rngs, int64_t *hist, int64_t *lengths);
+void worm_release(sv_ctx *ctx);  // frees the context's worm scratch (sv_ctx_destroy)
+}  // namespace sv
 
 struct sv_worldline {
     sv_ctx *ctx = nullptr;

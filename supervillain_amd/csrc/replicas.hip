@@ -422,4 +422,19 @@ int sv_replicas_run(sv_replicas *b, double kappa, int64_t W, double interval_phi
     }
 }
 
+int sv_replicas_worm_run(sv_replicas *b, double kappa, int64_t W, int32_t worms, int64_t max_moves, sv_rng *rngs,
+                         int64_t *hist, int64_t *lengths) {
+    if (!b || !rngs) return -1;
+    sv_ctx *ctx = b->ctx;
+    try {
+        SV_HIP(hipSetDevice(ctx->device));
+        villain_worms_device(ctx, b->R, b->N, b->phi[b->cur], b->n[b->cur], kappa, W, worms, max_moves, rngs, hist,
+                             lengths);
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
 }  // extern "C"

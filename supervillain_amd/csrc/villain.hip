@@ -23,6 +23,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include "villain.h"
 
@@ -882,10 +883,10 @@ __global__ void villain_observables_kernel(int32_t N, double half_kappa, const d
     s_n0 = wave_sum(s_n0);
     s_n1 = wave_sum(s_n1);
     if ((threadIdx.x & 63) == 0) {
-        unsafeAtomicAdd(&out[0], half_kappa * s_act);
-        unsafeAtomicAdd(&out[1], s_w2);
-        unsafeAtomicAdd(&out[2], s_n0);
-        unsafeAtomicAdd(&out[3], s_n1);
+        atomicAdd(&out[0], half_kappa * s_act);
+        atomicAdd(&out[1], s_w2);
+        atomicAdd(&out[2], s_n0);
+        atomicAdd(&out[3], s_n1);
     }
 }
 
@@ -1295,6 +1296,8 @@ int sv_villain_destroy(sv_villain *st) {
     (void)hipFree(st->sites);
     if (st->d_aux) (void)hipFree(st->d_aux);
     if (st->h_aux) (void)hipHostFree(st->h_aux);
+    if (st->d_obs) (void)hipFree(st->d_obs);
+    if (st->h_obs) (void)hipHostFree(st->h_obs);
     delete st;
     return 0;
 }
@@ -1379,16 +1382,22 @@ int sv_villain_observables(sv_villain *st, double kappa, double *out) {
     try {
         sv_ctx *ctx = st->ctx;
         SV_HIP(hipSetDevice(ctx->device));
-        double *d = nullptr;
-        SV_HIP(hipMallocAsync((void **)&d, 4 * sizeof(double), ctx->stream));
+        // persistent device sums + pinned host image: a stream-ordered DMA, then a host copy after the sync
+        // (a pooled hipMallocAsync buffer read back into pageable memory once returned zeros)
+        if (!st->d_obs) {
+            SV_HIP(hipMalloc((void **)&st->d_obs, 4 * sizeof(double)));
+            SV_HIP(hipHostMalloc((void **)&st->h_obs, 4 * sizeof(double), hipHostMallocDefault));
+        }
+        double *d = st->d_obs;
         SV_HIP(hipMemsetAsync(d, 0, 4 * sizeof(double), ctx->stream));
         const int64_t V = (int64_t)st->N * st->N;
         const int grid = (int)std::min<int64_t>((V + 255) / 256, 2048);
         villain_observables_kernel<<<grid, 256, 0, ctx->stream>>>(st->N, kappa / 2.0, st->phi[st->cur], st->n[st->cur],
                                                                    d);
-        SV_HIP(hipMemcpyAsync(out, d, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-        SV_HIP(hipFreeAsync(d, ctx->stream));
+        SV_HIP(hipGetLastError());
+        SV_HIP(hipMemcpyAsync(st->h_obs, d, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
         SV_HIP(hipStreamSynchronize(ctx->stream));
+        memcpy(out, st->h_obs, 4 * sizeof(double));
         return 0;
     } catch (const std::exception &e) {
         st->ctx->err = e.what();

@@ -356,11 +356,98 @@ class CohomologyUpdate(_VillainLocal):
         return L.sv_villain_cohomology_run(h, float(self.kappa), int(self.interval_h), sweeps, ctypes.byref(r), st)
 
 
+# ------------------------------------------------------------------------------------------------
+# the ClassicWorm.
+
+def _worm_report(lengths):
+    l = np.array(lengths)
+    return f'There were {len(l)} worms.\nWorms lengths:\n    mean {l.mean()}\n    std  {l.std()}\n    max  {max(l)}'
+
+
+class ClassicWorm(DeviceState, Generator):
+    r'''The Prokof'ev-Svistunov worm on the Villain links (supervillain/generator/villain/worm.py:17-131):
+    head and tail on plaquettes, the head crosses links changing n by ±1, and the displacement histogram of
+    every move is the inline ``Vortex_Vortex`` measurement.  A worm is a sequential walk, so the device runs
+    one chain per GPU lane (``sv_villain_worm_run``); batches of chains use
+    :meth:`supervillain_amd.replicas.VillainReplicas.worm`.  ``max_moves`` (0: unbounded) caps one worm.'''
+
+    DEVICE_KIND = 'villain'
+
+    def __init__(self, S, *, device=None, max_moves=0):
+        if not _is_villain(S):
+            raise ValueError('Need a Villain action')
+        if S.Lattice.D != 2:
+            raise NotImplementedError('ClassicWorm is only implemented for D=2')
+        self.Action = S
+        self.rng = np.random.default_rng()
+        self.worm_lengths = __import__('collections').deque()
+        self.plaquette = np.array([+1, +1, -1, -1])  # east, north, west, south (worm.py:68)
+        self.device = device
+        self.max_moves = int(max_moves)
+
+    def __str__(self):
+        return 'ClassicWorm'
+
+    _state = _VillainLocal._state
+    __del__ = _VillainLocal.__del__
+    _fields = _VillainLocal._fields
+
+    @property
+    def Lattice(self):
+        return self.Action.Lattice
+
+    def inline_observables(self, steps):
+        L = self.Action.Lattice
+        return {
+            'Vortex_Vortex': Batch(steps, shape=(L.N, L.N)),
+            'Worm_Length': Batch(steps, shape=(), dtype=float),
+        }
+
+    def _run_on(self, ctx, h, count):
+        """`count` worms on the device-resident (phi, n); returns (last histogram, last length)."""
+        N = self.Action.Lattice.N
+        hist = np.zeros((N, N), dtype=np.int64)
+        lengths = np.zeros(count, dtype=np.int64)
+        W = self.Action.W
+        r = rng_from_numpy(self.rng)
+        ctx.check(_native.lib().sv_villain_worm_run(h, float(self.Action.kappa), 1 if W == 1 else 0, int(count),
+                                                    self.max_moves, ctypes.byref(r), _native.ptr(hist),
+                                                    _native.ptr(lengths)), 'sv_villain_worm_run')
+        rng_to_numpy(r, self.rng)
+        self.worm_lengths.extend(np.int64(x) for x in lengths)
+        return hist, lengths[-1]
+
+    def _inline_dict(self, out):
+        return {'Vortex_Vortex': out[0], 'Worm_Length': out[1]}
+
+    def _steps(self, cfg, count):
+        phi, n = self._fields(cfg)
+        ctx, N, h = self._state()
+        L = _native.lib()
+        ctx.check(L.sv_villain_upload(h, _native.ptr(phi), _native.ptr(n)), 'sv_villain_upload')
+        hist, wl = self._run_on(ctx, h, count)
+        ctx.check(L.sv_villain_download(h, _native.ptr(phi), _native.ptr(n)), 'sv_villain_download')
+        return cfg | {'n': wrap_like(cfg['n'], n, 1, self.Action.Lattice), 'Vortex_Vortex': hist, 'Worm_Length': wl}
+
+    def step(self, cfg):
+        return self._steps(cfg, 1)
+
+    def report(self):
+        return _worm_report(self.worm_lengths)
+
+
+Worm = ClassicWorm
+
+
 def Hammer(S, worms=1):
-    r'''The reference's Villain Hammer (supervillain/generator/villain/__init__.py:11-67) without its worm
-    (ClassicWorm is outside this build's hot path): Sequentially(Site, Link, Exact, Cohomology),
-    LinkUpdate omitted at W = infinity.'''
-    from supervillain_amd.generator.combining import Sequentially
+    r'''The reference's Villain Hammer (supervillain/generator/villain/__init__.py:11-67):
+    Sequentially(Site, Link, Exact, Cohomology, Worm), LinkUpdate omitted at W = infinity, the worm wrapped in
+    KeepEvery(worms, ...) when worms > 1.  worms=0 leaves the worm out (the round-1 Hammer).'''
+    from supervillain_amd.generator.combining import KeepEvery, Sequentially
+    worm = ()
+    if worms:
+        W = ClassicWorm(S)
+        worm = (KeepEvery(worms, W) if worms > 1 else W,)
     if S.W < float('inf'):
-        return Sequentially((SiteUpdate(S), LinkUpdate(S), ExactUpdate(S), CohomologyUpdate(S)))
-    return Sequentially((SiteUpdate(S), ExactUpdate(S), CohomologyUpdate(S)))
+        return Sequentially((SiteUpdate(S), LinkUpdate(S), ExactUpdate(S), CohomologyUpdate(S)) + worm)
+    return Sequentially((SiteUpdate(S), ExactUpdate(S), CohomologyUpdate(S)) + worm)

@@ -308,8 +308,78 @@ class WrappingUpdate(_WorldlineLocal):
                                            sweeps, ctypes.byref(r), st)
 
 
+class ClassicWorm(_WorldlineDevice, Generator):
+    r'''The Prokof'ev-Svistunov worm on the worldline links (supervillain/generator/worldline/worm.py:97-193):
+    head and tail on sites, the head crosses links changing m by ±1; the displacement histogram is the inline
+    ``Spin_Spin`` measurement.  One chain per GPU lane (``sv_worldline_worm_run``); batches of chains use
+    :func:`supervillain_amd.replicas.worldline_worms`.  ``max_moves`` (0: unbounded) caps one worm.'''
+
+    DEVICE_KIND = 'worldline'
+
+    def __init__(self, S, *, device=None, max_moves=0):
+        if not _is_worldline(S):
+            raise ValueError('The classic worm algorithm update requires the Worldline action.')
+        self.Action = S
+        self.rng = np.random.default_rng()
+        self.worm_lengths = __import__('collections').deque()
+        D = S.Lattice.D
+        self.divergence = np.array([+1] * D + [-1] * D, dtype=int)  # worm.py:135
+        self.device = device
+        self.max_moves = int(max_moves)
+
+    def __str__(self):
+        return 'ClassicWorm'
+
+    def inline_observables(self, steps):
+        from supervillain_amd.batch import Batch
+        L = self.Action.Lattice
+        return {
+            'Spin_Spin': Batch(steps, shape=L.dims),
+            'Worm_Length': Batch(steps, shape=(), dtype=float),
+        }
+
+    def _run_on(self, ctx, h, count):
+        N = self.Action.Lattice.N
+        hist = np.zeros((N, N), dtype=np.int64)
+        lengths = np.zeros(count, dtype=np.int64)
+        r = rng_from_numpy(self.rng)
+        ctx.check(_native.lib().sv_worldline_worm_run(h, float(self.Action.kappa), float(self.Action._W), int(count),
+                                                      self.max_moves, ctypes.byref(r), _native.ptr(hist),
+                                                      _native.ptr(lengths)), 'sv_worldline_worm_run')
+        rng_to_numpy(r, self.rng)
+        self.worm_lengths.extend(int(x) for x in lengths)
+        return hist, int(lengths[-1])
+
+    def _inline_dict(self, out):
+        return {'Spin_Spin': out[0], 'Worm_Length': out[1]}
+
+    def _steps(self, cfg, count):
+        ctx, _, h = self._state()
+        m, v = self._fields(cfg)
+        L = _native.lib()
+        ctx.check(L.sv_worldline_upload(h, _native.ptr(m), _native.ptr(v)), 'sv_worldline_upload')
+        hist, wl = self._run_on(ctx, h, count)
+        ctx.check(L.sv_worldline_download(h, _native.ptr(m), None), 'sv_worldline_download')
+        return cfg | {'m': wrap_like(cfg['m'], m, 1, self.Action.Lattice), 'Spin_Spin': hist, 'Worm_Length': wl}
+
+    def step(self, cfg):
+        return self._steps(cfg, 1)
+
+    def report(self):
+        l = np.array(self.worm_lengths)
+        return f'There were {len(l)} worms.\nWorms lengths:\n    mean {l.mean()}\n    std  {l.std()}\n    max  {max(l)}'
+
+
+Worm = ClassicWorm
+
+
 def Hammer(S, worms=1):
-    r'''The reference's Worldline Hammer (supervillain/generator/worldline/__init__.py:10-40) without its worm
-    (ClassicWorm is outside this build's hot path): Sequentially(Vortex, Coexact, Wrapping).'''
-    from supervillain_amd.generator.combining import Sequentially
-    return Sequentially((VortexUpdate(S), CoexactUpdate(S), WrappingUpdate(S)))
+    r'''The reference's Worldline Hammer (supervillain/generator/worldline/__init__.py:10-40):
+    Sequentially(Vortex, Coexact, Wrapping, Worm), the worm wrapped in KeepEvery(worms, ...) when worms > 1.
+    worms=0 leaves the worm out (the round-1 Hammer).'''
+    from supervillain_amd.generator.combining import KeepEvery, Sequentially
+    worm = ()
+    if worms:
+        W = ClassicWorm(S)
+        worm = (KeepEvery(worms, W) if worms > 1 else W,)
+    return Sequentially((VortexUpdate(S), CoexactUpdate(S), WrappingUpdate(S)) + worm)

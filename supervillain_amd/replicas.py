@@ -53,6 +53,23 @@ class VillainReplicas:
                        'sv_replicas_download')
         return phi, n
 
+    def worm(self, rngs, worms=1, max_moves=0):
+        """`worms` ClassicWorm steps of every replica (supervillain/generator/villain/worm.py:85-183), one GPU
+        lane per replica; rngs: R NumPy Generators, advanced in place.  Returns (Vortex_Vortex of each
+        replica's last worm (R, N, N) int64, Worm_Length (R, worms) int64)."""
+        if len(rngs) != self.R:
+            raise ValueError(f'need {self.R} generators')
+        r = (SvRng * self.R)(*[rng_from_numpy(g) for g in rngs])
+        hist = np.zeros((self.R, self.N, self.N), dtype=np.int64)
+        lengths = np.zeros((self.R, max(worms, 1)), dtype=np.int64)
+        W = 1 if self.W == 1 else 0
+        self.ctx.check(_native.lib().sv_replicas_worm_run(self.handle, self.kappa, W, int(worms), int(max_moves), r,
+                                                          _native.ptr(hist), _native.ptr(lengths)),
+                       'sv_replicas_worm_run')
+        for g, x in zip(rngs, r):
+            rng_to_numpy(x, g)
+        return hist, lengths[:, :worms]
+
     def run(self, sweeps, rngs, inline=False):
         """`sweeps` sweeps of every replica; rngs: R NumPy Generators, advanced in place.
 
@@ -83,3 +100,27 @@ class VillainReplicas:
             'WindingSquared': obs[..., 1] / V,
             'TorusWrapping': np.rint(obs[..., 2:4]).astype(np.int64),
         }
+
+
+def worldline_worms(m, v, kappa, W, rngs, worms=1, max_moves=0, device=None):
+    """`worms` Worldline ClassicWorm steps (supervillain/generator/worldline/worm.py:137-193) of R independent
+    chains, one GPU lane each: m (R, 2, N, N) int64 is updated in place, v (R, N, N) int64 (float64 at
+    W = infinity) is read.  Returns (Spin_Spin of each chain's last worm (R, N, N), Worm_Length (R, worms))."""
+    R, _, N, _ = m.shape
+    if m.dtype != np.int64 or not m.flags.c_contiguous:
+        raise ValueError('m must be a C-contiguous int64 (R, 2, N, N) array')
+    v_float = not (W < float('inf'))
+    v = np.ascontiguousarray(v, dtype=np.float64 if v_float else np.int64).reshape(R, N, N)
+    if len(rngs) != R:
+        raise ValueError(f'need {R} generators')
+    W_eff = 2 * np.pi if v_float else float(W)
+    ctx = _native.context(_native.default_device() if device is None else device)
+    r = (SvRng * R)(*[rng_from_numpy(g) for g in rngs])
+    hist = np.zeros((R, N, N), dtype=np.int64)
+    lengths = np.zeros((R, max(worms, 1)), dtype=np.int64)
+    ctx.check(_native.lib().sv_worldline_worm_batch(ctx.handle, R, N, float(kappa), W_eff, _native.ptr(m), _native.ptr(v),
+                                                    int(v_float), int(worms), int(max_moves), r, _native.ptr(hist),
+                                                    _native.ptr(lengths)), 'sv_worldline_worm_batch')
+    for g, x in zip(rngs, r):
+        rng_to_numpy(x, g)
+    return hist, lengths[:, :worms]

@@ -62,7 +62,7 @@ def test_program_flattening():
 @pytest.mark.parametrize('N,W', [(16, 1), (9, 2), (32, 3)])
 def test_villain_hammer_resident(N, W):
     S = sv.Villain(sv.Lattice2D(N), 0.4, W)
-    G0, G1 = both(lambda: villain_hammer(S, [1, 2, 3, 4]), S, 12, ['phi', 'n'])
+    G0, G1 = both(lambda: villain_hammer(S, [1, 2, 3, 4, 5]), S, 12, ['phi', 'n', 'Vortex_Vortex', 'Worm_Length'])
     assert rng_states(G0) == rng_states(G1)
 
 
@@ -82,10 +82,10 @@ def test_worldline_hammer_resident(W):
 
     def make():
         H = gw.Hammer(S)
-        for G, s in zip(H.generators, [7, 8, 9]):
+        for G, s in zip(H.generators, [7, 8, 9, 10]):
             G.rng = np.random.default_rng(s)
         return H
-    G0, G1 = both(make, S, 10, ['m', 'v'])
+    G0, G1 = both(make, S, 10, ['m', 'v', 'Spin_Spin', 'Worm_Length'])
     assert rng_states(G0) == rng_states(G1)
 
 
@@ -102,3 +102,17 @@ def test_plaquette_reference_order_resident():
         E = sv.Ensemble(S).generate(6, Sequentially((G, C)), device_resident=resident)
         res.append((np.asarray(E.m.array if hasattr(E.m, 'array') else E.m).copy(), G.report()))
     assert (res[0][0] == res[1][0]).all() and res[0][1] == res[1][1]
+
+
+def test_villain_hammer_worms_keepevery():
+    """Hammer(S, worms=3): the worm inside KeepEvery (blocked inline observables averaged, combining.py:100-112)
+    keeps the host loop; Hammer(S, worms=0) is the worm-free program."""
+    S = sv.Villain(sv.Lattice2D(8), 0.5, 2)
+    H = gv.Hammer(S, worms=3)
+    assert isinstance(H.generators[-1], KeepEvery) and device_program(H) is None
+    assert device_program(gv.Hammer(S, worms=0)) is not None
+    for G, s in zip(H.generators[:-1], [1, 2, 3, 4]):
+        G.rng = np.random.default_rng(s)
+    H.generators[-1].generator.rng = np.random.default_rng(5)
+    E = sv.Ensemble(S).generate(4, H)
+    assert np.asarray(E.Vortex_Vortex.array if hasattr(E.Vortex_Vortex, 'array') else E.Vortex_Vortex).shape == (4, 8, 8)

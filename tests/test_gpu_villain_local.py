@@ -102,11 +102,11 @@ def test_large_vs_oracle(oracle_lib, kind, N, sweeps, interval):
 
 
 def test_hammer_sequence_vs_oracle(oracle_lib):
-    """The Hammer minus its worm, Sequentially(Site, Link, Exact, Cohomology), over several steps."""
+    """The Hammer, Sequentially(Site, Link, Exact, Cohomology, Worm), over several steps."""
     N, kappa, W = 64, 0.6, 2
     S = sv.Villain(sv.Lattice2D(N), kappa, W)
     H = gv.Hammer(S)
-    seeds = [21, 22, 23, 24]
+    seeds = [21, 22, 23, 24, 25]
     for G, s in zip(H.generators, seeds):
         G.rng = np.random.default_rng(s)
     cfg = cfg_of(S, np.zeros((N, N)), np.zeros((2, N, N), dtype=np.int64))
@@ -117,5 +117,7 @@ def test_hammer_sequence_vs_oracle(oracle_lib):
     for _ in range(3):
         for kind, g in zip(['SiteUpdate', 'LinkUpdate', 'ExactUpdate', 'CohomologyUpdate'], gens):
             oracle_lib.villain_generator(kind, N, kappa, W, phi, n, 1, g)
+        hist, lengths = oracle_lib.villain_worm(N, kappa, W, phi, n, 1, gens[4])
+    assert (np.asarray(cfg['Vortex_Vortex']) == hist).all() and cfg['Worm_Length'] == lengths[-1]
     assert (np.asarray(cfg['phi']).reshape(N, N) == phi).all()
     assert (np.asarray(cfg['n']) == n).all()

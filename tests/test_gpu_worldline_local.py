@@ -81,18 +81,18 @@ def test_large_vs_oracle(oracle_lib, kind, N, W, sweeps, interval):
 
 
 def test_hammer_sequence():
-    """The Worldline Hammer minus its worm: Sequentially(Vortex, Coexact, Wrapping) vs the three generators
+    """The Worldline Hammer: Sequentially(Vortex, Coexact, Wrapping, Worm) vs the four generators
     stepped by hand with the same streams."""
     N, kappa, W = 32, 0.5, 1
     S = sv.Worldline(sv.Lattice2D(N), kappa, W)
     H = gw.Hammer(S)
-    seeds = [31, 32, 33]
+    seeds = [31, 32, 33, 34]
     for G, s in zip(H.generators, seeds):
         G.rng = np.random.default_rng(s)
     cfg = cfg_of(S, np.zeros((2, N, N), dtype=np.int64), np.zeros((N, N), dtype=np.int64))
     for _ in range(3):
         cfg = H.step(cfg)
-    gens = [gw.VortexUpdate(S), gw.CoexactUpdate(S), gw.WrappingUpdate(S)]
+    gens = [gw.VortexUpdate(S), gw.CoexactUpdate(S), gw.WrappingUpdate(S), gw.ClassicWorm(S)]
     for G, s in zip(gens, seeds):
         G.rng = np.random.default_rng(s)
     c2 = cfg_of(S, np.zeros((2, N, N), dtype=np.int64), np.zeros((N, N), dtype=np.int64))
@@ -101,4 +101,6 @@ def test_hammer_sequence():
             c2 = c2 | G.step(c2)
     assert (np.asarray(cfg['m']) == np.asarray(c2['m'])).all()
     assert (np.asarray(cfg['v']) == np.asarray(c2['v'])).all()
+    assert (np.asarray(cfg['Spin_Spin']) == np.asarray(c2['Spin_Spin'])).all()
+    assert gens[3].report() == H.generators[3].report()
     assert H.generators[0].accepted + H.generators[2].accepted > 0

@@ -139,3 +139,10 @@ def test_keepevery_sequentially_matches_golden(oracle_lib):
     E = sv.Ensemble(S).generate(c['steps'], G)
     assert (E.configuration.phi.array == c['phi']).all() and (E.configuration.n.array == c['n']).all()
     assert G.report() == c['report']
+
+
+def test_worm_wrong_action_raises():
+    with pytest.raises(ValueError):
+        __import__('supervillain_amd.generator.villain', fromlist=['Worm']).Worm(sv.Worldline(sv.Lattice2D(4), 0.5, 1))
+    with pytest.raises(ValueError):
+        __import__('supervillain_amd.generator.worldline', fromlist=['Worm']).Worm(sv.Villain(sv.Lattice2D(4), 0.5, 1))
