@@ -23,6 +23,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <cstring>
 
 #include "villain.h"
@@ -136,6 +137,10 @@ struct sv_domain_tile {
     std::vector<int64_t *> n;
     uint64_t *send = nullptr, *recv = nullptr;
     Summary *sum = nullptr;         // device
+    // message layout: the messages bound for (or coming from) one remote peer are contiguous, so one
+    // ncclSend / ncclRecv per distinct peer carries them all (e.g. 4 peers instead of 8 for 2 x 4 tiles)
+    int64_t soff[NDIR] = {0}, roff[NDIR] = {0};
+    std::vector<std::array<int64_t, 3>> sends, recvs;  // {peer, offset, words}
 };
 
 struct sv_domain {
@@ -152,6 +157,14 @@ struct sv_domain {
     bool loopback = false;              // 1 rank, 1 tile, halos through RCCL to itself (tests the RCCL path)
     Summary *gathered = nullptr;        // device, nranks summaries (RCCL mode)
     std::vector<Summary> host_sum;
+    // split sweeps: interior strips on ctx->stream while the halos travel on `halo_stream` (high
+    // priority), then the boundary strips there; events order the two streams
+    bool split = true;
+    hipStream_t halo_stream = nullptr;
+    hipStream_t interior_stream = nullptr;  // CU-masked: a few CUs stay free for the halo path (RCCL's kernel)
+    hipEvent_t ev_interior = nullptr, ev_boundary = nullptr;
+    int32_t *d_strips = nullptr;        // interior strip indices, then boundary strip indices
+    int n_interior = 0, n_boundary = 0;
 };
 
 namespace {
@@ -176,9 +189,10 @@ void geometry(sv_domain *d) {
     d->pitch = ((LEFT_PAD + d->Wt + GHOST_RIGHT + 15) / 16) * 16;
     d->plane = (int64_t)(d->Ht + GHOST_TOP + GHOST_BOTTOM) * d->pitch;
     d->org = (int64_t)GHOST_TOP * d->pitch + LEFT_PAD;
-    // ring depth: an abort travels one tile-hop (8-neighbour torus) per sweep
+    // ring depth: an abort travels one tile-hop (8-neighbour torus) per sweep; with split sweeps the
+    // interior launch of the sweep that receives the abort still runs, so one more buffer
     const int D = std::max(d->ty / 2, d->tx / 2);
-    d->R = std::max(2, D + 1);
+    d->R = std::max(2, D + 2);
     int64_t off = 0;
     for (int s = 0; s < NDIR; s++) {
         d->H.rect[s] = send_rect(s, d->Ht, d->Wt);
@@ -194,8 +208,44 @@ HaloTable recv_table(const sv_domain *d) {
     return h;
 }
 
-void exchange(sv_domain *d) {
+// Per-tile message offsets grouped by remote peer (see sv_domain_tile).  Sender and receiver order a
+// peer's messages by direction s: the sender's {s : nbr[s] == B} equals the receiver's
+// {s : nbr[opp(s)] == A}, so the concatenations line up word for word.
+void halo_layout(sv_domain *d) {
+    auto words = [&](int s) { return 2 + 3 * (int64_t)d->H.rect[s].rows * d->H.rect[s].cols; };
+    for (auto &T : d->tiles) {
+        auto remote = [&](int peer) { return d->loopback || d->local_of[peer] < 0; };
+        for (int side = 0; side < 2; side++) {
+            int64_t *off = side == 0 ? T.soff : T.roff;
+            auto &lst = side == 0 ? T.sends : T.recvs;
+            lst.clear();
+            int64_t o = 0;
+            std::vector<int> peers;
+            for (int s = 0; s < NDIR; s++) {
+                const int peer = side == 0 ? T.nbr[s] : T.nbr[opp(s)];
+                if (remote(peer) && std::find(peers.begin(), peers.end(), peer) == peers.end()) peers.push_back(peer);
+            }
+            for (int peer : peers) {
+                const int64_t o0 = o;
+                for (int s = 0; s < NDIR; s++)
+                    if ((side == 0 ? T.nbr[s] : T.nbr[opp(s)]) == peer) {
+                        off[s] = o;
+                        o += words(s);
+                    }
+                lst.push_back({peer, o0, o - o0});
+            }
+            for (int s = 0; s < NDIR; s++)
+                if (!remote(side == 0 ? T.nbr[s] : T.nbr[opp(s)])) {
+                    off[s] = o;
+                    o += words(s);
+                }
+        }
+    }
+}
+
+void exchange(sv_domain *d, hipStream_t stream) {
     sv_ctx *ctx = d->ctx;
+    (void)ctx;
     const int slot = d->cur;
     const int threads = 256;
     // pack every local tile
@@ -203,26 +253,19 @@ void exchange(sv_domain *d) {
         int64_t mx = 0;
         for (int s = 0; s < NDIR; s++) mx = std::max<int64_t>(mx, (int64_t)d->H.rect[s].rows * d->H.rect[s].cols);
         dim3 grid((unsigned)std::min<int64_t>((mx + threads - 1) / threads, 1024), NDIR);
-        halo_pack<<<grid, threads, 0, ctx->stream>>>(T.phi[slot], T.n[slot], d->pitch, d->plane, d->org, d->H, T.send,
+        HaloTable HS = d->H;
+        for (int s = 0; s < NDIR; s++) HS.off[s] = T.soff[s];
+        halo_pack<<<grid, threads, 0, stream>>>(T.phi[slot], T.n[slot], d->pitch, d->plane, d->org, HS, T.send,
                                                      &T.sum->abort);
     }
     // remote messages (one tile per rank in RCCL mode)
     if (d->comm) {
         sv_domain_tile &T = d->tiles[0];
-        const int me = d->rank;
         check_nccl(ncclGroupStart(), "ncclGroupStart");
-        for (int s = 0; s < NDIR; s++) {
-            const int peer = T.nbr[s];
-            if (peer == me && !d->loopback) continue;
-            const int64_t w = 2 + 3 * (int64_t)d->H.rect[s].rows * d->H.rect[s].cols;
-            check_nccl(ncclSend(T.send + d->H.off[s], (size_t)w, ncclUint64, peer, d->comm, ctx->stream), "ncclSend");
-        }
-        for (int s = 0; s < NDIR; s++) {
-            const int peer = T.nbr[opp(s)];  // the message of direction s comes from the tile at -s
-            if (peer == me && !d->loopback) continue;
-            const int64_t w = 2 + 3 * (int64_t)d->H.rect[s].rows * d->H.rect[s].cols;
-            check_nccl(ncclRecv(T.recv + d->H.off[s], (size_t)w, ncclUint64, peer, d->comm, ctx->stream), "ncclRecv");
-        }
+        for (const auto &m : T.sends)
+            check_nccl(ncclSend(T.send + m[1], (size_t)m[2], ncclUint64, (int)m[0], d->comm, stream), "ncclSend");
+        for (const auto &m : T.recvs)
+            check_nccl(ncclRecv(T.recv + m[1], (size_t)m[2], ncclUint64, (int)m[0], d->comm, stream), "ncclRecv");
         check_nccl(ncclGroupEnd(), "ncclGroupEnd");
     }
     // unpack: ghost block s takes the message of direction s from the neighbour at -s
@@ -233,11 +276,11 @@ void exchange(sv_domain *d) {
         for (int s = 0; s < NDIR; s++) {
             const int peer = T.nbr[opp(s)];
             const int li = d->local_of[peer];
-            src.msg[s] = (li >= 0 && !d->loopback) ? d->tiles[li].send + d->H.off[s] : T.recv + d->H.off[s];
+            src.msg[s] = (li >= 0 && !d->loopback) ? d->tiles[li].send + d->tiles[li].soff[s] : T.recv + T.roff[s];
             mx = std::max<int64_t>(mx, (int64_t)HR.rect[s].rows * HR.rect[s].cols);
         }
         dim3 grid((unsigned)std::min<int64_t>((mx + threads - 1) / threads, 1024), NDIR);
-        halo_unpack<<<grid, threads, 0, ctx->stream>>>(T.phi[slot], T.n[slot], d->pitch, d->plane, d->org, HR, src,
+        halo_unpack<<<grid, threads, 0, stream>>>(T.phi[slot], T.n[slot], d->pitch, d->plane, d->org, HR, src,
                                                        &T.sum->abort);
     }
 }
@@ -297,37 +340,71 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
         upload_plan(ctx, blocks, skipvec);
         for (auto &Tl : d->tiles) SV_HIP(hipMemsetAsync(Tl.sum, 0, sizeof(Summary), ctx->stream));
         const int cur0 = d->cur;
+        auto fargs = [&](sv_domain_tile &Tl, int k, int in, int out) {
+            FArgs A;
+            A.P = P;
+            A.G = FGeom{d->Nt, d->Nx, Tl.T0, Tl.X0, d->Ht, d->Wt, d->pitch, d->plane, d->org};
+            A.phi_in = Tl.phi[in];
+            A.n_in = Tl.n[in];
+            A.phi_out = Tl.phi[out];
+            A.n_out = Tl.n[out];
+            A.nsx = nsx;
+            A.TH = TH;
+            A.nsy = nsy;
+            A.blocks = ctx->d_blocks + (size_t)k * nb;
+            A.skips = ctx->d_skips;
+            A.T = T;
+            A.adv[0] = adv[0];
+            A.adv[1] = adv[1];
+            A.adv[2] = adv[2];
+            A.stat = &Tl.sum->stats[k];
+            A.S = DevScratch{&Tl.sum->abort, &Tl.sum->nreport, Tl.sum->reports};
+            A.sweep = (uint32_t)k;
+            farg_single(A, nsx, nsy);
+            return A;
+        };
+        hipEvent_t ev;
+        ctx->time_begin(&ev);
+        hipStream_t A_ = d->interior_stream ? d->interior_stream : ctx->stream;
+        if (d->split) {
+            // A (interior) and C (halo_stream) start after everything queued so far on ctx->stream
+            SV_HIP(hipEventRecord(d->ev_interior, ctx->stream));
+            SV_HIP(hipStreamWaitEvent(d->halo_stream, d->ev_interior, 0));
+            SV_HIP(hipStreamWaitEvent(A_, d->ev_interior, 0));
+            SV_HIP(hipEventRecord(d->ev_boundary, d->halo_stream));
+        }
         for (int k = 0; k < count; k++) {
-            exchange(d);
             const int in = d->cur, out = (d->cur + 1) % d->R;
-            for (auto &Tl : d->tiles) {
-                FArgs A;
-                A.P = P;
-                A.G = FGeom{d->Nt, d->Nx, Tl.T0, Tl.X0, d->Ht, d->Wt, d->pitch, d->plane, d->org};
-                A.phi_in = Tl.phi[in];
-                A.n_in = Tl.n[in];
-                A.phi_out = Tl.phi[out];
-                A.n_out = Tl.n[out];
-                A.nsx = nsx;
-                A.TH = TH;
-                A.nsy = nsy;
-                A.blocks = ctx->d_blocks + (size_t)k * nb;
-                A.skips = ctx->d_skips;
-                A.T = T;
-                A.adv[0] = adv[0];
-                A.adv[1] = adv[1];
-                A.adv[2] = adv[2];
-                A.stat = &Tl.sum->stats[k];
-                A.S = DevScratch{&Tl.sum->abort, &Tl.sum->nreport, Tl.sum->reports};
-                A.sweep = (uint32_t)k;
-                farg_single(A, nsx, nsy);
-                hipEvent_t ev;
-                ctx->time_begin(&ev);
-                launch_fused_tile(A, nsx * nsy, ctx->stream);
-                ctx->time_end(ev, 1);
+            if (!d->split) {
+                exchange(d, ctx->stream);
+                for (auto &Tl : d->tiles) launch_fused_tile(fargs(Tl, k, in, out), nsx * nsy, ctx->stream);
+            } else {
+                // A: interior strips of sweep k need the boundary strips of sweep k-1 (their input rows)
+                SV_HIP(hipStreamWaitEvent(A_, d->ev_boundary, 0));
+                // C: the halos of sweep k are read from the full output of sweep k-1
+                SV_HIP(hipStreamWaitEvent(d->halo_stream, d->ev_interior, 0));
+                if (d->n_interior)
+                    for (auto &Tl : d->tiles) {
+                        FArgs A = fargs(Tl, k, in, out);
+                        A.strip_map = d->d_strips;
+                        launch_fused_tile(A, d->n_interior, A_);
+                    }
+                SV_HIP(hipEventRecord(d->ev_interior, A_));
+                exchange(d, d->halo_stream);
+                for (auto &Tl : d->tiles) {
+                    FArgs A = fargs(Tl, k, in, out);
+                    A.strip_map = d->d_strips + d->n_interior;
+                    launch_fused_tile(A, d->n_boundary, d->halo_stream);
+                }
+                SV_HIP(hipEventRecord(d->ev_boundary, d->halo_stream));
             }
             d->cur = out;
         }
+        if (d->split) {
+            SV_HIP(hipStreamWaitEvent(ctx->stream, d->ev_boundary, 0));
+            SV_HIP(hipStreamWaitEvent(ctx->stream, d->ev_interior, 0));
+        }
+        ctx->time_end(ev, count);
         SV_HIP(hipGetLastError());
         gather(d);
         AbortInfo a{0, {}};
@@ -445,6 +522,7 @@ int sv_domain_create(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tiles_t, int32
             d->local_of[t] = (int)d->tiles.size();
             d->tiles.push_back(T);
         }
+        halo_layout(d);
         for (auto &T : d->tiles) {
             T.phi.assign(d->R, nullptr);
             T.n.assign(d->R, nullptr);
@@ -459,6 +537,53 @@ int sv_domain_create(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tiles_t, int32
             SV_HIP(hipMemset(T.recv, 0, d->msg_words * sizeof(uint64_t)));
             SV_HIP(hipMalloc(&T.sum, sizeof(Summary)));
             SV_HIP(hipMemset(T.sum, 0, sizeof(Summary)));
+        }
+        // split sweeps: strips whose stencil stays inside the tile run while the halos travel
+        {
+            const int TH = fused_th();
+            const int nsx = (d->Wt + FW_MAX - 1) / FW_MAX, nsy = (d->Ht + TH - 1) / TH;
+            std::vector<int32_t> inner, outer;
+            for (int iy = 0; iy < nsy; iy++)
+                for (int ix = 0; ix < nsx; ix++) {
+                    const int64_t x0 = (int64_t)ix * d->Wt / nsx, x1 = (int64_t)(ix + 1) * d->Wt / nsx;
+                    const int64_t t0 = (int64_t)iy * TH, t1 = std::min<int64_t>(t0 + TH, d->Ht);
+                    const bool in = x0 >= 3 && x1 + 3 <= d->Wt && t0 >= 3 && t1 + 3 <= d->Ht;
+                    (in ? inner : outer).push_back(iy * nsx + ix);
+                }
+            // measured on one MI355X (RCCL loopback, 4096^2 tile): sequential 390 us/sweep, split 406-418 us
+            // (RCCL's kernel waits for CU slots behind the interior launch; CU-masking the interior stream
+            // was slower still), so the split is opt-in: SV_DOMAIN_SPLIT=1
+            const char *env = getenv("SV_DOMAIN_SPLIT");
+            d->split = !inner.empty() && env && env[0] == '1';
+            if (d->split) {
+                d->n_interior = (int)inner.size();
+                d->n_boundary = (int)outer.size();
+                inner.insert(inner.end(), outer.begin(), outer.end());
+                SV_HIP(hipMalloc(&d->d_strips, inner.size() * sizeof(int32_t)));
+                SV_HIP(hipMemcpy(d->d_strips, inner.data(), inner.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+                int lo = 0, hi = 0;
+                SV_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+                SV_HIP(hipStreamCreateWithPriority(&d->halo_stream, hipStreamNonBlocking, hi));
+                // the interior launch would otherwise take every CU slot before RCCL's kernel is queued,
+                // and its workgroups run ~100 us each: keep `reserve` CUs (spread over the XCDs) for the halos
+                const char *re = getenv("SV_DOMAIN_RESERVE");
+                const int reserve = re ? atoi(re) : 0;
+                hipDeviceProp_t prop;
+                SV_HIP(hipGetDeviceProperties(&prop, ctx->device));
+                const int ncu = prop.multiProcessorCount;
+                if (reserve > 0 && reserve < ncu) {
+                    std::vector<uint32_t> mask((ncu + 31) / 32, 0);
+                    for (int c = 0; c < ncu; c++) mask[c / 32] |= 1u << (c % 32);
+                    const int stride = ncu / reserve;
+                    for (int i = 0; i < reserve; i++) {
+                        const int c = i * stride + stride - 1;
+                        mask[c / 32] &= ~(1u << (c % 32));
+                    }
+                    SV_HIP(hipExtStreamCreateWithCUMask(&d->interior_stream, (uint32_t)mask.size(), mask.data()));
+                }
+                SV_HIP(hipEventCreateWithFlags(&d->ev_interior, hipEventDisableTiming));
+                SV_HIP(hipEventCreateWithFlags(&d->ev_boundary, hipEventDisableTiming));
+            }
         }
         if (nranks > 1 || d->loopback) {
             ncclUniqueId u;
@@ -489,8 +614,14 @@ int sv_domain_destroy(sv_domain *d) {
         (void)hipFree(T.recv);
         (void)hipFree(T.sum);
     }
+    if (d->halo_stream) (void)hipStreamSynchronize(d->halo_stream);
     if (d->comm) (void)ncclCommDestroy(d->comm);
     (void)hipFree(d->gathered);
+    (void)hipFree(d->d_strips);
+    if (d->ev_interior) (void)hipEventDestroy(d->ev_interior);
+    if (d->ev_boundary) (void)hipEventDestroy(d->ev_boundary);
+    if (d->halo_stream) (void)hipStreamDestroy(d->halo_stream);
+    if (d->interior_stream) (void)hipStreamDestroy(d->interior_stream);
     delete d;
     return 0;
 }

@@ -57,6 +57,7 @@ struct FArgs {
     const JumpTables *const *Trep;  // per-replica tables, or nullptr (all use T)
     const Affine *advrep;           // per-replica adv[3], or nullptr (all use adv)
     double *obs;                    // OBS kernels: per replica {sum (d phi - 2 pi n)^2, sum (dn)^2, sum n0, sum n1}
+    const int32_t *strip_map = nullptr;  // TILE: launch index -> strip index (interior / boundary launches)
 };
 
 }  // namespace sv

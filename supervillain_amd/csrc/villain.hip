@@ -490,6 +490,8 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
         const int xcd = b & 7, k = b >> 3;
         b = xcd * per + (xcd < rem ? xcd : rem) + k;
     }
+    // domain tiles: the launch covers a subset of the strips (interior ones while the halos travel)
+    if (TILE && A.strip_map) b = __builtin_amdgcn_readfirstlane(A.strip_map[b]);
     // replica of this workgroup (replica batches; 0 otherwise)
     const int rep = REPS ? __builtin_amdgcn_readfirstlane(b / A.tiles_per_rep) : 0;  // uniform: keep it scalar
     if (REPS) b = __builtin_amdgcn_readfirstlane(b - rep * A.tiles_per_rep);
@@ -942,6 +944,7 @@ void farg_single(FArgs &A, int nsx, int nsy) {
     A.Trep = nullptr;
     A.advrep = nullptr;
     A.obs = nullptr;
+    A.strip_map = nullptr;
 }
 
 // plan `count` sweeps starting at sweep `first`, writing descriptors to ctx host staging
