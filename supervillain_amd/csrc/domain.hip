@@ -17,7 +17,7 @@
 // Rejections (NumPy's Lemire sampler rejecting a uint32, which shifts the rest of its block) are
 // found by whichever tile draws the position.  Each halo message carries its sender's abort flag,
 // so an abort spreads one tile-hop per sweep and every tile stops within D sweeps (D = tile-torus
-// radius); the tile states are kept in a ring of R = D + 1 buffers so the input of the failing sweep
+// radius); the tile states are kept in a ring of R = D + 2 buffers (one more for the opt-in split sweeps) so the input of the failing sweep
 // survives everywhere.  After each batch the ranks all-gather their reports (one collective per
 // batch) and take the same replay decision as the single-lattice driver.
 #include <rccl/rccl.h>

@@ -14,6 +14,8 @@ pytestmark = pytest.mark.gpu
 def test_worms_golden():
     """The generators, step by step, against the reference: every histogram, length, final field, rng, report."""
     for c in cases('worms.npz'):
+        if c['action'].startswith('hammer'):
+            continue
         N = c['N']
         L = sv.Lattice2D(N)
         if c['action'] == 'villain':
@@ -94,3 +96,25 @@ def test_worm_max_moves_is_an_error():
         for _ in range(50):
             cfg = G.step(cfg)
 
+
+
+def test_hammer_ensemble_golden():
+    """Ensemble(S).generate(steps, Hammer(S, worms)) -- every member generator of the reference's Hammer, the
+    worm included (KeepEvery-blocked histogram average for worms > 1) -- against the reference's own run."""
+    from supervillain_amd.generator.combining import KeepEvery
+    for c in cases('worms.npz'):
+        if not c['action'].startswith('hammer'):
+            continue
+        villain = c['action'] == 'hammer_villain'
+        L = sv.Lattice2D(c['N'])
+        S = (sv.Villain if villain else sv.Worldline)(L, c['kappa'], c['W'])
+        H = (gv if villain else gw).Hammer(S, c['worms'])
+        for G, seed in zip(H.generators, c['seeds']):
+            (G.generator if isinstance(G, KeepEvery) else G).rng = np.random.default_rng(int(seed))
+        E = sv.Ensemble(S).generate(c['steps'], H)
+        arr = lambda x: np.asarray(x.array if hasattr(x, 'array') else x)
+        for f in (('phi', 'n') if villain else ('m', 'v')):
+            assert (arr(getattr(E, f)) == c[f]).all(), (c['action'], f)
+        assert (arr(getattr(E, 'Vortex_Vortex' if villain else 'Spin_Spin')) == c['hist']).all(), c['action']
+        assert (arr(E.Worm_Length) == c['lengths']).all(), c['action']
+        assert H.report() == c['report']

@@ -146,6 +146,8 @@ def test_worms_golden(oracle_lib):
     """both ClassicWorms, step by step (every step's histogram and length)."""
     O = oracle_lib
     for c in cases('worms.npz'):
+        if c['action'].startswith('hammer'):
+            continue  # whole-Hammer Ensemble fixtures: tests/test_gpu_worms.py
         N, g = c['N'], generator_from(c['rng0'])
         for k in range(c['steps']):
             if c['action'] == 'villain':

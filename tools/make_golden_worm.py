@@ -6,6 +6,8 @@ Sources exercised (all /root/reference paths):
   villain ClassicWorm.step    supervillain/generator/villain/worm.py:85-131, worm_kernel :133-183
   worldline ClassicWorm.step  supervillain/generator/worldline/worm.py:137-193, worm_kernel :26-94
   _Lattice2D moves            supervillain/lattice/two_dimensional.py:221-300
+  Hammer (worm included) through Ensemble.generate: villain/__init__.py:11-67, worldline/__init__.py:10-40,
+                              ensemble.py:47-100, combining.py:9-116 (worms.npz 'hammer' cases)
 """
 import numpy as np
 
@@ -71,6 +73,27 @@ def worldline_case(sv, N, kappa, W, steps, seed, hot):
                 rng1=rng_state(G.rng), report=np.array(G.report()))
 
 
+def hammer_case(sv, action, N, kappa, W, steps, seed, worms):
+    """Ensemble(S).generate(steps, Hammer(S, worms)) from a cold start, every member generator seeded."""
+    L = sv.lattice.Lattice2D(N)
+    S = (sv.action.Villain if action == 'villain' else sv.action.Worldline)(L, kappa, W)
+    H = (sv.generator.villain if action == 'villain' else sv.generator.worldline).Hammer(S, worms)
+    seeds = []
+    for i, G in enumerate(H.generators):
+        g = G.generator if hasattr(G, 'stride') else G
+        g.rng = np.random.default_rng(seed + i)
+        seeds.append(seed + i)
+    E = sv.Ensemble(S).generate(steps, H)
+    key = 'Vortex_Vortex' if action == 'villain' else 'Spin_Spin'
+    fields = ('phi', 'n') if action == 'villain' else ('m', 'v')
+    out = dict(action='hammer_' + action, N=N, kappa=kappa, W=W, steps=steps, worms=worms, seeds=np.array(seeds),
+               hist=np.asarray(getattr(E, key)).copy(), lengths=np.asarray(E.Worm_Length).copy(),
+               report=np.array(H.report()))
+    for f in fields:
+        out[f] = np.asarray(getattr(E, f)).copy()
+    return out
+
+
 def main():
     sv = refshim.load()
     out = []
@@ -83,8 +106,14 @@ def main():
                                           (6, 0.7, 3, 8, 14, True), (7, 0.4, float('inf'), 8, 15, True),
                                           (16, 0.5, 2, 4, 16, True), (9, 1.0, 1, 6, 17, False)]:
         out.append(worldline_case(sv, N, kappa, W, steps, seed, hot))
+    for action, N, kappa, W, steps, seed, worms in [('villain', 8, 0.5, 2, 5, 100, 1), ('villain', 6, 0.7, 1, 4, 110, 1),
+                                                      ('villain', 8, 0.6, 3, 3, 115, 3),
+                                                      ('worldline', 8, 0.5, 1, 5, 120, 1),
+                                                      ('worldline', 6, 0.4, 2, 4, 130, 1),
+                                                      ('worldline', 6, 0.6, float('inf'), 3, 140, 2)]:
+        out.append(hammer_case(sv, action, N, kappa, W, steps, seed, worms))
     for c in out:
-        print(c['action'], c['N'], c['kappa'], c['W'], 'lengths', c['lengths'].tolist())
+        print(c['action'], c['N'], c['kappa'], c['W'], 'lengths', np.asarray(c['lengths']).tolist())
     save('worms.npz', out)
 
 
