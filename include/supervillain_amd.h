@@ -176,6 +176,10 @@ int sv_domain_run(sv_domain *d, double kappa, int64_t W, double interval_phi, in
  * and the message of direction s received from `recv_from` fills the ghost block at (dst_row0, dst_col0)
  * (tile-local coordinates; ghosts are negative or >= the tile extent). */
 int sv_domain_exchange_plan(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t rank, int64_t *out);
+/* Host-only: the RCCL message layout of `rank` when every tile is its own rank (messages grouped per
+ * remote peer, one ncclSend / ncclRecv each).  out (>= 2 + 3*16 + 8 + 8 + 8 + 1 int64) = {nsend, nrecv,
+ * nsend x {peer, offset, words}, nrecv x {peer, offset, words}, soff[8], roff[8], words[8], msg_words}. */
+int sv_domain_message_layout(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t rank, int64_t *out);
 
 
 /* ---- Villain replica batches (BASELINE config 5; SURVEY.md 8e: replicas need no collectives) ------- */

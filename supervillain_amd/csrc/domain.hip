@@ -243,6 +243,28 @@ void halo_layout(sv_domain *d) {
     }
 }
 
+// The local tiles (all of them with one rank, else the rank's own) and their neighbour tables.
+void build_tiles(sv_domain *d) {
+    const int ntiles = d->ty * d->tx;
+    d->local_of.assign(ntiles, -1);
+    d->tiles.clear();
+    for (int t = 0; t < ntiles; t++) {
+        if (d->nranks > 1 && t != d->rank) continue;
+        sv_domain_tile T;
+        T.iy = t / d->tx;
+        T.ix = t % d->tx;
+        T.T0 = T.iy * d->Ht;
+        T.X0 = T.ix * d->Wt;
+        for (int s = 0; s < NDIR; s++) {
+            int dy, dx;
+            dir_of(s, dy, dx);
+            T.nbr[s] = tile_index(d, T.iy + dy, T.ix + dx);
+        }
+        d->local_of[t] = (int)d->tiles.size();
+        d->tiles.push_back(T);
+    }
+}
+
 void exchange(sv_domain *d, hipStream_t stream) {
     sv_ctx *ctx = d->ctx;
     (void)ctx;
@@ -483,6 +505,35 @@ int sv_domain_exchange_plan(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t til
     }
 }
 
+int sv_domain_message_layout(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t rank, int64_t *out) {
+    try {
+        if (!out || tiles_t < 1 || tiles_x < 1 || rank < 0 || rank >= tiles_t * tiles_x) return -1;
+        sv_domain d;
+        d.Nt = Nt;
+        d.Nx = Nx;
+        d.ty = tiles_t;
+        d.tx = tiles_x;
+        d.nranks = tiles_t * tiles_x;
+        d.rank = rank;
+        geometry(&d);
+        build_tiles(&d);
+        halo_layout(&d);
+        const sv_domain_tile &T = d.tiles[0];
+        int64_t *o = out;
+        *o++ = (int64_t)T.sends.size();
+        *o++ = (int64_t)T.recvs.size();
+        for (const auto &m : T.sends) o = std::copy(m.begin(), m.end(), o);
+        for (const auto &m : T.recvs) o = std::copy(m.begin(), m.end(), o);
+        o = std::copy(T.soff, T.soff + NDIR, o);
+        o = std::copy(T.roff, T.roff + NDIR, o);
+        for (int s = 0; s < NDIR; s++) *o++ = 2 + 3 * (int64_t)d.H.rect[s].rows * d.H.rect[s].cols;
+        *o++ = d.msg_words;
+        return 0;
+    } catch (const std::exception &) {
+        return -2;
+    }
+}
+
 int sv_domain_create(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t nranks,
                      int32_t rank, const uint8_t *unique_id, sv_domain **out) {
     if (!ctx || !out) return -1;
@@ -505,23 +556,7 @@ int sv_domain_create(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tiles_t, int32
         d->loopback = nranks == 1 && unique_id != nullptr;
         if (d->loopback && tiles_t * tiles_x != 1) throw std::invalid_argument("RCCL loopback mode needs a 1 x 1 tile grid");
         geometry(d);
-        const int ntiles = tiles_t * tiles_x;
-        d->local_of.assign(ntiles, -1);
-        for (int t = 0; t < ntiles; t++) {
-            if (nranks > 1 && t != rank) continue;
-            sv_domain_tile T;
-            T.iy = t / tiles_x;
-            T.ix = t % tiles_x;
-            T.T0 = T.iy * d->Ht;
-            T.X0 = T.ix * d->Wt;
-            for (int s = 0; s < NDIR; s++) {
-                int dy, dx;
-                dir_of(s, dy, dx);
-                T.nbr[s] = tile_index(d, T.iy + dy, T.ix + dx);
-            }
-            d->local_of[t] = (int)d->tiles.size();
-            d->tiles.push_back(T);
-        }
+        build_tiles(d);
         halo_layout(d);
         for (auto &T : d->tiles) {
             T.phi.assign(d->R, nullptr);

@@ -47,6 +47,26 @@ def exchange_plan(Nt, Nx, tiles, rank):
     return plan
 
 
+def message_layout(Nt, Nx, tiles, rank):
+    """The RCCL message layout libsvhip.so uses for `rank` when every tile is a rank (host-only).
+
+    Returns dict: sends / recvs = [(peer, offset, words)], soff / roff = per-direction word offsets of
+    message s in the send / receive buffer, words = per-direction message size, msg_words = buffer size."""
+    out = (ctypes.c_int64 * 128)()
+    rc = _native.lib().sv_domain_message_layout(int(Nt), int(Nx), int(tiles[0]), int(tiles[1]), int(rank), out)
+    if rc != 0:
+        raise ValueError(f'invalid decomposition {Nt}x{Nx} into {tiles} (rank {rank})')
+    o = [int(v) for v in out]
+    ns, nr = o[0], o[1]
+    p = 2
+    sends = [tuple(o[p + 3 * i:p + 3 * i + 3]) for i in range(ns)]
+    p += 3 * ns
+    recvs = [tuple(o[p + 3 * i:p + 3 * i + 3]) for i in range(nr)]
+    p += 3 * nr
+    return {'sends': sends, 'recvs': recvs, 'soff': o[p:p + 8], 'roff': o[p + 8:p + 16],
+            'words': o[p + 16:p + 24], 'msg_words': o[p + 24]}
+
+
 class VillainDomain:
     """An Nt x Nx Villain (phi, n) state cut into tiles, resident in HBM."""
 

@@ -8,7 +8,7 @@ import socket
 import numpy as np
 import pytest
 
-from supervillain_amd.domain import exchange_plan, tile_grid
+from supervillain_amd.domain import exchange_plan, message_layout, tile_grid
 
 GT, GB, GL, GR = 2, 3, 2, 3  # ghost rows above / below, columns left / right
 
@@ -113,20 +113,30 @@ def _exchange_worker(rank, world, port, tiles, Nt, Nx, errfile):
     try:
         G = np.random.default_rng(1).normal(size=(Nt, Nx))
         plan = exchange_plan(Nt, Nx, tiles, rank)
+        lay = message_layout(Nt, Nx, tiles, rank)
         P = padded_tile(G, tiles, rank)
-        ops, recv = [], {}
-        # the C++ RCCL loop: sends in direction order, then receives in direction order (self: local)
+        # the C++ RCCL loop: a send buffer laid out per peer (message s at soff[s] = [flag, pad, phi, n0, n1]),
+        # one send per distinct peer, one receive per distinct source; self messages stay local
+        send = np.zeros(lay['msg_words'])
         for s, m in enumerate(plan):
-            if m['send_to'] != rank:
-                ops.append(dist.P2POp(dist.isend, torch.from_numpy(message(P, m)), m['send_to']))
+            blk = message(P, m).ravel()
+            o = lay['soff'][s]
+            assert lay['words'][s] == 2 + 3 * blk.size
+            send[o + 2:o + 2 + blk.size] = blk
+        recvbuf = torch.zeros(lay['msg_words'], dtype=torch.float64)
+        ops = [dist.P2POp(dist.isend, torch.from_numpy(send[o:o + w].copy()), peer) for peer, o, w in lay['sends']]
+        ops += [dist.P2POp(dist.irecv, recvbuf[o:o + w], peer) for peer, o, w in lay['recvs']]
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        remote = {s for s, m in enumerate(plan) if m['recv_from'] != rank}
         for s, m in enumerate(plan):
-            if m['recv_from'] != rank:
-                recv[s] = torch.empty(m['shape'], dtype=torch.float64)
-                ops.append(dist.P2POp(dist.irecv, recv[s], m['recv_from']))
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
-        for s, m in enumerate(plan):
-            block = recv[s].numpy() if s in recv else message(P, plan[s])
+            cnt = int(np.prod(m['shape']))
+            if s in remote:
+                o = lay['roff'][s]
+                block = recvbuf.numpy()[o + 2:o + 2 + cnt].reshape(m['shape'])
+            else:
+                block = message(P, plan[s])
             place(P, m, block)
         np.testing.assert_array_equal(P, expected_frame(G, tiles, rank))
     except Exception as e:  # report to the parent
@@ -137,11 +147,42 @@ def _exchange_worker(rank, world, port, tiles, Nt, Nx, errfile):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('tiles', [(1, 2), (2, 1)])
+@pytest.mark.parametrize('tiles', [(1, 2), (2, 1), (2, 2)])
 def test_two_rank_gloo_exchange(tiles, tmp_path):
     import torch.multiprocessing as mp
     errfile = str(tmp_path / 'err.txt')
     Nt, Nx = 8 * tiles[0], 6 * tiles[1]
-    mp.start_processes(_exchange_worker, args=(2, _free_port(), tiles, Nt, Nx, errfile), nprocs=2, join=True,
-                       start_method='spawn')
+    world = tiles[0] * tiles[1]
+    mp.start_processes(_exchange_worker, args=(world, _free_port(), tiles, Nt, Nx, errfile), nprocs=world,
+                       join=True, start_method='spawn')
     assert not os.path.exists(errfile), open(errfile).read()
+
+
+@pytest.mark.parametrize('tiles', GRIDS)
+def test_rccl_blocks_line_up(tiles):
+    """The per-peer message blocks libsvhip.so sends (one ncclSend / ncclRecv per distinct peer): rank a's block
+    for b and rank b's block from a have the same size, and every message s sits at the same offset inside
+    both blocks, so the receiver's ghost block s gets exactly the sender's message s."""
+    from supervillain_amd.domain import exchange_plan, message_layout
+    ty, tx = tiles
+    Nt, Nx = 8 * ty, 6 * tx
+    ntiles = ty * tx
+    lay = [message_layout(Nt, Nx, tiles, r) for r in range(ntiles)]
+    plans = [exchange_plan(Nt, Nx, tiles, r) for r in range(ntiles)]
+    for a in range(ntiles):
+        L = lay[a]
+        # blocks are disjoint, inside the buffer, and one per distinct remote peer
+        spans = sorted((o, o + w) for _, o, w in L['sends'])
+        assert all(e0 <= s1 for (_, e0), (s1, _) in zip(spans, spans[1:]))
+        assert all(e <= L['msg_words'] for _, e in spans)
+        assert len({p for p, _, _ in L['sends']}) == len(L['sends'])
+        assert {p for p, _, _ in L['sends']} == {m['send_to'] for m in plans[a] if m['send_to'] != a}
+        for b, off, words in L['sends']:
+            rb = [x for x in lay[b]['recvs'] if x[0] == a]
+            assert len(rb) == 1 and rb[0][2] == words
+            roff = rb[0][1]
+            dirs = [s for s in range(8) if plans[a][s]['send_to'] == b]
+            assert dirs == [s for s in range(8) if plans[b][s]['recv_from'] == a]
+            assert sum(L['words'][s] for s in dirs) == words
+            for s in dirs:
+                assert L['soff'][s] - off == lay[b]['roff'][s] - roff
