@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <array>
+#include <cmath>
 #include <cstring>
 
 #include "villain.h"
@@ -338,6 +339,24 @@ void fill_stats(const sv_domain *d, const SkipMap &skips, int nb, int sw, int co
     }
 }
 
+// Sweeps per batch.  A NumPy Lemire rejection anywhere in the (whole, decomposed) lattice aborts the
+// batch from its sweep on, and every sweep still queued behind it costs an exchange (RCCL pairs must
+// match on every rank, so the ranks cannot stop early) plus three early-exit launches; a batch costs
+// one all-gather and a host round trip.  With q rejections expected per sweep (4 V bounded draws of
+// threshold thr / 2^32), an aborted sweep costing r sweeps and a batch o sweeps, the overhead per sweep
+// is o / B + q (1 + r B / 2), least at B = sqrt(2 o / (q r)): the weak-scaled 2 x 4 lattice
+// (8192 x 16384, q = 12.5%) runs batches of ~5 sweeps, one L=4096 tile (q = 1.6%) the full 64.
+// SV_DOMAIN_BATCH overrides.
+int domain_batch(const sv_domain *d, const VParams &P) {
+    if (const char *e = getenv("SV_DOMAIN_BATCH")) return std::max(1, std::min(DOMAIN_BATCH, atoi(e)));
+    const double V = (double)d->Nt * d->Nx;
+    const double q = P.k > 1 ? 4.0 * V * (double)P.thr / 4294967296.0 : 0.0;
+    if (q <= 0) return DOMAIN_BATCH;
+    const double o = 0.3, r = d->comm ? 0.17 : 0.05;  // measured: RCCL exchange ~50 us, batch ~100 us, sweep 330 us
+    const int B = (int)std::lround(std::sqrt(2.0 * o / (q * r)));
+    return std::max(4, std::min(DOMAIN_BATCH, B));
+}
+
 void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u128 inc, sv_stats *stats) {
     sv_ctx *ctx = d->ctx;
     const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
@@ -354,9 +373,10 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
     SkipMap skips;
     std::vector<Block> blocks;
     std::vector<uint32_t> skipvec;
+    const int batch = domain_batch(d, P);
     int sw = 0;
     while (sw < sweeps) {
-        const int count = std::min(DOMAIN_BATCH, sweeps - sw);
+        const int count = std::min(batch, sweeps - sw);
         Cursor c = cur;
         plan_sweeps(ctx, c, inc, specs, sw, count, skips, blocks, skipvec);
         upload_plan(ctx, blocks, skipvec);
