@@ -484,7 +484,7 @@ def run_domain(args, world, rank, local, dist):
                               'reference chain (PCG64 replay)',
                   'L': L, 'lattice': [Nt, Nx], 'tiles': [ty, tx], 'path': 'domain',
                   'parallelism': f'{ty}x{tx} domain decomposition over {world} GPU(s)'}
-        report(args, world, Nt * Nx, Nt * Nx // (ty * tx), elapsed, acc, avg_launch_s, config, Nt // ty)
+        report(args, world, Nt * Nx, Nt * Nx // world, elapsed, acc, avg_launch_s, config, Nt // ty)
     dom.close()
 
 
