@@ -1033,8 +1033,9 @@ int fused_nw() {
 }
 int fused_th() {
     const char *e = getenv("SV_FUSED_TH");
-    int v = e ? atoi(e) : 64;
-    return v >= 8 ? v : 64;
+    // rows per strip: 52 measured best at L=4096 (322 us vs 328 at 64, 324 at 48, 345 at 80; r73 sweep)
+    int v = e ? atoi(e) : 52;
+    return v >= 8 && v % 4 == 0 ? v : 52;
 }
 
 bool fused_ok(int32_t N) { return N % 2 == 0 && N >= 4; }
