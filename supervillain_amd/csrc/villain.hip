@@ -366,6 +366,24 @@ __device__ __forceinline__ uint32_t fast_pack(const uint32_t *hasw, int32_t lane
     return pk;
 }
 
+// The row bases are the same for every lane of a wave (one row per wave): held in SGPRs they feed the
+// 128-bit multiplies as scalar operands instead of occupying VGPRs.
+#ifndef SV_SCALAR_BASES
+#define SV_SCALAR_BASES 0  // measured slower: 339 vs 320 us per L=4096 sweep (SGPR spills, readfirstlane chains)
+#endif
+__device__ __forceinline__ u128 wave_uniform(u128 v) {
+#if SV_SCALAR_BASES
+    auto rf = [](uint64_t x) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+        return ((uint64_t)hi << 32) | lo;
+    };
+    return u128{rf(v.lo), rf(v.hi)};
+#else
+    return v;
+#endif
+}
+
 __device__ __forceinline__ Draws draws_fastp(const FArgs &A, const Rep &RP, int c, bool active, int32_t lane,
                                              uint32_t pk, uint32_t rank, const u128 *bases, const Affine *sm) {
     const int bb = 1 + 5 * c;
@@ -689,7 +707,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             const bool active = row_ok && (FR ? x < w : x <= x1 + 1);
             u128 bs[6];
 #pragma unroll
-            for (int k = 0; k < 6; k++) bs[k] = s_base[wave][k];
+            for (int k = 0; k < 6; k++) bs[k] = wave_uniform(s_base[wave][k]);
             Draws D;
             if (fast[0])
                 D = draws_fastp(A, RL, 0, active, lane, pk0, ((uint32_t)gq * (uint32_t)Nx + (uint32_t)(Gm.X0 + x)) >> 1,
@@ -761,7 +779,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             const bool active = row_ok && (FR ? x < w : x <= x1);
             u128 bs[6];
 #pragma unroll
-            for (int k = 0; k < 6; k++) bs[k] = s_base[wave][8 + k];
+            for (int k = 0; k < 6; k++) bs[k] = wave_uniform(s_base[wave][8 + k]);
             Draws D;
             if (fast[1])
                 D = draws_fastp(A, RL, 1, active, lane, pk1, ((uint32_t)gq * (uint32_t)Nx + (uint32_t)(Gm.X0 + x)) >> 1,
