@@ -368,6 +368,9 @@ __device__ __forceinline__ uint32_t fast_pack(const uint32_t *hasw, int32_t lane
 
 // The row bases are the same for every lane of a wave (one row per wave): held in SGPRs they feed the
 // 128-bit multiplies as scalar operands instead of occupying VGPRs.
+#ifndef SV_FR_FAST
+#define SV_FR_FAST 1
+#endif
 #ifndef SV_SCALAR_BASES
 #define SV_SCALAR_BASES 0  // measured slower: 339 vs 320 us per L=4096 sweep (SGPR spills, readfirstlane chains)
 #endif
@@ -552,12 +555,17 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     const uint32_t has_c1[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(RP.blocks[7].has),
                                 (uint32_t)__builtin_amdgcn_readfirstlane(RP.blocks[9].has)};
     // fast draws need, per colour, no skips and equal buffers within each fwd/bwd pair
-    bool fast[2];
+    bool fast[2], fastfr[2];
 #pragma unroll
     for (int c = 0; c < 2; c++) {
         const Block *B = &RP.blocks[2 + 5 * c];
         fast[c] = interior && B[0].nskip == 0 && B[1].nskip == 0 && B[2].nskip == 0 && B[3].nskip == 0 &&
                   B[0].has == B[1].has && B[2].has == B[3].has;
+        // full-row strips (replica batches of N <= 128): every lane is busy, so the lane pairs that share a
+        // choice word must not straddle the row -- true when the fwd/bwd blocks start on a whole word
+        // (has == 0), which is the norm (each block draws an even V/2 half-words)
+        fastfr[c] = FR && SV_FR_FAST && B[0].nskip == 0 && B[1].nskip == 0 && B[2].nskip == 0 && B[3].nskip == 0 &&
+                    B[0].has == 0 && B[1].has == 0 && B[2].has == 0 && B[3].has == 0;
     }
 
     // ---- register prefetch of region rows [ra, ra+NW) (clipped to [t0-2, t1+2]): wave w moves row
@@ -712,6 +720,9 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             if (fast[0])
                 D = draws_fastp(A, RL, 0, active, lane, pk0, ((uint32_t)gq * (uint32_t)Nx + (uint32_t)(Gm.X0 + x)) >> 1,
                                 bs, s_small);
+            else if (fastfr[0])
+                D = draws_fast(A, RL, 0, has_c0, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)xs, (uint32_t)x, 0u,
+                               bs, s_small);
             else
                 D = draws_general(A, RL, 0, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small, edge, xw,
                                   &s_base[wave][16]);
@@ -784,6 +795,9 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             if (fast[1])
                 D = draws_fastp(A, RL, 1, active, lane, pk1, ((uint32_t)gq * (uint32_t)Nx + (uint32_t)(Gm.X0 + x)) >> 1,
                                 bs, s_small);
+            else if (fastfr[1])
+                D = draws_fast(A, RL, 1, has_c1, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)xs, (uint32_t)x, 0u,
+                               bs, s_small);
             else
                 D = draws_general(A, RL, 1, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small, edge, xw,
                                   &s_base[wave][24]);
