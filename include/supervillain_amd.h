@@ -61,6 +61,12 @@ int sv_device_count(void);
  * (batches that hit a Lemire rejection are not counted). */
 int sv_ctx_set_timing(sv_ctx *ctx, int32_t enable);
 int sv_ctx_kernel_time(sv_ctx *ctx, double *ms_total, int64_t *launches);
+/* Host-only: copy R NumPy PCG64 bit-generator states into (gather) or out of (scatter) sv_rng records, given
+ * each generator's `bit_generator.ctypes.state_address` (NumPy's pcg64_state, numpy/random/src/pcg64/pcg64.h,
+ * native 128-bit layout; the Python wrapper verifies it against the public state dict first).  Lets a
+ * batch of R chains cross the boundary without R Python state-dict round trips. */
+int sv_rng_gather(void *const *pcg64_states, int32_t R, sv_rng *out);
+int sv_rng_scatter(const sv_rng *in, int32_t R, void *const *pcg64_states);
 const char *sv_build_info(void);
 
 /* ---- Villain (phi, n): NeighborhoodUpdate ------------------------------------------------- */

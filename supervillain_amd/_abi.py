@@ -32,8 +32,42 @@ class SvStats(ctypes.Structure):
     ]
 
 
+class _PCG64State(ctypes.Structure):
+    """NumPy's pcg64_state (numpy/random/src/pcg64/pcg64.h): the PCG state pointer and the half-word buffer."""
+    _fields_ = [('pcg', ctypes.c_void_p), ('has_uint32', ctypes.c_int), ('uinteger', ctypes.c_uint32)]
+
+
+_RAW_OK = None  # the raw layout is checked against the state dict once per process
+
+
+def _raw(gen):
+    """(pcg64_state, uint64[4] = state lo, hi, inc lo, hi) views of a PCG64 bit generator, or None when this
+    NumPy build's layout differs (then the public state dict is used)."""
+    global _RAW_OK
+    bg = gen.bit_generator
+    if _RAW_OK is False or type(bg).__name__ != 'PCG64':
+        return None
+    try:
+        st = _PCG64State.from_address(bg.ctypes.state_address)
+        w = (ctypes.c_uint64 * 4).from_address(st.pcg)
+    except Exception:
+        _RAW_OK = False
+        return None
+    if _RAW_OK is None:
+        d = bg.state
+        _RAW_OK = (d['state']['state'] == (w[1] << 64 | w[0]) and d['state']['inc'] == (w[3] << 64 | w[2])
+                   and d['has_uint32'] == st.has_uint32 and d['uinteger'] == st.uinteger)
+        if not _RAW_OK:
+            return None
+    return st, w
+
+
 def rng_from_numpy(gen):
     """Snapshot a NumPy Generator(PCG64) into an SvRng."""
+    raw = _raw(gen)
+    if raw is not None:
+        st, w = raw
+        return SvRng(w[1], w[0], w[3], w[2], st.has_uint32, st.uinteger)
     st = gen.bit_generator.state
     if st.get('bit_generator') != 'PCG64':
         raise TypeError(f"the device generators replay NumPy's PCG64 stream; got {st.get('bit_generator')}")
@@ -43,8 +77,37 @@ def rng_from_numpy(gen):
 
 def rng_to_numpy(r, gen):
     """Write an SvRng back into the NumPy Generator, so host-side draws continue the same stream."""
+    raw = _raw(gen)
+    if raw is not None:
+        st, w = raw
+        w[0], w[1], w[2], w[3] = r.state_lo, r.state_hi, r.inc_lo, r.inc_hi
+        st.has_uint32, st.uinteger = r.has_uint32, r.uinteger
+        return
     st = gen.bit_generator.state
     st['state'] = {'state': (int(r.state_hi) << 64) | int(r.state_lo), 'inc': (int(r.inc_hi) << 64) | int(r.inc_lo)}
     st['has_uint32'] = int(r.has_uint32)
     st['uinteger'] = int(r.uinteger)
     gen.bit_generator.state = st
+
+
+def rngs_from_numpy(gens):
+    """SvRng array of many Generators: one C call over their raw states when the layout checks out."""
+    from supervillain_amd import _native
+    R = len(gens)
+    out = (SvRng * R)()
+    if R and _raw(gens[0]) is not None and all(type(g.bit_generator).__name__ == 'PCG64' for g in gens):
+        addrs = (ctypes.c_void_p * R)(*[g.bit_generator.ctypes.state_address for g in gens])
+        if _native.lib().sv_rng_gather(addrs, R, out) == 0:
+            return out, addrs
+    for i, g in enumerate(gens):
+        out[i] = rng_from_numpy(g)
+    return out, None
+
+
+def rngs_to_numpy(arr, gens, addrs=None):
+    """Write an SvRng array back into its Generators (the addresses from rngs_from_numpy when available)."""
+    from supervillain_amd import _native
+    if addrs is not None and _native.lib().sv_rng_scatter(arr, len(gens), addrs) == 0:
+        return
+    for x, g in zip(arr, gens):
+        rng_to_numpy(x, g)

@@ -180,4 +180,37 @@ int sv_ctx_destroy(sv_ctx *ctx) {
 
 const char *sv_last_error(sv_ctx *ctx) { return ctx ? ctx->err.c_str() : "no context"; }
 
+// NumPy's pcg64_state (numpy/random/src/pcg64/pcg64.h) with a native 128-bit pcg128_t: the Python side
+// checks this layout against the public state dict before it passes any address here.
+struct np_pcg64_state {
+    uint64_t *pcg;  // {state lo, state hi, inc lo, inc hi}
+    int has_uint32;
+    uint32_t uinteger;
+};
+
+int sv_rng_gather(void *const *pcg64_states, int32_t R, sv_rng *out) {
+    if (!pcg64_states || !out || R < 0) return -1;
+    for (int32_t r = 0; r < R; r++) {
+        const np_pcg64_state *st = (const np_pcg64_state *)pcg64_states[r];
+        if (!st || !st->pcg) return -1;
+        out[r] = sv_rng{st->pcg[1], st->pcg[0], st->pcg[3], st->pcg[2], st->has_uint32, st->uinteger};
+    }
+    return 0;
+}
+
+int sv_rng_scatter(const sv_rng *in, int32_t R, void *const *pcg64_states) {
+    if (!pcg64_states || !in || R < 0) return -1;
+    for (int32_t r = 0; r < R; r++) {
+        np_pcg64_state *st = (np_pcg64_state *)pcg64_states[r];
+        if (!st || !st->pcg) return -1;
+        st->pcg[0] = in[r].state_lo;
+        st->pcg[1] = in[r].state_hi;
+        st->pcg[2] = in[r].inc_lo;
+        st->pcg[3] = in[r].inc_hi;
+        st->has_uint32 = in[r].has_uint32;
+        st->uinteger = in[r].uinteger;
+    }
+    return 0;
+}
+
 }  // extern "C"

@@ -15,6 +15,8 @@
 //
 // Inline observables (ActionDensity, InternalEnergyDensity, WindingSquared, TorusWrapping) are summed
 // by the sweep kernel while it writes the finished rows (0 extra HBM bytes).
+#include <chrono>
+#include <cstdio>
 #include <algorithm>
 #include <cstring>
 
@@ -170,8 +172,12 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
     std::vector<sv_stats> hst;
     std::vector<double> hobs;
     int sw = 0;
+    const bool dbg = getenv("SV_DEBUG_TIMING") != nullptr;
+    using clk = std::chrono::steady_clock;
+    auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
     while (sw < sweeps) {
         const int count = std::min(REP_BATCH, sweeps - sw);
+        const auto t_a = clk::now();
         // --- plan: device closed form for every replica, host planner for replicas with skips
         for (int r = 0; r < R; r++) pin[r] = PlanIn{cur[r].s.lo, cur[r].s.hi, cur[r].has, cur[r].buf};
         SV_HIP(hipMemcpyAsync(b->d_plan, pin.data(), R * sizeof(PlanIn), hipMemcpyHostToDevice, ctx->stream));
@@ -204,6 +210,7 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         SV_HIP(hipMemsetAsync(b->d_stats, 0, (size_t)R * count * sizeof(sv_stats), ctx->stream));
         if (obs) SV_HIP(hipMemsetAsync(b->d_obs, 0, (size_t)R * count * 4 * sizeof(double), ctx->stream));
         // --- sweeps
+        const auto t_b = clk::now();
         const int cur0 = b->cur;
         hipEvent_t ev;
         ctx->time_begin(&ev);
@@ -242,7 +249,9 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         uint32_t nrep = 0;
         SV_HIP(hipMemcpyAsync(&ab, ctx->d_abort, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
         SV_HIP(hipMemcpyAsync(&nrep, ctx->d_nreport, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+        const auto t_c = clk::now();
         SV_HIP(hipStreamSynchronize(ctx->stream));
+        const auto t_d = clk::now();
         int good = count;
         if (ab) {
             ctx->time_discard();
@@ -299,6 +308,9 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         }
         b->cur = cur0 ^ (good & 1);
         sw += good;
+        if (dbg)
+            fprintf(stderr, "[sv replicas] plan %.1f us, launch %.1f us, wait %.1f us, post %.1f us, good %d/%d\n",
+                    us(t_a, t_b), us(t_b, t_c), us(t_c, t_d), us(t_d, clk::now()), good, count);
     }
     for (int r = 0; r < R; r++) {
         rngs[r].state_hi = cur[r].s.hi;

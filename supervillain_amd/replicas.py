@@ -12,7 +12,7 @@ import ctypes
 import numpy as np
 
 from supervillain_amd import _native
-from supervillain_amd._abi import SvRng, SvStats, rng_from_numpy, rng_to_numpy
+from supervillain_amd._abi import SvRng, SvStats, rng_from_numpy, rng_to_numpy, rngs_from_numpy, rngs_to_numpy
 
 # numpy image of sv_stats (include/supervillain_amd.h)
 STATS_DTYPE = np.dtype([('accepted', '<i8'), ('proposed', '<i8'), ('acceptance_sum', '<f8'), ('rejections', '<i8')])
@@ -59,15 +59,14 @@ class VillainReplicas:
         replica's last worm (R, N, N) int64, Worm_Length (R, worms) int64)."""
         if len(rngs) != self.R:
             raise ValueError(f'need {self.R} generators')
-        r = (SvRng * self.R)(*[rng_from_numpy(g) for g in rngs])
+        r, addrs = rngs_from_numpy(rngs)
         hist = np.zeros((self.R, self.N, self.N), dtype=np.int64)
         lengths = np.zeros((self.R, max(worms, 1)), dtype=np.int64)
         W = 1 if self.W == 1 else 0
         self.ctx.check(_native.lib().sv_replicas_worm_run(self.handle, self.kappa, W, int(worms), int(max_moves), r,
                                                           _native.ptr(hist), _native.ptr(lengths)),
                        'sv_replicas_worm_run')
-        for g, x in zip(rngs, r):
-            rng_to_numpy(x, g)
+        rngs_to_numpy(r, rngs, addrs)
         return hist, lengths[:, :worms]
 
     def run(self, sweeps, rngs, inline=False):
@@ -78,14 +77,13 @@ class VillainReplicas:
         dict of (R, sweeps) arrays (TorusWrapping: (R, sweeps, 2))."""
         if len(rngs) != self.R:
             raise ValueError(f'need {self.R} generators')
-        r = (SvRng * self.R)(*[rng_from_numpy(g) for g in rngs])
+        r, addrs = rngs_from_numpy(rngs)
         st = np.zeros((self.R, max(sweeps, 1)), dtype=STATS_DTYPE)  # sv_stats[R][sweeps]
         obs = np.zeros((self.R, max(sweeps, 1), 4)) if inline else None
         self.ctx.check(_native.lib().sv_replicas_run(self.handle, self.kappa, self.W, self.interval_phi,
                                                      self.interval_n, int(sweeps), r, _native.ptr(st),
                                                      _native.ptr(obs) if inline else None), 'sv_replicas_run')
-        for g, x in zip(rngs, r):
-            rng_to_numpy(x, g)
+        rngs_to_numpy(r, rngs, addrs)
         V = self.N * self.N
         st = st[:, :sweeps]
         stats = {'accepted': st['accepted'].copy(), 'acceptance': st['acceptance_sum'] / V,
@@ -115,12 +113,11 @@ def worldline_worms(m, v, kappa, W, rngs, worms=1, max_moves=0, device=None):
         raise ValueError(f'need {R} generators')
     W_eff = 2 * np.pi if v_float else float(W)
     ctx = _native.context(_native.default_device() if device is None else device)
-    r = (SvRng * R)(*[rng_from_numpy(g) for g in rngs])
+    r, addrs = rngs_from_numpy(rngs)
     hist = np.zeros((R, N, N), dtype=np.int64)
     lengths = np.zeros((R, max(worms, 1)), dtype=np.int64)
     ctx.check(_native.lib().sv_worldline_worm_batch(ctx.handle, R, N, float(kappa), W_eff, _native.ptr(m), _native.ptr(v),
                                                     int(v_float), int(worms), int(max_moves), r, _native.ptr(hist),
                                                     _native.ptr(lengths)), 'sv_worldline_worm_batch')
-    for g, x in zip(rngs, r):
-        rng_to_numpy(x, g)
+    rngs_to_numpy(r, rngs, addrs)
     return hist, lengths[:, :worms]

@@ -146,3 +146,23 @@ def test_worm_wrong_action_raises():
         __import__('supervillain_amd.generator.villain', fromlist=['Worm']).Worm(sv.Worldline(sv.Lattice2D(4), 0.5, 1))
     with pytest.raises(ValueError):
         __import__('supervillain_amd.generator.worldline', fromlist=['Worm']).Worm(sv.Villain(sv.Lattice2D(4), 0.5, 1))
+
+
+def test_rng_batch_roundtrip():
+    """sv_rng_gather / sv_rng_scatter (host-only C-ABI) read and write NumPy's PCG64 states exactly like the
+    public state dict, including the half-word buffer."""
+    from supervillain_amd._abi import rng_from_numpy, rngs_from_numpy, rngs_to_numpy
+    gens = [np.random.default_rng(s) for s in range(37)]
+    for i, g in enumerate(gens):
+        g.integers(0, 3, i % 5)  # odd counts leave a buffered half-word
+    arr, addrs = rngs_from_numpy(gens)
+    assert addrs is not None
+    for x, g in zip(arr, gens):
+        y = rng_from_numpy(g)
+        assert (x.state_hi, x.state_lo, x.inc_hi, x.inc_lo, x.has_uint32, x.uinteger) == \
+               (y.state_hi, y.state_lo, y.inc_hi, y.inc_lo, y.has_uint32, y.uinteger)
+    twins = [np.random.default_rng(99) for _ in gens]
+    rngs_to_numpy(arr, twins, rngs_from_numpy(twins)[1])
+    for a, b in zip(gens, twins):
+        assert a.bit_generator.state == b.bit_generator.state
+        assert (a.integers(0, 7, 9) == b.integers(0, 7, 9)).all()
