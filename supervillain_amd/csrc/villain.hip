@@ -1141,7 +1141,11 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     const int TH = fused_th();
     const int nsy = (N + TH - 1) / TH;
     const int grid = nsx * nsy;
-    const int BATCH = 64;
+    static const int BATCH = [] {  // sweeps per host round trip (SV_BATCH overrides; 64 measured best)
+        const char *e = getenv("SV_BATCH");
+        const int v = e ? atoi(e) : 64;
+        return v >= 1 ? v : 64;
+    }();
     // row-base advance maps for NW rows: NW*N metropolis draws, NW*N/2 ranks, NW*N/4 words
     if ((int64_t)NWv * N % 4) throw std::invalid_argument("fused path needs NW*N divisible by 4");
     const Affine adv[3] = {host_power(inc, (uint64_t)NWv * N), host_power(inc, (uint64_t)NWv * N / 2),
