@@ -107,6 +107,14 @@ __global__ __launch_bounds__(64) void villain_worm(WormArgs A) {
         const bool tally = hist && w == A.worms - 1;
         int64_t len = 0;
         for (;;) {
+            // every candidate move's operands are loaded before the draws, so the memory round trip
+            // overlaps the RNG arithmetic (the walk is latency-bound): phi on the plaquette's corners and
+            // n on its four sides
+            const int32_t tp = wrapi(ht + 1, N), xp = wrapi(hx + 1, N);
+            const int64_t s00 = (int64_t)ht * N + hx, s10 = (int64_t)tp * N + hx, s01 = (int64_t)ht * N + xp;
+            const int64_t s11 = (int64_t)tp * N + xp;
+            const double p00 = phi[s00], p10 = phi[s10], p01 = phi[s01], p11 = phi[s11];
+            const int64_t nE = n[s00], nN = n[V + s10], nWe = n[s01], nS = n[V + s00];
             if ((ht == tt && hx == tx) || A.w_is_one)                     // :143
                 if (g.uniform01() >= 0.8) break;
             if (len >= A.max_moves) {
@@ -116,17 +124,19 @@ __global__ __launch_bounds__(64) void villain_worm(WormArgs A) {
             const uint32_t c = g.bounded_pow2(4);                         // :148
             // neighbouring plaquette and crossed link (two_dimensional.py:255-300):
             // east (t, x-1) via (0, t, x); north (t+1, x) via (1, t+1, x); west (t, x+1) via (0, t, x+1);
-            // south (t-1, x) via (1, t, x)
-            int32_t nt = ht, nx = hx, lt = ht, lx = hx, lmu = c & 1;
-            if (c == 0) nx = wrapi(hx - 1, N);
-            else if (c == 1) nt = lt = wrapi(ht + 1, N);
-            else if (c == 2) nx = lx = wrapi(hx + 1, N);
-            else nt = wrapi(ht - 1, N);
-            const int64_t ls = (int64_t)lt * N + lx;
-            const int64_t fs = lmu == 0 ? (int64_t)wrapi(lt + 1, N) * N + lx : (int64_t)lt * N + wrapi(lx + 1, N);
-            const int64_t l = lmu * V + ls;
-            const double dphi = 0.0 + (phi[fs] - phi[ls]);                // d(phi), worm.py:104
-            const int64_t nl = n[l];
+            // south (t-1, x) via (1, t, x); d(phi) on link (mu, s) = 0 + (phi[s + e_mu] - phi[s]) (worm.py:104)
+            int32_t nt = ht, nx = hx;
+            int64_t l, nl;
+            double dphi;
+            if (c == 0) {
+                nx = wrapi(hx - 1, N), l = s00, nl = nE, dphi = 0.0 + (p10 - p00);
+            } else if (c == 1) {
+                nt = tp, l = V + s10, nl = nN, dphi = 0.0 + (p11 - p10);
+            } else if (c == 2) {
+                nx = xp, l = s01, nl = nWe, dphi = 0.0 + (p11 - p01);
+            } else {
+                nt = wrapi(ht - 1, N), l = V + s00, nl = nS, dphi = 0.0 + (p01 - p00);
+            }
             const double change_link = dphi - TWO_PI * (double)nl;         // :157
             const int64_t dn = (c < 2) ? orientation : -orientation;      // change_n[choice]
             const double dS = (half_kappa * ((-TWO_PI) * (double)dn)) * (2 * change_link - TWO_PI * (double)dn);
@@ -147,17 +157,16 @@ __global__ __launch_bounds__(64) void villain_worm(WormArgs A) {
     A.rng[r].buf = g.buf;
 }
 
-// delta(v)/W on link (k, s), reference.py:27-45 with ('delta',2) rows (0,0,1,-1),(1,0,0,+1):
+// delta(v)/W on link (k, s) from v[s] and v[b], reference.py:27-45 with ('delta',2) rows (0,0,1,-1),(1,0,0,+1):
 // k=0: (0 - (-(v[s] - v[s-e1]))) / W;  k=1: (0 - (v[s] - v[s-e0])) / W  (worldline/worm.py:164)
-__device__ __forceinline__ double dv_by_W(const void *v, int v_is_float, int64_t s, int64_t b, int k, double Weff) {
+// (raw 64-bit loads: int64, or float64 when v_is_float)
+__device__ __forceinline__ double dv_by_W_vals(uint64_t vs, uint64_t vb, int v_is_float, int k, double Weff) {
     double d;
     if (v_is_float) {
-        const double *vf = (const double *)v;
-        const double a = vf[s] - vf[b];
+        const double a = __longlong_as_double((long long)vs) - __longlong_as_double((long long)vb);
         d = k == 0 ? 0.0 - (-a) : 0.0 - a;
     } else {
-        const int64_t *vi = (const int64_t *)v;
-        const int64_t a = vi[s] - vi[b];
+        const int64_t a = (int64_t)vs - (int64_t)vb;
         d = (double)(k == 0 ? 0 - (-a) : 0 - a);
     }
     return d / Weff;
@@ -184,6 +193,14 @@ __global__ __launch_bounds__(64) void worldline_worm(WormArgs A) {
         const bool tally = hist && w == A.worms - 1;
         int64_t len = 0;
         for (;;) {
+            // operands of all four candidate moves first (latency overlaps the draws): m on the four links
+            // at and behind the head, v on the four sites their delta(v) reads
+            const int32_t tm = wrapi(ht - 1, N), xm = wrapi(hx - 1, N);
+            const int64_t s00 = (int64_t)ht * N + hx, s0m = (int64_t)ht * N + xm, sm0 = (int64_t)tm * N + hx;
+            const int64_t smm = (int64_t)tm * N + xm;
+            const int64_t m0f = m[s00], m1f = m[V + s00], m0b = m[sm0], m1b = m[V + s0m];
+            const uint64_t *vr = (const uint64_t *)v;
+            const uint64_t v00 = vr[s00], v0m = vr[s0m], vm0 = vr[sm0], vmm = vr[smm];
             if (ht == tt && hx == tx)                                     // :49-50
                 if (g.uniform01() < 1.0 / 5) break;
             if (len >= A.max_moves) {
@@ -193,15 +210,21 @@ __global__ __launch_bounds__(64) void worldline_worm(WormArgs A) {
             const uint32_t c = g.bounded_pow2(4);                         // :53
             const int k = c & 1;
             const bool forward = c < 2;
+            // +e0 crosses (0, head), +e1 (1, head), -e0 (0, head - e0), -e1 (1, head - e1) (:70-73);
+            // delta(v)/W on (k, s) reads v[s] and v[s - e1] (k = 0) or v[s - e0] (k = 1)
             int32_t nt = ht, nx = hx;
-            if (k == 0) nt = wrapi(ht + (forward ? 1 : -1), N);
-            else nx = wrapi(hx + (forward ? 1 : -1), N);
-            const int32_t at = forward ? ht : nt, ax = forward ? hx : nx;  // :70-73
-            const int64_t s = (int64_t)at * N + ax;
-            const int64_t b = k == 0 ? (int64_t)at * N + wrapi(ax - 1, N) : (int64_t)wrapi(at - 1, N) * N + ax;
-            const int64_t l = k * V + s;
-            const int64_t ml = m[l];
-            const double change_link = (double)ml - dv_by_W(v, A.v_is_float, s, b, k, A.Weff);  // :76
+            int64_t l, ml;
+            uint64_t va, vb;
+            if (c == 0) {
+                nt = wrapi(ht + 1, N), l = s00, ml = m0f, va = v00, vb = v0m;
+            } else if (c == 1) {
+                nx = wrapi(hx + 1, N), l = V + s00, ml = m1f, va = v00, vb = vm0;
+            } else if (c == 2) {
+                nt = tm, l = sm0, ml = m0b, va = vm0, vb = vmm;
+            } else {
+                nx = xm, l = V + s0m, ml = m1b, va = v0m, vb = vmm;
+            }
+            const double change_link = (double)ml - dv_by_W_vals(va, vb, A.v_is_float, k, A.Weff);  // :76
             const int64_t dm = forward ? orientation : -orientation;      // change_m[choice]
             const double dS = (inv2k * (double)dm) * (2.0 * change_link + (double)dm);
             double Ap = exp(-dS);                                         // :83
