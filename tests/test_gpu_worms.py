@@ -118,3 +118,31 @@ def test_hammer_ensemble_golden():
         assert (arr(getattr(E, 'Vortex_Vortex' if villain else 'Spin_Spin')) == c['hist']).all(), c['action']
         assert (arr(E.Worm_Length) == c['lengths']).all(), c['action']
         assert H.report() == c['report']
+
+
+@pytest.mark.parametrize('N', [2, 3])
+def test_tiny_lattices(oracle_lib, N):
+    """N = 2, 3 (every neighbour wraps; FFT coordinates fold onto themselves) for both worms, W = 1 and 2."""
+    for W in (1, 2):
+        R = 5
+        B = VillainReplicas(R, N, 0.8, W)
+        phi = np.random.default_rng(N).uniform(-np.pi, np.pi, (R, N, N))
+        n = np.zeros((R, 2, N, N), dtype=np.int64)
+        B.upload(phi, n)
+        rngs = [np.random.default_rng(50 + r) for r in range(R)]
+        hist, lengths = B.worm(rngs, worms=6)
+        _, n1 = B.download()
+        for r in range(R):
+            g = np.random.default_rng(50 + r)
+            nr = n[r].copy()
+            h, l = oracle_lib.villain_worm(N, 0.8, W, phi[r], nr, 6, g)
+            assert (nr == n1[r]).all() and (h == hist[r]).all() and (l == lengths[r]).all()
+        B.close()
+        m = np.zeros((R, 2, N, N), dtype=np.int64)
+        v = (W * np.random.default_rng(N + 1).integers(-1, 2, (R, N, N))).astype(np.int64)
+        rngs = [np.random.default_rng(70 + r) for r in range(R)]
+        hist, lengths = worldline_worms(m, v, 0.8, W, rngs, worms=6)
+        for r in range(R):
+            mr = np.zeros((2, N, N), dtype=np.int64)
+            h, l = oracle_lib.worldline_worm(N, 0.8, float(W), mr, v[r], 6, np.random.default_rng(70 + r))
+            assert (mr == m[r]).all() and (h == hist[r]).all() and (l == lengths[r]).all()
