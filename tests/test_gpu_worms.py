@@ -122,22 +122,25 @@ def test_hammer_ensemble_golden():
 
 @pytest.mark.parametrize('N', [2, 3])
 def test_tiny_lattices(oracle_lib, N):
-    """N = 2, 3 (every neighbour wraps; FFT coordinates fold onto themselves) for both worms, W = 1 and 2."""
+    """N = 2, 3 (every neighbour wraps; FFT coordinates fold onto themselves) for both worms, W = 1 and 2.
+    (Replica batches of the Villain sweep need an even N >= 4, so the Villain worm runs as the generator.)"""
     for W in (1, 2):
-        R = 5
-        B = VillainReplicas(R, N, 0.8, W)
-        phi = np.random.default_rng(N).uniform(-np.pi, np.pi, (R, N, N))
-        n = np.zeros((R, 2, N, N), dtype=np.int64)
-        B.upload(phi, n)
-        rngs = [np.random.default_rng(50 + r) for r in range(R)]
-        hist, lengths = B.worm(rngs, worms=6)
-        _, n1 = B.download()
-        for r in range(R):
+        L = sv.Lattice2D(N)
+        S = sv.Villain(L, 0.8, W)
+        for r in range(3):
+            phi = np.random.default_rng(N + r).uniform(-np.pi, np.pi, (1, N, N))
+            G = gv.Worm(S)
+            G.rng = np.random.default_rng(50 + r)
+            cfg = {'phi': sv.Form(phi, degree=0, lattice=L), 'n': sv.Form(np.zeros((2, N, N), dtype=np.int64), degree=1,
+                                                                          lattice=L)}
             g = np.random.default_rng(50 + r)
-            nr = n[r].copy()
-            h, l = oracle_lib.villain_worm(N, 0.8, W, phi[r], nr, 6, g)
-            assert (nr == n1[r]).all() and (h == hist[r]).all() and (l == lengths[r]).all()
-        B.close()
+            n = np.zeros((2, N, N), dtype=np.int64)
+            for _ in range(6):
+                cfg = G.step(cfg)
+                h, l = oracle_lib.villain_worm(N, 0.8, W, phi[0], n, 1, g)
+                assert (np.asarray(cfg['n']) == n).all() and (np.asarray(cfg['Vortex_Vortex']) == h).all()
+                assert cfg['Worm_Length'] == l[0]
+        R = 5
         m = np.zeros((R, 2, N, N), dtype=np.int64)
         v = (W * np.random.default_rng(N + 1).integers(-1, 2, (R, N, N))).astype(np.int64)
         rngs = [np.random.default_rng(70 + r) for r in range(R)]
