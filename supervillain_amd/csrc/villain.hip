@@ -1261,6 +1261,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             return false;
         }
         const int bad = absorb_reports(a, sw, skips);
+        if (dbg) fprintf(stderr, "[sv] abort at sweep %d of %d\n", bad, count);
         // sweeps before `bad` in this batch are valid: keep them
         if (bad > 0) {
             Cursor c2 = cur;
