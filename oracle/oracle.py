@@ -41,6 +41,7 @@ def lib():
         L.sv_o_villain_cohomology.argtypes = [i32, f64, i64, vp, vp, i32, P(SvRng), vp]
         L.sv_o_worldline_vortex.argtypes = [i32, f64, f64, i64, vp, vp, i32, i32, P(SvRng), vp]
         L.sv_o_worldline_wrapping.argtypes = [i32, f64, f64, i64, vp, vp, i32, i32, P(SvRng), vp]
+        L.sv_o_villain_neighborhood_mt.argtypes = [i32, f64, i64, f64, i64, vp, vp, i32, P(SvRng), vp, i32]
         L.sv_o_villain_worm.argtypes = [i32, f64, i64, vp, vp, i32, P(SvRng), vp, vp]
         L.sv_o_worldline_worm.argtypes = [i32, f64, f64, vp, vp, i32, i32, P(SvRng), vp, vp]
         _LIB = L
@@ -226,3 +227,16 @@ def worldline_worm(N, kappa, W_eff, m, v, worms, gen):
         raise ValueError('oracle rejected the arguments')
     rng_to_numpy(r, gen)
     return hist, lengths[:worms]
+
+
+def villain_neighborhood_mt(N, kappa, W, phi, n, sweeps, gen, threads, interval_phi=np.pi, interval_n=1):
+    """villain_neighborhood with the draws and the per-site work split over `threads` OpenMP threads (bench.py's
+    multi-core CPU baseline); the same chain as the sequential restatement."""
+    assert phi.dtype == np.float64 and n.dtype == np.int64 and phi.flags.c_contiguous and n.flags.c_contiguous
+    r = rng_from_numpy(gen)
+    st = _stats_array(sweeps)
+    if lib().sv_o_villain_neighborhood_mt(N, kappa, W, interval_phi, interval_n, _ptr(phi), _ptr(n), sweeps,
+                                          ctypes.byref(r), st, int(threads)):
+        raise ValueError('oracle rejected the arguments')
+    rng_to_numpy(r, gen)
+    return [st[i] for i in range(sweeps)]

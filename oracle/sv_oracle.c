@@ -26,6 +26,9 @@
  * Build: oracle/Makefile (gcc -O2 -ffp-contract=off, no fast-math: the op order IS the spec).
  */
 #include <math.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -1057,5 +1060,170 @@ int sv_o_worldline_worm(int32_t N_, double kappa, double Weff, int64_t *m, const
     if (hist) memcpy(hist, h, sizeof(int64_t) * V);
     pcg_store(&g, rng);
     free(dvw), free(h);
+    return 0;
+}
+
+/* ---------------------------------------------------------------- multi-core CPU baseline */
+/* The same NeighborhoodUpdate chain with the sweep's draws generated in parallel by jumping the PCG64
+ * stream (s_p = A^p s_0 + C_p, square-and-multiply) and the per-site arithmetic split over OpenMP
+ * threads.  Used only as bench.py's multi-core CPU baseline ("run once on all cores and
+ * once on 1 core"); tests check it equals the sequential restatement above.  Parallel sweeps need an even
+ * N and no buffered half-word at the sweep start (the draws then fall on whole u64s: 4V per sweep); any
+ * NumPy Lemire rejection met in a sweep makes that sweep rerun sequentially. */
+static void pcg_jump(u128 *s, u128 inc, uint64_t steps) {
+    u128 A = 1, C = 0, M = PCG_MULT, Ci = inc;
+    while (steps) {
+        if (steps & 1) {
+            A = A * M;
+            C = C * M + Ci;
+        }
+        Ci = Ci * (M + 1);
+        M = M * M;
+        steps >>= 1;
+    }
+    *s = A * *s + C;
+}
+
+static inline uint64_t xslrr(u128 s) {
+    uint64_t x = (uint64_t)(s >> 64) ^ (uint64_t)s;
+    unsigned rot = (unsigned)(s >> 122);
+    return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+
+int sv_o_villain_neighborhood_mt(int32_t N_, double kappa, int64_t W, double interval_phi, int64_t interval_n,
+                                 double *phi, int64_t *n, int32_t sweeps, sv_rng *rng, sv_stats *stats,
+                                 int32_t threads) {
+    const int64_t N = N_, V = N * N;
+    if (N < 2 || sweeps < 0 || threads < 1) return -1;
+    colors_t C = colors_make(N);
+    double *work = (double *)malloc(sizeof(double) * 6 * V + sizeof(int64_t) * 3 * V);
+    uint64_t *raw = (uint64_t *)malloc(sizeof(uint64_t) * 4 * V);
+    double *r = (double *)malloc(sizeof(double) * 2 * V), *cphi = (double *)malloc(sizeof(double) * V);
+    double *dSl = (double *)malloc(sizeof(double) * 2 * V);
+    int64_t *cn = (int64_t *)malloc(sizeof(int64_t) * 2 * V);
+    unsigned char *acc = (unsigned char *)malloc(V);
+    const uint32_t k = (uint32_t)(2 * interval_n + 1), thr = (uint32_t)((0u - k) % k);
+    const double half_kappa = kappa / 2.0, range_phi = interval_phi - (-interval_phi);
+    pcg g = pcg_load(rng);
+    for (int32_t sw = 0; sw < sweeps; sw++) {
+        sv_stats *st = &stats[sw];
+        if ((N % 2) || g.has || C.ncol != 2 || k < 2) { /* general case: the sequential sweep */
+            villain_sweep(N, N, kappa, W, interval_phi, interval_n, phi, n, &g, &C, st, work);
+            continue;
+        }
+        /* 1. the sweep's 4V raw outputs, chunked over threads by stream position */
+        int rejected = 0;
+#pragma omp parallel num_threads(threads)
+        {
+            int T = 1, t = 0;
+#ifdef _OPENMP
+            T = omp_get_num_threads(), t = omp_get_thread_num();
+#endif
+            const int64_t total = 4 * V, a = total * t / T, b = total * (t + 1) / T;
+            u128 s = g.s;
+            pcg_jump(&s, g.inc, (uint64_t)a);
+            for (int64_t p = a; p < b; p++) {
+                s = s * PCG_MULT + g.inc;
+                raw[p] = xslrr(s);
+            }
+        }
+        /* positions: metro [0, V); colour c at o_c = V + c 3V/2: dphi [o_c, o_c + V/2), choice blocks of V/4 u64 */
+        {
+#pragma omp parallel for num_threads(threads) reduction(| : rejected)
+            for (int64_t q = 0; q < 2 * V; q++) { /* the 2 x 4 blocks hold 2V uint32 draws in 8 runs of V/4 u64 */
+                const int c = (int)(q / V), j = (int)((q % V) / (V / 4));
+                const int64_t p = V + c * (3 * V / 2) + V / 2 + j * (V / 4) + (q % (V / 4));
+                const uint64_t x = raw[p];
+                const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+                if ((uint32_t)((uint64_t)lo * k) < thr || (uint32_t)((uint64_t)hi * k) < thr) rejected = 1;
+            }
+        }
+        if (rejected) { /* a Lemire rejection shifts its block: redo this sweep in order */
+            villain_sweep(N, N, kappa, W, interval_phi, interval_n, phi, n, &g, &C, st, work);
+            continue;
+        }
+        memset(st, 0, sizeof(*st));
+        /* 2. the sweep, neighborhood.py:87-135, elementwise loops in parallel */
+#pragma omp parallel for num_threads(threads)
+        for (int64_t s = 0; s < V; s++)
+            for (int mu = 0; mu < 2; mu++)
+                r[mu * V + s] = (0.0 + (phi[fwd(s, mu, N)] - phi[s])) - TWO_PI * (double)n[mu * V + s];
+        for (int c = 0; c < 2; c++) {
+            const int64_t nc = C.count[c], *sites = C.sites[c], o = V + c * (3 * V / 2);
+#pragma omp parallel for num_threads(threads)
+            for (int64_t s = 0; s < V; s++) {
+                cphi[s] = 0.0;
+                cn[s] = 0;
+                cn[V + s] = 0;
+            }
+#pragma omp parallel for num_threads(threads)
+            for (int64_t i = 0; i < nc; i++) {
+                const int64_t s = sites[i];
+                cphi[s] = -interval_phi + range_phi * ((double)(raw[o + i] >> 11) * (1.0 / 9007199254740992.0));
+                for (int mu = 0; mu < 2; mu++) {
+                    const uint64_t xf = raw[o + nc + (2 * mu) * (nc / 2) + i / 2];
+                    const uint64_t xb = raw[o + nc + (2 * mu + 1) * (nc / 2) + i / 2];
+                    const uint32_t uf = (i & 1) ? (uint32_t)(xf >> 32) : (uint32_t)xf;
+                    const uint32_t ub = (i & 1) ? (uint32_t)(xb >> 32) : (uint32_t)xb;
+                    cn[mu * V + s] = W * ((int64_t)(((uint64_t)uf * k) >> 32) - interval_n);
+                    cn[mu * V + bwd(s, mu, N)] = W * ((int64_t)(((uint64_t)ub * k) >> 32) - interval_n);
+                }
+            }
+#pragma omp parallel for num_threads(threads)
+            for (int64_t s = 0; s < V; s++)
+                for (int mu = 0; mu < 2; mu++) {
+                    const double cr = (0.0 + (cphi[fwd(s, mu, N)] - cphi[s])) - TWO_PI * (double)cn[mu * V + s];
+                    dSl[mu * V + s] = (half_kappa * cr) * ((2.0 * r[mu * V + s]) + cr);
+                }
+            int64_t accepted = 0;
+            double psum = 0.0;
+#pragma omp parallel for num_threads(threads) reduction(+ : accepted, psum)
+            for (int64_t i = 0; i < nc; i++) {
+                const int64_t s = sites[i];
+                double dS = 0.0;
+                dS += dSl[s];
+                dS += dSl[bwd(s, 0, N)];
+                dS += dSl[V + s];
+                dS += dSl[V + bwd(s, 1, N)];
+                double p = exp(-dS);
+                p = p < 0.0 ? 0.0 : p;
+                p = p > 1.0 ? 1.0 : p;
+                const double u = (double)(raw[s] >> 11) * (1.0 / 9007199254740992.0);
+                acc[s] = u < p;
+                accepted += acc[s];
+                psum += p;
+            }
+            st->accepted += accepted;
+            st->acceptance_sum += psum;
+#pragma omp parallel for num_threads(threads)
+            for (int64_t i = 0; i < nc; i++) {
+                const int64_t s = sites[i];
+                const int64_t a = acc[s];
+                cphi[s] = cphi[s] * (double)a;
+                for (int mu = 0; mu < 2; mu++) {
+                    cn[mu * V + s] *= a;
+                    cn[mu * V + bwd(s, mu, N)] *= a;
+                }
+            }
+#pragma omp parallel for num_threads(threads)
+            for (int64_t s = 0; s < V; s++) {
+                phi[s] = phi[s] + cphi[s];
+                n[s] = n[s] + cn[s];
+                n[V + s] = n[V + s] + cn[V + s];
+            }
+#pragma omp parallel for num_threads(threads)
+            for (int64_t s = 0; s < V; s++)
+                for (int mu = 0; mu < 2; mu++) {
+                    const double dcp = 0.0 + (cphi[fwd(s, mu, N)] - cphi[s]);
+                    r[mu * V + s] = (r[mu * V + s] + dcp) - TWO_PI * (double)cn[mu * V + s];
+                }
+        }
+        st->proposed = V;
+        pcg_jump(&g.s, g.inc, (uint64_t)(4 * V)); /* whole words only: the buffer stays empty, */
+        g.buf = (uint32_t)(raw[4 * V - 1] >> 32);  /* holding (stale) the last word's high half, as NumPy's does */
+    }
+    pcg_store(&g, rng);
+    free(work), free(raw), free(r), free(cphi), free(dSl), free(cn), free(acc);
+    colors_free(&C);
     return 0;
 }

@@ -160,3 +160,27 @@ def test_worms_golden(oracle_lib):
             assert lengths[0] == c['lengths'][k] == hist.sum()
         assert ((n if c['action'] == 'villain' else m) == (c['n'] if c['action'] == 'villain' else c['m'])).all()
         assert (state_of(g) == c['rng1']).all()
+
+
+def test_multicore_oracle_matches(oracle_lib):
+    """The OpenMP restatement (bench.py's multi-core CPU baseline) is the same chain: the reference's golden
+    rejection fixtures (forced NumPy Lemire rejections -> the sequential fallback) and plain seeded chains."""
+    O = oracle_lib
+    checked = 0
+    for c in cases('villain_rejections.npz'):
+        if c['N'] % 2:
+            continue
+        checked += 1
+        phi, n = c['phi0'].copy(), c['n0'].copy()
+        g = generator_from(c['rng0'])
+        O.villain_neighborhood_mt(c['N'], c['kappa'], c['W'], phi, n, c['sweeps'], g, 4,
+                                  interval_phi=c['interval_phi'], interval_n=c['interval_n'])
+        assert (phi == c['phi']).all() and (n == c['n']).all() and (state_of(g) == c['rng1']).all()
+    assert checked >= 4
+    for N, W in [(32, 1), (20, 2)]:
+        a = [np.zeros((N, N)), np.zeros((2, N, N), dtype=np.int64), np.random.default_rng(N)]
+        b = [np.zeros((N, N)), np.zeros((2, N, N), dtype=np.int64), np.random.default_rng(N)]
+        O.villain_neighborhood(N, 0.4, W, a[0], a[1], 5, a[2])
+        O.villain_neighborhood_mt(N, 0.4, W, b[0], b[1], 5, b[2], 3)
+        assert (a[0] == b[0]).all() and (a[1] == b[1]).all()
+        assert a[2].bit_generator.state == b[2].bit_generator.state
