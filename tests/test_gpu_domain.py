@@ -91,10 +91,14 @@ def test_golden(fixture):
     assert ran > 0
 
 
+@pytest.mark.parametrize('batch', ['', '1', '2'])
 @pytest.mark.parametrize('tiles', [(2, 2), (1, 8), (4, 4), (2, 4)])
-def test_forced_rejections(tiles, oracle_lib):
+def test_forced_rejections(tiles, batch, oracle_lib, monkeypatch):
     """Rejections placed in different blocks (and so in different tiles); the abort must reach every
-    tile before its ring buffer is overwritten."""
+    tile before its ring buffer is overwritten.  batch: SV_DOMAIN_BATCH (the adaptive batch of a large
+    lattice is a few sweeps: aborts then land on batch boundaries)."""
+    if batch:
+        monkeypatch.setenv('SV_DOMAIN_BATCH', batch)
     N = 128
     V = N * N
     for pos, half in [(V + V // 2 + 7, 0), (V + V // 2 + V // 4 + 3, 1), (4 * V - 1, 1), (4 * V + V + V // 2 + 11, 0),
@@ -145,9 +149,12 @@ def test_equals_single_lattice_at_scale(tiles):
     assert sum(s.accepted for s in st) == G.accepted
 
 
-def test_natural_rejections_bench_size():
+@pytest.mark.parametrize('batch', ['', '5'])
+def test_natural_rejections_bench_size(batch, monkeypatch):
     """L=4096 in 2 x 4 tiles for 96 sweeps: NumPy rejects ~1.6% of sweeps' draws somewhere, so the
-    abort / replay protocol runs on real data; the chain equals the single-lattice one."""
+    abort / replay protocol runs on real data; the chain equals the single-lattice one.  batch: as above."""
+    if batch:
+        monkeypatch.setenv('SV_DOMAIN_BATCH', batch)
     N = 4096
     phi0, n0 = np.zeros((N, N)), np.zeros((2, N, N), dtype=np.int64)
     gen = np.random.default_rng(2024)
