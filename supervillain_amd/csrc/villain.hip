@@ -288,17 +288,29 @@ struct Rep {
     uint32_t id;
 };
 
+template <bool K3 = false>
 __device__ __forceinline__ int32_t choice_value(const FArgs &A, const Rep &RP, uint32_t word, uint32_t bidx,
                                                 uint32_t spos) {
-    bool rej;
-    const uint32_t idx = lemire(word, A.P.k, A.P.thr, &rej);
-    if (rej) report(A.S, A.sweep, bidx, spos, RP.id);
-    return (int32_t)A.P.W * ((int32_t)idx - (int32_t)A.P.interval_n);
+    if constexpr (K3) {
+        // choice((-1, 0, 1)) (interval_n = 1): 3x by one shift-add, Lemire threshold (2^32 - 3) % 3 = 1 (a
+        // rejection iff the low word is 0), the value a select instead of W * (idx - 1)
+        const uint64_t m = ((uint64_t)word << 1) + word;
+        if ((uint32_t)m == 0u) report(A.S, A.sweep, bidx, spos, RP.id);
+        const uint32_t idx = (uint32_t)(m >> 32);
+        const int32_t w = (int32_t)A.P.W;
+        return idx == 0 ? -w : (idx == 1 ? 0 : w);
+    } else {
+        bool rej;
+        const uint32_t idx = lemire(word, A.P.k, A.P.thr, &rej);
+        if (rej) report(A.S, A.sweep, bidx, spos, RP.id);
+        return (int32_t)A.P.W * ((int32_t)idx - (int32_t)A.P.interval_n);
+    }
 }
 
 // General draws: any strip (wrapped columns), skips, mismatched buffers.  6 compositions per site.
 // Columns of an edge strip that wrap around the lattice (global columns outside [xb, xb + RW)) draw
 // from the wave's second set of row bases `wb`, kept at global column xw, so no lane needs a full jump.
+template <bool K3 = false>
 __device__ __forceinline__ Draws draws_general(const FArgs &A, const Rep &RP, int c, bool active, int64_t gq, int64_t gx,
                                                int64_t xb, const u128 *bases, const Affine *sm, bool edge,
                                                int64_t xw, const u128 *wb) {
@@ -332,7 +344,7 @@ __device__ __forceinline__ Draws draws_general(const FArgs &A, const Rep &RP, in
                 word = bounded_word(T, *B, spos);
                 __builtin_amdgcn_s_waitcnt(0);
             }
-            D.cn[q] = choice_value(A, RP, word, (uint32_t)(bb + 1 + q), spos);
+            D.cn[q] = choice_value<K3>(A, RP, word, (uint32_t)(bb + 1 + q), spos);
         }
     }
     return D;
@@ -368,6 +380,9 @@ __device__ __forceinline__ uint32_t fast_pack(const uint32_t *hasw, int32_t lane
 
 // The row bases are the same for every lane of a wave (one row per wave): held in SGPRs they feed the
 // 128-bit multiplies as scalar operands instead of occupying VGPRs.
+#ifndef SV_K3
+#define SV_K3 0  // choice((-1, 0, 1)) specialised at compile time: measured slower (329.5 vs 320.5 us, r92)
+#endif
 #ifndef SV_FR_FAST
 #define SV_FR_FAST 1
 #endif
@@ -387,6 +402,7 @@ __device__ __forceinline__ u128 wave_uniform(u128 v) {
 #endif
 }
 
+template <bool K3 = false>
 __device__ __forceinline__ Draws draws_fastp(const FArgs &A, const Rep &RP, int c, bool active, int32_t lane,
                                              uint32_t pk, uint32_t rank, const u128 *bases, const Affine *sm) {
     const int bb = 1 + 5 * c;
@@ -413,14 +429,15 @@ __device__ __forceinline__ Draws draws_fastp(const FArgs &A, const Rep &RP, int 
             const uint32_t wf = half ? got : (uint32_t)X;
             const uint32_t wb = half ? (uint32_t)(X >> 32) : got;
             if (active) {
-                D.cn[2 * mu] = choice_value(A, RP, wf, (uint32_t)(bb + 1 + 2 * mu), rank);
-                D.cn[2 * mu + 1] = choice_value(A, RP, wb, (uint32_t)(bb + 2 + 2 * mu), rank);
+                D.cn[2 * mu] = choice_value<K3>(A, RP, wf, (uint32_t)(bb + 1 + 2 * mu), rank);
+                D.cn[2 * mu + 1] = choice_value<K3>(A, RP, wb, (uint32_t)(bb + 2 + 2 * mu), rank);
             }
         }
     }
     return D;
 }
 
+template <bool K3 = false>
 __device__ __forceinline__ Draws draws_fast(const FArgs &A, const Rep &RP, int c, const uint32_t *hasw, bool active,
                                             int32_t lane, uint32_t rowlin,
                                             uint32_t xs, uint32_t gx, uint32_t xb, const u128 *bases,
@@ -458,8 +475,8 @@ __device__ __forceinline__ Draws draws_fast(const FArgs &A, const Rep &RP, int c
             const uint32_t wf = half ? got : (uint32_t)X;
             const uint32_t wb = half ? (uint32_t)(X >> 32) : got;
             if (active) {
-                D.cn[2 * mu] = choice_value(A, RP, wf, (uint32_t)(bb + 1 + 2 * mu), rank);
-                D.cn[2 * mu + 1] = choice_value(A, RP, wb, (uint32_t)(bb + 2 + 2 * mu), rank);
+                D.cn[2 * mu] = choice_value<K3>(A, RP, wf, (uint32_t)(bb + 1 + 2 * mu), rank);
+                D.cn[2 * mu + 1] = choice_value<K3>(A, RP, wb, (uint32_t)(bb + 2 + 2 * mu), rank);
             }
         }
     }
@@ -468,7 +485,7 @@ __device__ __forceinline__ Draws draws_fast(const FArgs &A, const Rep &RP, int c
 
 // FR (full rows, periodic lattices of Nx <= 128): one strip spans the whole row, its LDS columns ARE
 // the lattice columns and neighbours wrap inside LDS -- no column halo, every lane busy at N = 128.
-template <int NW, bool TILE, bool REPS, bool OBS, bool FR>
+template <int NW, bool TILE, bool REPS, bool OBS, bool FR, bool K3 = false>
 __device__ __forceinline__ void sweep_body(const FArgs &A) {
     static_assert(!(FR && TILE), "full-row strips are for periodic lattices");
     constexpr int R = FusedGeom<NW>::R;
@@ -718,13 +735,13 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             for (int k = 0; k < 6; k++) bs[k] = wave_uniform(s_base[wave][k]);
             Draws D;
             if (fast[0])
-                D = draws_fastp(A, RL, 0, active, lane, pk0, ((uint32_t)gq * (uint32_t)Nx + (uint32_t)(Gm.X0 + x)) >> 1,
+                D = draws_fastp<K3>(A, RL, 0, active, lane, pk0, ((uint32_t)gq * (uint32_t)Nx + (uint32_t)(Gm.X0 + x)) >> 1,
                                 bs, s_small);
             else if (fastfr[0])
-                D = draws_fast(A, RL, 0, has_c0, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)xs, (uint32_t)x, 0u,
+                D = draws_fast<K3>(A, RL, 0, has_c0, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)xs, (uint32_t)x, 0u,
                                bs, s_small);
             else
-                D = draws_general(A, RL, 0, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small, edge, xw,
+                D = draws_general<K3>(A, RL, 0, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small, edge, xw,
                                   &s_base[wave][16]);
             if (active) {
                 const int lr = q - rbase;
@@ -793,13 +810,13 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             for (int k = 0; k < 6; k++) bs[k] = wave_uniform(s_base[wave][8 + k]);
             Draws D;
             if (fast[1])
-                D = draws_fastp(A, RL, 1, active, lane, pk1, ((uint32_t)gq * (uint32_t)Nx + (uint32_t)(Gm.X0 + x)) >> 1,
+                D = draws_fastp<K3>(A, RL, 1, active, lane, pk1, ((uint32_t)gq * (uint32_t)Nx + (uint32_t)(Gm.X0 + x)) >> 1,
                                 bs, s_small);
             else if (fastfr[1])
-                D = draws_fast(A, RL, 1, has_c1, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)xs, (uint32_t)x, 0u,
+                D = draws_fast<K3>(A, RL, 1, has_c1, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)xs, (uint32_t)x, 0u,
                                bs, s_small);
             else
-                D = draws_general(A, RL, 1, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small, edge, xw,
+                D = draws_general<K3>(A, RL, 1, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small, edge, xw,
                                   &s_base[wave][24]);
             if (active) {
                 const int lr = q - rbase;
@@ -873,9 +890,9 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
 }
 
 // 3 waves / SIMD (12 per CU, what the LDS ring allows): caps the kernel at 168 VGPRs
-template <int NW, bool TILE, bool REPS, bool FR>
+template <int NW, bool TILE, bool REPS, bool FR, bool K3 = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(3))) void villain_sweep_fused(FArgs A) {
-    sweep_body<NW, TILE, REPS, false, FR>(A);
+    sweep_body<NW, TILE, REPS, false, FR, K3>(A);
 }
 // replica batch with the inline observables fused into the row stores: held to 3 waves / SIMD
 template <bool FR>
@@ -884,6 +901,9 @@ __global__ __launch_bounds__(4 * 64) __attribute__((amdgpu_waves_per_eu(3))) voi
 }
 
 template __global__ void villain_sweep_fused<4, false, false, false>(FArgs);
+#if SV_K3
+template __global__ void villain_sweep_fused<4, false, false, false, true>(FArgs);
+#endif
 template __global__ void villain_sweep_fused<6, false, false, false>(FArgs);
 template __global__ void villain_sweep_fused<4, true, false, false>(FArgs);
 template __global__ void villain_sweep_fused<4, false, true, false>(FArgs);
@@ -1194,6 +1214,9 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             A.sweep = (uint32_t)k;
             farg_single(A, nsx, nsy);
             if (NWv == 6) villain_sweep_fused<6, false, false, false><<<grid, 6 * 64, 0, ctx->stream>>>(A);
+#if SV_K3
+            else if (P.k == 3) villain_sweep_fused<4, false, false, false, true><<<grid, 4 * 64, 0, ctx->stream>>>(A);
+#endif
             else villain_sweep_fused<4, false, false, false><<<grid, 4 * 64, 0, ctx->stream>>>(A);
             if (per_launch) ctx->time_end(ev1, 1);
             st->cur ^= 1;
