@@ -519,7 +519,7 @@ def main():
         return
 
     from supervillain_amd import _native
-    from supervillain_amd._abi import SvRng, rng_from_numpy
+    from supervillain_amd._abi import rng_from_numpy
 
     Lib = _native.lib()
     ctx = _native.context(local)

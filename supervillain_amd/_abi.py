@@ -7,8 +7,6 @@ NumPy's bounded-integer sampler keeps in the bit generator (``has_uint32``/``uin
 """
 import ctypes
 
-import numpy as np
-
 _M64 = (1 << 64) - 1
 
 

@@ -13,6 +13,7 @@
 // global atomic on the lane's private histogram: no wait on its latency).  d(phi) and delta(v)/W are
 // formed on the fly in the reference's operator order, so no derived arrays are kept.
 #include <cstring>
+#include <mutex>
 
 #include "common.h"
 
@@ -251,8 +252,10 @@ struct WormScratch {
 };
 
 std::map<sv_ctx *, WormScratch> g_scratch;
+std::mutex g_scratch_mu;  // contexts live on different threads; the map is shared
 
 char *worm_scratch(sv_ctx *ctx, size_t bytes) {
+    std::lock_guard<std::mutex> lock(g_scratch_mu);
     WormScratch &w = g_scratch[ctx];
     if (bytes > w.cap) {
         SV_HIP(hipStreamSynchronize(ctx->stream));
@@ -328,6 +331,7 @@ WormArgs base_args(int32_t R, int32_t N, double kappa, int32_t worms, int64_t ma
 }  // namespace
 
 void worm_release(sv_ctx *ctx) {
+    std::lock_guard<std::mutex> lock(g_scratch_mu);
     auto it = g_scratch.find(ctx);
     if (it == g_scratch.end()) return;
     if (it->second.d) (void)hipFree(it->second.d);

@@ -12,7 +12,7 @@ import ctypes
 import numpy as np
 
 from supervillain_amd import _native
-from supervillain_amd._abi import SvRng, SvStats, rng_from_numpy, rng_to_numpy, rngs_from_numpy, rngs_to_numpy
+from supervillain_amd._abi import SvStats, rngs_from_numpy, rngs_to_numpy
 
 # numpy image of sv_stats (include/supervillain_amd.h)
 STATS_DTYPE = np.dtype([('accepted', '<i8'), ('proposed', '<i8'), ('acceptance_sum', '<f8'), ('rejections', '<i8')])
