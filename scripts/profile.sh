@@ -8,7 +8,7 @@ TAG=${1:-r01}
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT profiles
-B="python bench.py --steps 20 --warmup 2 --no-cpu-baseline"
+B="python bench.py --no-cpu-baseline"  # the default command (200 + 20 sweeps) without the CPU leg
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- $B > $OUT/trace.log 2>&1 || exit 3
 P="timeout -k 10 300 rocprofv3 --kernel-include-regex villain_sweep_fused"
 Bs="python bench.py --steps 4 --warmup 1 --no-cpu-baseline"

@@ -39,6 +39,12 @@ trace = [r for r in csv.DictReader(open(os.path.join(out, 'trace', 'run_kernel_t
 dur = [int(r['End_Timestamp']) - int(r['Start_Timestamp']) for r in trace]
 full = [x for x in dur if x > 0.1 * max(dur)]
 L = 4096
+# the profiled bench run's own JSON line: its live hipEvent average (measured under the tracer) is what the
+# trace's full-sweep average must agree with; the tracer slows the kernel itself by ~10% against untraced runs
+traced = None
+for line in open(os.path.join(out, 'trace.log')):
+    if line.startswith('{'):
+        traced = json.loads(line)
 summary = {
     f'villain_sweep_fused_L{L}': {
         'avg_duration_ns': float(fused['AverageNs']), 'calls': int(fused['Calls']),
@@ -49,6 +55,8 @@ summary = {
         'algorithmic_bytes_per_launch': 88 * L * L,          # SURVEY.md 8(d), what bench.py's roofline uses
         'fused_min_bytes_per_launch': 48 * L * L,            # one read + one write of (phi, n) per sweep
         'counters_per_dispatch': pmc,
+        'bench_avg_launch_us_same_run': traced['roofline']['avg_launch_us'] if traced else None,
+        'bench_ms_per_step_same_run': traced['ms_per_step'] if traced else None,
     }
 }
 json.dump(summary, open('profiles/pmc_summary.json', 'w'), indent=1)
