@@ -8,6 +8,17 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+def pytest_sessionstart(session):
+    """A fresh checkout has no built libsvhip.so (build artefacts stay out of git): build it once, in tree,
+    the way __graft_entry__.build() does, so the CPU suite's ABI tests can load it."""
+    import shutil
+    import subprocess
+    lib = os.path.join(ROOT, 'supervillain_amd', 'libsvhip.so')
+    if not os.path.exists(lib) and shutil.which('make') and os.path.exists('/opt/rocm/bin/hipcc'):
+        subprocess.run(['make', '-j', str(min(8, os.cpu_count() or 1)), '-C', os.path.join(ROOT, 'supervillain_amd', 'csrc')],
+                       check=False, capture_output=True)
+
+
 def pytest_configure(config):
     config.addinivalue_line('markers', 'gpu: needs an MI355X (run with -m gpu on the GPU box)')
     config.addinivalue_line('markers', 'slow: long-running CPU test')
