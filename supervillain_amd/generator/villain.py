@@ -13,6 +13,7 @@ from supervillain_amd import _native
 from supervillain_amd.batch import Batch
 from supervillain_amd.generator._common import DeviceState, rng_from_numpy, rng_to_numpy, wrap_like
 from supervillain_amd.generator.generator import Generator
+from supervillain_amd.replicas import WORM_MAX_MOVES
 
 
 def _is_villain(action):
@@ -369,11 +370,11 @@ class ClassicWorm(DeviceState, Generator):
     head and tail on plaquettes, the head crosses links changing n by ±1, and the displacement histogram of
     every move is the inline ``Vortex_Vortex`` measurement.  A worm is a sequential walk, so the device runs
     one chain per GPU lane (``sv_villain_worm_run``); batches of chains use
-    :meth:`supervillain_amd.replicas.VillainReplicas.worm`.  ``max_moves`` (0: unbounded) caps one worm.'''
+    :meth:`supervillain_amd.replicas.VillainReplicas.worm`.  ``max_moves`` (default 10^8; 0: unbounded) caps one worm.'''
 
     DEVICE_KIND = 'villain'
 
-    def __init__(self, S, *, device=None, max_moves=0):
+    def __init__(self, S, *, device=None, max_moves=WORM_MAX_MOVES):
         if not _is_villain(S):
             raise ValueError('Need a Villain action')
         if S.Lattice.D != 2:

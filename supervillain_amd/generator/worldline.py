@@ -13,6 +13,7 @@ import numpy as np
 from supervillain_amd import _native
 from supervillain_amd.generator._common import DeviceState, rng_from_numpy, rng_to_numpy, wrap_like
 from supervillain_amd.generator.generator import Generator
+from supervillain_amd.replicas import WORM_MAX_MOVES
 
 
 def _is_worldline(action):
@@ -312,11 +313,11 @@ class ClassicWorm(_WorldlineDevice, Generator):
     r'''The Prokof'ev-Svistunov worm on the worldline links (supervillain/generator/worldline/worm.py:97-193):
     head and tail on sites, the head crosses links changing m by ±1; the displacement histogram is the inline
     ``Spin_Spin`` measurement.  One chain per GPU lane (``sv_worldline_worm_run``); batches of chains use
-    :func:`supervillain_amd.replicas.worldline_worms`.  ``max_moves`` (0: unbounded) caps one worm.'''
+    :func:`supervillain_amd.replicas.worldline_worms`.  ``max_moves`` (default 10^8; 0: unbounded) caps one worm.'''
 
     DEVICE_KIND = 'worldline'
 
-    def __init__(self, S, *, device=None, max_moves=0):
+    def __init__(self, S, *, device=None, max_moves=WORM_MAX_MOVES):
         if not _is_worldline(S):
             raise ValueError('The classic worm algorithm update requires the Worldline action.')
         self.Action = S

@@ -14,6 +14,11 @@ import numpy as np
 from supervillain_amd import _native
 from supervillain_amd._abi import SvStats, rngs_from_numpy, rngs_to_numpy
 
+# Default bound on one worm's moves: a worm that never closes (a far-from-equilibrium start can make one) would
+# otherwise keep its GPU lane -- and the launch -- running indefinitely.  10^8 moves is ~100x a critical
+# L=4096 worm; exceeding it raises (pass max_moves=0 for no bound).
+WORM_MAX_MOVES = 100_000_000
+
 # numpy image of sv_stats (include/supervillain_amd.h)
 STATS_DTYPE = np.dtype([('accepted', '<i8'), ('proposed', '<i8'), ('acceptance_sum', '<f8'), ('rejections', '<i8')])
 assert STATS_DTYPE.itemsize == __import__('ctypes').sizeof(SvStats)
@@ -53,7 +58,7 @@ class VillainReplicas:
                        'sv_replicas_download')
         return phi, n
 
-    def worm(self, rngs, worms=1, max_moves=0):
+    def worm(self, rngs, worms=1, max_moves=WORM_MAX_MOVES):
         """`worms` ClassicWorm steps of every replica (supervillain/generator/villain/worm.py:85-183), one GPU
         lane per replica; rngs: R NumPy Generators, advanced in place.  Returns (Vortex_Vortex of each
         replica's last worm (R, N, N) int64, Worm_Length (R, worms) int64)."""
@@ -100,7 +105,7 @@ class VillainReplicas:
         }
 
 
-def worldline_worms(m, v, kappa, W, rngs, worms=1, max_moves=0, device=None):
+def worldline_worms(m, v, kappa, W, rngs, worms=1, max_moves=WORM_MAX_MOVES, device=None):
     """`worms` Worldline ClassicWorm steps (supervillain/generator/worldline/worm.py:137-193) of R independent
     chains, one GPU lane each: m (R, 2, N, N) int64 is updated in place, v (R, N, N) int64 (float64 at
     W = infinity) is read.  Returns (Spin_Spin of each chain's last worm (R, N, N), Worm_Length (R, worms))."""
