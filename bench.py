@@ -279,8 +279,7 @@ def run_worms(args, world, rank, dist):
                   'parallelism': f'{world} GPU(s), chains sharded, no collectives'}
         # bytes per move: n of the crossed link + the two phi of d(phi) on it (8 + 16), the conditional n store
         # and the histogram increment (8 + 8); a latency-bound walk, the roofline fraction is informational
-        out_moves = moves / max(args.steps, 1) * args.steps
-        report(args, world, out_moves / args.steps, out_moves / world, elapsed, 0.0, launch_s, config, L,
+        report(args, world, moves / args.steps, moves / world, elapsed, 0.0, launch_s, config, L,
                metric=f'worm moves/sec, {Rt} x L={L} Villain ClassicWorm chains, W={args.W}', unit='worm moves/s',
                kernel='villain_worm', alg_bytes=40, min_bytes=40, baseline=baseline)
     B.close()
