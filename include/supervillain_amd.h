@@ -203,6 +203,11 @@ int sv_replicas_upload(sv_replicas *b, const double *phi, const int64_t *n);
 int sv_replicas_download(sv_replicas *b, double *phi, int64_t *n);
 int sv_replicas_run(sv_replicas *b, double kappa, int64_t W, double interval_phi, int64_t interval_n, int32_t sweeps,
                     sv_rng *rngs, sv_stats *stats, double *obs);
+/* One-shot form over host arrays: phi (R, N, N) f64 and n (R, 2, N, N) int64 in/out, rngs[R] in/out,
+ * stats[R * sweeps], inline_out (R * sweeps * 4, may be NULL) as sv_replicas_run's obs. */
+int sv_replicas_villain(sv_ctx *ctx, int32_t R, int32_t N, double kappa, int64_t W, double interval_phi,
+                        int64_t interval_n, double *phi, int64_t *n, int32_t sweeps, sv_rng *rngs, sv_stats *stats,
+                        double *inline_out);
 
 /* ---- ClassicWorm ---------------------------------------------------------
  * `worms` consecutive worm steps of every chain, one GPU lane per chain (a worm is sequential).

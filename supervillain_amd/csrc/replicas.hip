@@ -449,4 +449,18 @@ int sv_replicas_worm_run(sv_replicas *b, double kappa, int64_t W, int32_t worms,
     }
 }
 
+// One-shot form over host arrays (SURVEY.md 8(b)'s sv_replicas_villain): create, upload, run, download.
+int sv_replicas_villain(sv_ctx *ctx, int32_t R, int32_t N, double kappa, int64_t W, double interval_phi,
+                        int64_t interval_n, double *phi, int64_t *n, int32_t sweeps, sv_rng *rngs, sv_stats *stats,
+                        double *inline_out) {
+    if (!ctx || !phi || !n || !rngs) return -1;
+    sv_replicas *b = nullptr;
+    int rc = sv_replicas_create(ctx, R, N, &b);
+    if (!rc) rc = sv_replicas_upload(b, phi, n);
+    if (!rc) rc = sv_replicas_run(b, kappa, W, interval_phi, interval_n, sweeps, rngs, stats, inline_out);
+    if (!rc) rc = sv_replicas_download(b, phi, n);
+    if (b) sv_replicas_destroy(b);
+    return rc;
+}
+
 }  // extern "C"

@@ -113,3 +113,29 @@ def test_config5_shape_against_single_chains():
         assert G.rng.bit_generator.state == gens[r].bit_generator.state
         assert G.accepted == stats['accepted'][r].sum()
         assert S.valid(cfg)
+
+
+def test_one_shot_entry_point(oracle_lib):
+    """sv_replicas_villain (SURVEY.md 8b's one-shot form over host arrays) == the oracle per replica."""
+    import ctypes
+    from supervillain_amd import _native
+    from supervillain_amd._abi import SvStats, rngs_from_numpy, rngs_to_numpy
+    R, N, W, sweeps = 5, 16, 2, 4
+    phi0, n0 = hot(R, N, W, 3)
+    phi, n = phi0.copy(), n0.copy()
+    gens = [np.random.default_rng(40 + r) for r in range(R)]
+    r, addrs = rngs_from_numpy(gens)
+    st = (SvStats * (R * sweeps))()
+    obs = np.zeros((R, sweeps, 4))
+    ctx = _native.context()
+    ctx.check(_native.lib().sv_replicas_villain(ctx.handle, R, N, 0.4, W, float(np.pi), 1, _native.ptr(phi), _native.ptr(n),
+                                                sweeps, r, st, _native.ptr(obs)), 'sv_replicas_villain')
+    rngs_to_numpy(r, gens, addrs)
+    for i in range(R):
+        g = np.random.default_rng(40 + i)
+        p, m = phi0[i].copy(), n0[i].copy()
+        ref = oracle_lib.villain_neighborhood(N, 0.4, W, p, m, sweeps, g)
+        assert (p == phi[i]).all() and (m == n[i]).all()
+        assert g.bit_generator.state == gens[i].bit_generator.state
+        assert [s.accepted for s in ref] == [st[i * sweeps + k].accepted for k in range(sweeps)]
+        np.testing.assert_allclose(obs[i, -1, 0], offline(p, m)[0], rtol=1e-12)
