@@ -195,6 +195,10 @@ static inline void run_batches(sv_ctx *ctx, const std::vector<BlockSpec> &specs,
             for (int k = 0; k < count; k++) launch_sweep(k, ctx->d_blocks + (size_t)k * nb, ctx->d_stats + k);
             ctx->time_end(ev, count);
             SV_HIP(hipGetLastError());
+            if (!may_reject) {  // threshold 0: no rejection can occur, so the stats copy is the one sync
+                cur = c;
+                break;
+            }
             AbortInfo a = read_abort(ctx);
             if (a.abort) ctx->time_discard();
             ctx->time_collect();
@@ -208,6 +212,7 @@ static inline void run_batches(sv_ctx *ctx, const std::vector<BlockSpec> &specs,
         }
         SV_HIP(hipMemcpyAsync(stats + sw, ctx->d_stats, count * sizeof(sv_stats), hipMemcpyDeviceToHost, ctx->stream));
         SV_HIP(hipStreamSynchronize(ctx->stream));
+        if (!may_reject) ctx->time_collect();
         for (int k = 0; k < count; k++) stats[sw + k].rejections = rejections_in(skips, sw + k, nb);
         sw += count;
     }
