@@ -550,6 +550,10 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
             ctx->time_end(ev, count);
             fold_stripes<<<(count * nstat + 63) / 64, 64, 0, ctx->stream>>>(ss, ctx->d_stats, count * nstat);
             SV_HIP(hipGetLastError());
+            if (!may_reject) {  // threshold 0: no rejection can occur, so the stats copy is the one sync
+                cur = c;
+                break;
+            }
             if (!wcheck(ctx, reps)) {
                 ctx->time_collect();
                 cur = c;
@@ -563,6 +567,7 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
         SV_HIP(hipMemcpyAsync(stats + (size_t)sw * nstat, ctx->d_stats, (size_t)count * nstat * sizeof(sv_stats),
                               hipMemcpyDeviceToHost, ctx->stream));
         SV_HIP(hipStreamSynchronize(ctx->stream));
+        if (!may_reject) ctx->time_collect();
         for (int k = 0; k < count; k++) {
             for (int j = 0; j < nstat; j++) {
                 stats[(size_t)(sw + k) * nstat + j].proposed = V;
