@@ -255,6 +255,15 @@ __device__ __forceinline__ int64_t base_pos(int ty, int64_t gq, int64_t N, int64
     return p < 0 ? 0 : (p >> 1);
 }
 
+// The small-offset maps in LDS as two arrays (A, C) of 16-B entries: lanes read consecutive entries, and
+// at a 16-B stride the 16 lanes of a ds_read_b128 group hit 64 distinct banks (the 64-B Affine stride of
+// an array of structs put 4 lanes on each bank).
+struct alignas(16) SmallTab {
+    u128 A[SMALL_LDS];
+    u128 C[SMALL_LDS];
+    __device__ __forceinline__ Affine operator[](int64_t i) const { return Affine{A[i], C[i]}; }
+};
+
 struct Draws {
     double u, dphi;
     int32_t cn[4];  // W * (choice - interval_n); |W * interval_n| < 2^28 on this path
@@ -268,7 +277,7 @@ __device__ __forceinline__ u128 full_jump(const JumpTables *T, const Block *blk,
     return r;
 }
 
-__device__ __forceinline__ u128 from_base(const JumpTables *T, const Block *blk, const Affine *sm, u128 base,
+__device__ __forceinline__ u128 from_base(const JumpTables *T, const Block *blk, const SmallTab &sm, u128 base,
                                           int64_t bpos, int64_t pos) {
     const int64_t off = pos - bpos;
     u128 st;
@@ -312,7 +321,7 @@ __device__ __forceinline__ int32_t choice_value(const FArgs &A, const Rep &RP, u
 // from the wave's second set of row bases `wb`, kept at global column xw, so no lane needs a full jump.
 template <bool K3 = false>
 __device__ __forceinline__ Draws draws_general(const FArgs &A, const Rep &RP, int c, bool active, int64_t gq, int64_t gx,
-                                               int64_t xb, const u128 *bases, const Affine *sm, bool edge,
+                                               int64_t xb, const u128 *bases, const SmallTab &sm, bool edge,
                                                int64_t xw, const u128 *wb) {
     const JumpTables *T = RP.T;
     const int64_t N = A.G.Nx;  // row length of the global stream layout
@@ -404,7 +413,7 @@ __device__ __forceinline__ u128 wave_uniform(u128 v) {
 
 template <bool K3 = false>
 __device__ __forceinline__ Draws draws_fastp(const FArgs &A, const Rep &RP, int c, bool active, int32_t lane,
-                                             uint32_t pk, uint32_t rank, const u128 *bases, const Affine *sm) {
+                                             uint32_t pk, uint32_t rank, const u128 *bases, const SmallTab &sm) {
     const int bb = 1 + 5 * c;
     Draws D;
     {
@@ -441,7 +450,7 @@ template <bool K3 = false>
 __device__ __forceinline__ Draws draws_fast(const FArgs &A, const Rep &RP, int c, const uint32_t *hasw, bool active,
                                             int32_t lane, uint32_t rowlin,
                                             uint32_t xs, uint32_t gx, uint32_t xb, const u128 *bases,
-                                            const Affine *sm) {
+                                            const SmallTab &sm) {
     const int bb = 1 + 5 * c;
     const uint32_t lin = rowlin + gx, rank = lin >> 1;
     const uint32_t PM = rowlin + xb, PR = PM >> 1;
@@ -496,7 +505,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     __shared__ double s_r1[R][RW];
     __shared__ int32_t s_n0[R][RW];
     __shared__ int32_t s_n1[R][RW];
-    __shared__ Affine s_small[SMALL_LDS];
+    __shared__ SmallTab s_small;
     __shared__ Affine s_adv[3];
     __shared__ u128 s_base[NW][32];  // per wave: [8c + ty] = block ty's base for the colour-c row; [16 + ..] at xw
     __shared__ int32_t s_bad;
@@ -558,7 +567,10 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     const bool edge = !(Nx <= SMALL_LDS && !interior) && (gx0 - 2 < 0 || gx0 + w + 2 >= Nx);
     const int32_t xw = gx0 - 2 < 0 ? Nx - 2 : 0;
 
-    for (int e = threadIdx.x; e < SMALL_LDS; e += nthreads) s_small[e] = RP.T->small[e];
+    for (int e = threadIdx.x; e < SMALL_LDS; e += nthreads) {
+        s_small.A[e] = RP.T->small[e].A;
+        s_small.C[e] = RP.T->small[e].C;
+    }
     if (threadIdx.x < 11) s_blk[threadIdx.x] = RP.blocks[threadIdx.x];
     const Rep RL{s_blk, RP.T, RP.id};  // the loop's view (valid after the prologue barrier)
     if (threadIdx.x < 3) s_adv[threadIdx.x] = REPS ? A.advrep[3 * rep + threadIdx.x] : A.adv[threadIdx.x];
