@@ -167,6 +167,7 @@ int sv_ctx_destroy(sv_ctx *ctx) {
     }
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
     (void)hipFree(ctx->d_abort);
+    if (ctx->h_abort) (void)hipHostFree(ctx->h_abort);
     (void)hipFree(ctx->d_nreport);
     (void)hipFree(ctx->d_reports);
     (void)hipFree(ctx->d_blocks);

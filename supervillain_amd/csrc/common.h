@@ -81,9 +81,8 @@ struct sv_ctx {
     size_t skips_cap = 0;
     sv_stats *d_stats = nullptr;
     size_t stats_cap = 0;
-    // pinned host staging
-    sv::Block *h_blocks = nullptr;
-    size_t h_blocks_cap = 0;
+    // pinned host image of d_abort: batches that cannot meet a rejection copy it with their stats (one sync)
+    int32_t *h_abort = nullptr;
     // optional per-launch timing of the sweep kernels (hipEvents on ctx->stream)
     bool timing = false;
     int timing_mode = 0;  // 1: events around each batch of launches, 2: around every launch

@@ -118,6 +118,16 @@ __device__ __forceinline__ int64_t even_site(int64_t e, int64_t N, int color) {
 
 namespace svh {
 namespace loc {
+
+// Batches with no possible rejection skip the abort read: the flag is queued to pinned memory ahead of
+// the stats copy and checked after that copy's synchronization.
+static inline void queue_abort_copy(sv_ctx *ctx) {
+    if (!ctx->h_abort) SV_HIP(hipHostMalloc((void **)&ctx->h_abort, sizeof(int32_t), hipHostMallocDefault));
+    SV_HIP(hipMemcpyAsync(ctx->h_abort, ctx->d_abort, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+}
+static inline void check_abort_copy(sv_ctx *ctx) {
+    if (*ctx->h_abort) throw std::runtime_error("unexpected NumPy Lemire rejection report");
+}
 using namespace sv;
 
 static inline int gcd_i(int64_t a, int64_t b) { return (int)std::gcd(a, b); }
@@ -206,13 +216,16 @@ static inline void run_batches(sv_ctx *ctx, const std::vector<BlockSpec> &specs,
                 cur = c;
                 break;
             }
-            if (!may_reject) throw std::runtime_error("unexpected NumPy Lemire rejection report");
             absorb_reports(a, sw, skips);
             restore();
         }
+        if (!may_reject) queue_abort_copy(ctx);
         SV_HIP(hipMemcpyAsync(stats + sw, ctx->d_stats, count * sizeof(sv_stats), hipMemcpyDeviceToHost, ctx->stream));
         SV_HIP(hipStreamSynchronize(ctx->stream));
-        if (!may_reject) ctx->time_collect();
+        if (!may_reject) {
+            check_abort_copy(ctx);
+            ctx->time_collect();
+        }
         for (int k = 0; k < count; k++) stats[sw + k].rejections = rejections_in(skips, sw + k, nb);
         sw += count;
     }

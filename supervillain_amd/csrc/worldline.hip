@@ -560,14 +560,17 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
                 break;
             }
             ctx->time_discard();
-            if (!may_reject) throw std::runtime_error("unexpected NumPy Lemire rejection report");
             wabsorb(reps, sw, skips);
             snapshot(st, true);
         }
+        if (!may_reject) svh::loc::queue_abort_copy(ctx);
         SV_HIP(hipMemcpyAsync(stats + (size_t)sw * nstat, ctx->d_stats, (size_t)count * nstat * sizeof(sv_stats),
                               hipMemcpyDeviceToHost, ctx->stream));
         SV_HIP(hipStreamSynchronize(ctx->stream));
-        if (!may_reject) ctx->time_collect();
+        if (!may_reject) {
+            svh::loc::check_abort_copy(ctx);
+            ctx->time_collect();
+        }
         for (int k = 0; k < count; k++) {
             for (int j = 0; j < nstat; j++) {
                 stats[(size_t)(sw + k) * nstat + j].proposed = V;
