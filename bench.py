@@ -7,10 +7,13 @@ reference's own chain semantics (NumPy PCG64 stream replayed on the device, bit-
 with the fields resident in HBM.
 
   N = 1: one L x L lattice on one GPU (the single-lattice fused sweep kernel).
-  N > 1: one process per GPU (torch.distributed.run); ONE lattice of (ty L) x (tx L) sites is
-         domain-decomposed into ty x tx tiles of L x L (1x2, 2x2, 2x4 for N = 2, 4, 8), one tile per
-         GPU, with an RCCL halo exchange every sweep (weak scaling: L x L sites per GPU).  The chain
-         is bit-identical to running that lattice on one GPU.  --strong keeps the lattice at L x L.
+  N > 1: one process per GPU (torch.distributed.run; `python bench.py --gpus N` launches it itself when
+         WORLD_SIZE is unset, before anything touches a GPU).  BASELINE config 4: the ONE L x L lattice
+         is domain-decomposed into ty x tx tiles (1x2, 2x2, 2x4 for N = 2, 4, 8), one tile per GPU, with
+         RCCL halo exchanges (strong scaling; the chain is bit-identical to the 1-GPU chain).  Each rank
+         also times its own tile alone as a periodic lattice (R1 of SURVEY.md 8(d)'s weak-scaling
+         E_N = R_N / (N R1)), reported under config.weak_scaling.  --weak grows the lattice to
+         (ty L) x (tx L) instead (L x L per GPU).
 Rank 0 prints one JSON line.
 
 Secondary workloads (not the headline line; BASELINE.json configs 5 and 3):
@@ -61,7 +64,8 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--gpus', type=int, default=None,
+                    help='number of GPUs (ranks); N > 1 without WORLD_SIZE launches torch.distributed.run itself')
     ap.add_argument('--steps', type=int, default=200)
     ap.add_argument('--warmup', type=int, default=20)
     ap.add_argument('--L', type=int, default=4096)
@@ -70,15 +74,22 @@ def parse():
     ap.add_argument('--path', type=int, default=2, help='0 auto, 1 per-colour kernels, 2 fused sweep kernel')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-sweeps', type=int, default=5)
-    ap.add_argument('--strong', action='store_true', help='N>1: decompose one L x L lattice (strong scaling)')
+    ap.add_argument('--weak', action='store_true', help='N>1: an L x L tile per GPU (weak scaling) instead of one '
+                                                        'L x L lattice decomposed (strong scaling, the default)')
+    ap.add_argument('--warmup-s', type=float, default=1.0,
+                    help='after the W warmup steps, keep warming (untimed) until this many seconds have passed: '
+                         'clocks and page mappings reach steady state before the timed region')
+    ap.add_argument('--no-copy-ceiling', action='store_true', help='skip the measured copy-kernel HBM ceiling')
     ap.add_argument('--tiles', default=None, help='tile grid TYxTX (default from N); with N=1 emulates the '
                                                    'decomposition on one GPU')
-    ap.add_argument('--workload', default='villain', choices=['villain', 'replicas', 'worldline', 'site', 'link', 'exact', 'cohomology', 'hammer', 'vortex',
-                             'wrapping', 'wlhammer', 'worms'])
+    ap.add_argument('--workload', default='villain', choices=['villain', 'replicas', 'worldline', 'site', 'link', 'exact',
+                                                              'cohomology', 'hammer', 'vortex', 'wrapping', 'wlhammer',
+                                                              'worms', 'ranks'])
     ap.add_argument('--event-timing', default='batch', choices=['launch', 'batch'],
                     help='hipEvents around each batch of 64 fused launches (default) or around every launch')
     ap.add_argument('--replicas', type=int, default=1024, help='replicas workload: total replica count')
     args = ap.parse_args()
+    args.strong = not args.weak
     if args.workload in ('replicas', 'worms'):
         args.L = 128 if args.L == 4096 else args.L
         args.W = 2 if args.W == 1 else args.W
@@ -122,6 +133,35 @@ def cpu_baseline(L, kappa, W, sweeps):
                       '1 core (the sequential restatement: value_1core)'}
 
 
+def warm_up(run, args, dist=None):
+    """Untimed warmup: the W steps the driver asks for, then more until --warmup-s seconds have passed (GPU
+    clocks and page mappings at steady state).  Collective runs agree on the extra step count (max over ranks)."""
+    t0 = time.perf_counter()
+    if args.warmup:
+        run(args.warmup)
+    if args.warmup_s <= 0:
+        return
+    t1 = time.perf_counter()
+    run(1)
+    per = max(time.perf_counter() - t1, 1e-6)
+    extra = int(max(0.0, args.warmup_s - (time.perf_counter() - t0)) / per) if args.warmup_s > 0 else 0
+    extra = int(max_over_ranks(dist, float(min(extra, 100000))))
+    while extra > 0:
+        k = min(extra, 4096)
+        run(k)
+        extra -= k
+
+
+def copy_ceiling(ctx):
+    """Measured HBM ceiling on this GPU: a streaming copy of two 1 GiB buffers (16-B lanes), read + write bytes
+    per second (report the roofline fraction against it as well as against the 8 TB/s spec)."""
+    from supervillain_amd import _native
+    g = ctypes.c_double()
+    if _native.lib().sv_hbm_copy(ctx.handle, 1 << 30, 16, 20, ctypes.byref(g)) != 0:
+        return None
+    return g.value
+
+
 def max_over_ranks(dist, x):
     if dist is None:
         return x
@@ -142,8 +182,9 @@ def kernel_time(Lib, ctx):
 def report(args, world, sites_per_step, sites_per_launch, elapsed, acc, avg_launch_s, config, traffic_L,
            metric='lattice-site updates/sec (sweeps/s × L²), L=4096 Villain, 1→8 MI355X',
            unit='lattice-site updates/s', kernel='villain_sweep_fused', alg_bytes=SURVEY_BYTES_PER_SITE,
-           min_bytes=FUSED_MIN_BYTES_PER_SITE, baseline=None):
+           min_bytes=FUSED_MIN_BYTES_PER_SITE, baseline=None, ctx=None, scaling=None):
     achieved = alg_bytes * sites_per_launch / avg_launch_s / 1e9
+    ceiling = copy_ceiling(ctx) if ctx is not None and not getattr(args, 'no_copy_ceiling', False) else None
     out = {
         'metric': metric,
         'value': args.steps * sites_per_step / elapsed,
@@ -153,7 +194,7 @@ def report(args, world, sites_per_step, sites_per_launch, elapsed, acc, avg_laun
         'warmup': args.warmup,
         'ms_per_step': elapsed / args.steps * 1e3,
         'higher_is_better': True,
-        'scaling': 'strong' if args.strong else 'weak',
+        'scaling': scaling or ('strong' if args.strong else 'weak'),
         'vs_baseline': None,
         'dtype': 'f64+int64',
         'data': 'synthetic (cold start, NumPy PCG64 seed 0)',
@@ -165,7 +206,9 @@ def report(args, world, sites_per_step, sites_per_launch, elapsed, acc, avg_laun
                      'alg_bytes_per_unit': alg_bytes,
                      'fused_min_bytes_per_unit': min_bytes,
                      'fused_min_GBps': min_bytes * sites_per_launch / avg_launch_s / 1e9,
-                     'fused_min_frac': min_bytes * sites_per_launch / avg_launch_s / 1e9 / HBM_PEAK_GBS},
+                     'fused_min_frac': min_bytes * sites_per_launch / avg_launch_s / 1e9 / HBM_PEAK_GBS,
+                     'copy_ceiling_GBps': ceiling,
+                     'frac_of_copy_ceiling': achieved / ceiling if ceiling else None},
         'cpu_baseline': None,
     }
     if world == 1 and not args.no_cpu_baseline:
@@ -185,8 +228,7 @@ def run_replicas(args, world, rank, dist):
     B.cold()
     gens = [np.random.default_rng(first + r) for r in range(per)]
     Lib = _native.lib()
-    if args.warmup:
-        B.run(args.warmup, gens, inline=True)
+    warm_up(lambda k: B.run(k, gens, inline=True), args, dist)
     Lib.sv_ctx_set_timing(B.ctx.handle, 1)
     if dist:
         dist.barrier()
@@ -219,7 +261,8 @@ def run_replicas(args, world, rank, dist):
                   'parallelism': f'{world} GPU(s), replicas sharded, no collectives'}
         report(args, world, Rt * L * L, per * L * L, elapsed, acc, launches_s, config, L,
                metric=f'replica-site updates/sec, {Rt} x L={L} Villain replicas, W={args.W}, inline observables',
-               unit='replica-site updates/s', kernel='villain_sweep_fused_obs', baseline=baseline)
+               unit='replica-site updates/s', kernel='villain_sweep_fused_obs', baseline=baseline, ctx=B.ctx,
+               scaling='strong')
     B.close()
 
 
@@ -237,8 +280,7 @@ def run_worms(args, world, rank, dist):
     B.run(100, gens)  # thermalize: worms on a cold start are short
     wgens = [np.random.default_rng(10 ** 6 + first + r) for r in range(per)]
     Lib = _native.lib()
-    if args.warmup:
-        B.worm(wgens, worms=args.warmup)
+    warm_up(lambda k: B.worm(wgens, worms=k), args, dist)
     Lib.sv_ctx_set_timing(B.ctx.handle, 1)
     if dist:
         dist.barrier()
@@ -281,7 +323,7 @@ def run_worms(args, world, rank, dist):
         # and the histogram increment (8 + 8); a latency-bound walk, the roofline fraction is informational
         report(args, world, moves / args.steps, moves / world, elapsed, 0.0, launch_s, config, L,
                metric=f'worm moves/sec, {Rt} x L={L} Villain ClassicWorm chains, W={args.W}', unit='worm moves/s',
-               kernel='villain_worm', alg_bytes=40, min_bytes=40, baseline=baseline)
+               kernel='villain_worm', alg_bytes=40, min_bytes=40, baseline=baseline, ctx=B.ctx, scaling='strong')
     B.close()
 
 
@@ -307,8 +349,7 @@ def run_worldline(args, world, rank, dist):
                   'sv_worldline_plaquette_coexact_run')
         return sum(st[2 * i].accepted for i in range(k))  # Plaquette acceptances
 
-    if args.warmup:
-        step(args.warmup)
+    warm_up(step, args, dist)
     Lib.sv_ctx_set_timing(ctx.handle, 1)
     if dist:
         dist.barrier()
@@ -344,7 +385,7 @@ def run_worldline(args, world, rank, dist):
         report(args, world, world * L * L, L * L, elapsed, acc / (args.steps * L * L), step_kernel_s, config, L,
                metric=f'plaquette-steps/sec (Plaquette + Coexact sweep), L={L} Worldline, W={args.W}',
                unit='plaquette-steps/s', kernel='plaquette_cb_gs+coexact_gs', alg_bytes=WORLDLINE_BYTES,
-               min_bytes=WORLDLINE_BYTES, baseline=baseline)
+               min_bytes=WORLDLINE_BYTES, baseline=baseline, ctx=ctx, scaling='weak')
     Lib.sv_worldline_destroy(h)
 
 
@@ -396,8 +437,7 @@ def run_local(args, world, rank, dist):
             acc = sum(st[i].accepted for i in range(k))
         return acc
 
-    if args.warmup:
-        run(args.warmup)
+    warm_up(run, args, dist)
     Lib.sv_ctx_set_timing(ctx.handle, 1)
     if dist:
         dist.barrier()
@@ -449,12 +489,12 @@ def run_local(args, world, rank, dist):
         report(args, world, world * L * L, L * L, elapsed, acc / (args.steps * L * L), step_kernel_s, config, L,
                metric=f'{unit[:-2]}/sec ({what}), L={L} {model}', unit=unit,
                kernel=f'{kind} (all kernels of a step)', alg_bytes=LOCAL_BYTES.get(kind, 0),
-               min_bytes=LOCAL_BYTES.get(kind, 0), baseline=baseline)
+               min_bytes=LOCAL_BYTES.get(kind, 0), baseline=baseline, ctx=ctx, scaling='weak')
     (Lib.sv_worldline_destroy if worldline else Lib.sv_villain_destroy)(h)
 
 
 def run_domain(args, world, rank, local, dist):
-    """N > 1 (or --tiles on one GPU): one lattice, domain-decomposed, RCCL halos."""
+    """N > 1 (or --tiles on one GPU): BASELINE config 4, one lattice domain-decomposed, RCCL halos."""
     from supervillain_amd import _native
     from supervillain_amd.domain import VillainDomain, tile_grid
     L = args.L
@@ -463,6 +503,7 @@ def run_domain(args, world, rank, local, dist):
     else:
         ty, tx = tile_grid(world)
     Nt, Nx = (L, L) if args.strong else (ty * L, tx * L)
+    Ht, Wt = Nt // ty, Nx // tx
     kw = dict(kappa=args.kappa, W=args.W)  # device: $SV_DEVICE, else $LOCAL_RANK
     if world > 1:
         dom = VillainDomain.distributed(Nt, Nx, (ty, tx), **kw)
@@ -471,8 +512,7 @@ def run_domain(args, world, rank, local, dist):
     dom.cold()
     gen = np.random.default_rng(0)  # one chain: every rank holds the same stream
     Lib = _native.lib()
-    if args.warmup:
-        dom.run(args.warmup, gen)
+    warm_up(lambda k: dom.run(k, gen), args, dist)
     Lib.sv_ctx_set_timing(dom.ctx.handle, 1)
     if dist:
         dist.barrier()
@@ -484,29 +524,85 @@ def run_domain(args, world, rank, local, dist):
     elapsed = max_over_ranks(dist, t1 - t0)
     avg_launch_s = kernel_time(Lib, dom.ctx)
     acc = sum(s.accepted for s in st) / (args.steps * Nt * Nx)
-    if rank == 0:
-        config = {'workload': f'{Nt}x{Nx} Villain NeighborhoodUpdate sweep, domain-decomposed into {ty}x{tx} tiles of '
-                              f'{Nt // ty}x{Nx // tx} (one per GPU), RCCL halo exchange every sweep, bit-exact '
-                              'reference chain (PCG64 replay)',
-                  'L': L, 'lattice': [Nt, Nx], 'tiles': [ty, tx], 'path': 'domain',
-                  'parallelism': f'{ty}x{tx} domain decomposition over {world} GPU(s)'}
-        report(args, world, Nt * Nx, Nt * Nx // world, elapsed, acc, avg_launch_s, config, Nt // ty)
+    ctx = dom.ctx
     dom.close()
+
+    # R1: this rank's tile alone, as a periodic Ht x Wt lattice on its own GPU, no exchange
+    one = VillainDomain(Ht, Wt, (1, 1), **kw)
+    one.cold()
+    g1 = np.random.default_rng(1)
+    one.run(max(args.warmup, 5), g1)
+    k1 = max(args.steps, 20)
+    t = time.perf_counter()
+    one.run(k1, g1)
+    r1 = Ht * Wt * k1 / (time.perf_counter() - t)
+    one.close()
+    r1_mean = r1 if dist is None else _mean_over_ranks(dist, r1)
+
+    if rank == 0:
+        value = args.steps * Nt * Nx / elapsed
+        config = {'workload': f'{Nt}x{Nx} Villain NeighborhoodUpdate sweep, kappa={args.kappa}, W={args.W}, '
+                              f'domain-decomposed into {ty}x{tx} tiles of {Ht}x{Wt} (one per GPU), RCCL halo '
+                              'exchange, bit-exact reference chain (PCG64 replay)',
+                  'L': L, 'lattice': [Nt, Nx], 'tiles': [ty, tx], 'path': 'domain',
+                  'parallelism': f'{ty}x{tx} domain decomposition over {world} GPU(s)',
+                  'weak_scaling': {'tile': [Ht, Wt], 'R1': r1_mean,
+                                   'E_N': value / (world * r1_mean),
+                                   'definition': 'E_N = R_N / (N R1), R1 = one GPU running one periodic tile '
+                                                 'of this size alone (SURVEY.md 8(d))'}}
+        report(args, world, Nt * Nx, Nt * Nx // world, elapsed, acc, avg_launch_s, config, Ht, ctx=ctx)
+
+
+def _mean_over_ranks(dist, x):
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t)
+    return float(t.item()) / dist.get_world_size()
+
+
+def run_ranks(args, world, rank, dist):
+    """--workload ranks: the launcher's rank / world plumbing alone, no GPU (a CPU test drives it)."""
+    tot = _mean_over_ranks(dist, float(rank)) * world if dist else 0.0
+    if rank == 0:
+        print(json.dumps({'workload': 'ranks', 'world': world, 'rank_sum': tot,
+                          'master_addr': os.environ.get('MASTER_ADDR'),
+                          'local_ranks': world}), flush=True)
+
+
+def launch_command(gpus, argv, port):
+    """The torch.distributed.run command that re-runs this script with one rank per GPU (no exec: the parent
+    waits for it; it has touched no GPU)."""
+    return [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={gpus}',
+            '--master-addr', '127.0.0.1', f'--master-port={port}', os.path.abspath(__file__)] + list(argv)
+
+
+def spawn(gpus, argv):
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    return subprocess.call(launch_command(gpus, argv, port))
 
 
 def main():
     args = parse()
+    if args.gpus is not None and args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(spawn(args.gpus, sys.argv[1:]))  # one rank per GPU, before any HIP call in this process
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if args.gpus is not None and args.gpus != world:
+        print(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={world}', file=sys.stderr)
+        sys.exit(2)
     dist = None
     if world > 1:
-        import torch
         import torch.distributed as dist
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         dist.init_process_group('gloo', rank=rank, world_size=world)
     if args.workload != 'villain':
-        fn = {'replicas': run_replicas, 'worldline': run_worldline, 'worms': run_worms}.get(args.workload, run_local)
+        fn = {'replicas': run_replicas, 'worldline': run_worldline, 'worms': run_worms,
+              'ranks': run_ranks}.get(args.workload, run_local)
         fn(args, world, rank, dist)
         if dist:
             dist.destroy_process_group()
@@ -536,18 +632,19 @@ def main():
                   'sv_villain_run')
         return st
 
-    if args.warmup:
-        run(args.warmup)
+    warm_up(run, args)
     Lib.sv_ctx_set_timing(ctx.handle, 2 if args.event_timing == 'launch' else 1)
     t0 = time.perf_counter()
     st = run(args.steps)  # synchronous on return (stream synchronized)
     t1 = time.perf_counter()
     avg_launch_s = kernel_time(Lib, ctx)
     acc = sum(st[i].accepted for i in range(args.steps)) / (args.steps * L * L)
+    rej = sum(st[i].rejections for i in range(args.steps))
     config = {'workload': f'L={L} Villain NeighborhoodUpdate sweep, kappa={args.kappa}, W={args.W}, '
                           'bit-exact reference chain (PCG64 replay), fused two-colour sweep kernel',
-              'L': L, 'lattice': [L, L], 'path': args.path, 'parallelism': 'single GPU'}
-    report(args, 1, L * L, L * L, t1 - t0, acc, avg_launch_s, config, L)
+              'L': L, 'lattice': [L, L], 'path': args.path, 'parallelism': 'single GPU',
+              'lemire_rejections_in_timed_steps': int(rej)}
+    report(args, 1, L * L, L * L, t1 - t0, acc, avg_launch_s, config, L, ctx=ctx)
     Lib.sv_villain_destroy(h)
 
 

@@ -68,6 +68,11 @@ int sv_ctx_kernel_time(sv_ctx *ctx, double *ms_total, int64_t *launches);
 int sv_rng_gather(void *const *pcg64_states, int32_t R, sv_rng *out);
 int sv_rng_scatter(const sv_rng *in, int32_t R, void *const *pcg64_states);
 const char *sv_build_info(void);
+/* Measurement only: a streaming device copy of `bytes` (two buffers, well above the 256 MB Infinity Cache
+ * for a ceiling) with `width`-byte lanes (16 or 8), `iters` timed launches after one warm-up; *GBps = read +
+ * write bytes / time.  The roofline is reported against this measured ceiling beside the 8 TB/s spec
+ * (SURVEY.md 8(d)); under rocprofv3 --pmc its known byte count calibrates FETCH_SIZE / WRITE_SIZE. */
+int sv_hbm_copy(sv_ctx *ctx, int64_t bytes, int32_t width, int32_t iters, double *GBps);
 
 /* ---- Villain (phi, n): NeighborhoodUpdate ------------------------------------------------- */
 /* Replaces NeighborhoodUpdate.step, supervillain/generator/villain/neighborhood.py:59-137

@@ -41,6 +41,7 @@ def lib():
         L.sv_build_info.restype = ctypes.c_char_p
         L.sv_ctx_set_timing.argtypes = [vp, i32]
         L.sv_ctx_kernel_time.argtypes = [vp, P(f64), P(i64)]
+        L.sv_hbm_copy.argtypes = [vp, i64, i32, i32, P(f64)]
         L.sv_rng_gather.argtypes = [vp, i32, vp]
         L.sv_rng_scatter.argtypes = [vp, i32, vp]
         L.sv_villain_neighborhood.argtypes = [vp, i32, f64, i64, f64, i64, vp, vp, i32, P(SvRng), P(SvStats)]
@@ -89,7 +90,7 @@ def lib():
 
 
 EXPORTED = ('sv_ctx_create', 'sv_ctx_destroy', 'sv_last_error', 'sv_device_count', 'sv_build_info',
-            'sv_ctx_set_timing', 'sv_ctx_kernel_time', 'sv_rng_gather', 'sv_rng_scatter',
+            'sv_ctx_set_timing', 'sv_ctx_kernel_time', 'sv_hbm_copy', 'sv_rng_gather', 'sv_rng_scatter',
             'sv_villain_neighborhood', 'sv_villain_create', 'sv_villain_destroy', 'sv_villain_upload',
             'sv_villain_download', 'sv_villain_run', 'sv_villain_observables',
             'sv_villain_site_run', 'sv_villain_link_run', 'sv_villain_exact_run', 'sv_villain_cohomology_run', 'sv_worldline_create',

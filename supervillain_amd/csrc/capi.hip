@@ -94,6 +94,15 @@ void sv_ctx::time_discard() {
     ev_launches.clear();
 }
 
+// Streaming copy b[i] = a[i] with W-byte lanes (16: dwordx4, 8: dwordx2): the measured HBM ceiling the
+// roofline fraction is also reported against, and the known byte count that calibrates
+// the PMC FETCH_SIZE / WRITE_SIZE counters for this repo's access widths (MI355X_MICROARCH.md, HBM).
+template <typename T>
+__global__ __launch_bounds__(256) void hbm_copy(const T *__restrict__ a, T *__restrict__ b, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) b[i] = a[i];
+}
+
 extern "C" {
 
 int sv_ctx_set_timing(sv_ctx *ctx, int32_t enable) {
@@ -116,6 +125,49 @@ int sv_ctx_kernel_time(sv_ctx *ctx, double *ms_total, int64_t *launches) {
     if (ms_total) *ms_total = ctx->timed_ms;
     if (launches) *launches = ctx->timed_launches;
     return 0;
+}
+
+int sv_hbm_copy(sv_ctx *ctx, int64_t bytes, int32_t width, int32_t iters, double *GBps) {
+    if (!ctx || bytes < 4096 || iters < 1 || (width != 8 && width != 16)) return -1;
+    void *a = nullptr, *b = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = 0;
+    try {
+        SV_HIP(hipSetDevice(ctx->device));
+        bytes &= ~(int64_t)4095;
+        SV_HIP(hipMalloc(&a, bytes));
+        SV_HIP(hipMalloc(&b, bytes));
+        SV_HIP(hipMemsetAsync(a, 1, bytes, ctx->stream));
+        SV_HIP(hipMemsetAsync(b, 0, bytes, ctx->stream));
+        SV_HIP(hipEventCreate(&e0));
+        SV_HIP(hipEventCreate(&e1));
+        hipDeviceProp_t prop;
+        SV_HIP(hipGetDeviceProperties(&prop, ctx->device));
+        const int grid = prop.multiProcessorCount * 8;  // grid-stride: 2048 threads per CU
+        auto launch = [&]() {
+            if (width == 16)
+                hbm_copy<uint4><<<grid, 256, 0, ctx->stream>>>((const uint4 *)a, (uint4 *)b, bytes / 16);
+            else
+                hbm_copy<uint2><<<grid, 256, 0, ctx->stream>>>((const uint2 *)a, (uint2 *)b, bytes / 8);
+        };
+        launch();  // warm: page mappings, clocks
+        SV_HIP(hipEventRecord(e0, ctx->stream));
+        for (int i = 0; i < iters; i++) launch();
+        SV_HIP(hipEventRecord(e1, ctx->stream));
+        SV_HIP(hipEventSynchronize(e1));
+        SV_HIP(hipGetLastError());
+        float ms = 0.f;
+        SV_HIP(hipEventElapsedTime(&ms, e0, e1));
+        if (GBps) *GBps = 2.0 * (double)bytes * iters / (ms * 1e-3) / 1e9;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        rc = -2;
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipFree(a);
+    (void)hipFree(b);
+    return rc;
 }
 
 int sv_device_count(void) {

@@ -440,15 +440,17 @@ class ClassicWorm(DeviceState, Generator):
 Worm = ClassicWorm
 
 
-def Hammer(S, worms=1):
-    r'''The reference's Villain Hammer (supervillain/generator/villain/__init__.py:11-67):
-    Sequentially(Site, Link, Exact, Cohomology, Worm), LinkUpdate omitted at W = infinity, the worm wrapped in
-    KeepEvery(worms, ...) when worms > 1.  worms=0 leaves the worm out (the round-1 Hammer).'''
+def Hammer(S, worms=1, *, worm=True):
+    r'''The reference's Villain Hammer (supervillain/generator/villain/__init__.py:11-64):
+    Sequentially(Site, Link, Exact, Cohomology, Worm), LinkUpdate omitted at W = infinity.  As in the reference
+    the worm is included whenever D == 2, whatever `worms` is, and wrapped in KeepEvery(worms, ...) when
+    worms > 1; for D != 2 it is omitted.  ``worm=False`` (not a reference argument) builds the worm-free
+    program.'''
     from supervillain_amd.generator.combining import KeepEvery, Sequentially
-    worm = ()
-    if worms:
+    tail = ()
+    if worm and S.Lattice.D == 2:
         W = ClassicWorm(S)
-        worm = (KeepEvery(worms, W) if worms > 1 else W,)
+        tail = (KeepEvery(worms, W) if worms > 1 else W,)
     if S.W < float('inf'):
-        return Sequentially((SiteUpdate(S), LinkUpdate(S), ExactUpdate(S), CohomologyUpdate(S)) + worm)
-    return Sequentially((SiteUpdate(S), ExactUpdate(S), CohomologyUpdate(S)) + worm)
+        return Sequentially((SiteUpdate(S), LinkUpdate(S), ExactUpdate(S), CohomologyUpdate(S)) + tail)
+    return Sequentially((SiteUpdate(S), ExactUpdate(S), CohomologyUpdate(S)) + tail)

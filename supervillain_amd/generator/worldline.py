@@ -374,13 +374,14 @@ class ClassicWorm(_WorldlineDevice, Generator):
 Worm = ClassicWorm
 
 
-def Hammer(S, worms=1):
-    r'''The reference's Worldline Hammer (supervillain/generator/worldline/__init__.py:10-40):
-    Sequentially(Vortex, Coexact, Wrapping, Worm), the worm wrapped in KeepEvery(worms, ...) when worms > 1.
-    worms=0 leaves the worm out (the round-1 Hammer).'''
+def Hammer(S, worms=1, *, worm=True):
+    r'''The reference's Worldline Hammer (supervillain/generator/worldline/__init__.py:10-41):
+    Sequentially(Vortex, Coexact, Wrapping, Worm), the worm always included, whatever `worms` is, and wrapped in
+    KeepEvery(worms, ...) when worms > 1.  ``worm=False`` (not a reference argument) builds the worm-free
+    program.'''
     from supervillain_amd.generator.combining import KeepEvery, Sequentially
-    worm = ()
-    if worms:
+    tail = ()
+    if worm:
         W = ClassicWorm(S)
-        worm = (KeepEvery(worms, W) if worms > 1 else W,)
-    return Sequentially((VortexUpdate(S), CoexactUpdate(S), WrappingUpdate(S)) + worm)
+        tail = (KeepEvery(worms, W) if worms > 1 else W,)
+    return Sequentially((VortexUpdate(S), CoexactUpdate(S), WrappingUpdate(S)) + tail)

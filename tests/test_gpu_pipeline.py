@@ -106,11 +106,11 @@ def test_plaquette_reference_order_resident():
 
 def test_villain_hammer_worms_keepevery():
     """Hammer(S, worms=3): the worm inside KeepEvery (blocked inline observables averaged, combining.py:100-112)
-    keeps the host loop; Hammer(S, worms=0) is the worm-free program."""
+    keeps the host loop; Hammer(S, worm=False) is the worm-free program."""
     S = sv.Villain(sv.Lattice2D(8), 0.5, 2)
     H = gv.Hammer(S, worms=3)
     assert isinstance(H.generators[-1], KeepEvery) and device_program(H) is None
-    assert device_program(gv.Hammer(S, worms=0)) is not None
+    assert device_program(gv.Hammer(S, worm=False)) is not None
     for G, s in zip(H.generators[:-1], [1, 2, 3, 4]):
         G.rng = np.random.default_rng(s)
     H.generators[-1].generator.rng = np.random.default_rng(5)

@@ -162,3 +162,32 @@ def test_ensemble_golden():
     E = sv.Ensemble(S).generate(c['steps'], G)
     assert (E.configuration.phi.array == c['phi']).all() and (E.configuration.n.array == c['n']).all()
     assert G.report() == c['report']
+
+
+def test_config2_exact_parameters(oracle_lib):
+    """BASELINE config 2 as stated: L=256, kappa=0.5, W=1 (interval_n=1), cold start, seed 0; 20 sweeps one per
+    call (as Ensemble.generate makes them) against the oracle."""
+    N, kappa, W, sweeps = 256, 0.5, 1, 20
+    phi0, n0 = np.zeros((N, N)), np.zeros((2, N, N), dtype=np.int64)
+    G, phi, n, accepted, acceptance = run_gpu(N, kappa, W, phi0, n0, sweeps, np.random.default_rng(0), path=2)
+    g = np.random.default_rng(0)
+    p, m = phi0.copy(), n0.copy()
+    st = oracle_lib.villain_neighborhood(N, kappa, W, p, m, sweeps, g)
+    assert (phi == p).all() and (n == m).all()
+    assert G.rng.bit_generator.state == g.bit_generator.state
+    assert accepted[-1] == sum(s.accepted for s in st)
+    np.testing.assert_allclose(acceptance[-1], sum(s.acceptance_sum for s in st) / N ** 2, rtol=1e-12)
+
+
+def test_config2_batched_long_chain(oracle_lib):
+    """Config 2's bench shape: 300 sweeps of L=256 (kappa=0.5, W=1) in one device call (several 64-sweep
+    batches), against the oracle."""
+    N, sweeps = 256, 300
+    phi0, n0 = np.zeros((N, N)), np.zeros((2, N, N), dtype=np.int64)
+    G, phi, n, _, _ = run_gpu(N, 0.5, 1, phi0, n0, sweeps, np.random.default_rng(0), path=2, batched=True)
+    g = np.random.default_rng(0)
+    p, m = phi0.copy(), n0.copy()
+    st = oracle_lib.villain_neighborhood(N, 0.5, 1, p, m, sweeps, g)
+    assert (phi == p).all() and (n == m).all()
+    assert G.rng.bit_generator.state == g.bit_generator.state
+    assert G.accepted == sum(s.accepted for s in st)

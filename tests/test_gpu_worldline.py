@@ -192,3 +192,74 @@ def test_plaquette_coexact_steps_oracle(N, W, sweeps, oracle_lib):
                                    [sp.acceptance_sum, sc.acceptance_sum], rtol=1e-12)
     assert (m == mm).all() and (v == vv).all()
     assert gen.bit_generator.state == g.bit_generator.state
+
+
+def _worldline_run(N, kappa, Weff, m0, v0, steps, gen, interval_t=1):
+    import ctypes
+    from supervillain_amd import _native
+    from supervillain_amd._abi import rng_from_numpy, rng_to_numpy
+    Lib = _native.lib()
+    ctx = _native.context(_native.default_device())
+    h = ctypes.c_void_p()
+    ctx.check(Lib.sv_worldline_create(ctx.handle, N, int(v0.dtype == np.float64), ctypes.byref(h)), 'create')
+    ctx.check(Lib.sv_worldline_upload(h, _native.ptr(m0), _native.ptr(v0)), 'upload')
+    r = rng_from_numpy(gen)
+    st = _native.stats_array(2 * steps)
+    ctx.check(Lib.sv_worldline_plaquette_coexact_run(h, kappa, Weff, interval_t, steps, ctypes.byref(r), st), 'run')
+    rng_to_numpy(r, gen)
+    m, v = np.empty_like(m0), np.empty_like(v0)
+    ctx.check(Lib.sv_worldline_download(h, _native.ptr(m), _native.ptr(v)), 'download')
+    Lib.sv_worldline_destroy(h)
+    return m, v, [st[i] for i in range(2 * steps)]
+
+
+@pytest.mark.parametrize('start', ['cold', 'v_random'])
+def test_config3_at_size(start, oracle_lib):
+    """BASELINE config 3 at its own size: L=1024 Worldline, W=1, kappa=0.5, Plaquette (checkerboard) + Coexact
+    per step, exactly as bench.py --workload worldline runs it (sv_worldline_plaquette_coexact_run), against the
+    oracle step by step; from a cold start and from v ~ U{-3..3} (test_coexact_sparse.py:15-22 style)."""
+    N, kappa, steps = 1024, 0.5, 4
+    m0 = np.zeros((2, N, N), dtype=np.int64)
+    v0 = (np.random.default_rng(11).integers(-3, 4, (N, N)) if start == 'v_random'
+          else np.zeros((N, N))).astype(np.int64)
+    gen = np.random.default_rng(0)
+    m, v, st = _worldline_run(N, kappa, 1.0, m0, v0, steps, gen)
+    g = np.random.default_rng(0)
+    mm, vv = m0.copy(), v0.copy()
+    for s in range(steps):
+        sp = oracle_lib.worldline_plaquette_cb(N, kappa, 1.0, mm, vv, 1, g)[0]
+        sc = oracle_lib.worldline_coexact(N, kappa, 1.0, mm, vv, 1, g)[0]
+        assert st[2 * s].accepted == sp.accepted and st[2 * s + 1].accepted == sc.accepted, s
+    assert (m == mm).all() and (v == vv).all()
+    assert gen.bit_generator.state == g.bit_generator.state
+    S = sv.Worldline(sv.Lattice2D(N), kappa, 1)
+    assert S.valid({'m': sv.Form(m, degree=1, lattice=S.Lattice)})
+
+
+def test_config3_reference_order_plaquette_at_size(oracle_lib):
+    """The reference-order PlaquetteUpdate (plaquette.py:35-104, NumPy's global permutation) at config 3's size,
+    one sweep after a Coexact sweep (so m != 0), against the sequential oracle."""
+    N, kappa = 1024, 0.5
+    L = sv.Lattice2D(N)
+    S = sv.Worldline(L, kappa, 1)
+    C = sv.generator.worldline.CoexactUpdate(S)
+    C.rng = np.random.default_rng(3)
+    cfg = S.configurations(1)[0]
+    cfg = cfg | C.step(cfg)
+    m0 = np.asarray(cfg['m']).copy()
+    G = sv.generator.worldline.PlaquetteUpdate(S)
+    G.rng = np.random.default_rng(4)
+    saved = np.random.get_state()
+    np.random.seed(2024)
+    try:
+        st0 = np.random.get_state()
+        o = np.random.permutation(L.coordinates)
+        np.random.set_state(st0)
+        cfg = cfg | G.step(cfg)
+    finally:
+        np.random.set_state(saved)
+    m, v = m0.copy(), np.zeros((N, N), dtype=np.int64)
+    g = np.random.default_rng(4)
+    s = oracle_lib.worldline_plaquette_seq(N, kappa, 1.0, m, v, (o[:, 0] % N) * N + (o[:, 1] % N), g)
+    assert (np.asarray(cfg['m']) == m).all() and (np.asarray(cfg['v'])[0] == v).all()
+    assert G.accepted == s.accepted and G.rng.bit_generator.state == g.bit_generator.state

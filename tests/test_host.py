@@ -148,6 +148,30 @@ def test_worm_wrong_action_raises():
         __import__('supervillain_amd.generator.worldline', fromlist=['Worm']).Worm(sv.Villain(sv.Lattice2D(4), 0.5, 1))
 
 
+def test_hammer_composition_matches_reference():
+    """Hammer(S, worms) as supervillain/generator/{villain,worldline}/__init__.py build it: the worm is always
+    the last member in D = 2 (worms = 0 and 1 alike), inside KeepEvery only when worms > 1; LinkUpdate is
+    left out at W = infinity; worm=False (an extension) drops the worm."""
+    from supervillain_amd.generator import villain as gv, worldline as gw
+    from supervillain_amd.generator.combining import KeepEvery
+    L = sv.Lattice2D(4)
+    for W, names in ((1, ['SiteUpdate', 'LinkUpdate', 'ExactUpdate', 'CohomologyUpdate']),
+                     (float('inf'), ['SiteUpdate', 'ExactUpdate', 'CohomologyUpdate'])):
+        S = sv.Villain(L, 0.5, W)
+        for worms in (0, 1):
+            H = gv.Hammer(S, worms)
+            assert [type(g).__name__ for g in H.generators] == names + ['ClassicWorm']
+        H = gv.Hammer(S, 3)
+        assert isinstance(H.generators[-1], KeepEvery) and H.generators[-1].stride == 3
+        assert [type(g).__name__ for g in gv.Hammer(S, worm=False).generators] == names
+    Sw = sv.Worldline(L, 0.5, 1)
+    for worms in (0, 1):
+        assert [type(g).__name__ for g in gw.Hammer(Sw, worms).generators] == \
+            ['VortexUpdate', 'CoexactUpdate', 'WrappingUpdate', 'ClassicWorm']
+    assert isinstance(gw.Hammer(Sw, 2).generators[-1], KeepEvery)
+    assert len(gw.Hammer(Sw, worm=False).generators) == 3
+
+
 def test_rng_batch_roundtrip():
     """sv_rng_gather / sv_rng_scatter (host-only C-ABI) read and write NumPy's PCG64 states exactly like the
     public state dict, including the half-word buffer."""
