@@ -365,8 +365,8 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
     const auto specs = villain_specs(V, 2, counts, P.k > 1);
     const int nb = (int)specs.size();
     constexpr int NWv = 4;
-    const int TH = fused_th();
     const int nsx = (d->Wt + FW_MAX - 1) / FW_MAX;
+    const int TH = fused_th(d->Ht, nsx);
     const int nsy = (d->Ht + TH - 1) / TH;
     const Affine adv[3] = {host_power(inc, (uint64_t)NWv * d->Nx), host_power(inc, (uint64_t)NWv * d->Nx / 2),
                            host_power(inc, (uint64_t)NWv * d->Nx / 4)};
@@ -595,8 +595,8 @@ int sv_domain_create(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tiles_t, int32
         }
         // split sweeps: strips whose stencil stays inside the tile run while the halos travel
         {
-            const int TH = fused_th();
-            const int nsx = (d->Wt + FW_MAX - 1) / FW_MAX, nsy = (d->Ht + TH - 1) / TH;
+            const int nsx = (d->Wt + FW_MAX - 1) / FW_MAX;
+            const int TH = fused_th(d->Ht, nsx), nsy = (d->Ht + TH - 1) / TH;
             std::vector<int32_t> inner, outer;
             for (int iy = 0; iy < nsy; iy++)
                 for (int ix = 0; ix < nsx; ix++) {

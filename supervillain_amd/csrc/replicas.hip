@@ -163,7 +163,7 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
     std::vector<SkipMap> skips(R);
     const int nsx = b->N <= RW ? 1 : (b->N + FW_MAX - 1) / FW_MAX;  // one full-row strip up to 128 columns
     // 64-row tiles, or 32 when that leaves the chip short of workgroups (measured: R=128, N=128)
-    const int TH = getenv("SV_FUSED_TH") ? fused_th() : ((int64_t)R * nsx * ((b->N + 63) / 64) < 768 ? 32 : 64);
+    const int TH = getenv("SV_FUSED_TH") ? fused_th(b->N, nsx) : ((int64_t)R * nsx * ((b->N + 63) / 64) < 768 ? 32 : 64);
     const int nsy = (b->N + TH - 1) / TH;
     const int tiles = nsx * nsy;
     std::vector<PlanIn> pin(R);

@@ -85,7 +85,7 @@ DevScratch scratch(sv_ctx *ctx);
 AbortInfo read_abort(sv_ctx *ctx);  // synchronizes the stream
 void clear_abort(sv_ctx *ctx);
 int64_t rejections_in(const SkipMap &skips, int sweep, int nblocks);
-int fused_th();
+int fused_th(int32_t N, int nsx);  // rows per strip (SV_FUSED_TH overrides)
 // launch villain_sweep_fused<4, true> (tile mode) with `grid` workgroups
 void launch_fused_tile(const FArgs &A, int grid, hipStream_t stream);
 // launch villain_sweep_fused<4, false, obs> over a replica batch (grid = replicas * tiles_per_rep)

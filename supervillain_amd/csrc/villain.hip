@@ -1095,11 +1095,25 @@ int fused_nw() {
     int v = e ? atoi(e) : 4;
     return v == 6 ? 6 : 4;
 }
-int fused_th() {
+// rows per strip.  52 measured best at L=4096 (322 us vs 328 at 64, 324 at 48, 345 at 80; r73 sweep).
+// Small lattices have few strips: there the strips are cut shorter (down to 4 rows, more halo rows
+// recomputed) until the grid has `fill` = 512 workgroups, so that every CU has work (SURVEY.md 8(d)
+// config 2; r203 sweep, us per sweep kernel: L=256 at 52 / 16 / 8 / 4 rows: 88.1 / 35.5 / 24.2 / 19.8;
+// L=1024 at 52 / 32 / 24 / 16 / 12 / 8 rows: 90.8 / 67.3 / 54.6 / 47.9 / 55.7 / 59.5).
+int fused_th(int32_t N, int nsx) {
     const char *e = getenv("SV_FUSED_TH");
-    // rows per strip: 52 measured best at L=4096 (322 us vs 328 at 64, 324 at 48, 345 at 80; r73 sweep)
-    int v = e ? atoi(e) : 52;
-    return v >= 8 && v % 4 == 0 ? v : 52;
+    if (e) {
+        const int v = atoi(e);
+        if (v >= 4 && v % 4 == 0) return v;
+    }
+    static const int fill = [] {
+        const char *f = getenv("SV_FUSED_FILL");
+        const int v = f ? atoi(f) : 512;
+        return v > 0 ? v : 512;
+    }();
+    int th = 52;
+    while (th > 4 && (int64_t)nsx * ((N + th - 1) / th) < fill) th -= 4;
+    return th;
 }
 
 bool fused_ok(int32_t N) { return N % 2 == 0 && N >= 4; }
@@ -1170,7 +1184,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     const int nb = (int)specs.size();
     const int nsx = (N + FW_MAX - 1) / FW_MAX;
     const int NWv = fused_nw();
-    const int TH = fused_th();
+    const int TH = fused_th(N, nsx);
     const int nsy = (N + TH - 1) / TH;
     const int grid = nsx * nsy;
     static const int BATCH = [] {  // sweeps per host round trip (SV_BATCH overrides; 64 measured best)

@@ -263,3 +263,55 @@ def test_config3_reference_order_plaquette_at_size(oracle_lib):
     s = oracle_lib.worldline_plaquette_seq(N, kappa, 1.0, m, v, (o[:, 0] % N) * N + (o[:, 1] % N), g)
     assert (np.asarray(cfg['m']) == m).all() and (np.asarray(cfg['v'])[0] == v).all()
     assert G.accepted == s.accepted and G.rng.bit_generator.state == g.bit_generator.state
+
+
+def _gpu_chain(N, kappa, W, mode, steps, seed):
+    """Plaquette (checkerboard or reference order) + Coexact per step on the GPU from a cold start, through the
+    C-ABI, fields resident on the device; the observables of tests/statparity.py per step."""
+    import ctypes
+    from supervillain_amd import _native
+    from supervillain_amd._abi import rng_from_numpy
+    from tests.statparity import NAMES, observables
+    Lib = _native.lib()
+    ctx = _native.context(_native.default_device())
+    h = ctypes.c_void_p()
+    ctx.check(Lib.sv_worldline_create(ctx.handle, N, 0, ctypes.byref(h)), 'create')
+    m = np.zeros((2, N, N), dtype=np.int64)
+    v = np.zeros((N, N), dtype=np.int64)
+    ctx.check(Lib.sv_worldline_upload(h, _native.ptr(m), _native.ptr(v)), 'upload')
+    r = rng_from_numpy(np.random.default_rng(seed))
+    legacy = np.random.RandomState(seed + 1)  # the reference's global-RandomState permutation (plaquette.py:63)
+    coords = np.array([(t, x) for t in range(N) for x in range(N)])
+    st = _native.stats_array(1)
+    out = np.empty((steps, len(NAMES)))
+    try:
+        for s in range(steps):
+            if mode == 'checkerboard':
+                ctx.check(Lib.sv_worldline_plaquette_checkerboard_run(h, kappa, W, 1, ctypes.byref(r), st), 'cb')
+            else:
+                o = legacy.permutation(coords)
+                lin = np.ascontiguousarray((o[:, 0] % N) * N + o[:, 1] % N, dtype=np.int64)
+                ctx.check(Lib.sv_worldline_plaquette_ordered_run(h, kappa, W, _native.ptr(lin), ctypes.byref(r), st),
+                          'ordered')
+            ctx.check(Lib.sv_worldline_coexact_run(h, kappa, W, 1, 1, ctypes.byref(r), st), 'coexact')
+            ctx.check(Lib.sv_worldline_download(h, _native.ptr(m), _native.ptr(v)), 'download')
+            out[s] = observables(m, v, kappa, W)
+    finally:
+        Lib.sv_worldline_destroy(h)
+    return out
+
+
+@pytest.mark.parametrize('N,steps', [(8, 20000), (16, 10000)])
+def test_plaquette_checkerboard_statistical_parity(N, steps):
+    """the checkerboard PlaquetteUpdate chain (the one config 3 benches) has the reference's
+    stationary distribution.  Checkerboard Plaquette + Coexact against the golden-pinned reference-order
+    Plaquette (plaquette.py:35-104) + Coexact, both on the GPU: blocked-bootstrap means of the Worldline action
+    density and the per-direction (m - delta v / W)^2 agree within 4 standard errors
+    (worldline-algorithm-comparison.py:38-95 is the reference's own template for such comparisons)."""
+    from tests.statparity import NAMES, compare
+    cb = _gpu_chain(N, 0.5, 1.0, 'checkerboard', steps, 1)
+    ref = _gpu_chain(N, 0.5, 1.0, 'reference', steps, 2)
+    zs = compare(cb, ref, steps // 20)
+    for name, (z, ma, ea, mb, eb) in zs.items():
+        assert abs(z) < 4.0, f'N={N} {name}: checkerboard {ma:.5f} +- {ea:.5f} vs reference order {mb:.5f} +- {eb:.5f}'
+    assert all(0 < zs[n][2] < 0.01 for n in NAMES)
