@@ -1,0 +1,382 @@
+// fused.h -- device helpers shared by the fused sweep kernels (villain.hip: the general fused kernel,
+// villain_hot.hip: the fast-draw kernel): NumPy-stream draws by position, rejection reports, statistics,
+// the LDS small-offset jump table.
+#pragma once
+#include "villain.h"
+
+namespace sv {
+
+#ifndef TWO_PI
+#define TWO_PI 6.283185307179586
+#endif
+
+// Block order inside one sweep's descriptor array:
+//   [0] metropolis (uniform V), then per colour c: [1+5c] dphi (uniform), [2+5c] fwd mu=0,
+//   [3+5c] bwd mu=0, [4+5c] fwd mu=1, [5+5c] bwd mu=1 (bounded choice).
+__device__ __forceinline__ u128 block_base(const Block &b) { return u128{b.base_lo, b.base_hi}; }
+
+__device__ __forceinline__ void report(const DevScratch &S, uint32_t sweep, uint32_t block, uint32_t pos,
+                                       uint32_t rep = 0) {
+    uint32_t i = atomicAdd(S.nreport, 1u);
+    if (i < (uint32_t)MAX_REPORTS) S.reports[i] = Report{sweep, block, pos, rep};
+    __hip_atomic_store(S.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // drain here, on the rare path: a result still pending at the join would make the compiler wait
+    // for every outstanding load and store (the row prefetch, the finished-row stores) on the common path
+    __builtin_amdgcn_s_waitcnt(0);
+}
+
+// stream position of bounded draw d, accounting for known rejected positions (sorted)
+__device__ __forceinline__ uint32_t skip_pos(const Block &b, const uint32_t *skips, uint32_t d) {
+    uint32_t q = d;
+    for (int i = 0; i < b.nskip; i++)
+        if (skips[b.skip0 + i] <= q) q++;
+    return q;
+}
+
+// uint32 at stream position q of a bounded block, by full jump from the block base
+__device__ __forceinline__ uint32_t bounded_word(const JumpTables *T, const Block &b, uint32_t q) {
+    if (b.has && q == 0) return b.buf;
+    uint32_t qq = q - b.has;
+    uint64_t X = xsl_rr(jump(T, block_base(b), qq >> 1));
+    return (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
+}
+
+// bounded draw d (index into the choice array), any path; reports rejections
+__device__ __forceinline__ int64_t bounded_draw(const JumpTables *T, const Block &b, const uint32_t *skips, uint32_t d,
+                                                const VParams &P, const DevScratch &S, uint32_t sweep, uint32_t bidx) {
+    uint32_t q = skip_pos(b, skips, d);
+    bool rej;
+    uint32_t idx = lemire(bounded_word(T, b, q), P.k, P.thr, &rej);
+    if (rej) report(S, sweep, bidx, q);
+    return P.W * ((int64_t)idx - P.interval_n);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// One atomic pair per WORKGROUP (every thread must call this): same-address atomics from thousands
+// of waves serialize in one L2 channel.
+__device__ __forceinline__ void flush_stats(sv_stats *st, int64_t acc, double psum) {
+    __shared__ unsigned long long s_acc[16];
+    __shared__ double s_ps[16];
+    unsigned long long a = (unsigned long long)acc;
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+    psum = wave_sum(psum);
+    if ((threadIdx.x & 63) == 0) {
+        s_acc[threadIdx.x >> 6] = a;
+        s_ps[threadIdx.x >> 6] = psum;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long ta = 0;
+        double tp = 0.0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); w++) {
+            ta += s_acc[w];
+            tp += s_ps[w];
+        }
+        atomicAdd((unsigned long long *)&st->accepted, ta);
+        unsafeAtomicAdd(&st->acceptance_sum, tp);  // hardware f64 atomic (coarse-grained HBM)
+    }
+}
+
+template <int NW>
+struct FusedGeom {
+    static constexpr int R = 2 * NW + 3;  // ring rows: outputs t.. up to prefetched rows t+2+2NW
+};
+
+
+
+// v mod N for v in [-2N, 3N) without a division
+__device__ __forceinline__ int32_t wrapN(int32_t v, int32_t N) {
+    v = v < 0 ? v + N : v;
+    v = v < 0 ? v + N : v;
+    v = v >= N ? v - N : v;
+    v = v >= N ? v - N : v;
+    return v;
+}
+
+#ifndef SV_SCALAR_WAVE
+#define SV_SCALAR_WAVE 1
+#endif
+#ifndef SV_ABLATE
+#define SV_ABLATE 0  // timing experiments only: 1 = no exp, 2 = no RNG compositions, 4 = no wrapped-column jumps,
+                     // 8 = no HBM stores, 16 = no HBM loads, 64 = no choice draws
+#endif
+__device__ __forceinline__ double sv_exp(double x) {
+#if SV_ABLATE & 1
+    return 1.0 + x * 0.5;
+#else
+    return exp(x);
+#endif
+}
+__device__ __forceinline__ u128 sv_apply(const Affine &f, u128 s) {
+#if SV_ABLATE & 2
+    return u128{s.lo ^ f.A.lo, s.hi + f.C.hi};
+#else
+    return apply(f, s);
+#endif
+}
+
+__device__ __forceinline__ u128 readlane128(u128 v, int lane) {
+    u128 r;
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v.lo, lane);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v.lo >> 32), lane);
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v.hi, lane);
+    const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v.hi >> 32), lane);
+    r.lo = ((uint64_t)b << 32) | a;
+    r.hi = ((uint64_t)d << 32) | c;
+    return r;
+}
+
+// Row-base position of block type `ty` (0 metropolis, 1 dphi, 2..5 bounded words) for global row gq.
+// Bases sit at column xb, the strip's first non-wrapped region column.
+__device__ __forceinline__ int64_t base_pos(int ty, int64_t gq, int64_t N, int64_t xb, uint32_t has) {
+    const int64_t lin = gq * N + xb;
+    if (ty == 0) return lin;
+    const int64_t rank = lin >> 1;
+    if (ty == 1) return rank;
+    const int64_t p = rank - (int64_t)has;
+    return p < 0 ? 0 : (p >> 1);
+}
+
+// The small-offset maps in LDS as two arrays (A, C) of 16-B entries: lanes read consecutive entries, and
+// at a 16-B stride the 16 lanes of a ds_read_b128 group hit 64 distinct banks (the 64-B Affine stride of
+// an array of structs put 4 lanes on each bank).
+struct alignas(16) SmallTab {
+    u128 A[SMALL_LDS];
+    u128 C[SMALL_LDS];
+    __device__ __forceinline__ Affine operator[](int64_t i) const { return Affine{A[i], C[i]}; }
+};
+
+struct Draws {
+    double u, dphi;
+    int32_t cn[4];  // W * (choice - interval_n); |W * interval_n| < 2^28 on this path
+};
+
+// Slow paths (branched around when no lane needs them).  The trailing wait keeps table loads from
+// leaving a pending-VMEM hazard on merged values, which would drain the row prefetch early.
+__device__ __forceinline__ u128 full_jump(const JumpTables *T, const Block *blk, uint32_t pos) {
+    u128 r = jump(T, block_base(*blk), pos);
+    __builtin_amdgcn_s_waitcnt(0);
+    return r;
+}
+
+__device__ __forceinline__ u128 from_base(const JumpTables *T, const Block *blk, const SmallTab &sm, u128 base,
+                                          int64_t bpos, int64_t pos) {
+    const int64_t off = pos - bpos;
+    u128 st;
+    if (off >= 0 && off < SMALL_LDS) st = apply(sm[off], base);
+#if SV_ABLATE & 4
+    else st = apply(sm[off & (SMALL_LDS - 1)], base);  // timing experiment: no full jumps at wrapped columns
+#else
+    else st = full_jump(T, blk, (uint32_t)pos);
+#endif
+    return st;
+}
+
+// What one workgroup's replica reads: its sweep descriptors and its PCG64 jump tables.
+struct Rep {
+    const Block *blocks;
+    const JumpTables *T;
+    uint32_t id;
+};
+
+template <bool K3 = false>
+__device__ __forceinline__ int32_t choice_value(const FArgs &A, const Rep &RP, uint32_t word, uint32_t bidx,
+                                                uint32_t spos) {
+    if constexpr (K3) {
+        // choice((-1, 0, 1)) (interval_n = 1): 3x by one shift-add, Lemire threshold (2^32 - 3) % 3 = 1 (a
+        // rejection iff the low word is 0), the value a select instead of W * (idx - 1)
+        const uint64_t m = ((uint64_t)word << 1) + word;
+        if ((uint32_t)m == 0u) report(A.S, A.sweep, bidx, spos, RP.id);
+        const uint32_t idx = (uint32_t)(m >> 32);
+        const int32_t w = (int32_t)A.P.W;
+        return idx == 0 ? -w : (idx == 1 ? 0 : w);
+    } else {
+        bool rej;
+        const uint32_t idx = lemire(word, A.P.k, A.P.thr, &rej);
+        if (rej) report(A.S, A.sweep, bidx, spos, RP.id);
+        return (int32_t)A.P.W * ((int32_t)idx - (int32_t)A.P.interval_n);
+    }
+}
+
+// General draws: any strip (wrapped columns), skips, mismatched buffers.  6 compositions per site.
+// Columns of an edge strip that wrap around the lattice (global columns outside [xb, xb + RW)) draw
+// from the wave's second set of row bases `wb`, kept at global column xw, so no lane needs a full jump.
+template <bool K3 = false>
+__device__ __forceinline__ Draws draws_general(const FArgs &A, const Rep &RP, int c, bool active, int64_t gq, int64_t gx,
+                                               int64_t xb, const u128 *bases, const SmallTab &sm, bool edge,
+                                               int64_t xw, const u128 *wb) {
+    const JumpTables *T = RP.T;
+    const int64_t N = A.G.Nx;  // row length of the global stream layout
+    const int bb = 1 + 5 * c;
+    const int64_t lin = gq * N + gx, rank = lin >> 1;
+    Draws D;
+    D.u = 0.0;
+    D.dphi = 0.0;
+    D.cn[0] = D.cn[1] = D.cn[2] = D.cn[3] = 0;
+    if (!active) return D;
+    const bool wr = edge && (gx < xb || gx >= xb + RW);
+    const int64_t xr = wr ? xw : xb;
+    D.u = 0.0 + 1.0 * to_double(xsl_rr(from_base(T, &RP.blocks[0], sm, wr ? wb[0] : bases[0], gq * N + xr, lin)));
+    D.dphi = A.P.lo_phi + A.P.range_phi * to_double(xsl_rr(from_base(T, &RP.blocks[bb], sm, wr ? wb[1] : bases[1],
+                                                                     (gq * N + xr) >> 1, rank)));
+    if (A.P.k > 1) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const Block *B = &RP.blocks[bb + 1 + q];
+            uint32_t word, spos = (uint32_t)rank;
+            if (B->nskip == 0) {
+                const int64_t qq = rank - (int64_t)B->has;
+                const int64_t wi = qq < 0 ? 0 : (qq >> 1);
+                const uint64_t X = xsl_rr(from_base(T, B, sm, wr ? wb[2 + q] : bases[2 + q], base_pos(2, gq, N, xr, B->has), wi));
+                word = (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
+                if (qq < 0) word = B->buf;  // has && rank == 0: the buffered half-word
+            } else {
+                spos = skip_pos(*B, A.skips, (uint32_t)rank);
+                word = bounded_word(T, *B, spos);
+                __builtin_amdgcn_s_waitcnt(0);
+            }
+            D.cn[q] = choice_value<K3>(A, RP, word, (uint32_t)(bb + 1 + q), spos);
+        }
+    }
+    return D;
+}
+
+// Fast draws for interior strips (no wrapped columns, no skips, equal buffers within each
+// forward/backward pair).  4 compositions per site: the fwd and bwd choice blocks of a direction
+// read the SAME u64 word for two adjacent lanes (its two 32-bit halves), so each lane of a pair
+// computes one block's word and swaps the other half with its partner.
+// Per-lane constants of the fast draws, packed in one register per colour: the small-table offsets of
+// the metropolis (bits 0-6), dphi (7-13) and the two choice words (14-20, 21-27) and which half of
+// each word pair the lane computes (28, 29).  They are the same for every row a wave visits (rows
+// advance NW = 4 at a time, so every parity involved is fixed), hence computed once per kernel.
+__device__ __forceinline__ uint32_t fast_pack(const uint32_t *hasw, int32_t lane, uint32_t rowlin, uint32_t xs,
+                                              uint32_t gx, uint32_t xb) {
+    const uint32_t lin = rowlin + gx, rank = lin >> 1;
+    const uint32_t PR = (rowlin + xb) >> 1;
+    uint32_t pk = ((gx - xb) & (SMALL_LDS - 1)) | (((rank - PR) & (SMALL_LDS - 1)) << 7);
+    const uint32_t R0 = (rowlin + xs) >> 1;  // rank of lane 0
+#pragma unroll
+    for (int mu = 0; mu < 2; mu++) {
+        const uint32_t h = hasw[mu];
+        const uint32_t P = (R0 - h) & 1u;   // pairing parity of the row
+        const uint32_t PW = (PR - h) >> 1;  // word index of the row base
+        uint32_t qq = rank - h;
+        if (lane == 63 && P) qq = R0 - h;  // lane 63 serves lane 0's word
+        const uint32_t half = (lane == 63 && P) ? 0u : (qq & 1u);
+        pk |= (((qq >> 1) - PW) & (SMALL_LDS - 1)) << (14 + 7 * mu);
+        pk |= half << (28 + mu);
+    }
+    return pk;
+}
+
+// The row bases are the same for every lane of a wave (one row per wave): held in SGPRs they feed the
+// 128-bit multiplies as scalar operands instead of occupying VGPRs.
+#ifndef SV_K3
+#define SV_K3 0  // choice((-1, 0, 1)) specialised at compile time: measured slower (329.5 vs 320.5 us, r92)
+#endif
+#ifndef SV_FR_FAST
+#define SV_FR_FAST 1
+#endif
+#ifndef SV_SCALAR_BASES
+#define SV_SCALAR_BASES 0  // measured slower: 339 vs 320 us per L=4096 sweep (SGPR spills, readfirstlane chains)
+#endif
+__device__ __forceinline__ u128 wave_uniform(u128 v) {
+#if SV_SCALAR_BASES
+    auto rf = [](uint64_t x) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+        return ((uint64_t)hi << 32) | lo;
+    };
+    return u128{rf(v.lo), rf(v.hi)};
+#else
+    return v;
+#endif
+}
+
+template <bool K3 = false>
+__device__ __forceinline__ Draws draws_fastp(const FArgs &A, const Rep &RP, int c, bool active, int32_t lane,
+                                             uint32_t pk, uint32_t rank, const u128 *bases, const SmallTab &sm) {
+    const int bb = 1 + 5 * c;
+    Draws D;
+    {
+        const u128 st = sv_apply(sm[pk & (SMALL_LDS - 1)], bases[0]);
+        D.u = 0.0 + 1.0 * to_double(xsl_rr(st));
+    }
+    {
+        const u128 st = sv_apply(sm[(pk >> 7) & (SMALL_LDS - 1)], bases[1]);
+        D.dphi = A.P.lo_phi + A.P.range_phi * to_double(xsl_rr(st));
+    }
+    D.cn[0] = D.cn[1] = D.cn[2] = D.cn[3] = 0;
+    if (!(SV_ABLATE & 64) && A.P.k > 1) {
+#pragma unroll
+        for (int mu = 0; mu < 2; mu++) {
+            const uint32_t half = (pk >> (28 + mu)) & 1u;
+            const u128 st = sv_apply(sm[(pk >> (14 + 7 * mu)) & (SMALL_LDS - 1)], half ? bases[3 + 2 * mu] : bases[2 + 2 * mu]);
+            const uint64_t X = xsl_rr(st);
+            // lo lanes computed the fwd word (send its high half), hi lanes the bwd word (send its low half)
+            const uint32_t send = half ? (uint32_t)X : (uint32_t)(X >> 32);
+            const int partner = half ? ((lane - 1) & 63) : lane + 1;
+            const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute(partner << 2, (int)send);
+            const uint32_t wf = half ? got : (uint32_t)X;
+            const uint32_t wb = half ? (uint32_t)(X >> 32) : got;
+            if (active) {
+                D.cn[2 * mu] = choice_value<K3>(A, RP, wf, (uint32_t)(bb + 1 + 2 * mu), rank);
+                D.cn[2 * mu + 1] = choice_value<K3>(A, RP, wb, (uint32_t)(bb + 2 + 2 * mu), rank);
+            }
+        }
+    }
+    return D;
+}
+
+template <bool K3 = false>
+__device__ __forceinline__ Draws draws_fast(const FArgs &A, const Rep &RP, int c, const uint32_t *hasw, bool active,
+                                            int32_t lane, uint32_t rowlin,
+                                            uint32_t xs, uint32_t gx, uint32_t xb, const u128 *bases,
+                                            const SmallTab &sm) {
+    const int bb = 1 + 5 * c;
+    const uint32_t lin = rowlin + gx, rank = lin >> 1;
+    const uint32_t PM = rowlin + xb, PR = PM >> 1;
+    Draws D;
+    {
+        const u128 st = sv_apply(sm[(gx - xb) & (SMALL_LDS - 1)], bases[0]);
+        D.u = 0.0 + 1.0 * to_double(xsl_rr(st));
+    }
+    {
+        const u128 st = sv_apply(sm[(rank - PR) & (SMALL_LDS - 1)], bases[1]);
+        D.dphi = A.P.lo_phi + A.P.range_phi * to_double(xsl_rr(st));
+    }
+    D.cn[0] = D.cn[1] = D.cn[2] = D.cn[3] = 0;
+    if (!(SV_ABLATE & 64) && A.P.k > 1) {
+        const uint32_t R0 = (rowlin + xs) >> 1;  // rank of lane 0
+#pragma unroll
+        for (int mu = 0; mu < 2; mu++) {
+            const uint32_t h = hasw[mu];  // has of this direction's fwd (= bwd) choice block, preloaded
+            const uint32_t P = (R0 - h) & 1u;                        // pairing parity of this row
+            const uint32_t PW = (PR - h) >> 1;                       // word index of the row base
+            uint32_t qq = rank - h;
+            if (lane == 63 && P) qq = R0 - h;                        // lane 63 serves lane 0's word
+            const uint32_t half = (lane == 63 && P) ? 0u : (qq & 1u);
+            const uint32_t w = qq >> 1;
+            const u128 st = sv_apply(sm[(w - PW) & (SMALL_LDS - 1)], half ? bases[3 + 2 * mu] : bases[2 + 2 * mu]);
+            const uint64_t X = xsl_rr(st);
+            // lo lanes computed the fwd word (send its high half), hi lanes the bwd word (send its low half)
+            const uint32_t send = half ? (uint32_t)X : (uint32_t)(X >> 32);
+            const int partner = half ? (lane == 0 ? 63 : lane - 1) : lane + 1;
+            const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute(partner << 2, (int)send);
+            const uint32_t wf = half ? got : (uint32_t)X;
+            const uint32_t wb = half ? (uint32_t)(X >> 32) : got;
+            if (active) {
+                D.cn[2 * mu] = choice_value<K3>(A, RP, wf, (uint32_t)(bb + 1 + 2 * mu), rank);
+                D.cn[2 * mu + 1] = choice_value<K3>(A, RP, wb, (uint32_t)(bb + 2 + 2 * mu), rank);
+            }
+        }
+    }
+    return D;
+}
+
+}  // namespace sv

@@ -90,6 +90,10 @@ int fused_th(int32_t N, int nsx);  // rows per strip (SV_FUSED_TH overrides)
 void launch_fused_tile(const FArgs &A, int grid, hipStream_t stream);
 // launch villain_sweep_fused<4, false, obs> over a replica batch (grid = replicas * tiles_per_rep)
 void launch_fused_batch(const FArgs &A, int grid, bool obs, hipStream_t stream);
+// villain_hot.hip: whether the fast-draw kernel covers the sweep whose 11 descriptors start at `blocks`,
+// and its launch (periodic single lattice or a domain tile, from the geometry)
+bool hot_ok(const VParams &P, const Block *blocks);
+void launch_hot(const FArgs &A, int grid, hipStream_t stream);
 // plain single-lattice FArgs defaults (one replica, no observables)
 void farg_single(FArgs &A, int nsx, int nsy);
 

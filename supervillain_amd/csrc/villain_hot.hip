@@ -1,0 +1,537 @@
+// villain_hot.hip -- the headline sweep kernel: one NeighborhoodUpdate sweep
+// (supervillain/generator/villain/neighborhood.py:59-137), both colours, in one launch.
+//
+// Same decomposition and exact arithmetic as villain.hip's villain_sweep_fused (column strips streamed
+// through an LDS ring of rows), specialised to the sweeps that make up all but a few percent
+// of a chain -- no NumPy Lemire rejection known in the sweep's choice blocks, and equal buffered-half flags
+// within each forward/backward block pair -- so that the instruction stream carries nothing else:
+//
+//  * every strip draws from LDS-cached small-offset maps: interior strips with the paired choice words
+//    (4 PCG64 compositions per site-update), edge strips with a second row-base set at the first wrapped
+//    column and unpaired words (6 compositions, ~6% of the waves at L=4096);
+//  * the 128-bit affine step is written out with the carries of v_mad_u64_u32 (6 v_mad_u64_u32,
+//    4 v_mul_lo_u32, 4 v_addc: the compiler's form of the same product spends ~12 moves and 7 64-bit adds);
+//  * a rejected choice word is detected with one compare per word and reported on a rare branch;
+//  * what a rejected proposal leaves unchanged is not recomputed: phi is normalised (+0.0) once when a row
+//    enters LDS, and n, phi and the incremental r of neighborhood.py:129 are rewritten only by lanes whose
+//    proposal was accepted (0.7% of them at kappa = 0.5), behind a wave-uniform ballot.
+//
+// Exactness: every value that reaches phi or n is computed in the reference's operation order.
+// The residual r and dS reach nothing but exp(-dS); the `0.0 +` the reference's d() and face_sum() put in
+// front of them changes at most the sign of a zero, and exp(+-0) = 1.
+#include "fused.h"
+
+namespace sv {
+
+// ---- 128-bit affine step with explicit carries -------------------------------------------------------
+// Each carry-out of v_mad_u64_u32 is consumed in the same asm statement, through VCC: no SGPR pair stays live
+// (lane-mask carries held in SGPRs across statements spilled the kernel's scalar registers).
+// d = a*b + c (64-bit); (hi:lo) += carry-out, returned in place
+__device__ __forceinline__ uint64_t mad_kk(uint32_t a, uint32_t b, uint64_t c, uint32_t &lo, uint32_t &hi) {
+    uint64_t d;
+    asm("v_mad_u64_u32 %0, vcc, %3, %4, %5\n\t"
+        "v_addc_co_u32 %1, vcc, %1, 0, vcc\n\t"
+        "v_addc_co_u32 %2, vcc, %2, 0, vcc"
+        : "=&v"(d), "+v"(lo), "+v"(hi) : "v"(a), "v"(b), "v"(c) : "vcc");
+    return d;
+}
+// d = a*b + c (64-bit); x += carry-out
+__device__ __forceinline__ uint64_t mad_k(uint32_t a, uint32_t b, uint64_t c, uint32_t &x) {
+    uint64_t d;
+    asm("v_mad_u64_u32 %0, vcc, %2, %3, %4\n\t"
+        "v_addc_co_u32 %1, vcc, %1, 0, vcc"
+        : "=&v"(d), "+v"(x) : "v"(a), "v"(b), "v"(c) : "vcc");
+    return d;
+}
+// d = a*b + c (64-bit), carry-out dropped
+__device__ __forceinline__ uint64_t mad_n(uint32_t a, uint32_t b, uint64_t c) {
+    uint64_t d;
+    asm("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c) : "vcc");
+    return d;
+}
+
+// a*s + c (mod 2^128) on 32-bit limbs:
+//   T  = a0 s0 + (c1:c0)                 -> r0; its carry (weight 2^64) goes into (c3:c2)
+//   U  = a0 s1 + (c2:T.hi)                  carry (2^96) into c3
+//   U2 = a1 s0 + U                       -> r1; carry (2^96) into c3
+//   X  = a0 s2 + a1 s1 + a2 s0 + (c3:U2.hi) -> r2 (carries beyond 2^128 dropped)
+//   r3 = X.hi + lo(a0 s3 + a1 s2 + a2 s1 + a3 s0)
+__device__ __forceinline__ u128 mad128c(u128 a, u128 s, u128 c) {
+    const uint32_t a0 = (uint32_t)a.lo, a1 = (uint32_t)(a.lo >> 32), a2 = (uint32_t)a.hi, a3 = (uint32_t)(a.hi >> 32);
+    const uint32_t s0 = (uint32_t)s.lo, s1 = (uint32_t)(s.lo >> 32), s2 = (uint32_t)s.hi, s3 = (uint32_t)(s.hi >> 32);
+    uint32_t c2 = (uint32_t)c.hi, c3 = (uint32_t)(c.hi >> 32);
+    const uint64_t T = mad_kk(a0, s0, c.lo, c2, c3);
+    const uint64_t U = mad_k(a0, s1, ((uint64_t)c2 << 32) | (T >> 32), c3);
+    const uint64_t U2 = mad_k(a1, s0, U, c3);
+    uint64_t X = mad_n(a0, s2, ((uint64_t)c3 << 32) | (U2 >> 32));
+    X = mad_n(a1, s1, X);
+    X = mad_n(a2, s0, X);
+    const uint32_t r3 = (uint32_t)(X >> 32) + a0 * s3 + a1 * s2 + a2 * s1 + a3 * s0;
+    return u128{((U2 & 0xFFFFFFFFull) << 32) | (T & 0xFFFFFFFFull), ((uint64_t)r3 << 32) | (X & 0xFFFFFFFFull)};
+}
+__device__ __forceinline__ u128 hot_apply(const SmallTab &sm, uint32_t i, u128 base) {
+    return mad128c(sm.A[i], base, sm.C[i]);
+}
+
+// NumPy random(): (x >> 11) * 2^-53
+__device__ __forceinline__ double u53(uint64_t x) { return to_double(x); }
+
+struct HotDraws {
+    double u, dphi;
+    uint32_t w[4];  // the uint32 each choice block (f0, b0, f1, b1) draws for this site
+};
+
+// Interior strips: the fwd/bwd blocks of a direction read the two halves of one u64 for two adjacent lanes
+// (draws_fastp in fused.h explains the packing of pk)
+__device__ __forceinline__ HotDraws hot_draws_paired(const FArgs &A, int32_t lane, uint32_t pk, const u128 *bs,
+                                                     const SmallTab &sm) {
+    HotDraws D;
+    D.u = u53(xsl_rr(hot_apply(sm, pk & (SMALL_LDS - 1), bs[0])));
+    D.dphi = A.P.lo_phi + A.P.range_phi * u53(xsl_rr(hot_apply(sm, (pk >> 7) & (SMALL_LDS - 1), bs[1])));
+#pragma unroll
+    for (int mu = 0; mu < 2; mu++) {
+        const uint32_t half = (pk >> (28 + mu)) & 1u;
+        const uint64_t X = xsl_rr(hot_apply(sm, (pk >> (14 + 7 * mu)) & (SMALL_LDS - 1), half ? bs[3 + 2 * mu] : bs[2 + 2 * mu]));
+        // lo lanes computed the fwd word (send its high half), hi lanes the bwd word (send its low half)
+        const uint32_t send = half ? (uint32_t)X : (uint32_t)(X >> 32);
+        const int partner = half ? ((lane - 1) & 63) : lane + 1;
+        const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute(partner << 2, (int)send);
+        D.w[2 * mu] = half ? got : (uint32_t)X;
+        D.w[2 * mu + 1] = half ? (uint32_t)(X >> 32) : got;
+    }
+    return D;
+}
+
+// Edge strips: columns that wrap around the row draw from the second base set (at global column xw); every
+// offset is < SMALL_LDS by construction; words unpaired (the wrap breaks the lane pairing).
+__device__ __forceinline__ HotDraws hot_draws_edge(const FArgs &A, int64_t gq, int32_t gx, int32_t xb, int32_t xw,
+                                                   const u128 *bA, const u128 *bB, const SmallTab &sm,
+                                                   const uint32_t *has, const uint32_t *buf) {
+    const int64_t N = A.G.Nx;
+    const bool wr = !(gx >= xb && gx < xb + SMALL_LDS);
+    const int32_t xr = wr ? xw : xb;
+    const int64_t lin = gq * N + gx, rank = lin >> 1, rb = (gq * N + xr) >> 1;
+    HotDraws D;
+    D.u = u53(xsl_rr(hot_apply(sm, (uint32_t)(gx - xr), wr ? bB[0] : bA[0])));
+    D.dphi = A.P.lo_phi + A.P.range_phi * u53(xsl_rr(hot_apply(sm, (uint32_t)(rank - rb), wr ? bB[1] : bA[1])));
+#pragma unroll
+    for (int mu = 0; mu < 2; mu++) {
+        const int64_t qq = rank - (int64_t)has[mu];
+        const int64_t w0 = (rb - (int64_t)has[mu]) < 0 ? 0 : ((rb - (int64_t)has[mu]) >> 1);
+        const uint32_t off = (uint32_t)((qq < 0 ? 0 : (qq >> 1)) - w0);
+#pragma unroll
+        for (int fb = 0; fb < 2; fb++) {
+            const uint64_t X = xsl_rr(hot_apply(sm, off, wr ? bB[2 + 2 * mu + fb] : bA[2 + 2 * mu + fb]));
+            uint32_t word = (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
+            if (qq < 0) word = buf[2 * mu + fb];  // has && rank == 0: the block's buffered half-word
+            D.w[2 * mu + fb] = word;
+        }
+    }
+    return D;
+}
+
+// The workgroup's LDS (one allocation shared by the two bodies below)
+struct HotLDS {
+    static constexpr int R = FusedGeom<4>::R;
+    double phi[R][RW];
+    double r0[R][RW];
+    double r1[R][RW];
+    int32_t n0[R][RW];
+    int32_t n1[R][RW];
+    SmallTab small;
+    Affine adv[3];
+    u128 base[4][32];  // per wave: [8c + ty] block ty's base for the colour-c row at xb; [16 + ..] at xw
+    int32_t bad;
+};
+
+// EDGE: the strip's region wraps around the lattice rows (or sits within 4 columns of an edge); a
+// template parameter so that the two draw forms are two code paths, not one if-converted stream
+template <bool TILE, bool EDGE>
+__device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
+    constexpr int NW = 4;
+    constexpr int R = HotLDS::R;
+    constexpr int PF = RW / 64;
+    auto &s_phi = Ls.phi;
+    auto &s_r0 = Ls.r0;
+    auto &s_r1 = Ls.r1;
+    auto &s_n0 = Ls.n0;
+    auto &s_n1 = Ls.n1;
+    auto &s_small = Ls.small;
+    auto &s_adv = Ls.adv;
+    auto &s_base = Ls.base;
+    int32_t &s_bad = Ls.bad;
+
+    if (*(volatile const int32_t *)A.S.abort) return;
+
+    const FGeom &Gm = A.G;
+    const int32_t Nt = Gm.Nt, Nx = Gm.Nx;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+    const int64_t V = Gm.plane;
+    auto grow = [&](int32_t q) { return wrapN(Gm.T0 + q, Nt); };
+    auto mrow = [&](int32_t q) -> int64_t { return TILE ? Gm.org + (int64_t)q * Gm.pitch : (int64_t)wrapN(q, Nt) * Nx; };
+    auto mcol = [&](int32_t c) -> int32_t { return TILE ? c : wrapN(c, Nx); };
+    const int32_t par0 = (Gm.T0 + Gm.X0) & 1;
+
+    int b = blockIdx.x;
+    {
+        const int G = gridDim.x, per = G / 8, rem = G % 8;
+        const int xcd = b & 7, k = b >> 3;
+        b = xcd * per + (xcd < rem ? xcd : rem) + k;
+    }
+    if (TILE && A.strip_map) b = __builtin_amdgcn_readfirstlane(A.strip_map[b]);
+    const double *phi_in = A.phi_in;
+    const int64_t *n_in = A.n_in;
+    double *phi_out = A.phi_out;
+    int64_t *n_out = A.n_out;
+    const int ix = b % A.nsx, iy = b / A.nsx;
+    const int32_t x0 = (int32_t)((int64_t)ix * Gm.Wt / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * Gm.Wt / A.nsx);
+    const int32_t w = x1 - x0;
+    const int32_t t0 = iy * A.TH;
+    const int32_t t1 = t0 + A.TH < Gm.Ht ? t0 + A.TH : Gm.Ht;
+    const int32_t rbase = t0 - 2;  // local row 0
+    const int32_t cols = w + 5;
+    const int32_t cofs = x0 - 2;   // LDS column of local column x is x - cofs
+    const int32_t gx0 = Gm.X0 + x0;
+    const bool interior = gx0 >= 4 && gx0 + w + 2 < Nx;
+    const int32_t xb = ((Nx <= SMALL_LDS && !interior) || gx0 - 2 < 0) ? 0 : gx0 - 2;
+    constexpr bool edge = EDGE;
+    (void)interior;
+    const bool two_sets = edge && Nx > SMALL_LDS;   // wrapped columns need the second base set
+    const int32_t xw = gx0 - 2 < 0 ? Nx - 2 : 0;
+
+    for (int e = threadIdx.x; e < SMALL_LDS; e += NW * 64) {
+        s_small.A[e] = A.T->small[e].A;
+        s_small.C[e] = A.T->small[e].C;
+    }
+    if (threadIdx.x < 3) s_adv[threadIdx.x] = A.adv[threadIdx.x];
+    if (threadIdx.x == 0) s_bad = 0;
+
+    // per colour: the buffered-half flags and words of the choice blocks (equal within each fwd/bwd pair on
+    // this kernel), uniform
+    uint32_t has_c[2][2], buf_c[2][4];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+#pragma unroll
+        for (int mu = 0; mu < 2; mu++)
+            has_c[c][mu] = (uint32_t)__builtin_amdgcn_readfirstlane(A.blocks[2 + 5 * c + 2 * mu].has);
+        if (edge) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) buf_c[c][j] = (uint32_t)__builtin_amdgcn_readfirstlane(A.blocks[2 + 5 * c + j].buf);
+        }
+    }
+    const VParams P = A.P;
+    const uint32_t kc = P.k, thr = P.thr;
+    const int32_t Wn = (int32_t)P.W, nW = (int32_t)(P.W * P.interval_n);
+
+    // ---- register prefetch of region rows [ra, ra+NW): wave w moves row ra + w, lane l columns l, l + 64
+    double pf_phi[PF];
+    int64_t pf_n0[PF], pf_n1[PF];
+    int pf_gx[PF];
+#pragma unroll
+    for (int k = 0; k < PF; k++) pf_gx[k] = mcol(x0 - 2 + lane + 64 * k);
+    auto prefetch = [&](int32_t ra) {
+        const int32_t q = ra + wave;
+        if (q >= t0 - 2 && q <= t1 + 2) {
+            const int64_t g0 = mrow(q);
+#pragma unroll
+            for (int k = 0; k < PF; k++) {
+                if (lane + 64 * k < cols) {
+                    const int64_t g = g0 + pf_gx[k];
+                    pf_phi[k] = phi_in[g];
+                    pf_n0[k] = n_in[g];
+                    pf_n1[k] = n_in[V + g];
+                }
+            }
+        }
+    };
+    auto commit = [&](int32_t ra) {
+        const int32_t q = ra + wave;
+        if (q >= t0 - 2 && q <= t1 + 2) {
+            const int slot = (q - rbase) % R;
+            uint32_t bad = 0;
+#pragma unroll
+            for (int k = 0; k < PF; k++) {
+                const int cc = lane + 64 * k;
+                if (cc < cols) {
+                    // the +0.0 every site receives in one of the two colour passes (neighborhood.py:128),
+                    // applied up front: the accepted change is added to the normalised value
+                    s_phi[slot][cc] = pf_phi[k] + 0.0;
+                    const int32_t a = (int32_t)pf_n0[k], c = (int32_t)pf_n1[k];
+                    // the int32 image must hold n exactly, with headroom for one sweep's changes
+                    bad |= (uint32_t)((uint64_t)((pf_n0[k] >> 30) + 1) > 1) | (uint32_t)((uint64_t)((pf_n1[k] >> 30) + 1) > 1);
+                    s_n0[slot][cc] = a;
+                    s_n1[slot][cc] = c;
+                }
+            }
+            if (bad) s_bad = 1;
+        }
+    };
+
+    // ---- per-wave running row bases: lane 8c+ty holds block ty's base for this wave's colour-c row
+    // (at column xb); lanes 16 + 8c + ty the same at column xw (edge strips of rows longer than SMALL_LDS)
+    const bool base_lane = (lane & 7) < 6 && (lane < 16 || (two_sets && lane < 32));
+    const int bc = (lane >> 3) & 1, bty = lane & 7;
+    const int32_t bx = lane >= 16 ? xw : xb;
+    const int bblk = bty == 0 ? 0 : 1 + 5 * bc + bty - 1;
+    const uint32_t bhas = (base_lane && bty >= 2) ? A.blocks[bblk].has : 0u;
+    const int32_t tfirst = t0 - 3;
+    int32_t brow = tfirst + 2 - bc + wave;  // colour 0 row t+2+wave, colour 1 row t+1+wave
+    u128 bases{0, 0};
+    if (base_lane) bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)base_pos(bty, grow(brow), Nx, bx, bhas));
+    __builtin_amdgcn_s_waitcnt(0);
+    if (base_lane) s_base[wave][lane] = bases;
+
+    // paired-draw lane constants per colour (interior strips; valid for every row of this wave)
+    uint32_t pk0 = 0, pk1 = 0;
+    if constexpr (!edge) {
+        {
+            const int32_t q = tfirst + 2 + wave;
+            const int32_t xs = (x0 - 1) + ((par0 + q + x0 - 1) & 1);
+            pk0 = fast_pack(has_c[0], lane, (uint32_t)grow(q) * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
+                            (uint32_t)(Gm.X0 + xs + 2 * lane), (uint32_t)xb);
+        }
+        {
+            const int32_t q = tfirst + 1 + wave;
+            const int32_t xs = x0 + ((par0 + q + x0 + 1) & 1);
+            pk1 = fast_pack(has_c[1], lane, (uint32_t)grow(q) * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
+                            (uint32_t)(Gm.X0 + xs + 2 * lane), (uint32_t)xb);
+        }
+    }
+
+    int64_t acc_count = 0;
+    double psum = 0.0;
+
+    auto store_rows = [&](int32_t ra) {
+        const int32_t q = ra + wave;
+        if (q >= t0 && q < t1) {
+            const int slot = (q - rbase) % R;
+            const int64_t g0 = mrow(q) + x0;
+#pragma unroll
+            for (int k = 0; k < PF; k++) {
+                const int cc = lane + 64 * k;
+                if (cc < w) {
+                    const int64_t g = g0 + cc;
+                    phi_out[g] = s_phi[slot][cc + 2];
+                    n_out[g] = (int64_t)s_n0[slot][cc + 2];
+                    n_out[V + g] = (int64_t)s_n1[slot][cc + 2];
+                }
+            }
+        }
+    };
+
+    // draws of colour c for global row gq, local column x; the 4 choice values; a rejected word is reported
+    auto draw = [&](int c, int32_t q, int32_t x, bool active, HotDraws &D, int32_t cn[4]) {
+        const int32_t gq = grow(q);
+        u128 bs[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) bs[k] = s_base[wave][8 * c + k];
+        if constexpr (!edge) {
+            D = hot_draws_paired(A, lane, c == 0 ? pk0 : pk1, bs, s_small);
+        } else {
+            u128 bw[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) bw[k] = two_sets ? s_base[wave][16 + 8 * c + k] : bs[k];
+            D = hot_draws_edge(A, gq, wrapN(Gm.X0 + x, Nx), xb, two_sets ? xw : xb, bs, bw, s_small, has_c[c], buf_c[c]);
+        }
+        bool rej = false;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint64_t m = (uint64_t)D.w[j] * kc;
+            rej |= (uint32_t)m < thr;
+            cn[j] = (int32_t)(m >> 32) * Wn - nW;  // W * (index - interval_n), neighborhood.py:105-107
+        }
+        if (__builtin_expect(rej && active, 0)) {
+            const uint32_t rank = (uint32_t)(((int64_t)gq * Nx + wrapN(Gm.X0 + x, Nx)) >> 1);
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if ((uint32_t)((uint64_t)D.w[j] * kc) < thr) report(A.S, A.sweep, (uint32_t)(1 + 5 * c + 1 + j), rank);
+        }
+    };
+
+    for (int32_t ra = t0 - 2; ra < tfirst + 3 + NW; ra += NW) {
+        prefetch(ra);
+        commit(ra);
+    }
+    __syncthreads();
+
+    const double hk = P.half_kappa;
+    for (int32_t t = tfirst; t < t1; t += NW) {
+        prefetch(t + 3 + NW);
+        store_rows(t - NW);
+        // ---------------- colour 0 on row q = t+2+wave
+        {
+            const int32_t q = t + 2 + wave;
+            const bool row_ok = (q >= t0 - 1) && (q <= t1 + 1);
+            const int32_t xs = (x0 - 1) + ((par0 + q + x0 - 1) & 1);
+            const int32_t x = xs + 2 * lane;
+            const bool active = row_ok && x <= x1 + 1;
+            HotDraws D;
+            int32_t cn[4];
+            draw(0, q, x, active, D, cn);
+            if (active) {
+                const int lr = q - rbase;
+                const int sm = (lr - 1) % R, s0 = lr % R, sp = (lr + 1) % R;
+                const int cx = x - cofs, cp = cx + 1, cm = cx - 1;
+                const double ph = s_phi[s0][cx];
+                const int32_t n_f0 = s_n0[s0][cx], n_b0 = s_n0[sm][cx], n_f1 = s_n1[s0][cx], n_b1 = s_n1[s0][cm];
+                // r on the four links f0=(0,q,x), b0=(0,q-1,x), f1=(1,q,x), b1=(1,q,x-1) (neighborhood.py:91)
+                double r0[4];
+                r0[0] = (s_phi[sp][cx] - ph) - TWO_PI * (double)n_f0;
+                r0[1] = (ph - s_phi[sm][cx]) - TWO_PI * (double)n_b0;
+                r0[2] = (s_phi[s0][cp] - ph) - TWO_PI * (double)n_f1;
+                r0[3] = (ph - s_phi[s0][cm]) - TWO_PI * (double)n_b1;
+                double tc[4], cr[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) tc[k] = TWO_PI * (double)cn[k];
+                const double mdp = 0.0 - D.dphi;  // d(change_phi) on a forward link, neighborhood.py:110
+                cr[0] = mdp - tc[0];
+                cr[1] = D.dphi - tc[1];
+                cr[2] = mdp - tc[2];
+                cr[3] = D.dphi - tc[3];
+                double dS = (hk * cr[0]) * ((2.0 * r0[0]) + cr[0]);
+#pragma unroll
+                for (int k = 1; k < 4; k++) dS += (hk * cr[k]) * ((2.0 * r0[k]) + cr[k]);
+                double p = sv_exp(-dS);
+                p = p > 1.0 ? 1.0 : p;
+                const bool acc = D.u < p;
+                if (q >= t0 && q < t1 && x >= x0 && x < x1) {
+                    acc_count += acc;
+                    psum += p;
+                }
+                double wr[4] = {r0[0], r0[1], r0[2], r0[3]};
+                if (__builtin_amdgcn_ballot_w64(acc)) {
+                    if (acc) {
+                        // neighborhood.py:124-129: phi += change_phi, n += change_n, r += d(change_phi) - 2 pi change_n
+                        s_phi[s0][cx] = ph + D.dphi;
+                        s_n0[s0][cx] = n_f0 + cn[0];
+                        s_n0[sm][cx] = n_b0 + cn[1];
+                        s_n1[s0][cx] = n_f1 + cn[2];
+                        s_n1[s0][cm] = n_b1 + cn[3];
+                        wr[0] = (r0[0] + mdp) - tc[0];
+                        wr[1] = (r0[1] + D.dphi) - tc[1];
+                        wr[2] = (r0[2] + mdp) - tc[2];
+                        wr[3] = (r0[3] + D.dphi) - tc[3];
+                    }
+                }
+                s_r0[s0][cx] = wr[0];
+                s_r0[sm][cx] = wr[1];
+                s_r1[s0][cx] = wr[2];
+                s_r1[s0][cm] = wr[3];
+            }
+        }
+        __syncthreads();
+        // ---------------- colour 1 on row q = t+1+wave; rows t.. become final
+        {
+            const int32_t q = t + 1 + wave;
+            const bool row_ok = (q >= t0) && (q <= t1);
+            const int32_t xs = x0 + ((par0 + q + x0 + 1) & 1);
+            const int32_t x = xs + 2 * lane;
+            const bool active = row_ok && x <= x1;
+            HotDraws D;
+            int32_t cn[4];
+            draw(1, q, x, active, D, cn);
+            if (active) {
+                const int lr = q - rbase;
+                const int sm = (lr - 1) % R, s0 = lr % R;
+                const int cx = x - cofs, cm = cx - 1;
+                double ri[4];
+                ri[0] = s_r0[s0][cx];
+                ri[1] = s_r0[sm][cx];
+                ri[2] = s_r1[s0][cx];
+                ri[3] = s_r1[s0][cm];
+                double cr[4];
+                const double mdp = 0.0 - D.dphi;
+                cr[0] = mdp - TWO_PI * (double)cn[0];
+                cr[1] = D.dphi - TWO_PI * (double)cn[1];
+                cr[2] = mdp - TWO_PI * (double)cn[2];
+                cr[3] = D.dphi - TWO_PI * (double)cn[3];
+                double dS = (hk * cr[0]) * ((2.0 * ri[0]) + cr[0]);
+#pragma unroll
+                for (int k = 1; k < 4; k++) dS += (hk * cr[k]) * ((2.0 * ri[k]) + cr[k]);
+                double p = sv_exp(-dS);
+                p = p > 1.0 ? 1.0 : p;
+                const bool acc = D.u < p;
+                if (q >= t0 && q < t1 && x >= x0 && x < x1) {
+                    acc_count += acc;
+                    psum += p;
+                }
+                if (__builtin_amdgcn_ballot_w64(acc)) {
+                    if (acc) {
+                        s_phi[s0][cx] = s_phi[s0][cx] + D.dphi;
+                        s_n0[s0][cx] += cn[0];
+                        s_n0[sm][cx] += cn[1];
+                        s_n1[s0][cx] += cn[2];
+                        s_n1[s0][cm] += cn[3];
+                    }
+                }
+            }
+        }
+        commit(t + 3 + NW);
+        if (base_lane) {
+            const int64_t p_old = base_pos(bty, grow(brow), Nx, bx, bhas);
+            const int64_t p_new = base_pos(bty, grow(brow + NW), Nx, bx, bhas);
+            const int ai = bty == 0 ? 0 : (bty == 1 ? 1 : 2);
+            const int64_t step = bty == 0 ? (int64_t)NW * Nx : (bty == 1 ? (int64_t)NW * Nx / 2 : (int64_t)NW * Nx / 4);
+            if (p_new - p_old == step) bases = apply(s_adv[ai], bases);
+            else bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)p_new);
+            brow += NW;
+            s_base[wave][lane] = bases;
+        }
+        __syncthreads();
+    }
+    {
+        int32_t tl = tfirst;
+        while (tl + NW < t1) tl += NW;
+        store_rows(tl);
+    }
+    if (s_bad && threadIdx.x == 0) report(A.S, A.sweep, OVERFLOW_BLOCK, 0, 0);
+    flush_stats(A.stat, acc_count, psum);
+}
+
+template <bool TILE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void villain_sweep_hot(FArgs A) {
+    __shared__ HotLDS Ls;
+    // the strip this workgroup owns (the same mapping hot_body makes), to pick the body
+    int b = blockIdx.x;
+    {
+        const int G = gridDim.x, per = G / 8, rem = G % 8;
+        const int xcd = b & 7, k = b >> 3;
+        b = xcd * per + (xcd < rem ? xcd : rem) + k;
+    }
+    if (TILE && A.strip_map) b = A.strip_map[b];
+    const int ix = b % A.nsx;
+    const int32_t x0 = (int32_t)((int64_t)ix * A.G.Wt / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * A.G.Wt / A.nsx);
+    const int32_t gx0 = A.G.X0 + x0;
+    const bool interior = gx0 >= 4 && gx0 + (x1 - x0) + 2 < A.G.Nx;
+    if (__builtin_amdgcn_readfirstlane((int)interior)) hot_body<TILE, false>(A, Ls);
+    else hot_body<TILE, true>(A, Ls);
+}
+
+template __global__ void villain_sweep_hot<false>(FArgs);
+template __global__ void villain_sweep_hot<true>(FArgs);
+
+}  // namespace sv
+
+namespace svh {
+
+// The hot kernel covers a sweep when its choice blocks carry no skip list and each fwd/bwd pair has equal
+// buffered-half flags, and the choice values W (index - interval_n) fit int32
+bool hot_ok(const VParams &P, const Block *blocks) {
+    const int64_t aw = P.W < 0 ? -P.W : P.W;
+    if (P.k <= 1 || P.k > (1u << 20) || aw > (1 << 20) || aw * (int64_t)P.k >= (1 << 28)) return false;  // int32 values
+    for (int c = 0; c < 2; c++) {
+        const Block *B = blocks + 2 + 5 * c;
+        if (B[0].nskip || B[1].nskip || B[2].nskip || B[3].nskip) return false;
+        if (B[0].has != B[1].has || B[2].has != B[3].has) return false;
+    }
+    return true;
+}
+
+void launch_hot(const FArgs &A, int grid, hipStream_t stream) {
+    if (A.G.org == 0 && A.G.pitch == A.G.Nx && A.G.T0 == 0 && A.G.X0 == 0 && A.G.Ht == A.G.Nt && A.G.Wt == A.G.Nx)
+        villain_sweep_hot<false><<<grid, 4 * 64, 0, stream>>>(A);
+    else
+        villain_sweep_hot<true><<<grid, 4 * 64, 0, stream>>>(A);
+}
+
+}  // namespace svh
