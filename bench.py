@@ -104,7 +104,7 @@ def traffic_from_profiles(L):
     try:
         with open(path) as f:
             d = json.load(f)
-        e = d.get(f'villain_sweep_fused_L{L}')
+        e = d.get(f'villain_sweep_hot_L{L}') or d.get(f'villain_sweep_fused_L{L}')
         return None if e is None else float(e['hbm_bytes_per_launch'])
     except Exception:
         return None
@@ -181,7 +181,7 @@ def kernel_time(Lib, ctx):
 
 def report(args, world, sites_per_step, sites_per_launch, elapsed, acc, avg_launch_s, config, traffic_L,
            metric='lattice-site updates/sec (sweeps/s × L²), L=4096 Villain, 1→8 MI355X',
-           unit='lattice-site updates/s', kernel='villain_sweep_fused', alg_bytes=SURVEY_BYTES_PER_SITE,
+           unit='lattice-site updates/s', kernel='villain_sweep_hot', alg_bytes=SURVEY_BYTES_PER_SITE,
            min_bytes=FUSED_MIN_BYTES_PER_SITE, baseline=None, ctx=None, scaling=None):
     achieved = alg_bytes * sites_per_launch / avg_launch_s / 1e9
     ceiling = copy_ceiling(ctx) if ctx is not None and not getattr(args, 'no_copy_ceiling', False) else None
@@ -201,7 +201,7 @@ def report(args, world, sites_per_step, sites_per_launch, elapsed, acc, avg_laun
         'config': dict(config, kappa=args.kappa, W=args.W, acceptance_rate=acc),
         'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS,
-                     'traffic': traffic_from_profiles(traffic_L) if kernel == 'villain_sweep_fused' else None,
+                     'traffic': traffic_from_profiles(traffic_L) if kernel == 'villain_sweep_hot' else None,
                      'kernel': kernel, 'avg_launch_us': avg_launch_s * 1e6,
                      'alg_bytes_per_unit': alg_bytes,
                      'fused_min_bytes_per_unit': min_bytes,
@@ -641,7 +641,7 @@ def main():
     acc = sum(st[i].accepted for i in range(args.steps)) / (args.steps * L * L)
     rej = sum(st[i].rejections for i in range(args.steps))
     config = {'workload': f'L={L} Villain NeighborhoodUpdate sweep, kappa={args.kappa}, W={args.W}, '
-                          'bit-exact reference chain (PCG64 replay), fused two-colour sweep kernel',
+                          'bit-exact reference chain (PCG64 replay), fused two-colour sweep kernel (villain_sweep_hot)',
               'L': L, 'lattice': [L, L], 'path': args.path, 'parallelism': 'single GPU',
               'lemire_rejections_in_timed_steps': int(rej)}
     report(args, 1, L * L, L * L, t1 - t0, acc, avg_launch_s, config, L, ctx=ctx)

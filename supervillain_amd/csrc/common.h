@@ -149,6 +149,12 @@ struct sv_worldline {
     int64_t offset[4] = {0, 0, 0, 0};
     char *d_aux = nullptr;  // WrappingUpdate scratch (cycle proposals, dS, flags, pairwise plan)
     size_t aux_cap = 0;
+    // worldline_fused.hip reads (m, v) and writes the other buffer pair; the pointers swap per fused step
+    int64_t *m_alt = nullptr;
+    void *v_alt = nullptr;
+    int64_t *m_at_snap = nullptr;  // the (m, v) pointers a snapshot was taken from (restore puts them back)
+    void *v_at_snap = nullptr;
+    bool wf_off = false;           // |m| or |v| outgrew the fused kernel's int32 image: four-pass kernels only
 };
 
 #define SV_HIP(call)                                                                                   \

@@ -380,6 +380,8 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
         Cursor c = cur;
         plan_sweeps(ctx, c, inc, specs, sw, count, skips, blocks, skipvec);
         upload_plan(ctx, blocks, skipvec);
+        std::vector<char> hot(count);
+        for (int k = 0; k < count; k++) hot[k] = hot_enabled() && hot_ok(P, &blocks[(size_t)k * nb]);
         for (auto &Tl : d->tiles) SV_HIP(hipMemsetAsync(Tl.sum, 0, sizeof(Summary), ctx->stream));
         const int cur0 = d->cur;
         auto fargs = [&](sv_domain_tile &Tl, int k, int in, int out) {
@@ -419,7 +421,7 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
             const int in = d->cur, out = (d->cur + 1) % d->R;
             if (!d->split) {
                 exchange(d, ctx->stream);
-                for (auto &Tl : d->tiles) launch_fused_tile(fargs(Tl, k, in, out), nsx * nsy, ctx->stream);
+                for (auto &Tl : d->tiles) launch_fused_tile(fargs(Tl, k, in, out), nsx * nsy, ctx->stream, hot[k]);
             } else {
                 // A: interior strips of sweep k need the boundary strips of sweep k-1 (their input rows)
                 SV_HIP(hipStreamWaitEvent(A_, d->ev_boundary, 0));
@@ -429,14 +431,14 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
                     for (auto &Tl : d->tiles) {
                         FArgs A = fargs(Tl, k, in, out);
                         A.strip_map = d->d_strips;
-                        launch_fused_tile(A, d->n_interior, A_);
+                        launch_fused_tile(A, d->n_interior, A_, hot[k]);
                     }
                 SV_HIP(hipEventRecord(d->ev_interior, A_));
                 exchange(d, d->halo_stream);
                 for (auto &Tl : d->tiles) {
                     FArgs A = fargs(Tl, k, in, out);
                     A.strip_map = d->d_strips + d->n_interior;
-                    launch_fused_tile(A, d->n_boundary, d->halo_stream);
+                    launch_fused_tile(A, d->n_boundary, d->halo_stream, hot[k]);
                 }
                 SV_HIP(hipEventRecord(d->ev_boundary, d->halo_stream));
             }

@@ -616,8 +616,17 @@ int64_t rejections_in(const SkipMap &skips, int sweep, int nblocks) {
     return rj;
 }
 
-void launch_fused_tile(const FArgs &A, int grid, hipStream_t stream) {
-    villain_sweep_fused<4, true, false, false><<<grid, 4 * 64, 0, stream>>>(A);
+void launch_fused_tile(const FArgs &A, int grid, hipStream_t stream, bool hot) {
+    if (hot) launch_hot(A, grid, stream);
+    else villain_sweep_fused<4, true, false, false><<<grid, 4 * 64, 0, stream>>>(A);
+}
+
+bool hot_enabled() {  // SV_HOT=0: every sweep on villain_sweep_fused (A/B measurements)
+    static const bool on = [] {
+        const char *e = getenv("SV_HOT");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
 }
 
 void launch_fused_batch(const FArgs &A, int grid, bool obs, hipStream_t stream) {
@@ -830,10 +839,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     std::vector<uint32_t> skipvec;
     int sw = 0;
     const bool dbg = getenv("SV_DEBUG_TIMING") != nullptr;
-    static const bool use_hot = [] {  // SV_HOT=0: every sweep on villain_sweep_fused (A/B measurements)
-        const char *e = getenv("SV_HOT");
-        return !(e && atoi(e) == 0);
-    }();
+    const bool use_hot = hot_enabled();
     while (sw < sweeps) {
         const int count = std::min(BATCH, sweeps - sw);
         Cursor c = cur;

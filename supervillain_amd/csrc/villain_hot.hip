@@ -23,59 +23,6 @@
 
 namespace sv {
 
-// ---- 128-bit affine step with explicit carries -------------------------------------------------------
-// Each carry-out of v_mad_u64_u32 is consumed in the same asm statement, through VCC: no SGPR pair stays live
-// (lane-mask carries held in SGPRs across statements spilled the kernel's scalar registers).
-// d = a*b + c (64-bit); (hi:lo) += carry-out, returned in place
-__device__ __forceinline__ uint64_t mad_kk(uint32_t a, uint32_t b, uint64_t c, uint32_t &lo, uint32_t &hi) {
-    uint64_t d;
-    asm("v_mad_u64_u32 %0, vcc, %3, %4, %5\n\t"
-        "v_addc_co_u32 %1, vcc, %1, 0, vcc\n\t"
-        "v_addc_co_u32 %2, vcc, %2, 0, vcc"
-        : "=&v"(d), "+v"(lo), "+v"(hi) : "v"(a), "v"(b), "v"(c) : "vcc");
-    return d;
-}
-// d = a*b + c (64-bit); x += carry-out
-__device__ __forceinline__ uint64_t mad_k(uint32_t a, uint32_t b, uint64_t c, uint32_t &x) {
-    uint64_t d;
-    asm("v_mad_u64_u32 %0, vcc, %2, %3, %4\n\t"
-        "v_addc_co_u32 %1, vcc, %1, 0, vcc"
-        : "=&v"(d), "+v"(x) : "v"(a), "v"(b), "v"(c) : "vcc");
-    return d;
-}
-// d = a*b + c (64-bit), carry-out dropped
-__device__ __forceinline__ uint64_t mad_n(uint32_t a, uint32_t b, uint64_t c) {
-    uint64_t d;
-    asm("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c) : "vcc");
-    return d;
-}
-
-// a*s + c (mod 2^128) on 32-bit limbs:
-//   T  = a0 s0 + (c1:c0)                 -> r0; its carry (weight 2^64) goes into (c3:c2)
-//   U  = a0 s1 + (c2:T.hi)                  carry (2^96) into c3
-//   U2 = a1 s0 + U                       -> r1; carry (2^96) into c3
-//   X  = a0 s2 + a1 s1 + a2 s0 + (c3:U2.hi) -> r2 (carries beyond 2^128 dropped)
-//   r3 = X.hi + lo(a0 s3 + a1 s2 + a2 s1 + a3 s0)
-__device__ __forceinline__ u128 mad128c(u128 a, u128 s, u128 c) {
-    const uint32_t a0 = (uint32_t)a.lo, a1 = (uint32_t)(a.lo >> 32), a2 = (uint32_t)a.hi, a3 = (uint32_t)(a.hi >> 32);
-    const uint32_t s0 = (uint32_t)s.lo, s1 = (uint32_t)(s.lo >> 32), s2 = (uint32_t)s.hi, s3 = (uint32_t)(s.hi >> 32);
-    uint32_t c2 = (uint32_t)c.hi, c3 = (uint32_t)(c.hi >> 32);
-    const uint64_t T = mad_kk(a0, s0, c.lo, c2, c3);
-    const uint64_t U = mad_k(a0, s1, ((uint64_t)c2 << 32) | (T >> 32), c3);
-    const uint64_t U2 = mad_k(a1, s0, U, c3);
-    uint64_t X = mad_n(a0, s2, ((uint64_t)c3 << 32) | (U2 >> 32));
-    X = mad_n(a1, s1, X);
-    X = mad_n(a2, s0, X);
-    const uint32_t r3 = (uint32_t)(X >> 32) + a0 * s3 + a1 * s2 + a2 * s1 + a3 * s0;
-    return u128{((U2 & 0xFFFFFFFFull) << 32) | (T & 0xFFFFFFFFull), ((uint64_t)r3 << 32) | (X & 0xFFFFFFFFull)};
-}
-__device__ __forceinline__ u128 hot_apply(const SmallTab &sm, uint32_t i, u128 base) {
-    return mad128c(sm.A[i], base, sm.C[i]);
-}
-
-// NumPy random(): (x >> 11) * 2^-53
-__device__ __forceinline__ double u53(uint64_t x) { return to_double(x); }
-
 struct HotDraws {
     double u, dphi;
     uint32_t w[4];  // the uint32 each choice block (f0, b0, f1, b1) draws for this site
@@ -338,7 +285,8 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
         for (int j = 0; j < 4; j++) {
             const uint64_t m = (uint64_t)D.w[j] * kc;
             rej |= (uint32_t)m < thr;
-            cn[j] = (int32_t)(m >> 32) * Wn - nW;  // W * (index - interval_n), neighborhood.py:105-107
+            // W * (index - interval_n), neighborhood.py:105-107: one v_mad_i32_i24 (hot_ok bounds |W|, k < 2^20)
+            cn[j] = SV_HOT_MUL24 ? __mul24((int32_t)(m >> 32), Wn) - nW : (int32_t)(m >> 32) * Wn - nW;
         }
         if (__builtin_expect(rej && active, 0)) {
             const uint32_t rank = (uint32_t)(((int64_t)gq * Nx + wrapN(Gm.X0 + x, Nx)) >> 1);

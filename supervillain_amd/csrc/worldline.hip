@@ -15,6 +15,15 @@
 #include <cmath>
 
 #include "local.h"
+#include "fused.h"
+
+namespace svh {
+// worldline_fused.hip
+bool wf_ok(int32_t N, bool v_is_float, double W_eff, int64_t it, const sv::Block *blocks);
+void launch_wf(int32_t N, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in, int64_t *m_out,
+               int64_t *v_out, const sv::Block *blocks, const sv::JumpTables *T, const sv::Affine adv[3], void *pstat,
+               void *cstat, sv::DevScratch S, uint32_t sweep, hipStream_t stream);
+}  // namespace svh
 
 namespace sv {
 
@@ -46,33 +55,6 @@ __device__ __forceinline__ uint32_t wbounded(const JumpTables *T, const Block &b
     uint32_t idx = lemire(word, k, thr, &rej);
     if (rej) wreport(S, sweep, bidx, q);
     return idx;
-}
-
-__device__ __forceinline__ double wsum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
-// Per-sweep statistics are accumulated in NSTRIPE stripes (one 128-B line each) picked by workgroup:
-// thousands of short waves adding into ONE address serialize in one L2 channel (measured: ~200 us
-// per L=1024 colour pass).  fold_stripes sums them into the sweep's sv_stats in a fixed order.
-static constexpr int NSTRIPE = 16;
-struct StatStripe {
-    unsigned long long acc;
-    double psum;
-    uint64_t pad[14];
-};
-
-__device__ __forceinline__ void wflush(StatStripe *ss, int64_t acc, double psum) {
-    unsigned long long a = (unsigned long long)acc;
-    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
-    psum = wsum(psum);
-    if ((threadIdx.x & 63) == 0) {
-        StatStripe *st = ss + ((blockIdx.x + blockIdx.y * 7 + (threadIdx.x >> 6) * 3) & (NSTRIPE - 1));
-        atomicAdd(&st->acc, a);
-        unsafeAtomicAdd(&st->psum, psum);  // hardware f64 atomic (coarse-grained HBM)
-    }
 }
 
 __global__ void fold_stripes(const StatStripe *ss, sv_stats *out, int count) {
@@ -505,9 +487,15 @@ void snapshot(sv_worldline *st, bool restore) {
     const size_t V = (size_t)st->N * st->N;
     const size_t vb = V * (st->v_is_float ? sizeof(double) : sizeof(int64_t));
     if (!restore) {
+        st->m_at_snap = st->m;
+        st->v_at_snap = st->v;
         SV_HIP(hipMemcpyAsync(st->snap_m, st->m, 2 * V * sizeof(int64_t), hipMemcpyDeviceToDevice, ctx->stream));
         SV_HIP(hipMemcpyAsync(st->snap_v, st->v, vb, hipMemcpyDeviceToDevice, ctx->stream));
     } else {
+        if (st->m_at_snap && st->m != st->m_at_snap) {  // fused steps swapped the buffer pairs since the snapshot
+            std::swap(st->m, st->m_alt);
+            std::swap(st->v, st->v_alt);
+        }
         SV_HIP(hipMemcpyAsync(st->m, st->snap_m, 2 * V * sizeof(int64_t), hipMemcpyDeviceToDevice, ctx->stream));
         SV_HIP(hipMemcpyAsync(st->v, st->snap_v, vb, hipMemcpyDeviceToDevice, ctx->stream));
     }
@@ -546,7 +534,8 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
             hipEvent_t ev;
             ctx->time_begin(&ev);
             for (int k = 0; k < count; k++)
-                launch(ctx->d_blocks + (size_t)k * nb, ss + (size_t)k * nstat * NSTRIPE, (uint32_t)k);
+                launch(ctx->d_blocks + (size_t)k * nb, ss + (size_t)k * nstat * NSTRIPE, (uint32_t)k,
+                       blocks.data() + (size_t)k * nb);
             ctx->time_end(ev, count);
             fold_stripes<<<(count * nstat + 63) / 64, 64, 0, ctx->stream>>>(ss, ctx->d_stats, count * nstat);
             SV_HIP(hipGetLastError());
@@ -560,7 +549,11 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
                 break;
             }
             ctx->time_discard();
-            wabsorb(reps, sw, skips);
+            if (std::any_of(reps.begin(), reps.end(), [](const Report &r) { return r.block == OVERFLOW_BLOCK; })) {
+                st->wf_off = true;  // the fused kernel's int32 image cannot hold the state: replay on the pass kernels
+            } else {
+                wabsorb(reps, sw, skips);
+            }
             snapshot(st, true);
         }
         if (!may_reject) svh::loc::queue_abort_copy(ctx);
@@ -697,6 +690,8 @@ int sv_worldline_destroy(sv_worldline *st) {
     (void)hipFree(st->v);
     (void)hipFree(st->snap_m);
     (void)hipFree(st->snap_v);
+    (void)hipFree(st->m_alt);
+    (void)hipFree(st->v_alt);
     (void)hipFree(st->stripes);
     (void)hipFree(st->sites);
     if (st->f) (void)hipFree(st->f);
@@ -751,7 +746,7 @@ int sv_worldline_coexact_run(sv_worldline *st, double kappa, double W_eff, int64
         const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
         run_colour_sweeps(
             st, coexact_specs(st), sweeps, cur, inc, stats,
-            [&](const Block *blocks, StatStripe *stat, uint32_t k) { launch_coexact(st, P, blocks, stat, k, T); }, 1, {},
+            [&](const Block *blocks, StatStripe *stat, uint32_t k, const Block *) { launch_coexact(st, P, blocks, stat, k, T); }, 1, {},
             P.thr != 0);
         rng->state_hi = cur.s.hi;
         rng->state_lo = cur.s.lo;
@@ -787,7 +782,7 @@ int sv_worldline_plaquette_checkerboard_run(sv_worldline *st, double kappa, doub
         Cursor cur{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
         const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
         run_colour_sweeps(st, plaquette_cb_specs(st), sweeps, cur, inc, stats,
-                          [&](const Block *blocks, StatStripe *stat, uint32_t k) { launch_plaquette_cb(st, P, blocks, stat, k, T); });
+                          [&](const Block *blocks, StatStripe *stat, uint32_t k, const Block *) { launch_plaquette_cb(st, P, blocks, stat, k, T); });
         rng->state_hi = cur.s.hi;
         rng->state_lo = cur.s.lo;
         rng->has_uint32 = (int32_t)cur.has;
@@ -820,11 +815,28 @@ int sv_worldline_plaquette_coexact_run(sv_worldline *st, double kappa, double W_
         for (const BlockSpec &b : coexact_specs(st)) specs.push_back(b);
         std::vector<int> stat_of(specs.size(), 0);
         for (size_t b = np; b < specs.size(); b++) stat_of[b] = 1;
+        const char *wf_env = getenv("SV_WF");  // SV_WF=0: the four pass kernels only (A/B measurements)
+        const bool use_wf = !(wf_env && atoi(wf_env) == 0);
+        const int64_t N = st->N;
+        const Affine adv[3] = {host_power(inc, 4 * (uint64_t)N), host_power(inc, 2 * (uint64_t)N),
+                               host_power(inc, (uint64_t)N)};
+        if (use_wf && N % 2 == 0 && !st->v_is_float && !st->m_alt) {
+            SV_HIP(hipMalloc(&st->m_alt, 2 * (size_t)N * N * sizeof(int64_t)));
+            SV_HIP(hipMalloc(&st->v_alt, (size_t)N * N * sizeof(int64_t)));
+        }
         run_colour_sweeps(
             st, specs, sweeps, cur, inc, stats,
-            [&](const Block *blocks, StatStripe *stat, uint32_t k) {
-                launch_plaquette_cb(st, Pp, blocks, stat, k, T);
-                launch_coexact(st, Pc, blocks + np, stat + NSTRIPE, k, T);
+            [&](const Block *blocks, StatStripe *stat, uint32_t k, const Block *hblocks) {
+                if (use_wf && !st->wf_off && svh::wf_ok(st->N, st->v_is_float, W_eff, interval_t, hblocks)) {
+                    // one launch for the whole step (worldline_fused.hip); it writes the other buffer pair
+                    svh::launch_wf(st->N, kappa, W_eff, interval_t, st->m, (const int64_t *)st->v, st->m_alt, (int64_t *)st->v_alt,
+                              blocks, T, adv, stat, stat + NSTRIPE, wscratch(ctx), k, ctx->stream);
+                    std::swap(st->m, st->m_alt);
+                    std::swap(st->v, st->v_alt);
+                } else {
+                    launch_plaquette_cb(st, Pp, blocks, stat, k, T);
+                    launch_coexact(st, Pc, blocks + np, stat + NSTRIPE, k, T);
+                }
             },
             2, stat_of);
         rng->state_hi = cur.s.hi;

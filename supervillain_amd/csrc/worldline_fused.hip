@@ -1,0 +1,485 @@
+// worldline_fused.hip -- BASELINE config 3's step in one launch: a checkerboard PlaquetteUpdate sweep (both
+// colours, the GPU-native chain of worldline.hip: plaquette_cb_gs) followed by a CoexactUpdate sweep (both
+// colours, coexact.py:53-128: coexact_gs), i.e. exactly what sv_worldline_plaquette_coexact_run launches as
+// four colour passes, with the same per-plaquette arithmetic (bit-identical results).
+//
+// The four passes are plaquette-local checkerboard updates whose stencil reaches one row / column: a
+// plaquette (t, x) reads and writes its four boundary links m0[t][x], m0[t][x+1], m1[t][x], m1[t+1][x] and
+// reads v on (t, x) and its four neighbours (f = m - delta(v)/W).  So, as in villain_sweep_hot, a workgroup
+// owns a column strip of <= 119 columns and streams down its rows with an LDS ring, each pass one row behind
+// the one before it:  P0 on row t+3+w, P1 on t+2+w, C0 on t+1+w, C1 on t+w (wave w), a barrier between
+// passes.  A strip stores the links of its own sites, which the plaquettes one row above and one column to
+// the left also change, so C1 covers those halo plaquettes too and every earlier pass one more ring (P0 4
+// rows/columns above/left of the strip and 3 below/right); every draw is addressed by its NumPy stream
+// position, so neighbouring strips agree bit for bit.  The fields are read once and written once per step (m 16 B + v 8 B each way per
+// plaquette) instead of four read-modify-write passes.
+//
+// Covered steps: even N, integer v, W a power of two (f and df exact as the pass kernels form them), no
+// Lemire rejection known in the step's blocks and equal buffered-half flags in each colour's change_m /
+// change_v pair; the host keeps the four pass kernels for the rest (worldline.hip).
+#include "fused.h"
+
+namespace sv {
+
+static constexpr int WF_W = 119;          // output columns per strip: region = WF_W + 9 <= RW
+static constexpr int WF_NW = 4;
+// ring rows: at the end of step t the ring holds rows t-5..t+7 (P0 reads up to v[t+7]; C1 still reads
+// v[t-1]); the next rows t+8..t+11 go into the slots of t-5..t-2, stored at the start of steps t-4 and t
+static constexpr int WF_R = 3 * WF_NW + 1;
+
+struct WFArgs {
+    int32_t N;
+    int32_t nsx, TH, nsy;
+    const int64_t *m_in;
+    const int64_t *v_in;
+    int64_t *m_out;
+    int64_t *v_out;
+    const Block *blocks;  // 5 plaquette blocks ([0] metropolis, [1+2c] change_m, [2+2c] change_v), then 3 coexact
+    const JumpTables *T;  // ([5] metropolis, [6+c] t)
+    Affine adv[3];        // advance a row base by NW rows: [0] NW N draws, [2] NW N / 4 words
+    StatStripe *pstat, *cstat;
+    DevScratch S;
+    uint32_t sweep;
+    double Winv;  // 1 / W (W a power of two: x * Winv == x / W exactly)
+    double c;     // 0.5 / kappa (coexact)
+    double df[6], dfk[6];  // plaquette: df = cm - cv / W and df / kappa for index 3 jm + jv
+    int32_t it;            // coexact: t in -it..-1, 1..it
+    uint32_t kt, thrt;     // its choice count 2 it and Lemire threshold
+};
+
+struct WFLDS {
+    int32_t m0[WF_R][RW];
+    int32_t m1[WF_R][RW];
+    int32_t v[WF_R][RW];
+    SmallTab small;
+    Affine adv[3];
+    u128 base[WF_NW][64];  // per wave: lane 8p + ty = block ty's base for pass p's row at xb; 32 + .. at xw
+    double df[6], dfk[6];
+    int32_t bad;
+};
+
+// row-base stream position: uniform blocks by site, bounded blocks by u64 word of the colour rank
+__device__ __forceinline__ int64_t wf_base_pos(bool bounded, int64_t gq, int64_t N, int64_t xb, uint32_t has) {
+    const int64_t lin = gq * N + xb;
+    if (!bounded) return lin;
+    const int64_t p = (lin >> 1) - (int64_t)has;
+    return p < 0 ? 0 : (p >> 1);
+}
+
+// delta(v)/W on a link from the two v values its difference takes (worldline.hip dvw_p): mu = 0:
+// (double)(0 - (-diff)) / W, mu = 1: (double)(0 - diff) / W, with diff = v[s] - v[s - e_nu]
+__device__ __forceinline__ double wf_dv0(int32_t vs, int32_t vn, double Winv) { return (double)(vs - vn) * Winv; }
+__device__ __forceinline__ double wf_dv1(int32_t vs, int32_t vn, double Winv) { return (double)(-(vs - vn)) * Winv; }
+
+template <bool EDGE>
+__device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS &Ls) {
+    constexpr int NW = WF_NW, R = WF_R, PF = RW / 64;
+    auto &s_m0 = Ls.m0;
+    auto &s_m1 = Ls.m1;
+    auto &s_v = Ls.v;
+    auto &s_small = Ls.small;
+    if (*(volatile const int32_t *)A.S.abort) return;
+
+    const int32_t N = A.N;
+    const int64_t V = (int64_t)N * N;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+    int b = blockIdx.x;
+    {
+        const int G = gridDim.x, per = G / 8, rem = G % 8;
+        const int xcd = b & 7, k = b >> 3;
+        b = xcd * per + (xcd < rem ? xcd : rem) + k;
+    }
+    const int ix = b % A.nsx, iy = b / A.nsx;
+    const int32_t x0 = (int32_t)((int64_t)ix * N / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * N / A.nsx);
+    const int32_t w = x1 - x0;
+    const int32_t t0 = iy * A.TH;
+    const int32_t t1 = t0 + A.TH < N ? t0 + A.TH : N;
+    const int32_t rbase = t0 - 5;  // local row 0
+    const int32_t cols = w + 9;
+    const int32_t cofs = x0 - 5;   // LDS column of lattice column x is x - cofs
+    auto grow = [&](int32_t q) { return wrapN(q, N); };
+    // row bases at the first region column (interior strips), or at column 0 and at the first wrapped column
+    const int32_t xb = (N <= SMALL_LDS || x0 - 5 < 0) ? 0 : x0 - 5;
+    const bool two_sets = EDGE && N > SMALL_LDS;
+    const int32_t xw = x0 - 5 < 0 ? N - 5 : 0;
+
+    for (int e = threadIdx.x; e < SMALL_LDS; e += NW * 64) {
+        s_small.A[e] = A.T->small[e].A;
+        s_small.C[e] = A.T->small[e].C;
+    }
+    if (threadIdx.x < 3) Ls.adv[threadIdx.x] = A.adv[threadIdx.x];
+    if (threadIdx.x < 6) {
+        Ls.df[threadIdx.x] = A.df[threadIdx.x];
+        Ls.dfk[threadIdx.x] = A.dfk[threadIdx.x];
+    }
+    if (threadIdx.x == 0) Ls.bad = 0;
+    const double Winv = A.Winv, cc = A.c;
+    const int32_t it = A.it;
+    const uint32_t kt = A.kt, thrt = A.thrt;
+    // buffered-half flags (uniform): plaquette colour c's change_m / change_v pair, coexact colour c's t block
+    uint32_t hasp[2], bufp[2][2], hast[2], buft[2];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        hasp[c] = (uint32_t)__builtin_amdgcn_readfirstlane(A.blocks[1 + 2 * c].has);
+        bufp[c][0] = (uint32_t)__builtin_amdgcn_readfirstlane(A.blocks[1 + 2 * c].buf);
+        bufp[c][1] = (uint32_t)__builtin_amdgcn_readfirstlane(A.blocks[2 + 2 * c].buf);
+        hast[c] = (uint32_t)__builtin_amdgcn_readfirstlane(A.blocks[6 + c].has);
+        buft[c] = (uint32_t)__builtin_amdgcn_readfirstlane(A.blocks[6 + c].buf);
+    }
+
+    // ---- register prefetch of region rows [ra, ra+NW): wave w moves row ra + w, lane l columns l, l + 64
+    int64_t pf_m0[PF], pf_m1[PF], pf_v[PF];
+    int pf_gx[PF];
+#pragma unroll
+    for (int k = 0; k < PF; k++) pf_gx[k] = wrapN(x0 - 5 + lane + 64 * k, N);
+    auto prefetch = [&](int32_t ra) {
+        const int32_t q = ra + wave;
+        if (q >= t0 - 5 && q < t1 + 4) {
+            const int64_t g0 = (int64_t)grow(q) * N;
+#pragma unroll
+            for (int k = 0; k < PF; k++) {
+                if (lane + 64 * k < cols) {
+                    const int64_t g = g0 + pf_gx[k];
+                    pf_m0[k] = A.m_in[g];
+                    pf_m1[k] = A.m_in[V + g];
+                    pf_v[k] = A.v_in[g];
+                }
+            }
+        }
+    };
+    auto commit = [&](int32_t ra) {
+        const int32_t q = ra + wave;
+        if (q >= t0 - 5 && q < t1 + 4) {
+            const int slot = (q - rbase) % R;
+            uint32_t bad = 0;
+#pragma unroll
+            for (int k = 0; k < PF; k++) {
+                const int cx = lane + 64 * k;
+                if (cx < cols) {
+                    // the int32 image must hold the fields exactly, with headroom for one step's changes
+                    bad |= (uint32_t)((uint64_t)((pf_m0[k] >> 30) + 1) > 1) | (uint32_t)((uint64_t)((pf_m1[k] >> 30) + 1) > 1) |
+                           (uint32_t)((uint64_t)((pf_v[k] >> 30) + 1) > 1);
+                    s_m0[slot][cx] = (int32_t)pf_m0[k];
+                    s_m1[slot][cx] = (int32_t)pf_m1[k];
+                    s_v[slot][cx] = (int32_t)pf_v[k];
+                }
+            }
+            if (bad) Ls.bad = 1;
+        }
+    };
+    auto store_rows = [&](int32_t ra) {
+        const int32_t q = ra + wave;
+        if (q >= t0 && q < t1) {
+            const int slot = (q - rbase) % R;
+            const int64_t g0 = (int64_t)q * N + x0;
+#pragma unroll
+            for (int k = 0; k < PF; k++) {
+                const int cc2 = lane + 64 * k;
+                if (cc2 < w) {
+                    const int64_t g = g0 + cc2;
+                    A.m_out[g] = (int64_t)s_m0[slot][cc2 + 5];
+                    A.m_out[V + g] = (int64_t)s_m1[slot][cc2 + 5];
+                    A.v_out[g] = (int64_t)s_v[slot][cc2 + 5];
+                }
+            }
+        }
+    };
+
+    // ---- per-wave running row bases.  Pass p (0: plaquette colour 0, 1: plaquette colour 1, 2: coexact
+    // colour 0, 3: coexact colour 1) works on row t + 3 - p + wave; block types ty: plaquette 0 metropolis,
+    // 1 change_m, 2 change_v; coexact 0 metropolis, 1 t.
+    const int bp = (lane >> 3) & 3, bty = lane & 7;
+    const bool base_lane = bty < (bp < 2 ? 3 : 2) && (lane < 32 || (two_sets && lane < 64));
+    const int32_t bx = lane >= 32 ? xw : xb;
+    const int bblk = bp < 2 ? (bty == 0 ? 0 : bty + 2 * bp) : (bty == 0 ? 5 : 6 + (bp - 2));
+    const bool bbnd = bty != 0;
+    const uint32_t bhas = (base_lane && bbnd) ? A.blocks[bblk].has : 0u;
+    const int32_t tfirst = t0 - 7;
+    int32_t brow = tfirst + 3 - bp + wave;
+    u128 bases{0, 0};
+    if (base_lane) bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)wf_base_pos(bbnd, grow(brow), N, bx, bhas));
+    __builtin_amdgcn_s_waitcnt(0);
+    if (base_lane) Ls.base[wave][lane] = bases;
+
+    // the first column of pass p's colour on row q: pass p covers rows [t0 - 4 + p, t1 + 3 - p) and columns
+    // [x0 - 4 + p, x1 + 3 - p): the links a strip stores are also changed by the plaquettes one row above and
+    // one column left of it, so even the last pass (C1) covers those, and each earlier pass one more ring
+    auto first_col = [&](int p, int32_t q) {
+        const int32_t lo = x0 - (4 - p);
+        const int c = p & 1;
+        return lo + ((grow(q) + wrapN(lo, N) + c) & 1);  // (t + x) % 2 == c
+    };
+    // interior strips: per-lane constants of the paired plaquette draws (metropolis offset, change_m/change_v
+    // word offset, half), the same for every row of the wave (rows advance 4 at a time)
+    uint32_t pk[2] = {0, 0};
+    if constexpr (!EDGE) {
+#pragma unroll
+        for (int p = 0; p < 2; p++) {
+            const int32_t q = tfirst + 3 - p + wave;
+            const uint32_t rowlin = (uint32_t)grow(q) * (uint32_t)N;
+            const int32_t xs = first_col(p, q);
+            const uint32_t gx = (uint32_t)(xs + 2 * lane);
+            const uint32_t rank = (rowlin + gx) >> 1, R0 = (rowlin + (uint32_t)xs) >> 1;
+            const uint32_t h = hasp[p], PR = (rowlin + (uint32_t)xb) >> 1;
+            const uint32_t P = (R0 - h) & 1u, PW = (PR - h) >> 1;
+            uint32_t qq = rank - h;
+            if (lane == 63 && P) qq = R0 - h;  // lane 63 serves lane 0's word
+            const uint32_t half = (lane == 63 && P) ? 0u : (qq & 1u);
+            pk[p] = ((gx - (uint32_t)xb) & (SMALL_LDS - 1)) | ((((qq >> 1) - PW) & (SMALL_LDS - 1)) << 7) | (half << 14);
+        }
+    }
+
+    int64_t pacc = 0, cacc = 0;
+    double ppsum = 0.0, cpsum = 0.0;
+
+    // uniform draw and bounded word at stream offsets of row q's base (set A or, for wrapped columns, set B)
+    auto draw_u = [&](const u128 &base, uint32_t off) { return u53(xsl_rr(hot_apply(s_small, off & (SMALL_LDS - 1), base))); };
+    auto word_at = [&](const u128 &base, int64_t rank, uint32_t has, uint32_t buf, int64_t rb) {
+        const int64_t qq = rank - (int64_t)has;
+        const int64_t w0 = (rb - (int64_t)has) < 0 ? 0 : ((rb - (int64_t)has) >> 1);
+        const uint64_t X = xsl_rr(hot_apply(s_small, (uint32_t)((qq < 0 ? 0 : (qq >> 1)) - w0) & (SMALL_LDS - 1), base));
+        uint32_t word = (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
+        return qq < 0 ? buf : word;
+    };
+
+    // ---------------- plaquette pass (colour c = p) on row q
+    auto plaquette = [&](int p, int32_t q) {
+        const int c = p;
+        const bool row_ok = q >= t0 - (4 - p) && q < t1 + (3 - p);
+        const int32_t x = first_col(p, q) + 2 * lane;
+        const bool active = row_ok && x < x1 + (3 - p);
+        const int32_t gq = grow(q), gx = wrapN(x, N);
+        const u128 *bs = &Ls.base[wave][8 * p];
+        double u;
+        uint32_t wm, wv;
+        if constexpr (!EDGE) {
+            u = draw_u(bs[0], pk[p]);
+            const uint32_t half = (pk[p] >> 14) & 1u;
+            const uint64_t X = xsl_rr(hot_apply(s_small, (pk[p] >> 7) & (SMALL_LDS - 1), half ? bs[2] : bs[1]));
+            // lo lanes computed the change_m word (send its high half), hi lanes the change_v word
+            const uint32_t send = half ? (uint32_t)X : (uint32_t)(X >> 32);
+            const int partner = half ? ((lane - 1) & 63) : lane + 1;
+            const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute(partner << 2, (int)send);
+            wm = half ? got : (uint32_t)X;
+            wv = half ? (uint32_t)(X >> 32) : got;
+        } else {
+            const bool wr = two_sets && !(gx >= xb && gx < xb + SMALL_LDS);
+            const int32_t xr = wr ? xw : xb;
+            const u128 *bb = wr ? &Ls.base[wave][32 + 8 * p] : bs;
+            const int64_t rank = ((int64_t)gq * N + gx) >> 1, rb = ((int64_t)gq * N + xr) >> 1;
+            u = draw_u(bb[0], (uint32_t)(gx - xr));
+            wm = word_at(bb[1], rank, hasp[c], bufp[c][0], rb);
+            wv = word_at(bb[2], rank, hasp[c], bufp[c][1], rb);
+        }
+        const uint32_t jm = (uint32_t)(((uint64_t)wm * 2u) >> 32);       // choice((-1, 1)): threshold 0
+        const uint64_t mv = (uint64_t)wv * 3u;                           // choice((-1, 0, 1)): threshold 1
+        const uint32_t jv = (uint32_t)(mv >> 32);
+        if (__builtin_expect((uint32_t)mv == 0u && active, 0))
+            report(A.S, A.sweep, (uint32_t)(2 + 2 * c), (uint32_t)(((int64_t)gq * N + gx) >> 1));
+        if (active) {
+            const int lr = q - rbase;
+            const int sm = (lr - 1) % R, s0 = lr % R, sp = (lr + 1) % R;
+            const int cx = x - cofs;
+            const int32_t vc = s_v[s0][cx];
+            // plaquette_cb_gs: f1 (0,q,x), f2 (1,q+1,x), f3 (0,q,x+1), f4 (1,q,x)
+            const int32_t m_1 = s_m0[s0][cx], m_2 = s_m1[sp][cx], m_3 = s_m0[s0][cx + 1], m_4 = s_m1[s0][cx];
+            const double f1 = (double)m_1 - wf_dv0(vc, s_v[s0][cx - 1], Winv);
+            const double f2 = (double)m_2 - wf_dv1(s_v[sp][cx], vc, Winv);
+            const double f3 = (double)m_3 - wf_dv0(s_v[s0][cx + 1], vc, Winv);
+            const double f4 = (double)m_4 - wf_dv1(vc, s_v[sm][cx], Winv);
+            const int di = 3 * (int)jm + (int)jv;
+            const double df = Ls.df[di], dfk = Ls.dfk[di];
+            const double dS = dfk * ((((f1 + f2) - f3) - f4) + 2.0 * df);
+            double pr = sv_exp(-dS);
+            pr = pr > 1.0 ? 1.0 : pr;
+            const bool acc = u < pr;
+            if (q >= t0 && q < t1 && x >= x0 && x < x1) {
+                pacc += acc;
+                ppsum += pr;
+            }
+            if (__builtin_amdgcn_ballot_w64(acc)) {
+                if (acc) {
+                    const int32_t cm = jm ? 1 : -1, cv = (int32_t)jv - 1;
+                    s_m0[s0][cx] = m_1 + cm;
+                    s_m1[sp][cx] = m_2 + cm;
+                    s_m0[s0][cx + 1] = m_3 - cm;
+                    s_m1[s0][cx] = m_4 - cm;
+                    s_v[s0][cx] = vc + cv;
+                }
+            }
+        }
+    };
+
+    // ---------------- coexact pass (colour c = p - 2) on row q
+    auto coexact = [&](int p, int32_t q) {
+        const int c = p - 2;
+        const bool row_ok = q >= t0 - (4 - p) && q < t1 + (3 - p);
+        const int32_t x = first_col(p, q) + 2 * lane;
+        const bool active = row_ok && x < x1 + (3 - p);
+        const int32_t gq = grow(q), gx = wrapN(x, N);
+        const bool wr = two_sets && !(gx >= xb && gx < xb + SMALL_LDS);
+        const int32_t xr = wr ? xw : xb;
+        const u128 *bb = wr ? &Ls.base[wave][32 + 8 * p] : &Ls.base[wave][8 * p];
+        const int64_t rank = ((int64_t)gq * N + gx) >> 1, rb = ((int64_t)gq * N + xr) >> 1;
+        const double u = draw_u(bb[0], (uint32_t)(gx - xr));
+        const uint32_t wt = word_at(bb[1], rank, hast[c], buft[c], rb);
+        const uint64_t mt = (uint64_t)wt * kt;
+        const int32_t j = (int32_t)(mt >> 32);
+        if (__builtin_expect((uint32_t)mt < thrt && active, 0)) report(A.S, A.sweep, (uint32_t)(6 + c), (uint32_t)rank);
+        if (active) {
+            const int32_t t = j < it ? j - it : j - it + 1;
+            const int lr = q - rbase;
+            const int sm = (lr - 1) % R, s0 = lr % R, sp = (lr + 1) % R;
+            const int cx = x - cofs;
+            const int32_t vc = s_v[s0][cx];
+            // coexact_gs, coface_sum_at order: (1,q,x) -t, (1,q+1,x) +t, (0,q,x) +t, (0,q,x+1) -t
+            const int32_t m_a = s_m1[s0][cx], m_b = s_m1[sp][cx], m_c = s_m0[s0][cx], m_d = s_m0[s0][cx + 1];
+            const double fa = (double)m_a - wf_dv1(vc, s_v[sm][cx], Winv);
+            const double fb = (double)m_b - wf_dv1(s_v[sp][cx], vc, Winv);
+            const double fc = (double)m_c - wf_dv0(vc, s_v[s0][cx - 1], Winv);
+            const double fd = (double)m_d - wf_dv0(s_v[s0][cx + 1], vc, Winv);
+            const double tp = (double)t, tm = (double)(-t);
+            double dS = (cc * tm) * ((2.0 * fa) + tm);
+            dS += (cc * tp) * ((2.0 * fb) + tp);
+            dS += (cc * tp) * ((2.0 * fc) + tp);
+            dS += (cc * tm) * ((2.0 * fd) + tm);
+            double pr = sv_exp(-dS);
+            pr = pr > 1.0 ? 1.0 : pr;
+            const bool acc = u < pr;
+            if (q >= t0 && q < t1 && x >= x0 && x < x1) {
+                cacc += acc;
+                cpsum += pr;
+            }
+            if (__builtin_amdgcn_ballot_w64(acc)) {
+                if (acc) {  // delta_sparse(t accepted): m0[x] += t, m0[x+e1] -= t, m1[x] -= t, m1[x+e0] += t
+                    s_m0[s0][cx] = m_c + t;
+                    s_m0[s0][cx + 1] = m_d - t;
+                    s_m1[s0][cx] = m_a - t;
+                    s_m1[sp][cx] = m_b + t;
+                }
+            }
+        }
+    };
+
+    for (int32_t ra = t0 - 5; ra < tfirst + 8; ra += NW) {
+        prefetch(ra);
+        commit(ra);
+    }
+    __syncthreads();
+
+    for (int32_t t = tfirst; t < t1; t += NW) {
+        prefetch(t + 8);
+        store_rows(t - NW);
+        plaquette(0, t + 3 + wave);
+        __syncthreads();
+        plaquette(1, t + 2 + wave);
+        __syncthreads();
+        coexact(2, t + 1 + wave);
+        __syncthreads();
+        coexact(3, t + wave);
+        commit(t + 8);
+        if (base_lane) {
+            const int64_t p_old = wf_base_pos(bbnd, grow(brow), N, bx, bhas);
+            const int64_t p_new = wf_base_pos(bbnd, grow(brow + NW), N, bx, bhas);
+            const int64_t step = bbnd ? (int64_t)NW * N / 4 : (int64_t)NW * N;
+            if (p_new - p_old == step) bases = apply(Ls.adv[bbnd ? 2 : 0], bases);
+            else bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)p_new);
+            brow += NW;
+            Ls.base[wave][lane] = bases;
+        }
+        __syncthreads();
+    }
+    {
+        int32_t tl = tfirst;
+        while (tl + NW < t1) tl += NW;
+        store_rows(tl);
+    }
+    if (Ls.bad && threadIdx.x == 0) report(A.S, A.sweep, OVERFLOW_BLOCK, 0, 0);
+    wflush(A.pstat, pacc, ppsum);
+    wflush(A.cstat, cacc, cpsum);
+}
+
+__global__ __launch_bounds__(256) void worldline_step_fused(WFArgs A) {
+    __shared__ WFLDS Ls;
+    int b = blockIdx.x;
+    {
+        const int G = gridDim.x, per = G / 8, rem = G % 8;
+        const int xcd = b & 7, k = b >> 3;
+        b = xcd * per + (xcd < rem ? xcd : rem) + k;
+    }
+    const int ix = b % A.nsx;
+    const int32_t x0 = (int32_t)((int64_t)ix * A.N / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * A.N / A.nsx);
+    const bool interior = x0 - 5 >= 0 && x1 + 4 <= A.N && A.N > SMALL_LDS;
+    if (__builtin_amdgcn_readfirstlane((int)interior)) wf_body<false>(A, Ls);
+    else wf_body<true>(A, Ls);
+}
+
+}  // namespace sv
+
+namespace svh {
+using namespace sv;
+
+// rows per strip (SV_WF_TH overrides): as fused_th, cut down until the grid has `fill` workgroups
+static int wf_th(int32_t N, int nsx) {
+    const char *e = getenv("SV_WF_TH");
+    if (e) {
+        const int v = atoi(e);
+        if (v >= 4 && v % 4 == 0) return v;
+    }
+    static const int fill = [] {
+        const char *f = getenv("SV_WF_FILL");
+        const int v = f ? atoi(f) : 512;
+        return v > 0 ? v : 512;
+    }();
+    int th = 64;
+    while (th > 4 && (int64_t)nsx * ((N + th - 1) / th) < fill) th -= 4;
+    return th;
+}
+
+// Whether one step (5 plaquette blocks then 3 coexact blocks) runs on worldline_step_fused
+bool wf_ok(int32_t N, bool v_is_float, double W_eff, int64_t it, const Block *blocks) {
+    int ex = 0;
+    if (N % 2 || N < 4 || v_is_float || !(W_eff > 0) || std::frexp(W_eff, &ex) != 0.5 || it < 1 || it > (1 << 20))
+        return false;
+    for (int c = 0; c < 2; c++) {
+        if (blocks[1 + 2 * c].nskip || blocks[2 + 2 * c].nskip || blocks[6 + c].nskip) return false;
+        if (blocks[1 + 2 * c].has != blocks[2 + 2 * c].has) return false;
+    }
+    return true;
+}
+
+void launch_wf(int32_t N, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in, int64_t *m_out,
+               int64_t *v_out, const Block *blocks, const JumpTables *T, const Affine adv[3], void *pstat, void *cstat,
+               DevScratch S, uint32_t sweep, hipStream_t stream) {
+    WFArgs A{};
+    A.N = N;
+    A.nsx = (N + WF_W - 1) / WF_W;
+    A.TH = wf_th(N, A.nsx);
+    A.nsy = (N + A.TH - 1) / A.TH;
+    A.m_in = m_in;
+    A.v_in = v_in;
+    A.m_out = m_out;
+    A.v_out = v_out;
+    A.blocks = blocks;
+    A.T = T;
+    for (int i = 0; i < 3; i++) A.adv[i] = adv[i];
+    A.pstat = (StatStripe *)pstat;
+    A.cstat = (StatStripe *)cstat;
+    A.S = S;
+    A.sweep = sweep;
+    A.Winv = 1.0 / W_eff;
+    A.c = 0.5 / kappa;
+    for (int jm = 0; jm < 2; jm++)
+        for (int jv = 0; jv < 3; jv++) {  // plaquette_cb_gs: df = cm - cv * Winv, dS = df / kappa * (...)
+            const double cm = jm ? 1.0 : -1.0, cv = (double)(jv - 1);
+            const double df = cm - cv * A.Winv;
+            A.df[3 * jm + jv] = df;
+            A.dfk[3 * jm + jv] = df / kappa;
+        }
+    A.it = (int32_t)it;
+    A.kt = (uint32_t)(2 * it);
+    A.thrt = (uint32_t)((0u - A.kt) % A.kt);
+    worldline_step_fused<<<A.nsx * A.nsy, WF_NW * 64, 0, stream>>>(A);
+}
+
+}  // namespace svh
