@@ -1,10 +1,11 @@
 source scripts/gpu/guard.sh
-T=${1:-r214}
+T=${1:-r216}
 O=gpurun_out/$T
 mkdir -p $O
 export TMPDIR=/tmp
-B="python bench.py --workload worldline --steps 20 --warmup 2 --warmup-s 0.2 --no-cpu-baseline --no-copy-ceiling"
-step sq1 timeout -s KILL 120 rocprofv3 --kernel-include-regex worldline_step_fused --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU -d $O/sq1 -o p --output-format csv -- $B > $O/sq1.log 2>&1
-step sq2 timeout -s KILL 120 rocprofv3 --kernel-include-regex worldline_step_fused --pmc SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE -d $O/sq2 -o p --output-format csv -- $B > $O/sq2.log 2>&1
-step tr timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- $B > $O/trace.log 2>&1
-echo done
+step wl timeout -k 10 400 python -u -m pytest tests/test_gpu_worldline.py -x -q --timeout 200 --timeout-method thread > $O/tests_wl.log 2>&1
+tail -2 $O/tests_wl.log
+step dbg timeout -k 10 120 python scripts/debug_wf.py > $O/dbg.log 2>&1
+cat $O/dbg.log
+step bwl timeout -k 10 300 python bench.py --workload worldline --steps 200 --warmup 20 --no-cpu-baseline --no-copy-ceiling > $O/bwl.log 2>&1
+grep -o '"value": [0-9.e+]*\|"avg_launch_us": [0-9.]*\|"frac": [0-9.]*' $O/bwl.log | tr '\n' ' '; echo

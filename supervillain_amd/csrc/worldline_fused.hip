@@ -28,13 +28,14 @@ static constexpr int WF_NW = 4;
 static constexpr int WF_R = 3 * WF_NW + 1;
 
 struct WFArgs {
-    int32_t N;
+    FGeom G;  // the periodic Nt x Nx lattice, or one domain tile with its ghost frame (villain.h)
     int32_t nsx, TH, nsy;
     const int64_t *m_in;
     const int64_t *v_in;
     int64_t *m_out;
     int64_t *v_out;
     const Block *blocks;  // 5 plaquette blocks ([0] metropolis, [1+2c] change_m, [2+2c] change_v), then 3 coexact
+    const uint32_t *skips;  // known rejected stream positions (GENERAL mode)
     const JumpTables *T;  // ([5] metropolis, [6+c] t)
     Affine adv[3];        // advance a row base by NW rows: [0] NW N draws, [2] NW N / 4 words
     StatStripe *pstat, *cstat;
@@ -45,6 +46,7 @@ struct WFArgs {
     double df[6], dfk[6];  // plaquette: df = cm - cv / W and df / kappa for index 3 jm + jv
     int32_t it;            // coexact: t in -it..-1, 1..it
     uint32_t kt, thrt;     // its choice count 2 it and Lemire threshold
+    int32_t general;       // MODE 2 for every strip (wf_body)
 };
 
 struct WFLDS {
@@ -71,8 +73,12 @@ __device__ __forceinline__ int64_t wf_base_pos(bool bounded, int64_t gq, int64_t
 __device__ __forceinline__ double wf_dv0(int32_t vs, int32_t vn, double Winv) { return (double)(vs - vn) * Winv; }
 __device__ __forceinline__ double wf_dv1(int32_t vs, int32_t vn, double Winv) { return (double)(-(vs - vn)) * Winv; }
 
-template <bool EDGE>
+// MODE 0: interior strip, paired plaquette words; 1: edge strip (rows wrap), unpaired words from two base sets;
+// 2: GENERAL, a step with known Lemire rejections (skip lists) or unequal buffered-half flags: bounded words by
+// a full table jump at their skip-adjusted stream position (the rare replay of a rejected step)
+template <bool TILE, int MODE>
 __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS &Ls) {
+    constexpr bool EDGE = MODE != 0;
     constexpr int NW = WF_NW, R = WF_R, PF = RW / 64;
     auto &s_m0 = Ls.m0;
     auto &s_m1 = Ls.m1;
@@ -80,8 +86,9 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS &Ls) {
     auto &s_small = Ls.small;
     if (*(volatile const int32_t *)A.S.abort) return;
 
-    const int32_t N = A.N;
-    const int64_t V = (int64_t)N * N;
+    const FGeom &Gm = A.G;
+    const int32_t N = Gm.Nx, Nt = Gm.Nt;  // global row length (stream layout) and row count
+    const int64_t V = Gm.plane;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
     int b = blockIdx.x;
     {
@@ -90,18 +97,22 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS &Ls) {
         b = xcd * per + (xcd < rem ? xcd : rem) + k;
     }
     const int ix = b % A.nsx, iy = b / A.nsx;
-    const int32_t x0 = (int32_t)((int64_t)ix * N / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * N / A.nsx);
+    const int32_t x0 = (int32_t)((int64_t)ix * Gm.Wt / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * Gm.Wt / A.nsx);
     const int32_t w = x1 - x0;
     const int32_t t0 = iy * A.TH;
-    const int32_t t1 = t0 + A.TH < N ? t0 + A.TH : N;
+    const int32_t t1 = t0 + A.TH < Gm.Ht ? t0 + A.TH : Gm.Ht;
     const int32_t rbase = t0 - 5;  // local row 0
     const int32_t cols = w + 9;
     const int32_t cofs = x0 - 5;   // LDS column of lattice column x is x - cofs
-    auto grow = [&](int32_t q) { return wrapN(q, N); };
-    // row bases at the first region column (interior strips), or at column 0 and at the first wrapped column
-    const int32_t xb = (N <= SMALL_LDS || x0 - 5 < 0) ? 0 : x0 - 5;
+    auto grow = [&](int32_t q) { return wrapN(Gm.T0 + q, Nt); };   // global row of local row q
+    auto gcol = [&](int32_t x) { return wrapN(Gm.X0 + x, N); };     // global column of local column x
+    auto mrow = [&](int32_t q) -> int64_t { return TILE ? Gm.org + (int64_t)q * Gm.pitch : (int64_t)wrapN(q, Nt) * N; };
+    auto mcol = [&](int32_t c) -> int32_t { return TILE ? c : wrapN(c, N); };
+    // row bases at the strip's first region column (global), or at column 0 and at the first wrapped column
+    const int32_t gx0 = Gm.X0 + x0;
+    const int32_t xb = (N <= SMALL_LDS || gx0 - 5 < 0) ? 0 : gx0 - 5;
     const bool two_sets = EDGE && N > SMALL_LDS;
-    const int32_t xw = x0 - 5 < 0 ? N - 5 : 0;
+    const int32_t xw = gx0 - 5 < 0 ? N - 5 : 0;
 
     for (int e = threadIdx.x; e < SMALL_LDS; e += NW * 64) {
         s_small.A[e] = A.T->small[e].A;
@@ -131,11 +142,11 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS &Ls) {
     int64_t pf_m0[PF], pf_m1[PF], pf_v[PF];
     int pf_gx[PF];
 #pragma unroll
-    for (int k = 0; k < PF; k++) pf_gx[k] = wrapN(x0 - 5 + lane + 64 * k, N);
+    for (int k = 0; k < PF; k++) pf_gx[k] = mcol(x0 - 5 + lane + 64 * k);
     auto prefetch = [&](int32_t ra) {
         const int32_t q = ra + wave;
         if (q >= t0 - 5 && q < t1 + 4) {
-            const int64_t g0 = (int64_t)grow(q) * N;
+            const int64_t g0 = mrow(q);
 #pragma unroll
             for (int k = 0; k < PF; k++) {
                 if (lane + 64 * k < cols) {
@@ -171,7 +182,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS &Ls) {
         const int32_t q = ra + wave;
         if (q >= t0 && q < t1) {
             const int slot = (q - rbase) % R;
-            const int64_t g0 = (int64_t)q * N + x0;
+            const int64_t g0 = mrow(q) + x0;  // own sites never wrap
 #pragma unroll
             for (int k = 0; k < PF; k++) {
                 const int cc2 = lane + 64 * k;
@@ -207,7 +218,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS &Ls) {
     auto first_col = [&](int p, int32_t q) {
         const int32_t lo = x0 - (4 - p);
         const int c = p & 1;
-        return lo + ((grow(q) + wrapN(lo, N) + c) & 1);  // (t + x) % 2 == c
+        return lo + ((grow(q) + gcol(lo) + c) & 1);  // global (t + x) % 2 == c (N even)
     };
     // interior strips: per-lane constants of the paired plaquette draws (metropolis offset, change_m/change_v
     // word offset, half), the same for every row of the wave (rows advance 4 at a time)
@@ -218,8 +229,8 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS &Ls) {
             const int32_t q = tfirst + 3 - p + wave;
             const uint32_t rowlin = (uint32_t)grow(q) * (uint32_t)N;
             const int32_t xs = first_col(p, q);
-            const uint32_t gx = (uint32_t)(xs + 2 * lane);
-            const uint32_t rank = (rowlin + gx) >> 1, R0 = (rowlin + (uint32_t)xs) >> 1;
+            const uint32_t gx = (uint32_t)(Gm.X0 + xs + 2 * lane);
+            const uint32_t rank = (rowlin + gx) >> 1, R0 = (rowlin + (uint32_t)(Gm.X0 + xs)) >> 1;
             const uint32_t h = hasp[p], PR = (rowlin + (uint32_t)xb) >> 1;
             const uint32_t P = (R0 - h) & 1u, PW = (PR - h) >> 1;
             uint32_t qq = rank - h;
@@ -248,10 +259,12 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS &Ls) {
         const bool row_ok = q >= t0 - (4 - p) && q < t1 + (3 - p);
         const int32_t x = first_col(p, q) + 2 * lane;
         const bool active = row_ok && x < x1 + (3 - p);
-        const int32_t gq = grow(q), gx = wrapN(x, N);
+        const int32_t gq = grow(q), gx = gcol(x);
         const u128 *bs = &Ls.base[wave][8 * p];
         double u;
         uint32_t wm, wv;
+        uint32_t qm = (uint32_t)(((int64_t)gq * N + gx) >> 1), qv = qm;  // stream positions (skip-adjusted)
+        (void)qm;
         if constexpr (!EDGE) {
             u = draw_u(bs[0], pk[p]);
             const uint32_t half = (pk[p] >> 14) & 1u;
@@ -268,14 +281,20 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS &Ls) {
             const u128 *bb = wr ? &Ls.base[wave][32 + 8 * p] : bs;
             const int64_t rank = ((int64_t)gq * N + gx) >> 1, rb = ((int64_t)gq * N + xr) >> 1;
             u = draw_u(bb[0], (uint32_t)(gx - xr));
-            wm = word_at(bb[1], rank, hasp[c], bufp[c][0], rb);
-            wv = word_at(bb[2], rank, hasp[c], bufp[c][1], rb);
+            if constexpr (MODE == 2) {
+                qm = skip_pos(A.blocks[1 + 2 * c], A.skips, (uint32_t)rank);
+                qv = skip_pos(A.blocks[2 + 2 * c], A.skips, (uint32_t)rank);
+                wm = bounded_word(A.T, A.blocks[1 + 2 * c], qm);
+                wv = bounded_word(A.T, A.blocks[2 + 2 * c], qv);
+            } else {
+                wm = word_at(bb[1], rank, hasp[c], bufp[c][0], rb);
+                wv = word_at(bb[2], rank, hasp[c], bufp[c][1], rb);
+            }
         }
         const uint32_t jm = (uint32_t)(((uint64_t)wm * 2u) >> 32);       // choice((-1, 1)): threshold 0
         const uint64_t mv = (uint64_t)wv * 3u;                           // choice((-1, 0, 1)): threshold 1
         const uint32_t jv = (uint32_t)(mv >> 32);
-        if (__builtin_expect((uint32_t)mv == 0u && active, 0))
-            report(A.S, A.sweep, (uint32_t)(2 + 2 * c), (uint32_t)(((int64_t)gq * N + gx) >> 1));
+        if (__builtin_expect((uint32_t)mv == 0u && active, 0)) report(A.S, A.sweep, (uint32_t)(2 + 2 * c), qv);
         if (active) {
             const int lr = q - rbase;
             const int sm = (lr - 1) % R, s0 = lr % R, sp = (lr + 1) % R;
@@ -316,16 +335,22 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS &Ls) {
         const bool row_ok = q >= t0 - (4 - p) && q < t1 + (3 - p);
         const int32_t x = first_col(p, q) + 2 * lane;
         const bool active = row_ok && x < x1 + (3 - p);
-        const int32_t gq = grow(q), gx = wrapN(x, N);
+        const int32_t gq = grow(q), gx = gcol(x);
         const bool wr = two_sets && !(gx >= xb && gx < xb + SMALL_LDS);
         const int32_t xr = wr ? xw : xb;
         const u128 *bb = wr ? &Ls.base[wave][32 + 8 * p] : &Ls.base[wave][8 * p];
         const int64_t rank = ((int64_t)gq * N + gx) >> 1, rb = ((int64_t)gq * N + xr) >> 1;
         const double u = draw_u(bb[0], (uint32_t)(gx - xr));
-        const uint32_t wt = word_at(bb[1], rank, hast[c], buft[c], rb);
+        uint32_t qt = (uint32_t)rank, wt;
+        if constexpr (MODE == 2) {
+            qt = skip_pos(A.blocks[6 + c], A.skips, (uint32_t)rank);
+            wt = bounded_word(A.T, A.blocks[6 + c], qt);
+        } else {
+            wt = word_at(bb[1], rank, hast[c], buft[c], rb);
+        }
         const uint64_t mt = (uint64_t)wt * kt;
         const int32_t j = (int32_t)(mt >> 32);
-        if (__builtin_expect((uint32_t)mt < thrt && active, 0)) report(A.S, A.sweep, (uint32_t)(6 + c), (uint32_t)rank);
+        if (__builtin_expect((uint32_t)mt < thrt && active, 0)) report(A.S, A.sweep, (uint32_t)(6 + c), qt);
         if (active) {
             const int32_t t = j < it ? j - it : j - it + 1;
             const int lr = q - rbase;
@@ -399,6 +424,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS &Ls) {
     wflush(A.cstat, cacc, cpsum);
 }
 
+template <bool TILE>
 __global__ __launch_bounds__(256) void worldline_step_fused(WFArgs A) {
     __shared__ WFLDS Ls;
     int b = blockIdx.x;
@@ -408,11 +434,15 @@ __global__ __launch_bounds__(256) void worldline_step_fused(WFArgs A) {
         b = xcd * per + (xcd < rem ? xcd : rem) + k;
     }
     const int ix = b % A.nsx;
-    const int32_t x0 = (int32_t)((int64_t)ix * A.N / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * A.N / A.nsx);
-    const bool interior = x0 - 5 >= 0 && x1 + 4 <= A.N && A.N > SMALL_LDS;
-    if (__builtin_amdgcn_readfirstlane((int)interior)) wf_body<false>(A, Ls);
-    else wf_body<true>(A, Ls);
+    const int32_t x0 = (int32_t)((int64_t)ix * A.G.Wt / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * A.G.Wt / A.nsx);
+    const int32_t gx0 = A.G.X0 + x0;
+    const bool interior = gx0 - 5 >= 0 && gx0 + (x1 - x0) + 4 <= A.G.Nx && A.G.Nx > SMALL_LDS;
+    if (A.general) wf_body<TILE, 2>(A, Ls);
+    else if (__builtin_amdgcn_readfirstlane((int)interior)) wf_body<TILE, 0>(A, Ls);
+    else wf_body<TILE, 1>(A, Ls);
 }
+template __global__ void worldline_step_fused<false>(WFArgs);
+template __global__ void worldline_step_fused<true>(WFArgs);
 
 }  // namespace sv
 
@@ -436,11 +466,15 @@ static int wf_th(int32_t N, int nsx) {
     return th;
 }
 
-// Whether one step (5 plaquette blocks then 3 coexact blocks) runs on worldline_step_fused
-bool wf_ok(int32_t N, bool v_is_float, double W_eff, int64_t it, const Block *blocks) {
+// Whether worldline_step_fused can run these parameters at all (even N, integer v, W a power of two: f and df
+// exact as the pass kernels form them)
+bool wf_usable(int32_t N, bool v_is_float, double W_eff, int64_t it) {
     int ex = 0;
-    if (N % 2 || N < 4 || v_is_float || !(W_eff > 0) || std::frexp(W_eff, &ex) != 0.5 || it < 1 || it > (1 << 20))
-        return false;
+    return !(N % 2 || N < 4 || v_is_float || !(W_eff > 0) || std::frexp(W_eff, &ex) != 0.5 || it < 1 || it > (1 << 20));
+}
+// Whether one step (5 plaquette blocks then 3 coexact blocks) runs in the fast modes (no skip list, equal
+// buffered-half flags in each change_m / change_v pair); otherwise it runs in the GENERAL mode
+bool wf_fast(const Block *blocks) {
     for (int c = 0; c < 2; c++) {
         if (blocks[1 + 2 * c].nskip || blocks[2 + 2 * c].nskip || blocks[6 + c].nskip) return false;
         if (blocks[1 + 2 * c].has != blocks[2 + 2 * c].has) return false;
@@ -448,14 +482,17 @@ bool wf_ok(int32_t N, bool v_is_float, double W_eff, int64_t it, const Block *bl
     return true;
 }
 
-void launch_wf(int32_t N, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in, int64_t *m_out,
-               int64_t *v_out, const Block *blocks, const JumpTables *T, const Affine adv[3], void *pstat, void *cstat,
-               DevScratch S, uint32_t sweep, hipStream_t stream) {
+void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in,
+               int64_t *m_out, int64_t *v_out, const Block *blocks, const uint32_t *skips, bool general,
+               const JumpTables *T, const Affine adv[3], void *pstat, void *cstat, DevScratch S, uint32_t sweep,
+               hipStream_t stream) {
     WFArgs A{};
-    A.N = N;
-    A.nsx = (N + WF_W - 1) / WF_W;
-    A.TH = wf_th(N, A.nsx);
-    A.nsy = (N + A.TH - 1) / A.TH;
+    A.skips = skips;
+    A.general = general ? 1 : 0;
+    A.G = G;
+    A.nsx = (G.Wt + WF_W - 1) / WF_W;
+    A.TH = wf_th(G.Ht, A.nsx);
+    A.nsy = (G.Ht + A.TH - 1) / A.TH;
     A.m_in = m_in;
     A.v_in = v_in;
     A.m_out = m_out;
@@ -479,7 +516,9 @@ void launch_wf(int32_t N, double kappa, double W_eff, int64_t it, const int64_t 
     A.it = (int32_t)it;
     A.kt = (uint32_t)(2 * it);
     A.thrt = (uint32_t)((0u - A.kt) % A.kt);
-    worldline_step_fused<<<A.nsx * A.nsy, WF_NW * 64, 0, stream>>>(A);
+    const bool tile = !(G.T0 == 0 && G.X0 == 0 && G.Ht == G.Nt && G.Wt == G.Nx && G.pitch == G.Nx && G.org == 0);
+    if (tile) worldline_step_fused<true><<<A.nsx * A.nsy, WF_NW * 64, 0, stream>>>(A);
+    else worldline_step_fused<false><<<A.nsx * A.nsy, WF_NW * 64, 0, stream>>>(A);
 }
 
 }  // namespace svh

@@ -315,3 +315,31 @@ def test_plaquette_checkerboard_statistical_parity(N, steps):
     for name, (z, ma, ea, mb, eb) in zs.items():
         assert abs(z) < 4.0, f'N={N} {name}: checkerboard {ma:.5f} +- {ea:.5f} vs reference order {mb:.5f} +- {eb:.5f}'
     assert all(0 < zs[n][2] < 0.01 for n in NAMES)
+
+
+@pytest.mark.parametrize('N', [16, 256])
+def test_plaquette_coexact_forced_rejection(N, oracle_lib):
+    """A NumPy Lemire rejection forced into the change_v blocks of a combined Plaquette + Coexact run (the
+    config-3 step, worldline_step_fused): in step 0's colour-0 block and in step 1's colour-1 block (raw u64
+    positions: a step draws metropolis V, then four V/4-word bounded blocks, then Coexact V + 2 V/4).  The
+    replayed step runs the fused kernel's GENERAL mode (skip lists); fields, statistics and the rng state
+    match the oracle."""
+    V = N * N
+    per_step = 2 * V + V + V // 2
+    for pos, half in [(V + V // 4 + 3, 0), (per_step + V + 3 * V // 4 + 1, 1)]:
+        v0 = np.random.default_rng(5).integers(-2, 3, (N, N)).astype(np.int64)
+        m0 = np.zeros((2, N, N), dtype=np.int64)
+        gen = crafted_generator(pos, pos, half)
+        m, v, st = _worldline_run(N, 0.5, 1.0, m0, v0, 3, gen)
+        g = crafted_generator(pos, pos, half)
+        mm, vv = m0.copy(), v0.copy()
+        rej = 0
+        for s in range(3):
+            sp = oracle_lib.worldline_plaquette_cb(N, 0.5, 1.0, mm, vv, 1, g)[0]
+            sc = oracle_lib.worldline_coexact(N, 0.5, 1.0, mm, vv, 1, g)[0]
+            rej += sp.rejections + sc.rejections
+            assert st[2 * s].accepted == sp.accepted and st[2 * s + 1].accepted == sc.accepted, s
+            assert st[2 * s].rejections == sp.rejections, s
+        assert rej >= 1
+        assert (m == mm).all() and (v == vv).all()
+        assert gen.bit_generator.state == g.bit_generator.state
