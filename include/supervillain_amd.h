@@ -192,6 +192,20 @@ int sv_domain_exchange_plan(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t til
  * nsend x {peer, offset, words}, nrecv x {peer, offset, words}, soff[8], roff[8], words[8], msg_words}. */
 int sv_domain_message_layout(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t rank, int64_t *out);
 
+/* ---- Worldline on a domain-decomposed lattice ("Worldline (config 3) decomposes the same way")
+ * One step = the checkerboard PlaquetteUpdate sweep + the CoexactUpdate sweep of
+ * sv_worldline_plaquette_coexact_run (plaquette.py:35-104 in its GPU-native colour order, coexact.py:53-128),
+ * the same chain bit for bit, on an even Nt x Nx lattice cut into tiles (one halo exchange of (v, m) per step,
+ * a 5/4-wide ghost frame).  Same rank / RCCL conventions as sv_domain_*.  Integer v, W_eff a power of two.
+ * Arrays: m (2, Nt, Nx) int64, v (Nt, Nx) int64; m == NULL: cold start.  stats: 2 per step
+ * ({Plaquette, Coexact}, summed over tiles). */
+int sv_domain_create_worldline(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t nranks,
+                               int32_t rank, const uint8_t *unique_id, sv_domain **out);
+int sv_domain_upload_worldline(sv_domain *d, const int64_t *m, const int64_t *v);
+int sv_domain_download_worldline(sv_domain *d, int64_t *m, int64_t *v);
+int sv_domain_run_worldline(sv_domain *d, double kappa, double W_eff, int64_t interval_t, int32_t steps, sv_rng *rng,
+                            sv_stats *stats);
+
 
 /* ---- Villain replica batches (BASELINE config 5; SURVEY.md 8e: replicas need no collectives) ------- */
 /* R independent NeighborhoodUpdate chains of one even N >= 4 advanced together (one launch per sweep

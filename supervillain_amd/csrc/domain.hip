@@ -27,11 +27,29 @@
 #include <cmath>
 #include <cstring>
 
+#include "fused.h"
 #include "villain.h"
+
+namespace svh {
+// worldline_fused.hip
+bool wf_usable(int32_t N, bool v_is_float, double W_eff, int64_t it);
+bool wf_fast(const sv::Block *blocks);
+void launch_wf(const sv::FGeom &G, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in,
+               int64_t *m_out, int64_t *v_out, const sv::Block *blocks, const uint32_t *skips, bool general,
+               const sv::JumpTables *T, const sv::Affine adv[3], void *pstat, void *cstat, sv::DevScratch S,
+               uint32_t sweep, hipStream_t stream);
+}  // namespace svh
 
 namespace sv {
 
-static constexpr int GHOST_TOP = 2, GHOST_BOTTOM = 3, GHOST_LEFT = 2, GHOST_RIGHT = 3;
+// Ghost frames (rows above / below, columns left / right of a tile) = what one sweep's kernel reads around
+// the tile: villain_sweep_hot / _fused 2, 3, 2, 3; worldline_step_fused (four passes, each one ring wider)
+// 5, 4, 5, 4.  The three 8-byte planes a tile holds are (phi, n0, n1) for Villain and (v, m0, m1) for
+// Worldline: the halo code moves them as bits.
+struct Ghost {
+    int32_t top, bottom, left, right;
+};
+static constexpr Ghost VILLAIN_GHOST{2, 3, 2, 3}, WORLDLINE_GHOST{5, 4, 5, 4};
 static constexpr int LEFT_PAD = 16;  // interior starts 128 B-aligned
 static constexpr int DOMAIN_BATCH = 64;
 static constexpr int NDIR = 8;
@@ -49,23 +67,23 @@ inline int opp(int s) { return NDIR - 1 - s; }  // (-dy, -dx)
 struct Rect {
     int32_t r0, c0, rows, cols;
 };
-inline Rect send_rect(int s, int32_t Ht, int32_t Wt) {
+inline Rect send_rect(int s, int32_t Ht, int32_t Wt, const Ghost &g) {
     int dy, dx;
     dir_of(s, dy, dx);
     Rect R;
-    R.r0 = dy > 0 ? Ht - GHOST_TOP : 0;
-    R.rows = dy == 0 ? Ht : (dy > 0 ? GHOST_TOP : GHOST_BOTTOM);
-    R.c0 = dx > 0 ? Wt - GHOST_LEFT : 0;
-    R.cols = dx == 0 ? Wt : (dx > 0 ? GHOST_LEFT : GHOST_RIGHT);
+    R.r0 = dy > 0 ? Ht - g.top : 0;
+    R.rows = dy == 0 ? Ht : (dy > 0 ? g.top : g.bottom);
+    R.c0 = dx > 0 ? Wt - g.left : 0;
+    R.cols = dx == 0 ? Wt : (dx > 0 ? g.left : g.right);
     return R;
 }
 // Ghost block filled by the message of direction s (it arrives from the tile at (-dy, -dx)).
-inline Rect recv_rect(int s, int32_t Ht, int32_t Wt) {
+inline Rect recv_rect(int s, int32_t Ht, int32_t Wt, const Ghost &g) {
     int dy, dx;
     dir_of(s, dy, dx);
-    Rect R = send_rect(s, Ht, Wt);
-    R.r0 = dy > 0 ? -GHOST_TOP : (dy == 0 ? 0 : Ht);
-    R.c0 = dx > 0 ? -GHOST_LEFT : (dx == 0 ? 0 : Wt);
+    Rect R = send_rect(s, Ht, Wt, g);
+    R.r0 = dy > 0 ? -g.top : (dy == 0 ? 0 : Ht);
+    R.c0 = dx > 0 ? -g.left : (dx == 0 ? 0 : Wt);
     return R;
 }
 
@@ -124,8 +142,22 @@ struct Summary {
     uint32_t nreport;
     uint64_t pad;
     Report reports[MAX_REPORTS];
-    sv_stats stats[DOMAIN_BATCH];
+    sv_stats stats[2 * DOMAIN_BATCH];  // Villain: one per sweep; Worldline: (Plaquette, Coexact) per step
 };
+
+// Worldline tiles: the per-step StatStripes of worldline_step_fused folded into the tile's Summary
+__global__ void wd_fold(const StatStripe *ss, sv_stats *out, int count) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= count) return;
+    unsigned long long a = 0;
+    double p = 0.0;
+    for (int j = 0; j < NSTRIPE; j++) {
+        a += ss[k * NSTRIPE + j].acc;
+        p += ss[k * NSTRIPE + j].psum;
+    }
+    out[k].accepted = (int64_t)a;
+    out[k].acceptance_sum = p;
+}
 
 }  // namespace sv
 
@@ -138,6 +170,7 @@ struct sv_domain_tile {
     std::vector<int64_t *> n;
     uint64_t *send = nullptr, *recv = nullptr;
     Summary *sum = nullptr;         // device
+    StatStripe *stripes = nullptr;  // Worldline: DOMAIN_BATCH x 2 x NSTRIPE
     // message layout: the messages bound for (or coming from) one remote peer are contiguous, so one
     // ncclSend / ncclRecv per distinct peer carries them all (e.g. 4 peers instead of 8 for 2 x 4 tiles)
     int64_t soff[NDIR] = {0}, roff[NDIR] = {0};
@@ -146,6 +179,8 @@ struct sv_domain_tile {
 
 struct sv_domain {
     sv_ctx *ctx = nullptr;
+    int model = 0;                  // 0 Villain (phi, n), 1 Worldline (v, m)
+    Ghost ghost = VILLAIN_GHOST;
     int32_t Nt = 0, Nx = 0, ty = 1, tx = 1, Ht = 0, Wt = 0;
     int nranks = 1, rank = 0;
     int64_t pitch = 0, plane = 0, org = 0;
@@ -187,16 +222,19 @@ void geometry(sv_domain *d) {
     if (d->Ht % 2 || d->Wt % 2 || d->Ht < 4 || d->Wt < 4)
         throw std::invalid_argument("tiles must be at least 4 x 4 with even extents");
     if ((int64_t)d->Nt * d->Nx >= (1LL << 32)) throw std::invalid_argument("lattice too large for 32-bit stream positions");
-    d->pitch = ((LEFT_PAD + d->Wt + GHOST_RIGHT + 15) / 16) * 16;
-    d->plane = (int64_t)(d->Ht + GHOST_TOP + GHOST_BOTTOM) * d->pitch;
-    d->org = (int64_t)GHOST_TOP * d->pitch + LEFT_PAD;
+    const Ghost &g = d->ghost;
+    if (d->Ht < std::max(g.top, g.bottom) || d->Wt < std::max(g.left, g.right))
+        throw std::invalid_argument("tiles must be at least as large as their ghost frame");
+    d->pitch = ((LEFT_PAD + d->Wt + g.right + 15) / 16) * 16;
+    d->plane = (int64_t)(d->Ht + g.top + g.bottom) * d->pitch;
+    d->org = (int64_t)g.top * d->pitch + LEFT_PAD;
     // ring depth: an abort travels one tile-hop (8-neighbour torus) per sweep; with split sweeps the
     // interior launch of the sweep that receives the abort still runs, so one more buffer
     const int D = std::max(d->ty / 2, d->tx / 2);
     d->R = std::max(2, D + 2);
     int64_t off = 0;
     for (int s = 0; s < NDIR; s++) {
-        d->H.rect[s] = send_rect(s, d->Ht, d->Wt);
+        d->H.rect[s] = send_rect(s, d->Ht, d->Wt, d->ghost);
         d->H.off[s] = off;
         off += 2 + 3 * (int64_t)d->H.rect[s].rows * d->H.rect[s].cols;
     }
@@ -205,7 +243,7 @@ void geometry(sv_domain *d) {
 
 HaloTable recv_table(const sv_domain *d) {
     HaloTable h = d->H;
-    for (int s = 0; s < NDIR; s++) h.rect[s] = recv_rect(s, d->Ht, d->Wt);
+    for (int s = 0; s < NDIR; s++) h.rect[s] = recv_rect(s, d->Ht, d->Wt, d->ghost);
     return h;
 }
 
@@ -347,14 +385,16 @@ void fill_stats(const sv_domain *d, const SkipMap &skips, int nb, int sw, int co
 // is o / B + q (1 + r B / 2), least at B = sqrt(2 o / (q r)): the weak-scaled 2 x 4 lattice
 // (8192 x 16384, q = 12.5%) runs batches of ~5 sweeps, one L=4096 tile (q = 1.6%) the full 64.
 // SV_DOMAIN_BATCH overrides.
-int domain_batch(const sv_domain *d, const VParams &P) {
+int domain_batch_q(const sv_domain *d, double q) {
     if (const char *e = getenv("SV_DOMAIN_BATCH")) return std::max(1, std::min(DOMAIN_BATCH, atoi(e)));
-    const double V = (double)d->Nt * d->Nx;
-    const double q = P.k > 1 ? 4.0 * V * (double)P.thr / 4294967296.0 : 0.0;
     if (q <= 0) return DOMAIN_BATCH;
     const double o = 0.3, r = d->comm ? 0.17 : 0.05;  // measured: RCCL exchange ~50 us, batch ~100 us, sweep 330 us
     const int B = (int)std::lround(std::sqrt(2.0 * o / (q * r)));
     return std::max(4, std::min(DOMAIN_BATCH, B));
+}
+int domain_batch(const sv_domain *d, const VParams &P) {
+    const double V = (double)d->Nt * d->Nx;
+    return domain_batch_q(d, P.k > 1 ? 4.0 * V * (double)P.thr / 4294967296.0 : 0.0);
 }
 
 void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u128 inc, sv_stats *stats) {
@@ -482,6 +522,103 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
     }
 }
 
+// Worldline (config 3 decomposed): one step = checkerboard PlaquetteUpdate sweep + CoexactUpdate
+// sweep, run per tile by worldline_step_fused in tile mode after one halo exchange of (v, m0, m1) with the
+// 5/4-wide ghost frame.  Same batch / abort / replay protocol as run_domain; two statistics per step.
+void run_wdomain(sv_domain *d, double kappa, double W_eff, int64_t it, int32_t steps, Cursor &cur, u128 inc,
+                 sv_stats *stats) {
+    sv_ctx *ctx = d->ctx;
+    const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
+    const int64_t V = (int64_t)d->Nt * d->Nx;
+    const uint32_t half = (uint32_t)(V / 2);
+    // worldline.hip plaquette_cb_specs + coexact_specs (even lattices: two colours of V/2 plaquettes)
+    const std::vector<BlockSpec> specs = {{UNIFORM, (uint32_t)V}, {BOUNDED, half}, {BOUNDED, half}, {BOUNDED, half},
+                                          {BOUNDED, half}, {UNIFORM, (uint32_t)V}, {BOUNDED, half}, {BOUNDED, half}};
+    const int nb = (int)specs.size();
+    const Affine adv[3] = {host_power(inc, 4 * (uint64_t)d->Nx), host_power(inc, 2 * (uint64_t)d->Nx),
+                           host_power(inc, (uint64_t)d->Nx)};
+    // rejections possible in the change_v blocks (threshold 1) and, for interval_t > 2, the t blocks
+    const uint32_t kt = (uint32_t)(2 * it), thrt = (0u - kt) % kt;
+    const double q = (double)V * (1.0 + (double)thrt) / 4294967296.0;
+    const int batch = domain_batch_q(d, q);
+    SkipMap skips;
+    std::vector<Block> blocks;
+    std::vector<uint32_t> skipvec;
+    auto fill = [&](int sw, int count) {
+        for (int k = 0; k < count; k++)
+            for (int j = 0; j < 2; j++) {
+                sv_stats st{0, V, 0.0, 0};
+                for (const Summary &S : d->host_sum) {
+                    st.accepted += S.stats[2 * k + j].accepted;
+                    st.acceptance_sum += S.stats[2 * k + j].acceptance_sum;
+                }
+                for (int bi = j == 0 ? 0 : 5; bi < (j == 0 ? 5 : nb); bi++) {
+                    auto itk = skips.find({sw + k, bi});
+                    if (itk != skips.end()) st.rejections += (int64_t)itk->second.size();
+                }
+                stats[2 * (sw + k) + j] = st;
+            }
+    };
+    int sw = 0;
+    while (sw < steps) {
+        const int count = std::min(batch, steps - sw);
+        Cursor c = cur;
+        plan_sweeps(ctx, c, inc, specs, sw, count, skips, blocks, skipvec);
+        upload_plan(ctx, blocks, skipvec);
+        for (auto &Tl : d->tiles) {
+            SV_HIP(hipMemsetAsync(Tl.sum, 0, sizeof(Summary), ctx->stream));
+            SV_HIP(hipMemsetAsync(Tl.stripes, 0, (size_t)count * 2 * NSTRIPE * sizeof(StatStripe), ctx->stream));
+        }
+        const int cur0 = d->cur;
+        hipEvent_t ev;
+        ctx->time_begin(&ev);
+        for (int k = 0; k < count; k++) {
+            const int in = d->cur, out = (d->cur + 1) % d->R;
+            exchange(d, ctx->stream);
+            const bool general = !wf_fast(&blocks[(size_t)k * nb]);
+            for (auto &Tl : d->tiles)
+                launch_wf(FGeom{d->Nt, d->Nx, Tl.T0, Tl.X0, d->Ht, d->Wt, d->pitch, d->plane, d->org}, kappa, W_eff, it,
+                          Tl.n[in], (const int64_t *)Tl.phi[in], Tl.n[out], (int64_t *)Tl.phi[out],
+                          ctx->d_blocks + (size_t)k * nb, ctx->d_skips, general, T, adv,
+                          Tl.stripes + (size_t)k * 2 * NSTRIPE, Tl.stripes + (size_t)k * 2 * NSTRIPE + NSTRIPE,
+                          DevScratch{&Tl.sum->abort, &Tl.sum->nreport, Tl.sum->reports}, (uint32_t)k, ctx->stream);
+            d->cur = out;
+        }
+        for (auto &Tl : d->tiles) wd_fold<<<(2 * count + 63) / 64, 64, 0, ctx->stream>>>(Tl.stripes, Tl.sum->stats, 2 * count);
+        ctx->time_end(ev, count);
+        SV_HIP(hipGetLastError());
+        gather(d);
+        AbortInfo a{0, {}};
+        for (const Summary &S : d->host_sum) {
+            a.abort |= S.abort;
+            const uint32_t nr = std::min<uint32_t>(S.nreport, MAX_REPORTS);
+            a.reports.insert(a.reports.end(), S.reports, S.reports + nr);
+        }
+        if (a.abort) ctx->time_discard();
+        ctx->time_collect();
+        if (!a.abort) {
+            fill(sw, count);
+            cur = c;
+            sw += count;
+            continue;
+        }
+        for (const Report &r : a.reports)
+            if (r.block == OVERFLOW_BLOCK)
+                throw std::runtime_error("|m| or |v| exceeds worldline_step_fused's int32 LDS image (domain mode has no fallback)");
+        const int bad = absorb_reports(a, sw, skips);
+        if (bad > 0) {
+            Cursor c2 = cur;
+            std::vector<Block> b2;
+            std::vector<uint32_t> s2;
+            plan_sweeps(ctx, c2, inc, specs, sw, bad, skips, b2, s2);
+            fill(sw, bad);
+            cur = c2;
+        }
+        d->cur = (cur0 + bad) % d->R;
+        sw += bad;
+    }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------- C-ABI
@@ -508,7 +645,7 @@ int sv_domain_exchange_plan(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t til
         for (int s = 0; s < NDIR; s++) {
             int dy, dx;
             dir_of(s, dy, dx);
-            const Rect S = send_rect(s, d.Ht, d.Wt), Rr = recv_rect(s, d.Ht, d.Wt);
+            const Rect S = send_rect(s, d.Ht, d.Wt, d.ghost), Rr = recv_rect(s, d.Ht, d.Wt, d.ghost);
             int64_t *o = out + 10 * s;
             o[0] = dy;
             o[1] = dx;
@@ -556,14 +693,16 @@ int sv_domain_message_layout(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t ti
     }
 }
 
-int sv_domain_create(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t nranks,
-                     int32_t rank, const uint8_t *unique_id, sv_domain **out) {
+static int domain_create(sv_ctx *ctx, int model, int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x,
+                         int32_t nranks, int32_t rank, const uint8_t *unique_id, sv_domain **out) {
     if (!ctx || !out) return -1;
     *out = nullptr;
     sv_domain *d = new sv_domain();
     try {
         SV_HIP(hipSetDevice(ctx->device));
         d->ctx = ctx;
+        d->model = model;
+        d->ghost = model == 1 ? WORLDLINE_GHOST : VILLAIN_GHOST;
         d->Nt = Nt;
         d->Nx = Nx;
         d->ty = tiles_t;
@@ -594,9 +733,10 @@ int sv_domain_create(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tiles_t, int32
             SV_HIP(hipMemset(T.recv, 0, d->msg_words * sizeof(uint64_t)));
             SV_HIP(hipMalloc(&T.sum, sizeof(Summary)));
             SV_HIP(hipMemset(T.sum, 0, sizeof(Summary)));
+            if (model == 1) SV_HIP(hipMalloc(&T.stripes, (size_t)DOMAIN_BATCH * 2 * NSTRIPE * sizeof(StatStripe)));
         }
-        // split sweeps: strips whose stencil stays inside the tile run while the halos travel
-        {
+        // split sweeps (Villain): strips whose stencil stays inside the tile run while the halos travel
+        if (model == 0) {
             const int nsx = (d->Wt + FW_MAX - 1) / FW_MAX;
             const int TH = fused_th(d->Ht, nsx), nsy = (d->Ht + TH - 1) / TH;
             std::vector<int32_t> inner, outer;
@@ -658,6 +798,20 @@ int sv_domain_create(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tiles_t, int32
     }
 }
 
+int sv_domain_create(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t nranks,
+                     int32_t rank, const uint8_t *unique_id, sv_domain **out) {
+    return domain_create(ctx, 0, Nt, Nx, tiles_t, tiles_x, nranks, rank, unique_id, out);
+}
+
+int sv_domain_create_worldline(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t nranks,
+                               int32_t rank, const uint8_t *unique_id, sv_domain **out) {
+    if (Nt % 2 || Nx % 2) {
+        if (ctx) ctx->err = "the Worldline decomposition needs even lattice extents";
+        return -2;
+    }
+    return domain_create(ctx, 1, Nt, Nx, tiles_t, tiles_x, nranks, rank, unique_id, out);
+}
+
 int sv_domain_destroy(sv_domain *d) {
     if (!d) return 0;
     if (d->ctx) {
@@ -670,6 +824,7 @@ int sv_domain_destroy(sv_domain *d) {
         (void)hipFree(T.send);
         (void)hipFree(T.recv);
         (void)hipFree(T.sum);
+        (void)hipFree(T.stripes);
     }
     if (d->halo_stream) (void)hipStreamSynchronize(d->halo_stream);
     if (d->comm) (void)ncclCommDestroy(d->comm);
@@ -739,6 +894,7 @@ int sv_domain_run(sv_domain *d, double kappa, int64_t W, double interval_phi, in
     if (!d || !rng || (sweeps > 0 && !stats)) return -1;
     sv_ctx *ctx = d->ctx;
     try {
+        if (d->model != 0) throw std::invalid_argument("sv_domain_run runs a Villain domain (sv_domain_create)");
         if (sweeps < 0) throw std::invalid_argument("sweeps must be >= 0");
         if (interval_n < 0 || interval_n > (1 << 20)) throw std::invalid_argument("interval_n out of range");
         if ((W < 0 ? -W : W) * interval_n >= (1LL << 28)) throw std::invalid_argument("|W * interval_n| too large");
@@ -747,6 +903,48 @@ int sv_domain_run(sv_domain *d, double kappa, int64_t W, double interval_phi, in
         u128 inc{rng->inc_lo, rng->inc_hi};
         Cursor cur{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
         run_domain(d, P, sweeps, cur, inc, stats);
+        rng->state_hi = cur.s.hi;
+        rng->state_lo = cur.s.lo;
+        rng->has_uint32 = (int32_t)cur.has;
+        rng->uinteger = cur.buf;
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_domain_upload_worldline(sv_domain *d, const int64_t *m, const int64_t *v) {
+    if (!d) return -1;
+    if (d->model != 1) {
+        d->ctx->err = "not a Worldline domain";
+        return -2;
+    }
+    return sv_domain_upload(d, (const double *)v, m);  // the 8-byte planes are moved as bits
+}
+
+int sv_domain_download_worldline(sv_domain *d, int64_t *m, int64_t *v) {
+    if (!d) return -1;
+    if (d->model != 1) {
+        d->ctx->err = "not a Worldline domain";
+        return -2;
+    }
+    return sv_domain_download(d, (double *)v, m);
+}
+
+int sv_domain_run_worldline(sv_domain *d, double kappa, double W_eff, int64_t interval_t, int32_t steps, sv_rng *rng,
+                            sv_stats *stats) {
+    if (!d || !rng || (steps > 0 && !stats)) return -1;
+    sv_ctx *ctx = d->ctx;
+    try {
+        if (d->model != 1) throw std::invalid_argument("sv_domain_run_worldline runs a Worldline domain");
+        if (steps < 0) throw std::invalid_argument("steps must be >= 0");
+        if (!wf_usable(d->Nx, false, W_eff, interval_t) || d->Nt % 2)
+            throw std::invalid_argument("the decomposed Worldline step needs W a power of two and 1 <= interval_t <= 2^20");
+        SV_HIP(hipSetDevice(ctx->device));
+        u128 inc{rng->inc_lo, rng->inc_hi};
+        Cursor cur{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
+        run_wdomain(d, kappa, W_eff, interval_t, steps, cur, inc, stats);
         rng->state_hi = cur.s.hi;
         rng->state_lo = cur.s.lo;
         rng->has_uint32 = (int32_t)cur.has;

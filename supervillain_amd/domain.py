@@ -1,4 +1,5 @@
-"""Villain NeighborhoodUpdate on a domain-decomposed lattice (multi-GPU; SURVEY.md 8e, BASELINE config 4).
+"""Villain NeighborhoodUpdate, and the Worldline Plaquette + Coexact step, on a domain-decomposed lattice
+(multi-GPU; SURVEY.md 8e, BASELINE configs 4 and 3).
 
 The reference runs one lattice in one process (generator/villain/neighborhood.py:59-137); this is the
 same chain with the lattice cut into tiles (sv_domain_* in include/supervillain_amd.h).  One rank per
@@ -129,6 +130,56 @@ class VillainDomain:
                                                    int(sweeps), ctypes.byref(r), st), 'sv_domain_run')
         rng_to_numpy(r, rng)
         return [st[i] for i in range(sweeps)]
+
+
+class WorldlineDomain(VillainDomain):
+    """An Nt x Nx Worldline (m, v) state cut into tiles: one step = the checkerboard PlaquetteUpdate sweep and
+    the CoexactUpdate sweep of sv_worldline_plaquette_coexact_run (the config-3 step), one halo exchange per
+    step (sv_domain_*_worldline).  Integer v; W a power of two."""
+
+    def __init__(self, Nt, Nx=None, tiles=(1, 1), kappa=0.5, W=1, interval_t=1, *, device=None, nranks=1, rank=0,
+                 unique_id=None):
+        Nx = Nt if Nx is None else Nx
+        self.Nt, self.Nx, self.tiles = int(Nt), int(Nx), (int(tiles[0]), int(tiles[1]))
+        self.kappa, self.W, self.interval_t = float(kappa), float(W), int(interval_t)
+        self.nranks, self.rank = int(nranks), int(rank)
+        self.ctx = _native.context(_native.default_device() if device is None else device)
+        uid = None
+        if unique_id is not None:
+            uid = (ctypes.c_uint8 * UNIQUE_ID_BYTES).from_buffer_copy(bytes(unique_id))
+        h = ctypes.c_void_p()
+        self.ctx.check(_native.lib().sv_domain_create_worldline(self.ctx.handle, self.Nt, self.Nx, self.tiles[0],
+                                                                self.tiles[1], self.nranks, self.rank, uid,
+                                                                ctypes.byref(h)),
+                       'sv_domain_create_worldline')
+        self.handle = h
+
+    def cold(self):
+        self.ctx.check(_native.lib().sv_domain_upload_worldline(self.handle, None, None), 'sv_domain_upload_worldline')
+
+    def upload(self, m, v):
+        m = np.ascontiguousarray(m, dtype=np.int64).reshape(2, self.Nt, self.Nx)
+        v = np.ascontiguousarray(v, dtype=np.int64).reshape(self.Nt, self.Nx)
+        self.ctx.check(_native.lib().sv_domain_upload_worldline(self.handle, _native.ptr(m), _native.ptr(v)),
+                       'sv_domain_upload_worldline')
+
+    def download(self, m=None, v=None):
+        m = np.zeros((2, self.Nt, self.Nx), dtype=np.int64) if m is None else m
+        v = np.zeros((self.Nt, self.Nx), dtype=np.int64) if v is None else v
+        self.ctx.check(_native.lib().sv_domain_download_worldline(self.handle, _native.ptr(m), _native.ptr(v)),
+                       'sv_domain_download_worldline')
+        return m, v
+
+    def run(self, steps, rng):
+        """`steps` Plaquette + Coexact steps; advances `rng` like the reference's shared Generator.  Returns
+        2 * steps global stats ({Plaquette, Coexact} per step)."""
+        r = rng_from_numpy(rng)
+        st = _native.stats_array(max(2 * steps, 1))
+        self.ctx.check(_native.lib().sv_domain_run_worldline(self.handle, self.kappa, self.W, self.interval_t,
+                                                             int(steps), ctypes.byref(r), st),
+                       'sv_domain_run_worldline')
+        rng_to_numpy(r, rng)
+        return [st[i] for i in range(2 * steps)]
 
 
 def unique_id():
