@@ -20,7 +20,8 @@ Secondary workloads (not the headline line; BASELINE.json configs 5 and 3):
   --workload replicas   1024 independent L=128 Villain chains, W=2, inline observables, split over
                         the N ranks (config 5; replicas need no collectives)
   --workload worldline  L=1024 Worldline: one checkerboard PlaquetteUpdate + one CoexactUpdate sweep
-                        per step, W=1 (config 3); N > 1 runs independent replicas
+                        per step, W=1 (config 3); N > 1 (or --tiles) decomposes the lattice into tiles, one per
+                        GPU, with a (v, m) halo exchange per step
   --workload site|link|exact|cohomology|hammer
                         SURVEY.md 8(f) rows at L=4096: one sweep of SiteUpdate / LinkUpdate / ExactUpdate /
                         CohomologyUpdate per step, or one Villain Hammer step (Site, Link, Exact, Cohomology,
@@ -327,9 +328,70 @@ def run_worms(args, world, rank, dist):
     B.close()
 
 
+def run_worldline_domain(args, world, rank, dist):
+    """Config 3 decomposed (SURVEY.md 8(e)): one L x L Worldline lattice cut into ty x tx tiles (one per GPU;
+    --weak: an L x L tile per GPU), one (v, m) halo exchange per Plaquette + Coexact step; R1 = one GPU running
+    one periodic tile alone, as for config 4."""
+    from supervillain_amd import _native
+    from supervillain_amd.domain import WorldlineDomain, tile_grid
+    L = args.L
+    if args.tiles:
+        ty, tx = (int(v) for v in args.tiles.lower().split('x'))
+    else:
+        ty, tx = tile_grid(world)
+    Nt, Nx = (L, L) if args.strong else (ty * L, tx * L)
+    Ht, Wt = Nt // ty, Nx // tx
+    kw = dict(kappa=args.kappa, W=args.W)
+    dom = WorldlineDomain.distributed(Nt, Nx, (ty, tx), **kw) if world > 1 else WorldlineDomain(Nt, Nx, (ty, tx), **kw)
+    dom.cold()
+    gen = np.random.default_rng(0)
+    Lib = _native.lib()
+    warm_up(lambda k: dom.run(k, gen), args, dist)
+    Lib.sv_ctx_set_timing(dom.ctx.handle, 1)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    st = dom.run(args.steps, gen)
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = max_over_ranks(dist, t1 - t0)
+    avg_launch_s = kernel_time(Lib, dom.ctx)
+    acc = sum(st[2 * i].accepted for i in range(args.steps)) / (args.steps * Nt * Nx)
+    ctx = dom.ctx
+    dom.close()
+    one = WorldlineDomain(Ht, Wt, (1, 1), **kw)
+    one.cold()
+    g1 = np.random.default_rng(1)
+    one.run(max(args.warmup, 5), g1)
+    k1 = max(args.steps, 20)
+    t = time.perf_counter()
+    one.run(k1, g1)
+    r1 = Ht * Wt * k1 / (time.perf_counter() - t)
+    one.close()
+    r1_mean = r1 if dist is None else _mean_over_ranks(dist, r1)
+    if rank == 0:
+        value = args.steps * Nt * Nx / elapsed
+        config = {'workload': f'{Nt}x{Nx} Worldline: checkerboard PlaquetteUpdate + CoexactUpdate sweep per step, '
+                              f'W={args.W}, kappa={args.kappa}, domain-decomposed into {ty}x{tx} tiles of {Ht}x{Wt} '
+                              '(one per GPU), (v, m) halo exchange per step, bit-exact PCG64 replay',
+                  'L': L, 'lattice': [Nt, Nx], 'tiles': [ty, tx], 'path': 'worldline-domain',
+                  'parallelism': f'{ty}x{tx} domain decomposition over {world} GPU(s)',
+                  'weak_scaling': {'tile': [Ht, Wt], 'R1': r1_mean, 'E_N': value / (world * r1_mean),
+                                   'definition': 'E_N = R_N / (N R1), R1 = one GPU running one periodic tile '
+                                                 'of this size alone (SURVEY.md 8(d))'}}
+        report(args, world, Nt * Nx, Nt * Nx // world, elapsed, acc, avg_launch_s, config, Ht,
+               metric=f'plaquette-steps/sec (Plaquette + Coexact sweep), L={L} Worldline, W={args.W}',
+               unit='plaquette-steps/s', kernel='worldline_step_fused', alg_bytes=WORLDLINE_BYTES,
+               min_bytes=WORLDLINE_BYTES, ctx=ctx)
+
+
 def run_worldline(args, world, rank, dist):
     """BASELINE config 3: L x L Worldline, one checkerboard PlaquetteUpdate sweep + one CoexactUpdate
-    sweep per step, m = v = 0 cold start; N > 1 runs independent chains (seed = rank)."""
+    sweep per step (one worldline_step_fused launch), m = v = 0 cold start; N > 1 (or --tiles) decomposes
+    the lattice (run_worldline_domain)."""
+    if world > 1 or args.tiles:
+        return run_worldline_domain(args, world, rank, dist)
     from supervillain_amd import _native
     from supervillain_amd._abi import rng_from_numpy
     L = args.L
@@ -380,12 +442,13 @@ def run_worldline(args, world, rank, dist):
 
     if rank == 0:
         config = {'workload': f'L={L} Worldline: checkerboard PlaquetteUpdate + CoexactUpdate sweep per step, '
-                              f'W={args.W}, kappa={args.kappa}, bit-exact PCG64 replay (per-colour kernels)',
-                  'L': L, 'path': 'worldline', 'parallelism': f'{world} independent chain(s)'}
+                              f'W={args.W}, kappa={args.kappa}, bit-exact PCG64 replay (one worldline_step_fused '
+                              'launch per step)',
+                  'L': L, 'path': 'worldline', 'parallelism': 'single GPU'}
         report(args, world, world * L * L, L * L, elapsed, acc / (args.steps * L * L), step_kernel_s, config, L,
                metric=f'plaquette-steps/sec (Plaquette + Coexact sweep), L={L} Worldline, W={args.W}',
-               unit='plaquette-steps/s', kernel='plaquette_cb_gs+coexact_gs', alg_bytes=WORLDLINE_BYTES,
-               min_bytes=WORLDLINE_BYTES, baseline=baseline, ctx=ctx, scaling='weak')
+               unit='plaquette-steps/s', kernel='worldline_step_fused', alg_bytes=WORLDLINE_BYTES,
+               min_bytes=WORLDLINE_BYTES, baseline=baseline, ctx=ctx, scaling='strong')
     Lib.sv_worldline_destroy(h)
 
 

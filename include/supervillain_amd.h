@@ -205,6 +205,11 @@ int sv_domain_upload_worldline(sv_domain *d, const int64_t *m, const int64_t *v)
 int sv_domain_download_worldline(sv_domain *d, int64_t *m, int64_t *v);
 int sv_domain_run_worldline(sv_domain *d, double kappa, double W_eff, int64_t interval_t, int32_t steps, sv_rng *rng,
                             sv_stats *stats);
+/* Host-only geometry queries of a Worldline decomposition (as sv_domain_exchange_plan / _message_layout). */
+int sv_domain_exchange_plan_worldline(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t rank,
+                                      int64_t *out);
+int sv_domain_message_layout_worldline(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t rank,
+                                       int64_t *out);
 
 
 /* ---- Villain replica batches (BASELINE config 5; SURVEY.md 8e: replicas need no collectives) ------- */

@@ -79,6 +79,8 @@ def lib():
         L.sv_domain_upload_worldline.argtypes = [vp, vp, vp]
         L.sv_domain_download_worldline.argtypes = [vp, vp, vp]
         L.sv_domain_run_worldline.argtypes = [vp, f64, f64, i64, i32, P(SvRng), P(SvStats)]
+        L.sv_domain_exchange_plan_worldline.argtypes = [i32, i32, i32, i32, i32, vp]
+        L.sv_domain_message_layout_worldline.argtypes = [i32, i32, i32, i32, i32, vp]
         L.sv_replicas_create.argtypes = [vp, i32, i32, P(vp)]
         L.sv_replicas_destroy.argtypes = [vp]
         L.sv_replicas_upload.argtypes = [vp, vp, vp]
@@ -105,6 +107,7 @@ EXPORTED = ('sv_ctx_create', 'sv_ctx_destroy', 'sv_last_error', 'sv_device_count
             'sv_domain_unique_id', 'sv_domain_create', 'sv_domain_destroy', 'sv_domain_upload', 'sv_domain_download',
             'sv_domain_run', 'sv_domain_exchange_plan', 'sv_domain_message_layout', 'sv_domain_create_worldline',
             'sv_domain_upload_worldline', 'sv_domain_download_worldline', 'sv_domain_run_worldline',
+            'sv_domain_exchange_plan_worldline', 'sv_domain_message_layout_worldline',
             'sv_replicas_create', 'sv_replicas_destroy', 'sv_replicas_upload', 'sv_replicas_download',
             'sv_replicas_run', 'sv_replicas_villain', 'sv_villain_worm_run', 'sv_replicas_worm_run', 'sv_worldline_worm_run',
             'sv_worldline_worm_batch')

@@ -632,10 +632,12 @@ int sv_domain_unique_id(uint8_t *id) {
     return 0;
 }
 
-int sv_domain_exchange_plan(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t rank, int64_t *out) {
+static int exchange_plan_impl(int model, int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t rank,
+                              int64_t *out) {
     try {
         if (!out || tiles_t < 1 || tiles_x < 1 || rank < 0 || rank >= tiles_t * tiles_x) return -1;
         sv_domain d;
+        d.ghost = model == 1 ? WORLDLINE_GHOST : VILLAIN_GHOST;
         d.Nt = Nt;
         d.Nx = Nx;
         d.ty = tiles_t;
@@ -664,10 +666,12 @@ int sv_domain_exchange_plan(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t til
     }
 }
 
-int sv_domain_message_layout(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t rank, int64_t *out) {
+static int message_layout_impl(int model, int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t rank,
+                               int64_t *out) {
     try {
         if (!out || tiles_t < 1 || tiles_x < 1 || rank < 0 || rank >= tiles_t * tiles_x) return -1;
         sv_domain d;
+        d.ghost = model == 1 ? WORLDLINE_GHOST : VILLAIN_GHOST;
         d.Nt = Nt;
         d.Nx = Nx;
         d.ty = tiles_t;
@@ -691,6 +695,21 @@ int sv_domain_message_layout(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t ti
     } catch (const std::exception &) {
         return -2;
     }
+}
+
+int sv_domain_exchange_plan(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t rank, int64_t *out) {
+    return exchange_plan_impl(0, Nt, Nx, tiles_t, tiles_x, rank, out);
+}
+int sv_domain_exchange_plan_worldline(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t rank,
+                                      int64_t *out) {
+    return exchange_plan_impl(1, Nt, Nx, tiles_t, tiles_x, rank, out);
+}
+int sv_domain_message_layout(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t rank, int64_t *out) {
+    return message_layout_impl(0, Nt, Nx, tiles_t, tiles_x, rank, out);
+}
+int sv_domain_message_layout_worldline(int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t rank,
+                                       int64_t *out) {
+    return message_layout_impl(1, Nt, Nx, tiles_t, tiles_x, rank, out);
 }
 
 static int domain_create(sv_ctx *ctx, int model, int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x,

@@ -31,13 +31,18 @@ def tile_grid(nranks):
     return t, nranks // t
 
 
-def exchange_plan(Nt, Nx, tiles, rank):
-    """The halo messages of tile `rank` as computed by libsvhip.so (host-only; no GPU needed).
+GHOSTS = {'villain': (2, 3, 2, 3), 'worldline': (5, 4, 5, 4)}  # ghost rows above / below, columns left / right
+
+
+def exchange_plan(Nt, Nx, tiles, rank, model='villain'):
+    """The halo messages of tile `rank` as computed by libsvhip.so (host-only; no GPU needed), for a Villain or a
+    Worldline decomposition (their ghost frames differ: GHOSTS).
 
     Returns a list of 8 dicts in send order: dy, dx, send_to, src (row0, col0), shape (rows, cols),
     recv_from, dst (row0, col0) -- tile-local coordinates, ghosts outside [0, Ht) x [0, Wt)."""
     out = (ctypes.c_int64 * 80)()
-    rc = _native.lib().sv_domain_exchange_plan(int(Nt), int(Nx), int(tiles[0]), int(tiles[1]), int(rank), out)
+    fn = _native.lib().sv_domain_exchange_plan_worldline if model == 'worldline' else _native.lib().sv_domain_exchange_plan
+    rc = fn(int(Nt), int(Nx), int(tiles[0]), int(tiles[1]), int(rank), out)
     if rc != 0:
         raise ValueError(f'invalid decomposition {Nt}x{Nx} into {tiles} (rank {rank})')
     plan = []
@@ -48,13 +53,15 @@ def exchange_plan(Nt, Nx, tiles, rank):
     return plan
 
 
-def message_layout(Nt, Nx, tiles, rank):
+def message_layout(Nt, Nx, tiles, rank, model='villain'):
     """The RCCL message layout libsvhip.so uses for `rank` when every tile is a rank (host-only).
 
     Returns dict: sends / recvs = [(peer, offset, words)], soff / roff = per-direction word offsets of
     message s in the send / receive buffer, words = per-direction message size, msg_words = buffer size."""
     out = (ctypes.c_int64 * 128)()
-    rc = _native.lib().sv_domain_message_layout(int(Nt), int(Nx), int(tiles[0]), int(tiles[1]), int(rank), out)
+    fn = (_native.lib().sv_domain_message_layout_worldline if model == 'worldline'
+          else _native.lib().sv_domain_message_layout)
+    rc = fn(int(Nt), int(Nx), int(tiles[0]), int(tiles[1]), int(rank), out)
     if rc != 0:
         raise ValueError(f'invalid decomposition {Nt}x{Nx} into {tiles} (rank {rank})')
     o = [int(v) for v in out]

@@ -1,24 +1,26 @@
 """Domain decomposition host logic (CPU): the halo plan computed by libsvhip.so fills every ghost cell
 with the right periodic neighbour value, its send/receive order matches pairwise (the RCCL
 point-to-point matching rule), and a real 2-rank exchange over torch.distributed (gloo) executed
-from that plan reproduces the ghost frames.  The device kernels are covered by test_gpu_domain.py."""
+from that plan reproduces the ghost frames -- for the Villain decomposition (2/3-wide ghost frame) and the
+Worldline one (5/4-wide).  The device kernels are covered by test_gpu_domain.py and test_gpu_wdomain.py."""
 import os
 import socket
 
 import numpy as np
 import pytest
 
-from supervillain_amd.domain import exchange_plan, message_layout, tile_grid
+from supervillain_amd.domain import GHOSTS, exchange_plan, message_layout, tile_grid
 
-GT, GB, GL, GR = 2, 3, 2, 3  # ghost rows above / below, columns left / right
+MODELS = list(GHOSTS)
 
 
 def test_tile_grid():
     assert [tile_grid(n) for n in (1, 2, 4, 8, 6, 3)] == [(1, 1), (1, 2), (2, 2), (2, 4), (2, 3), (1, 3)]
 
 
-def padded_tile(G, tiles, rank):
+def padded_tile(G, tiles, rank, model):
     """Tile `rank` of global array G with an unfilled (NaN) ghost frame."""
+    GT, GB, GL, GR = GHOSTS[model]
     Nt, Nx = G.shape
     ty, tx = tiles
     Ht, Wt = Nt // ty, Nx // tx
@@ -28,7 +30,8 @@ def padded_tile(G, tiles, rank):
     return P
 
 
-def expected_frame(G, tiles, rank):
+def expected_frame(G, tiles, rank, model):
+    GT, GB, GL, GR = GHOSTS[model]
     Nt, Nx = G.shape
     ty, tx = tiles
     Ht, Wt = Nt // ty, Nx // tx
@@ -38,12 +41,14 @@ def expected_frame(G, tiles, rank):
     return G[np.ix_(rows, cols)]
 
 
-def message(P, m):
+def message(P, m, model):
+    GT, GB, GL, GR = GHOSTS[model]
     (r0, c0), (h, w) = m['src'], m['shape']
     return P[GT + r0:GT + r0 + h, GL + c0:GL + c0 + w].copy()
 
 
-def place(P, m, block):
+def place(P, m, block, model):
+    GT, GB, GL, GR = GHOSTS[model]
     (r0, c0), (h, w) = m['dst'], m['shape']
     P[GT + r0:GT + r0 + h, GL + c0:GL + c0 + w] = block
 
@@ -51,33 +56,35 @@ def place(P, m, block):
 GRIDS = [(1, 1), (1, 2), (2, 1), (2, 2), (2, 4), (3, 2), (1, 8), (4, 4)]
 
 
+@pytest.mark.parametrize('model', MODELS)
 @pytest.mark.parametrize('tiles', GRIDS)
-def test_plan_fills_every_ghost(tiles):
+def test_plan_fills_every_ghost(tiles, model):
     ty, tx = tiles
     Nt, Nx = 8 * ty, 6 * tx
     G = np.random.default_rng(0).normal(size=(Nt, Nx))
     ntiles = ty * tx
-    plans = [exchange_plan(Nt, Nx, tiles, r) for r in range(ntiles)]
-    P = [padded_tile(G, tiles, r) for r in range(ntiles)]
+    plans = [exchange_plan(Nt, Nx, tiles, r, model) for r in range(ntiles)]
+    P = [padded_tile(G, tiles, r, model) for r in range(ntiles)]
     sent = {}
     for r in range(ntiles):
         for s, m in enumerate(plans[r]):
-            sent[(r, m['send_to'], s)] = message(P[r], m)
+            sent[(r, m['send_to'], s)] = message(P[r], m, model)
     for r in range(ntiles):
         for s, m in enumerate(plans[r]):
-            place(P[r], m, sent[(m['recv_from'], r, s)])
+            place(P[r], m, sent[(m['recv_from'], r, s)], model)
     for r in range(ntiles):
-        np.testing.assert_array_equal(P[r], expected_frame(G, tiles, r))
+        np.testing.assert_array_equal(P[r], expected_frame(G, tiles, r, model))
 
 
+@pytest.mark.parametrize('model', MODELS)
 @pytest.mark.parametrize('tiles', GRIDS)
-def test_plan_pairwise_order_matches(tiles):
+def test_plan_pairwise_order_matches(tiles, model):
     """ncclSend/ncclRecv between one pair of ranks match in call order: rank a's sends to b (in send
     order) must be b's receives from a (in receive order), message by message."""
     ty, tx = tiles
     Nt, Nx = 8 * ty, 6 * tx
     ntiles = ty * tx
-    plans = [exchange_plan(Nt, Nx, tiles, r) for r in range(ntiles)]
+    plans = [exchange_plan(Nt, Nx, tiles, r, model) for r in range(ntiles)]
     for a in range(ntiles):
         for b in range(ntiles):
             if a == b:
@@ -96,6 +103,8 @@ def test_plan_rejects_bad_decompositions():
         exchange_plan(6, 12, (2, 2), 0)    # odd tile extent
     with pytest.raises(ValueError):
         exchange_plan(4, 4, (2, 2), 0)     # 2 x 2 tiles are too small
+    with pytest.raises(ValueError):
+        exchange_plan(8, 8, (2, 2), 0, 'worldline')  # 4 x 4 tiles are smaller than the 5-wide ghost frame
 
 
 def _free_port():
@@ -104,7 +113,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _exchange_worker(rank, world, port, tiles, Nt, Nx, errfile):
+def _exchange_worker(rank, world, port, tiles, Nt, Nx, errfile, model):
     import torch
     import torch.distributed as dist
     os.environ['MASTER_ADDR'] = '127.0.0.1'
@@ -112,14 +121,14 @@ def _exchange_worker(rank, world, port, tiles, Nt, Nx, errfile):
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
         G = np.random.default_rng(1).normal(size=(Nt, Nx))
-        plan = exchange_plan(Nt, Nx, tiles, rank)
-        lay = message_layout(Nt, Nx, tiles, rank)
-        P = padded_tile(G, tiles, rank)
+        plan = exchange_plan(Nt, Nx, tiles, rank, model)
+        lay = message_layout(Nt, Nx, tiles, rank, model)
+        P = padded_tile(G, tiles, rank, model)
         # the C++ RCCL loop: a send buffer laid out per peer (message s at soff[s] = [flag, pad, phi, n0, n1]),
         # one send per distinct peer, one receive per distinct source; self messages stay local
         send = np.zeros(lay['msg_words'])
         for s, m in enumerate(plan):
-            blk = message(P, m).ravel()
+            blk = message(P, m, model).ravel()
             o = lay['soff'][s]
             assert lay['words'][s] == 2 + 3 * blk.size
             send[o + 2:o + 2 + blk.size] = blk
@@ -136,9 +145,9 @@ def _exchange_worker(rank, world, port, tiles, Nt, Nx, errfile):
                 o = lay['roff'][s]
                 block = recvbuf.numpy()[o + 2:o + 2 + cnt].reshape(m['shape'])
             else:
-                block = message(P, plan[s])
-            place(P, m, block)
-        np.testing.assert_array_equal(P, expected_frame(G, tiles, rank))
+                block = message(P, plan[s], model)
+            place(P, m, block, model)
+        np.testing.assert_array_equal(P, expected_frame(G, tiles, rank, model))
     except Exception as e:  # report to the parent
         with open(errfile, 'a') as f:
             f.write(f'rank {rank}: {e!r}\n')
@@ -147,19 +156,21 @@ def _exchange_worker(rank, world, port, tiles, Nt, Nx, errfile):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize('model', MODELS)
 @pytest.mark.parametrize('tiles', [(1, 2), (2, 1), (2, 2)])
-def test_two_rank_gloo_exchange(tiles, tmp_path):
+def test_two_rank_gloo_exchange(tiles, model, tmp_path):
     import torch.multiprocessing as mp
     errfile = str(tmp_path / 'err.txt')
     Nt, Nx = 8 * tiles[0], 6 * tiles[1]
     world = tiles[0] * tiles[1]
-    mp.start_processes(_exchange_worker, args=(world, _free_port(), tiles, Nt, Nx, errfile), nprocs=world,
+    mp.start_processes(_exchange_worker, args=(world, _free_port(), tiles, Nt, Nx, errfile, model), nprocs=world,
                        join=True, start_method='spawn')
     assert not os.path.exists(errfile), open(errfile).read()
 
 
+@pytest.mark.parametrize('model', MODELS)
 @pytest.mark.parametrize('tiles', GRIDS)
-def test_rccl_blocks_line_up(tiles):
+def test_rccl_blocks_line_up(tiles, model):
     """The per-peer message blocks libsvhip.so sends (one ncclSend / ncclRecv per distinct peer): rank a's block
     for b and rank b's block from a have the same size, and every message s sits at the same offset inside
     both blocks, so the receiver's ghost block s gets exactly the sender's message s."""
@@ -167,8 +178,8 @@ def test_rccl_blocks_line_up(tiles):
     ty, tx = tiles
     Nt, Nx = 8 * ty, 6 * tx
     ntiles = ty * tx
-    lay = [message_layout(Nt, Nx, tiles, r) for r in range(ntiles)]
-    plans = [exchange_plan(Nt, Nx, tiles, r) for r in range(ntiles)]
+    lay = [message_layout(Nt, Nx, tiles, r, model) for r in range(ntiles)]
+    plans = [exchange_plan(Nt, Nx, tiles, r, model) for r in range(ntiles)]
     for a in range(ntiles):
         L = lay[a]
         # blocks are disjoint, inside the buffer, and one per distinct remote peer

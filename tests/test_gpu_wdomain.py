@@ -135,3 +135,25 @@ def test_rccl_loopback(N):
     a = run_domain(N, (1, 1), m0, v0, 4, g := np.random.default_rng(3), rccl=True) + (g,)
     b = run_single(N, m0, v0, 4, gg := np.random.default_rng(3)) + (gg,)
     assert_same(a, b)
+
+
+def test_rectangular_lattice_decomposes_consistently():
+    """An even rectangular Nt x Nx Worldline lattice (an engine extension: the reference's Lattice2D is square;
+    bench.py's R1 runs one periodic tile of a decomposition this way) gives the same chain as one tile and as
+    1 x 2 and 2 x 2 tiles."""
+    Nt, Nx, steps = 64, 128, 4
+    r = np.random.default_rng(6)
+    m0, v0 = np.zeros((2, Nt, Nx), dtype=np.int64), r.integers(-3, 4, (Nt, Nx)).astype(np.int64)
+    out = []
+    for tiles in [(1, 1), (1, 2), (2, 2)]:
+        dom = WorldlineDomain(Nt, Nx, tiles, 0.5, 1)
+        try:
+            dom.upload(m0, v0)
+            g = np.random.default_rng(4)
+            st = dom.run(steps, g)
+            m, v = dom.download()
+        finally:
+            dom.close()
+        out.append((m, v, st, g))
+    for o in out[1:]:
+        assert_same(o, out[0])
