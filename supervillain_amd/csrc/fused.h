@@ -105,9 +105,62 @@ __device__ __forceinline__ int32_t wrapN(int32_t v, int32_t N) {
 #define SV_ABLATE 0  // timing experiments only: 1 = no exp, 2 = no RNG compositions, 4 = no wrapped-column jumps,
                      // 8 = no HBM stores, 16 = no HBM loads, 64 = no choice draws
 #endif
+#ifndef SV_EXP_OCML
+#define SV_EXP_OCML 1
+#endif
+// d = a*b + c as the three-address v_fma_f64: the compiler writes ocml's Horner chain as v_fmac_f64 on a copy of
+// each hoisted coefficient (one v_mov_b64 per step); written out, the coefficients are read in place
+#ifndef SV_EXP_SCOEF
+#define SV_EXP_SCOEF 0
+#endif
+__device__ __forceinline__ double fma3(double a, double b, double c) {
+    double d;
+#if SV_EXP_SCOEF
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+#else
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+#endif
+    return d;
+}
+// a*b + 1.0 (inline constant operand)
+__device__ __forceinline__ double fma3_one(double a, double b) {
+    double d;
+    asm("v_fma_f64 %0, %1, %2, 1.0" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
+// a*b + c, b an SGPR pair
+__device__ __forceinline__ double fma3_s(double a, double b, double c) {
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "s"(b), "v"(c));
+    return d;
+}
+// ocml's __ocml_exp_f64 (ROCm device libs, ocml.bc) restated operation for operation -- the same
+// reduction, polynomial, ldexp and range selects, hence the same bits as exp()
+__device__ __forceinline__ double exp_ocml(double x) {
+    const double t = __builtin_rint(x * 0x1.71547652b82fep+0);
+    const double nt = -t;
+    double r = __builtin_fma(nt, 0x1.62e42fefa39efp-1, x);
+    r = __builtin_fma(nt, 0x1.abc9e3b39803fp-56, r);
+    double p = fma3_s(r, 0x1.ade156a5dcb37p-26, 0x1.28af3fca7ab0cp-22);
+    p = fma3(r, p, 0x1.71dee623fde64p-19);
+    p = fma3(r, p, 0x1.a01997c89e6b0p-16);
+    p = fma3(r, p, 0x1.a01a014761f6ep-13);
+    p = fma3(r, p, 0x1.6c16c1852b7b0p-10);
+    p = fma3(r, p, 0x1.1111111122322p-7);
+    p = fma3(r, p, 0x1.55555555502a1p-5);
+    p = fma3(r, p, 0x1.5555555555511p-3);
+    p = fma3(r, p, 0x1.000000000000bp-1);
+    p = fma3_one(r, p);
+    p = fma3_one(r, p);
+    double e = __builtin_amdgcn_ldexp(p, (int)t);
+    e = x > 1024.0 ? __builtin_inf() : e;
+    return x < -1075.0 ? 0.0 : e;
+}
 __device__ __forceinline__ double sv_exp(double x) {
 #if SV_ABLATE & 1
     return 1.0 + x * 0.5;
+#elif SV_EXP_OCML
+    return exp_ocml(x);
 #else
     return exp(x);
 #endif

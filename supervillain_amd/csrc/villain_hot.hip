@@ -21,6 +21,10 @@
 // front of them changes at most the sign of a zero, and exp(+-0) = 1.
 #include "fused.h"
 
+#ifndef SV_HOT_ADV
+#define SV_HOT_ADV 1  // row bases advanced by the precomputed maps behind a wave-uniform test (r3xx A/B)
+#endif
+
 namespace sv {
 
 struct HotDraws {
@@ -223,6 +227,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
     const uint32_t bhas = (base_lane && bty >= 2) ? A.blocks[bblk].has : 0u;
     const int32_t tfirst = t0 - 3;
     int32_t brow = tfirst + 2 - bc + wave;  // colour 0 row t+2+wave, colour 1 row t+1+wave
+    int32_t brow1 = tfirst + 1 + wave;      // the colour-1 row, wave-uniform
     u128 bases{0, 0};
     if (base_lane) bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)base_pos(bty, grow(brow), Nx, bx, bhas));
     __builtin_amdgcn_s_waitcnt(0);
@@ -415,7 +420,20 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
             }
         }
         commit(t + 3 + NW);
-        if (base_lane) {
+        // The bases of the wave's two rows (brow1, brow1 + 1) move NW rows down.  Unless a row wraps around the
+        // lattice or sits on global row 0 (where a buffered half-word clamps the word index), every block's
+        // position moves by exactly its stride, so each base lane applies its precomputed advance map; the
+        // wave-uniform test keeps the position arithmetic (64-bit, on every lane) off the common path.
+        const int32_t glo = grow(brow1);
+        brow1 += NW;
+        if (SV_HOT_ADV && glo >= 1 && glo + NW + 1 < Nt) {
+            if (base_lane) {
+                const int ai = bty == 0 ? 0 : (bty == 1 ? 1 : 2);
+                bases = mad128c(s_adv[ai].A, bases, s_adv[ai].C);
+                s_base[wave][lane] = bases;
+            }
+            brow += NW;
+        } else if (base_lane) {
             const int64_t p_old = base_pos(bty, grow(brow), Nx, bx, bhas);
             const int64_t p_new = base_pos(bty, grow(brow + NW), Nx, bx, bhas);
             const int ai = bty == 0 ? 0 : (bty == 1 ? 1 : 2);
@@ -424,6 +442,8 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
             else bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)p_new);
             brow += NW;
             s_base[wave][lane] = bases;
+        } else {
+            brow += NW;
         }
         __syncthreads();
     }
