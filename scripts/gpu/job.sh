@@ -1,8 +1,8 @@
 source scripts/gpu/guard.sh
-T=${1:-r301}
+T=${1:-r305}
 O=gpurun_out/$T
 mkdir -p $O
 export TMPDIR=/tmp
-step tests timeout -k 10 600 python -u -m pytest tests/test_gpu_villain.py tests/test_gpu_domain.py tests/test_gpu_boundary.py -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1
+step tests timeout -k 10 600 python -u -m pytest tests/test_gpu_villain.py tests/test_gpu_domain.py tests/test_gpu_boundary.py tests/test_gpu_pipeline.py -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1
 tail -3 $O/tests.log
-bash scripts/gpu/job_ab.sh $T/ab "v0 v1 v2 v3"
+REPS="1 2 3" bash scripts/gpu/job_ab.sh $T/ab "s0 s1"

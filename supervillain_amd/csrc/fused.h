@@ -111,7 +111,7 @@ __device__ __forceinline__ int32_t wrapN(int32_t v, int32_t N) {
 // d = a*b + c as the three-address v_fma_f64: the compiler writes ocml's Horner chain as v_fmac_f64 on a copy of
 // each hoisted coefficient (one v_mov_b64 per step); written out, the coefficients are read in place
 #ifndef SV_EXP_SCOEF
-#define SV_EXP_SCOEF 0
+#define SV_EXP_SCOEF 0  // coefficients as SGPR operands: 257 vs 253 us (r303), not kept
 #endif
 __device__ __forceinline__ double fma3(double a, double b, double c) {
     double d;
@@ -479,7 +479,11 @@ __device__ __forceinline__ u128 mad128c(u128 a, u128 s, u128 c) {
     return u128{((U2 & 0xFFFFFFFFull) << 32) | (T & 0xFFFFFFFFull), ((uint64_t)r3 << 32) | (X & 0xFFFFFFFFull)};
 }
 __device__ __forceinline__ u128 hot_apply(const SmallTab &sm, uint32_t i, u128 base) {
+#if SV_ABLATE & 2
+    return u128{base.lo ^ sm.A[i].lo, base.hi + sm.C[i].hi};
+#else
     return mad128c(sm.A[i], base, sm.C[i]);
+#endif
 }
 
 // NumPy random(): (x >> 11) * 2^-53, exactly: with m = x >> 11 = h 2^32 + l (h < 2^21),

@@ -180,7 +180,12 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
     int pf_gx[PF];
 #pragma unroll
     for (int k = 0; k < PF; k++) pf_gx[k] = mcol(x0 - 2 + lane + 64 * k);
+    if (SV_ABLATE & 16) {
+#pragma unroll
+        for (int k = 0; k < PF; k++) pf_phi[k] = 0.0, pf_n0[k] = pf_n1[k] = 0;
+    }
     auto prefetch = [&](int32_t ra) {
+        if (SV_ABLATE & 16) return;
         const int32_t q = ra + wave;
         if (q >= t0 - 2 && q <= t1 + 2) {
             const int64_t g0 = mrow(q);
@@ -254,6 +259,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
     double psum = 0.0;
 
     auto store_rows = [&](int32_t ra) {
+        if (SV_ABLATE & 8) return;
         const int32_t q = ra + wave;
         if (q >= t0 && q < t1) {
             const int slot = (q - rbase) % R;
@@ -293,7 +299,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
             // W * (index - interval_n), neighborhood.py:105-107: one v_mad_i32_i24 (hot_ok bounds |W|, k < 2^20)
             cn[j] = SV_HOT_MUL24 ? __mul24((int32_t)(m >> 32), Wn) - nW : (int32_t)(m >> 32) * Wn - nW;
         }
-        if (__builtin_expect(rej && active, 0)) {
+        if (__builtin_expect(rej && active && !(SV_ABLATE & 2), 0)) {
             const uint32_t rank = (uint32_t)(((int64_t)gq * Nx + wrapN(Gm.X0 + x, Nx)) >> 1);
 #pragma unroll
             for (int j = 0; j < 4; j++)
@@ -372,7 +378,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
                 s_r1[s0][cm] = wr[3];
             }
         }
-        __syncthreads();
+        if (!(SV_ABLATE & 32)) __syncthreads();
         // ---------------- colour 1 on row q = t+1+wave; rows t.. become final
         {
             const int32_t q = t + 1 + wave;
@@ -445,7 +451,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
         } else {
             brow += NW;
         }
-        __syncthreads();
+        if (!(SV_ABLATE & 32)) __syncthreads();
     }
     {
         int32_t tl = tfirst;
