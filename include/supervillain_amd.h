@@ -11,7 +11,7 @@
  *
  * Conventions
  *   - Every function returns 0 on success and a negative code on failure; sv_last_error(ctx) then
- *     holds the message.  Calls are synchronous on return.
+ *     holds the message.  Calls are synchronous on return (except sv_*_emit, which says so).
  *   - Host arrays are borrowed, C-contiguous, row-major (component axis first, then (t, x)), exactly
  *     the reference's Form layout (supervillain/lattice/compact.py:244-261): phi (1,N,N) float64,
  *     n and m (2,N,N) int64, v (1,N,N) int64 (float64 when W is infinite, worldline.py:110-112).
@@ -23,6 +23,7 @@
 #ifndef SUPERVILLAIN_AMD_H
 #define SUPERVILLAIN_AMD_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -87,6 +88,15 @@ int sv_villain_create(sv_ctx *ctx, int32_t N, sv_villain **out);
 int sv_villain_destroy(sv_villain *st);
 int sv_villain_upload(sv_villain *st, const double *phi, const int64_t *n);
 int sv_villain_download(sv_villain *st, double *phi, int64_t *n);
+/* Asynchronous emission of the resident configuration into host storage (the D2H of
+ * Ensemble.generate's kept configurations, ensemble.py:89-92, overlapped with the sweeps that follow).
+ * sv_villain_emit returns at once: the state as of every sweep queued so far is snapshotted on the device
+ * (two alternating emission buffers) and copied to phi / n on a copy stream.  The host arrays must stay
+ * valid and unread until sv_villain_emit_wait returns; register them with sv_host_register for a true DMA. */
+int sv_villain_emit(sv_villain *st, double *phi, int64_t *n);
+int sv_villain_emit_wait(sv_villain *st);
+int sv_host_register(void *p, size_t bytes);   /* pin host memory (hipHostRegister) */
+int sv_host_unregister(void *p);
 /* path: 0 = auto (fused two-colour sweep kernel for even N, per-colour kernels otherwise),
  *       1 = per-colour kernels (any N), 2 = fused (even N only). */
 int sv_villain_run(sv_villain *st, double kappa, int64_t W, double interval_phi, int64_t interval_n, int32_t sweeps,
@@ -124,6 +134,9 @@ int sv_worldline_create(sv_ctx *ctx, int32_t N, int32_t v_is_float, sv_worldline
 int sv_worldline_destroy(sv_worldline *st);
 int sv_worldline_upload(sv_worldline *st, const int64_t *m, const void *v);
 int sv_worldline_download(sv_worldline *st, int64_t *m, void *v);
+/* As sv_villain_emit / sv_villain_emit_wait, for (m, v). */
+int sv_worldline_emit(sv_worldline *st, int64_t *m, void *v);
+int sv_worldline_emit_wait(sv_worldline *st);
 
 /* Replaces CoexactUpdate.step, supervillain/generator/worldline/coexact.py:53-128 (interval_t from
  * coexact.py:32).  v is read only. */

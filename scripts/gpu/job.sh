@@ -1,8 +1,11 @@
 source scripts/gpu/guard.sh
-T=${1:-r305}
+T=${1:-r306}
 O=gpurun_out/$T
 mkdir -p $O
 export TMPDIR=/tmp
-step tests timeout -k 10 600 python -u -m pytest tests/test_gpu_villain.py tests/test_gpu_domain.py tests/test_gpu_boundary.py tests/test_gpu_pipeline.py -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1
+step tests timeout -k 10 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_villain.py -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1
 tail -3 $O/tests.log
-REPS="1 2 3" bash scripts/gpu/job_ab.sh $T/ab "s0 s1"
+step emit timeout -k 10 300 python scripts/perf/emit_overlap.py > $O/emit.log 2>&1
+tail -2 $O/emit.log
+step emit2 timeout -k 10 300 python scripts/perf/emit_overlap.py --keep 8 > $O/emit8.log 2>&1
+tail -2 $O/emit8.log

@@ -44,6 +44,63 @@ void sv_ctx::ensure_stats(size_t n) {
     SV_HIP(hipMalloc(&d_stats, stats_cap * sizeof(sv_stats)));
 }
 
+void sv::Emitter::emit(hipStream_t compute, const void *a, size_t bytes0, const void *b, size_t bytes1, void *ha,
+                       void *hb) {
+    SV_HIP(hipGetDevice(&device));
+    if (!copy) {
+        SV_HIP(hipStreamCreateWithFlags(&copy, hipStreamNonBlocking));
+        for (int i = 0; i < 2; i++) {
+            SV_HIP(hipEventCreateWithFlags(&snap[i], hipEventDisableTiming));
+            SV_HIP(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
+        }
+    }
+    if (bytes[0] != bytes0 || bytes[1] != bytes1) {
+        wait();
+        for (int i = 0; i < 2; i++)
+            for (int f = 0; f < 2; f++) {
+                if (buf[i][f]) SV_HIP(hipFree(buf[i][f]));
+                buf[i][f] = nullptr;
+                const size_t nb = f == 0 ? bytes0 : bytes1;
+                if (nb) SV_HIP(hipMalloc(&buf[i][f], nb));
+            }
+        bytes[0] = bytes0;
+        bytes[1] = bytes1;
+    }
+    const int i = k;
+    k ^= 1;
+    if (busy[i]) SV_HIP(hipStreamWaitEvent(compute, done[i], 0));  // the buffer's previous copy has left
+    const void *src[2] = {a, b};
+    void *dst[2] = {ha, hb};
+    for (int f = 0; f < 2; f++)
+        if (src[f] && dst[f] && bytes[f]) SV_HIP(hipMemcpyAsync(buf[i][f], src[f], bytes[f], hipMemcpyDeviceToDevice, compute));
+    SV_HIP(hipEventRecord(snap[i], compute));
+    SV_HIP(hipStreamWaitEvent(copy, snap[i], 0));
+    for (int f = 0; f < 2; f++)
+        if (src[f] && dst[f] && bytes[f]) SV_HIP(hipMemcpyAsync(dst[f], buf[i][f], bytes[f], hipMemcpyDeviceToHost, copy));
+    SV_HIP(hipEventRecord(done[i], copy));
+    busy[i] = true;
+}
+
+void sv::Emitter::wait() {
+    if (!copy) return;
+    SV_HIP(hipStreamSynchronize(copy));
+    busy[0] = busy[1] = false;
+}
+
+void sv::Emitter::release() {
+    if (!copy) return;
+    (void)hipSetDevice(device);
+    (void)hipStreamSynchronize(copy);
+    for (int i = 0; i < 2; i++) {
+        for (int f = 0; f < 2; f++)
+            if (buf[i][f]) (void)hipFree(buf[i][f]);
+        (void)hipEventDestroy(snap[i]);
+        (void)hipEventDestroy(done[i]);
+    }
+    (void)hipStreamDestroy(copy);
+    *this = Emitter();
+}
+
 static hipEvent_t take_event(std::vector<hipEvent_t> &pool) {
     if (!pool.empty()) {
         hipEvent_t e = pool.back();
@@ -183,6 +240,69 @@ int sv_hbm_copy(sv_ctx *ctx, int64_t bytes, int32_t width, int32_t iters, double
     (void)hipFree(a);
     (void)hipFree(b);
     return rc;
+}
+
+int sv_host_register(void *p, size_t bytes) {
+    if (!p || !bytes) return -1;
+    if (hipHostRegister(p, bytes, hipHostRegisterDefault) != hipSuccess) return -2;
+    return 0;
+}
+
+int sv_host_unregister(void *p) {
+    if (!p) return -1;
+    return hipHostUnregister(p) == hipSuccess ? 0 : -2;
+}
+
+int sv_villain_emit(sv_villain *st, double *phi, int64_t *n) {
+    if (!st || (!phi && !n)) return -1;
+    try {
+        SV_HIP(hipSetDevice(st->ctx->device));
+        const size_t V = (size_t)st->N * st->N;
+        st->emitter.emit(st->ctx->stream, st->phi[st->cur], V * sizeof(double), st->n[st->cur], 2 * V * sizeof(int64_t),
+                         phi, n);
+        return 0;
+    } catch (const std::exception &e) {
+        st->ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_villain_emit_wait(sv_villain *st) {
+    if (!st) return -1;
+    try {
+        SV_HIP(hipSetDevice(st->ctx->device));
+        st->emitter.wait();
+        return 0;
+    } catch (const std::exception &e) {
+        st->ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_worldline_emit(sv_worldline *st, int64_t *m, void *v) {
+    if (!st || (!m && !v)) return -1;
+    try {
+        SV_HIP(hipSetDevice(st->ctx->device));
+        const size_t V = (size_t)st->N * st->N;
+        st->emitter.emit(st->ctx->stream, st->m, 2 * V * sizeof(int64_t), st->v,
+                         V * (st->v_is_float ? sizeof(double) : sizeof(int64_t)), m, v);
+        return 0;
+    } catch (const std::exception &e) {
+        st->ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_worldline_emit_wait(sv_worldline *st) {
+    if (!st) return -1;
+    try {
+        SV_HIP(hipSetDevice(st->ctx->device));
+        st->emitter.wait();
+        return 0;
+    } catch (const std::exception &e) {
+        st->ctx->err = e.what();
+        return -2;
+    }
 }
 
 int sv_device_count(void) {

@@ -62,6 +62,24 @@ struct DevScratch {
     Report *reports;
 };
 
+// Asynchronous emission of a resident state: the state is snapshotted on the compute
+// stream (device copy, stream-ordered after every queued sweep) into one of two emission buffers, and the
+// buffer goes to the host on a copy stream of its own, overlapping the sweeps that follow.  Before a buffer
+// is reused the compute stream waits (on the device) for its previous copy.
+struct Emitter {
+    hipStream_t copy = nullptr;
+    void *buf[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    size_t bytes[2] = {0, 0};  // per field
+    hipEvent_t snap[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};
+    bool busy[2] = {false, false};
+    int k = 0;
+    int device = 0;
+    // copy fields (a: bytes0, b: bytes1, either may be null) of the state to the host arrays ha, hb
+    void emit(hipStream_t compute, const void *a, size_t bytes0, const void *b, size_t bytes1, void *ha, void *hb);
+    void wait();     // every emission has reached the host
+    void release();  // frees the buffers (after wait)
+};
+
 }  // namespace sv
 
 // ----------------------------------------------------------------------------------------------
@@ -115,6 +133,7 @@ struct sv_villain {
     int32_t ncol = 0;
     int64_t count[4] = {0, 0, 0, 0};
     int64_t offset[4] = {0, 0, 0, 0};
+    sv::Emitter emitter;
     std::vector<int64_t> partial;  // host scratch
     char *d_aux = nullptr;         // small per-call device block (CohomologyUpdate: rng | stats | plan)
     char *h_aux = nullptr;         // its pinned host image
@@ -143,6 +162,7 @@ struct sv_worldline {
     int32_t *pos = nullptr;      // sequential plaquette: visit position of each plaquette
     int32_t *done = nullptr;     // (unused)
     void *stripes = nullptr;     // striped per-sweep statistics (worldline.hip StatStripe[64][16])
+    sv::Emitter emitter;
     int32_t *sites = nullptr;
     int32_t ncol = 0;
     int64_t count[4] = {0, 0, 0, 0};

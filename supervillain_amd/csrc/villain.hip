@@ -1028,6 +1028,7 @@ int sv_villain_destroy(sv_villain *st) {
     if (st->h_aux) (void)hipHostFree(st->h_aux);
     if (st->d_obs) (void)hipFree(st->d_obs);
     if (st->h_obs) (void)hipHostFree(st->h_obs);
+    st->emitter.release();
     delete st;
     return 0;
 }

@@ -701,6 +701,7 @@ int sv_worldline_destroy(sv_worldline *st) {
     if (st->order) (void)hipFree(st->order);
     if (st->pos) (void)hipFree(st->pos);
     if (st->done) (void)hipFree(st->done);
+    st->emitter.release();
     delete st;
     return 0;
 }

@@ -10,7 +10,8 @@ device state for the run:
     chain.upload(seed)
     for i in range(steps):
         obs = chain.advance()              # every leaf runs its sweeps on the resident fields
-        chain.download_into(storage, i)    # one device-to-host copy per kept configuration
+        chain.emit(phi[i], n[i])           # snapshot on the device, copy to the host on a copy stream
+    chain.emit_wait()                      # (the copy of configuration i overlaps the sweeps of i+1)
 
 `device_program` flattens Sequentially (combining.py:9-45) and KeepEvery (combining.py:48-116) into the
 leaf generators' own device calls, in the order their `step` methods would run, so the chain -- and every
@@ -113,8 +114,46 @@ class DeviceChain:
                 obs |= g._inline_dict(out)
         return obs
 
+    def emit(self, a, b):
+        """Start copying the resident state into host arrays a, b (returns at once; see sv_villain_emit).  They must
+        have this chain's shapes and dtypes, be C-contiguous, and stay untouched until emit_wait()."""
+        for h, ref in ((a, self.a), (b, self.b)):
+            if h.shape != ref.shape or h.dtype != ref.dtype or not h.flags['C_CONTIGUOUS']:
+                raise ValueError(f'emission target {h.shape} {h.dtype} does not match the state {ref.shape} {ref.dtype}')
+        em = self.lib.sv_villain_emit if self.kind == 'villain' else self.lib.sv_worldline_emit
+        self.ctx.check(em(self.handle, _native.ptr(a), _native.ptr(b)), 'emit')
+
+    def emit_wait(self):
+        """Every emission started so far has reached the host."""
+        w = self.lib.sv_villain_emit_wait if self.kind == 'villain' else self.lib.sv_worldline_emit_wait
+        self.ctx.check(w(self.handle), 'emit_wait')
+
     def download(self):
         down = self.lib.sv_villain_download if self.kind == 'villain' else self.lib.sv_worldline_download
         self.ctx.check(down(self.handle, _native.ptr(self.a), _native.ptr(self.b)), 'download')
         x, y = self.names
         return {x: self.a, y: self.b}
+
+
+class PinnedHost:
+    """Page-locks host arrays for the duration of a run (hipHostRegister), so that emissions into them are DMA
+    copies that overlap the sweeps; arrays the runtime refuses to pin are used as they are (copies still
+    land, without the overlap)."""
+
+    def __init__(self, *arrays):
+        self.lib = _native.lib()
+        self.pinned = []
+        for a in arrays:
+            if a.nbytes and a.flags['C_CONTIGUOUS'] and self.lib.sv_host_register(_native.ptr(a), a.nbytes) == 0:
+                self.pinned.append(a)
+
+    def release(self):
+        for a in self.pinned:
+            self.lib.sv_host_unregister(_native.ptr(a))
+        self.pinned = []
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.release()

@@ -116,3 +116,52 @@ def test_villain_hammer_worms_keepevery():
     H.generators[-1].generator.rng = np.random.default_rng(5)
     E = sv.Ensemble(S).generate(4, H)
     assert np.asarray(E.Vortex_Vortex.array if hasattr(E.Vortex_Vortex, 'array') else E.Vortex_Vortex).shape == (4, 8, 8)
+
+
+def test_emissions_in_flight():
+    """Three emissions over the two device buffers before one wait: each host array holds its own step."""
+    from supervillain_amd.pipeline import DeviceChain
+    S = sv.Villain(sv.Lattice2D(64), 0.5, 1)
+    ref = []
+    for emit in (False, True):
+        G = gv.NeighborhoodUpdate(S)
+        G.rng = np.random.default_rng(11)
+        ch = DeviceChain(S, device_program(KeepEvery(2, G)))
+        try:
+            ch.upload(S.configurations(1)[0])
+            outs = []
+            for _ in range(3):
+                ch.advance()
+                if emit:
+                    a, b = np.empty_like(ch.a), np.empty_like(ch.b)
+                    ch.emit(a, b)
+                    outs.append((a, b))
+                else:
+                    d = ch.download()
+                    outs.append((d['phi'].copy(), d['n'].copy()))
+            if emit:
+                ch.emit_wait()
+        finally:
+            ch.close()
+        ref.append(outs)
+    for (a0, b0), (a1, b1) in zip(*ref):
+        assert (a0 == a1).all() and (b0 == b1).all()
+
+
+@pytest.mark.parametrize('N,resident', [(256, True), (48, False)])
+def test_generate_stream_resident(tmp_path, N, resident):
+    """Ensemble.generate(stream=...) with the emission path (pinned storage, copy stream) and the host loop: the
+    store equals the ensemble, and the chain equals the per-step loop."""
+    from supervillain_amd.store import ExtendableStore
+    S = sv.Villain(sv.Lattice2D(N), 0.5, 1)
+    out = []
+    for dev, path in ((False, None), (resident, tmp_path / 's')):
+        G = gv.NeighborhoodUpdate(S)
+        G.rng = np.random.default_rng(21)
+        E = sv.Ensemble(S).generate(9, KeepEvery(2, G), device_resident=dev, stream=path, stream_every=4)
+        out.append(E)
+    st = ExtendableStore(tmp_path / 's', create=False)
+    assert len(st) == 9
+    for f in ('phi', 'n'):
+        a = getattr(out[0].configuration, f).array
+        assert (getattr(out[1].configuration, f).array == a).all() and (st.read(f) == a).all()
