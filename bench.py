@@ -488,12 +488,15 @@ def run_local(args, world, rank, dist):
 
     def run(k):
         acc = 0
-        if len(kinds) > 1:  # a Hammer: Sequentially, one step of each generator in turn
-            for _ in range(k):
+        if len(kinds) > 1:  # a Hammer: Sequentially, one step of each generator in turn, one deferred step
+            for _ in range(k):  # (sv_ctx_set_deferred: one synchronization per Hammer step, as DeviceChain.advance)
+                ctx.begin_deferred()
+                sts = []
                 for g in kinds:
-                    st = _native.stats_array(1)
-                    ctx.check(calls[g](1, st), g)
-                    acc += st[0].accepted if g == kinds[0] else 0
+                    sts.append(_native.stats_array(1))
+                    ctx.check(calls[g](1, sts[-1]), g)
+                ctx.end_deferred()
+                acc += sts[0][0].accepted
         else:
             st = _native.stats_array(k)
             ctx.check(calls[kind](k, st), kind)

@@ -95,6 +95,12 @@ int sv_villain_download(sv_villain *st, double *phi, int64_t *n);
  * valid and unread until sv_villain_emit_wait returns; register them with sv_host_register for a true DMA. */
 int sv_villain_emit(sv_villain *st, double *phi, int64_t *n);
 int sv_villain_emit_wait(sv_villain *st);
+/* Deferred statistics: with on = 1, runs whose sweeps cannot meet a NumPy Lemire rejection (every bounded draw
+ * of the update has a power-of-two range) return without synchronizing; their sv_stats arrays are filled
+ * (and an unexpected device abort reported) by the next sv_ctx_sync, or by sv_ctx_set_deferred(ctx, 0).  Other
+ * calls synchronize as usual.  The stats arrays must stay valid until then. */
+int sv_ctx_set_deferred(sv_ctx *ctx, int32_t on);
+int sv_ctx_sync(sv_ctx *ctx);
 int sv_host_register(void *p, size_t bytes);   /* pin host memory (hipHostRegister) */
 int sv_host_unregister(void *p);
 /* path: 0 = auto (fused two-colour sweep kernel for even N, per-colour kernels otherwise),

@@ -54,6 +54,8 @@ def lib():
         L.sv_worldline_emit.argtypes = [vp, vp, vp]
         L.sv_worldline_emit_wait.argtypes = [vp]
         L.sv_host_register.argtypes = [vp, ctypes.c_size_t]
+        L.sv_ctx_set_deferred.argtypes = [vp, i32]
+        L.sv_ctx_sync.argtypes = [vp]
         L.sv_host_unregister.argtypes = [vp]
         L.sv_villain_run.argtypes = [vp, f64, i64, f64, i64, i32, P(SvRng), P(SvStats), i32]
         L.sv_villain_observables.argtypes = [vp, f64, vp]
@@ -106,6 +108,7 @@ EXPORTED = ('sv_ctx_create', 'sv_ctx_destroy', 'sv_last_error', 'sv_device_count
             'sv_villain_neighborhood', 'sv_villain_create', 'sv_villain_destroy', 'sv_villain_upload',
             'sv_villain_download', 'sv_villain_run', 'sv_villain_observables', 'sv_villain_emit', 'sv_villain_emit_wait',
             'sv_worldline_emit', 'sv_worldline_emit_wait', 'sv_host_register', 'sv_host_unregister',
+            'sv_ctx_set_deferred', 'sv_ctx_sync',
             'sv_villain_site_run', 'sv_villain_link_run', 'sv_villain_exact_run', 'sv_villain_cohomology_run', 'sv_worldline_create',
             'sv_worldline_destroy', 'sv_worldline_upload', 'sv_worldline_download', 'sv_worldline_coexact_run',
             'sv_worldline_coexact', 'sv_worldline_plaquette_ordered_run',
@@ -138,6 +141,27 @@ class Context:
             raise NativeError(f'cannot open HIP device {device} (sv_ctx_create returned {rc}); '
                               'the supervillain_amd generators run only on an MI355X')
         self.handle = h
+        self.folds = None  # open deferred step: counter folds waiting for sv_ctx_sync
+
+    def begin_deferred(self):
+        """Open a deferred step: runs that cannot meet a rejection return without synchronizing (sv_ctx_set_deferred)
+        and their counter folds (fold_later) wait for end_deferred."""
+        self.check(lib().sv_ctx_set_deferred(self.handle, 1), 'sv_ctx_set_deferred')
+        self.folds = []
+
+    def end_deferred(self):
+        """One synchronization lands every deferred statistic; then the folds run in call order."""
+        folds, self.folds = self.folds, None
+        self.check(lib().sv_ctx_set_deferred(self.handle, 0), 'sv_ctx_set_deferred')
+        for f in folds or ():
+            f()
+
+    def fold_later(self, fold):
+        """Run a counter fold that reads sv_stats now, or at end_deferred inside a deferred step."""
+        if self.folds is None:
+            fold()
+        else:
+            self.folds.append(fold)
 
     def check(self, rc, what):
         if rc != 0:

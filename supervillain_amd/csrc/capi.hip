@@ -44,6 +44,41 @@ void sv_ctx::ensure_stats(size_t n) {
     SV_HIP(hipMalloc(&d_stats, stats_cap * sizeof(sv_stats)));
 }
 
+bool sv_ctx::defer_stats(sv_stats *dst, int64_t count) {
+    if (!deferred) return false;
+    if (stage_used + (size_t)count > stage_cap || abort_used + 1 > abort_cap) {
+        SV_HIP(hipStreamSynchronize(stream));
+        land();
+        if (h_stage) SV_HIP(hipHostFree(h_stage));
+        if (h_stage_abort) SV_HIP(hipHostFree(h_stage_abort));
+        stage_cap = std::max<size_t>(std::max<size_t>(2 * stage_cap, (size_t)count), 1024);
+        abort_cap = std::max<size_t>(2 * abort_cap, 256);
+        SV_HIP(hipHostMalloc((void **)&h_stage, stage_cap * sizeof(sv_stats), hipHostMallocDefault));
+        SV_HIP(hipHostMalloc((void **)&h_stage_abort, abort_cap * sizeof(int32_t), hipHostMallocDefault));
+    }
+    SV_HIP(hipMemcpyAsync(h_stage + stage_used, d_stats, count * sizeof(sv_stats), hipMemcpyDeviceToHost, stream));
+    SV_HIP(hipMemcpyAsync(h_stage_abort + abort_used, d_abort, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+    landings.push_back(Landing{dst, stage_used, count, abort_used});
+    stage_used += count;
+    abort_used += 1;
+    return true;
+}
+
+void sv_ctx::land() {
+    bool bad = false;
+    for (const Landing &L : landings) {
+        for (int64_t i = 0; i < L.count; i++) {
+            L.dst[i].accepted = h_stage[L.off + i].accepted;
+            L.dst[i].acceptance_sum = h_stage[L.off + i].acceptance_sum;
+            L.dst[i].rejections = 0;  // deferred runs cannot meet a rejection
+        }
+        bad |= h_stage_abort[L.abort_slot] != 0;
+    }
+    landings.clear();
+    stage_used = abort_used = 0;
+    if (bad) throw std::runtime_error("unexpected NumPy Lemire rejection report");
+}
+
 void sv::Emitter::emit(hipStream_t compute, const void *a, size_t bytes0, const void *b, size_t bytes1, void *ha,
                        void *hb) {
     SV_HIP(hipGetDevice(&device));
@@ -242,6 +277,38 @@ int sv_hbm_copy(sv_ctx *ctx, int64_t bytes, int32_t width, int32_t iters, double
     return rc;
 }
 
+int sv_ctx_set_deferred(sv_ctx *ctx, int32_t on) {
+    if (!ctx) return -1;
+    try {
+        SV_HIP(hipSetDevice(ctx->device));
+        if (!on && ctx->deferred) {
+            ctx->deferred = false;
+            SV_HIP(hipStreamSynchronize(ctx->stream));
+            ctx->land();
+            ctx->time_collect();
+        }
+        ctx->deferred = on != 0;
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
+int sv_ctx_sync(sv_ctx *ctx) {
+    if (!ctx) return -1;
+    try {
+        SV_HIP(hipSetDevice(ctx->device));
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+        ctx->land();
+        ctx->time_collect();
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
 int sv_host_register(void *p, size_t bytes) {
     if (!p || !bytes) return -1;
     if (hipHostRegister(p, bytes, hipHostRegisterDefault) != hipSuccess) return -2;
@@ -355,6 +422,8 @@ int sv_ctx_destroy(sv_ctx *ctx) {
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
     (void)hipFree(ctx->d_abort);
     if (ctx->h_abort) (void)hipHostFree(ctx->h_abort);
+    if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+    if (ctx->h_stage_abort) (void)hipHostFree(ctx->h_stage_abort);
     (void)hipFree(ctx->d_nreport);
     (void)hipFree(ctx->d_reports);
     (void)hipFree(ctx->d_blocks);

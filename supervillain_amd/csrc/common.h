@@ -114,6 +114,24 @@ struct sv_ctx {
     void time_collect();  // after a stream sync
     void time_discard();  // drop pending (unsynchronized-safe: after a stream sync)
 
+    // deferred statistics (sv_ctx_set_deferred): a run whose sweeps cannot meet a NumPy Lemire rejection leaves
+    // its statistics (and abort flag) in a pinned staging area and returns without synchronizing; sv_ctx_sync
+    // lands them in the caller's arrays.  One synchronization per device-resident program step instead of one
+    // per member generator.
+    struct Landing {
+        sv_stats *dst;
+        size_t off;
+        int64_t count;
+        size_t abort_slot;
+    };
+    bool deferred = false;
+    sv_stats *h_stage = nullptr;
+    int32_t *h_stage_abort = nullptr;
+    size_t stage_cap = 0, stage_used = 0, abort_cap = 0, abort_used = 0;
+    std::vector<Landing> landings;
+    bool defer_stats(sv_stats *dst, int64_t count);  // queued (deferred mode) or false: the caller synchronizes
+    void land();                                      // after a stream synchronization
+
     const sv::JumpTables *jump_tables(uint64_t inc_hi, uint64_t inc_lo);
     void ensure_blocks(size_t n);
     void ensure_skips(size_t n);

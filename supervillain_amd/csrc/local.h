@@ -219,6 +219,10 @@ static inline void run_batches(sv_ctx *ctx, const std::vector<BlockSpec> &specs,
             absorb_reports(a, sw, skips);
             restore();
         }
+        if (!may_reject && ctx->defer_stats(stats + sw, count)) {  // landed by sv_ctx_sync
+            sw += count;
+            continue;
+        }
         if (!may_reject) queue_abort_copy(ctx);
         SV_HIP(hipMemcpyAsync(stats + sw, ctx->d_stats, count * sizeof(sv_stats), hipMemcpyDeviceToHost, ctx->stream));
         SV_HIP(hipStreamSynchronize(ctx->stream));

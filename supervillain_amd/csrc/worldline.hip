@@ -558,11 +558,14 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
             }
             snapshot(st, true);
         }
-        if (!may_reject) svh::loc::queue_abort_copy(ctx);
-        SV_HIP(hipMemcpyAsync(stats + (size_t)sw * nstat, ctx->d_stats, (size_t)count * nstat * sizeof(sv_stats),
-                              hipMemcpyDeviceToHost, ctx->stream));
-        SV_HIP(hipStreamSynchronize(ctx->stream));
-        if (!may_reject) {
+        const bool deferred = !may_reject && ctx->defer_stats(stats + (size_t)sw * nstat, (int64_t)count * nstat);
+        if (!may_reject && !deferred) svh::loc::queue_abort_copy(ctx);
+        if (!deferred) {
+            SV_HIP(hipMemcpyAsync(stats + (size_t)sw * nstat, ctx->d_stats, (size_t)count * nstat * sizeof(sv_stats),
+                                  hipMemcpyDeviceToHost, ctx->stream));
+            SV_HIP(hipStreamSynchronize(ctx->stream));
+        }
+        if (!may_reject && !deferred) {
             svh::loc::check_abort_copy(ctx);
             ctx->time_collect();
         }

@@ -91,11 +91,14 @@ class NeighborhoodUpdate(DeviceState, Generator):
                   'sv_villain_run')
         rng_to_numpy(r, self.rng)
         V = self.Lattice.sites
-        for k in range(sweeps):
-            self.sweeps += 1
-            self.proposed += V
-            self.acceptance += st[k].acceptance_sum / V
-            self.accepted += int(st[k].accepted)
+
+        def fold():
+            for k in range(sweeps):
+                self.sweeps += 1
+                self.proposed += V
+                self.acceptance += st[k].acceptance_sum / V
+                self.accepted += int(st[k].accepted)
+        ctx.fold_later(fold)
         if self.inline:
             out = np.zeros(4)
             ctx.check(L.sv_villain_observables(h, float(self.kappa), _native.ptr(out)), 'sv_villain_observables')
@@ -231,11 +234,14 @@ class _VillainLocal(DeviceState, Generator):
         ctx.check(self._run(L, h, sweeps, r, st), f'{self.NAME} run')
         rng_to_numpy(r, self.rng)
         P = self._proposals()
-        for k in range(sweeps):
-            self.sweeps += 1
-            self.proposed += P
-            self.acceptance += st[k].acceptance_sum / P
-            self.accepted += int(st[k].accepted)
+
+        def fold():
+            for k in range(sweeps):
+                self.sweeps += 1
+                self.proposed += P
+                self.acceptance += st[k].acceptance_sum / P
+                self.accepted += int(st[k].accepted)
+        ctx.fold_later(fold)
         return None
 
     def _advance(self, phi, n, sweeps):

@@ -83,11 +83,14 @@ class CoexactUpdate(_WorldlineDevice, Generator):
                                              sweeps, ctypes.byref(r), st), 'sv_worldline_coexact_run')
         rng_to_numpy(r, self.rng)
         P = self.Lattice.cells_of_degree[2]
-        for k in range(sweeps):  # coexact.py:122-124
-            self.sweeps += 1
-            self.proposed += P
-            self.acceptance += st[k].acceptance_sum / P
-            self.accepted += int(st[k].accepted)
+
+        def fold():
+            for k in range(sweeps):  # coexact.py:122-124
+                self.sweeps += 1
+                self.proposed += P
+                self.acceptance += st[k].acceptance_sum / P
+                self.accepted += int(st[k].accepted)
+        ctx.fold_later(fold)
         return None
 
     def _advance(self, cfg, sweeps):
@@ -149,25 +152,28 @@ class PlaquetteUpdate(_WorldlineDevice, Generator):
         r = rng_from_numpy(self.rng)
         kappa, W = float(self.Action.kappa), float(self.Action._W)
         if self.mode == 'reference':
-            st = _native.stats_array(1)
-            stats = []
+            sts = []
             for _ in range(sweeps):
                 order = np.random.permutation(L.coordinates)  # plaquette.py:63, global RandomState
                 lin = np.ascontiguousarray((order[:, 0] % L.N) * L.N + (order[:, 1] % L.N), dtype=np.int64)
-                ctx.check(Lib.sv_worldline_plaquette_ordered_run(h, kappa, W, _native.ptr(lin), ctypes.byref(r), st),
-                          'sv_worldline_plaquette_ordered_run')
-                stats.append((int(st[0].accepted), st[0].acceptance_sum))
+                sts.append(_native.stats_array(1))
+                ctx.check(Lib.sv_worldline_plaquette_ordered_run(h, kappa, W, _native.ptr(lin), ctypes.byref(r),
+                                                                 sts[-1]), 'sv_worldline_plaquette_ordered_run')
+            stats = lambda: [(int(s[0].accepted), s[0].acceptance_sum) for s in sts]  # noqa: E731
         else:
             st = _native.stats_array(sweeps)
             ctx.check(Lib.sv_worldline_plaquette_checkerboard_run(h, kappa, W, sweeps, ctypes.byref(r), st),
                       'sv_worldline_plaquette_checkerboard_run')
-            stats = [(int(st[k].accepted), st[k].acceptance_sum) for k in range(sweeps)]
+            stats = lambda: [(int(st[k].accepted), st[k].acceptance_sum) for k in range(sweeps)]  # noqa: E731
         rng_to_numpy(r, self.rng)
         P = L.sites * len(L.components[2])
-        for acc, psum in stats:  # plaquette.py:73, 101-103
-            self.acceptance += psum
-            self.accepted += acc
-            self.proposed += P
+
+        def fold():
+            for acc, psum in stats():  # plaquette.py:73, 101-103
+                self.acceptance += psum
+                self.accepted += acc
+                self.proposed += P
+        ctx.fold_later(fold)
         return None
 
     def _advance(self, cfg, sweeps):
@@ -228,11 +234,14 @@ class _WorldlineLocal(_WorldlineDevice, Generator):
         ctx.check(self._run(L, h, sweeps, r, st), f'{self.NAME} run')
         rng_to_numpy(r, self.rng)
         P = self._proposals()
-        for k in range(sweeps):
-            self.sweeps += 1
-            self.proposed += P
-            self.acceptance += st[k].acceptance_sum / P
-            self.accepted += int(st[k].accepted)
+
+        def fold():
+            for k in range(sweeps):
+                self.sweeps += 1
+                self.proposed += P
+                self.acceptance += st[k].acceptance_sum / P
+                self.accepted += int(st[k].accepted)
+        ctx.fold_later(fold)
         return None
 
     def _advance(self, cfg, sweeps):

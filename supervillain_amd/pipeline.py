@@ -106,12 +106,18 @@ class DeviceChain:
         self.ctx.check(up(self.handle, _native.ptr(self.a), _native.ptr(self.b)), 'upload')
 
     def advance(self):
-        """Run the program once; returns the inline observables the leaves produced (dict)."""
+        """Run the program once; returns the inline observables the leaves produced (dict).  The leaves run as one
+        deferred step (sv_ctx_set_deferred): members that cannot meet a NumPy Lemire rejection return without a
+        synchronization, and one sv_ctx_sync at the end lands every statistic before the counters fold."""
         obs = {}
-        for g, k in self.program:
-            out = g._run_on(self.ctx, self.handle, k)
-            if out is not None:
-                obs |= g._inline_dict(out)
+        self.ctx.begin_deferred()
+        try:
+            for g, k in self.program:
+                out = g._run_on(self.ctx, self.handle, k)
+                if out is not None:
+                    obs |= g._inline_dict(out)
+        finally:
+            self.ctx.end_deferred()
         return obs
 
     def emit(self, a, b):
