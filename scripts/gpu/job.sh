@@ -1,11 +1,8 @@
 source scripts/gpu/guard.sh
-T=${1:-r307}
+T=${1:-r309}
 O=gpurun_out/$T
 mkdir -p $O
 export TMPDIR=/tmp
-step tests timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1
+step tests timeout -k 10 600 python -u -m pytest tests/test_gpu_villain.py tests/test_gpu_domain.py tests/test_gpu_boundary.py tests/test_gpu_pipeline.py -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1
 tail -3 $O/tests.log
-for w in hammer wlhammer; do
-step b$w timeout -k 10 300 python bench.py --workload $w --steps 50 --warmup 5 --no-cpu-baseline --no-copy-ceiling > $O/b_$w.log 2>&1
-grep '^{' $O/b_$w.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$w', d['value']/1e9, d['ms_per_step'], d['roofline']['avg_launch_us'])"
-done
+REPS="1 2 3" bash scripts/gpu/job_ab.sh $T/ab "o0 o1"

@@ -19,6 +19,12 @@
 // Exactness: every value that reaches phi or n is computed in the reference's operation order.
 // The residual r and dS reach nothing but exp(-dS); the `0.0 +` the reference's d() and face_sum() put in
 // front of them changes at most the sign of a zero, and exp(+-0) = 1.
+#ifndef SV_HOT_OCC4
+#define SV_HOT_OCC4 1  // 4 waves per SIMD: LDS <= 40 KB (6-row residual ring, int16 n image), <= 128 VGPRs
+#endif
+#if SV_HOT_OCC4 && !defined(SV_EXP_SCOEF)
+#define SV_EXP_SCOEF 1  // exp coefficients as SGPR operands (18 VGPRs fewer)
+#endif
 #include "fused.h"
 
 #ifndef SV_HOT_ADV
@@ -62,9 +68,12 @@ __device__ __forceinline__ HotDraws hot_draws_edge(const FArgs &A, int64_t gq, i
     const bool wr = !(gx >= xb && gx < xb + SMALL_LDS);
     const int32_t xr = wr ? xw : xb;
     const int64_t lin = gq * N + gx, rank = lin >> 1, rb = (gq * N + xr) >> 1;
+    // bA, bB point at the wave's two base sets in LDS: each lane reads the set it draws from (one base in
+    // registers at a time, not both sets)
+    const u128 *bs = wr ? bB : bA;
     HotDraws D;
-    D.u = u53(xsl_rr(hot_apply(sm, (uint32_t)(gx - xr), wr ? bB[0] : bA[0])));
-    D.dphi = A.P.lo_phi + A.P.range_phi * u53(xsl_rr(hot_apply(sm, (uint32_t)(rank - rb), wr ? bB[1] : bA[1])));
+    D.u = u53(xsl_rr(hot_apply(sm, (uint32_t)(gx - xr), bs[0])));
+    D.dphi = A.P.lo_phi + A.P.range_phi * u53(xsl_rr(hot_apply(sm, (uint32_t)(rank - rb), bs[1])));
 #pragma unroll
     for (int mu = 0; mu < 2; mu++) {
         const int64_t qq = rank - (int64_t)has[mu];
@@ -72,7 +81,7 @@ __device__ __forceinline__ HotDraws hot_draws_edge(const FArgs &A, int64_t gq, i
         const uint32_t off = (uint32_t)((qq < 0 ? 0 : (qq >> 1)) - w0);
 #pragma unroll
         for (int fb = 0; fb < 2; fb++) {
-            const uint64_t X = xsl_rr(hot_apply(sm, off, wr ? bB[2 + 2 * mu + fb] : bA[2 + 2 * mu + fb]));
+            const uint64_t X = xsl_rr(hot_apply(sm, off, bs[2 + 2 * mu + fb]));
             uint32_t word = (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
             if (qq < 0) word = buf[2 * mu + fb];  // has && rank == 0: the block's buffered half-word
             D.w[2 * mu + fb] = word;
@@ -84,11 +93,15 @@ __device__ __forceinline__ HotDraws hot_draws_edge(const FArgs &A, int64_t gq, i
 // The workgroup's LDS (one allocation shared by the two bodies below)
 struct HotLDS {
     static constexpr int R = FusedGeom<4>::R;
+    // the residuals r live from the colour-0 pass of step t (rows t+1..t+5) to the colour-1 pass of step t+4
+    // (which reads row t+4 again): NW + 2 rows
+    static constexpr int RR = SV_HOT_OCC4 ? 4 + 2 : R;
+    using nint = std::conditional_t<SV_HOT_OCC4, int16_t, int32_t>;  // hot_ok / commit bound |n|
     double phi[R][RW];
-    double r0[R][RW];
-    double r1[R][RW];
-    int32_t n0[R][RW];
-    int32_t n1[R][RW];
+    double r0[RR][RW];
+    double r1[RR][RW];
+    nint n0[R][RW];
+    nint n1[R][RW];
     SmallTab small;
     Affine adv[3];
     u128 base[4][32];  // per wave: [8c + ty] block ty's base for the colour-c row at xb; [16 + ..] at xw
@@ -100,7 +113,7 @@ struct HotLDS {
 template <bool TILE, bool EDGE>
 __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
     constexpr int NW = 4;
-    constexpr int R = HotLDS::R;
+    constexpr int R = HotLDS::R, RR = HotLDS::RR;
     constexpr int PF = RW / 64;
     auto &s_phi = Ls.phi;
     auto &s_r0 = Ls.r0;
@@ -214,7 +227,8 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
                     s_phi[slot][cc] = pf_phi[k] + 0.0;
                     const int32_t a = (int32_t)pf_n0[k], c = (int32_t)pf_n1[k];
                     // the int32 image must hold n exactly, with headroom for one sweep's changes
-                    bad |= (uint32_t)((uint64_t)((pf_n0[k] >> 30) + 1) > 1) | (uint32_t)((uint64_t)((pf_n1[k] >> 30) + 1) > 1);
+                    constexpr int NB = SV_HOT_OCC4 ? 14 : 30;  // |n| < 2^NB, headroom for one sweep's 2|W| <= 2^13
+                    bad |= (uint32_t)((uint64_t)((pf_n0[k] >> NB) + 1) > 1) | (uint32_t)((uint64_t)((pf_n1[k] >> NB) + 1) > 1);
                     s_n0[slot][cc] = a;
                     s_n1[slot][cc] = c;
                 }
@@ -233,10 +247,12 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
     const int32_t tfirst = t0 - 3;
     int32_t brow = tfirst + 2 - bc + wave;  // colour 0 row t+2+wave, colour 1 row t+1+wave
     int32_t brow1 = tfirst + 1 + wave;      // the colour-1 row, wave-uniform
-    u128 bases{0, 0};
-    if (base_lane) bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)base_pos(bty, grow(brow), Nx, bx, bhas));
-    __builtin_amdgcn_s_waitcnt(0);
-    if (base_lane) s_base[wave][lane] = bases;
+    {  // (the running bases live in LDS only: the advance reads them back, no registers held across the loop)
+        u128 bases{0, 0};
+        if (base_lane) bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)base_pos(bty, grow(brow), Nx, bx, bhas));
+        __builtin_amdgcn_s_waitcnt(0);
+        if (base_lane) s_base[wave][lane] = bases;
+    }
 
     // paired-draw lane constants per colour (interior strips; valid for every row of this wave)
     uint32_t pk0 = 0, pk1 = 0;
@@ -280,16 +296,14 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
     // draws of colour c for global row gq, local column x; the 4 choice values; a rejected word is reported
     auto draw = [&](int c, int32_t q, int32_t x, bool active, HotDraws &D, int32_t cn[4]) {
         const int32_t gq = grow(q);
-        u128 bs[6];
-#pragma unroll
-        for (int k = 0; k < 6; k++) bs[k] = s_base[wave][8 * c + k];
         if constexpr (!edge) {
+            u128 bs[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) bs[k] = s_base[wave][8 * c + k];
             D = hot_draws_paired(A, lane, c == 0 ? pk0 : pk1, bs, s_small);
         } else {
-            u128 bw[6];
-#pragma unroll
-            for (int k = 0; k < 6; k++) bw[k] = two_sets ? s_base[wave][16 + 8 * c + k] : bs[k];
-            D = hot_draws_edge(A, gq, wrapN(Gm.X0 + x, Nx), xb, two_sets ? xw : xb, bs, bw, s_small, has_c[c], buf_c[c]);
+            D = hot_draws_edge(A, gq, wrapN(Gm.X0 + x, Nx), xb, two_sets ? xw : xb, &s_base[wave][8 * c],
+                               &s_base[wave][(two_sets ? 16 : 0) + 8 * c], s_small, has_c[c], buf_c[c]);
         }
         bool rej = false;
 #pragma unroll
@@ -372,10 +386,11 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
                         wr[3] = (r0[3] + D.dphi) - tc[3];
                     }
                 }
-                s_r0[s0][cx] = wr[0];
-                s_r0[sm][cx] = wr[1];
-                s_r1[s0][cx] = wr[2];
-                s_r1[s0][cm] = wr[3];
+                const int r0s = lr % RR, rms = (lr - 1) % RR;
+                s_r0[r0s][cx] = wr[0];
+                s_r0[rms][cx] = wr[1];
+                s_r1[r0s][cx] = wr[2];
+                s_r1[r0s][cm] = wr[3];
             }
         }
         if (!(SV_ABLATE & 32)) __syncthreads();
@@ -394,10 +409,11 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
                 const int sm = (lr - 1) % R, s0 = lr % R;
                 const int cx = x - cofs, cm = cx - 1;
                 double ri[4];
-                ri[0] = s_r0[s0][cx];
-                ri[1] = s_r0[sm][cx];
-                ri[2] = s_r1[s0][cx];
-                ri[3] = s_r1[s0][cm];
+                const int r0s = lr % RR, rms = (lr - 1) % RR;
+                ri[0] = s_r0[r0s][cx];
+                ri[1] = s_r0[rms][cx];
+                ri[2] = s_r1[r0s][cx];
+                ri[3] = s_r1[r0s][cm];
                 double cr[4];
                 const double mdp = 0.0 - D.dphi;
                 cr[0] = mdp - TWO_PI * (double)cn[0];
@@ -435,8 +451,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
         if (SV_HOT_ADV && glo >= 1 && glo + NW + 1 < Nt) {
             if (base_lane) {
                 const int ai = bty == 0 ? 0 : (bty == 1 ? 1 : 2);
-                bases = mad128c(s_adv[ai].A, bases, s_adv[ai].C);
-                s_base[wave][lane] = bases;
+                s_base[wave][lane] = mad128c(s_adv[ai].A, s_base[wave][lane], s_adv[ai].C);
             }
             brow += NW;
         } else if (base_lane) {
@@ -444,6 +459,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
             const int64_t p_new = base_pos(bty, grow(brow + NW), Nx, bx, bhas);
             const int ai = bty == 0 ? 0 : (bty == 1 ? 1 : 2);
             const int64_t step = bty == 0 ? (int64_t)NW * Nx : (bty == 1 ? (int64_t)NW * Nx / 2 : (int64_t)NW * Nx / 4);
+            u128 bases = s_base[wave][lane];
             if (p_new - p_old == step) bases = apply(s_adv[ai], bases);
             else bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)p_new);
             brow += NW;
@@ -463,7 +479,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
 }
 
 template <bool TILE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void villain_sweep_hot(FArgs A) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4 ? 4 : 3))) void villain_sweep_hot(FArgs A) {
     __shared__ HotLDS Ls;
     // the strip this workgroup owns (the same mapping hot_body makes), to pick the body
     int b = blockIdx.x;
@@ -493,6 +509,7 @@ namespace svh {
 bool hot_ok(const VParams &P, const Block *blocks) {
     const int64_t aw = P.W < 0 ? -P.W : P.W;
     if (P.k <= 1 || P.k > (1u << 20) || aw > (1 << 20) || aw * (int64_t)P.k >= (1 << 28)) return false;  // int32 values
+    if (SV_HOT_OCC4 && aw > (1 << 12)) return false;  // the int16 n image: |n| < 2^14 plus 2|W| per sweep
     for (int c = 0; c < 2; c++) {
         const Block *B = blocks + 2 + 5 * c;
         if (B[0].nskip || B[1].nskip || B[2].nskip || B[3].nskip) return false;
