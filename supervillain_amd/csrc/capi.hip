@@ -423,6 +423,7 @@ int sv_ctx_destroy(sv_ctx *ctx) {
     (void)hipFree(ctx->d_abort);
     if (ctx->h_abort) (void)hipHostFree(ctx->h_abort);
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+    if (ctx->h_tail) (void)hipHostFree(ctx->h_tail);
     if (ctx->h_stage_abort) (void)hipHostFree(ctx->h_stage_abort);
     (void)hipFree(ctx->d_nreport);
     (void)hipFree(ctx->d_reports);

@@ -101,6 +101,9 @@ struct sv_ctx {
     size_t stats_cap = 0;
     // pinned host image of d_abort: batches that cannot meet a rejection copy it with their stats (one sync)
     int32_t *h_abort = nullptr;
+    // pinned batch tail (abort flag, report count, statistics) of the single-lattice Villain run: one sync
+    char *h_tail = nullptr;
+    size_t tail_cap = 0;
     // optional per-launch timing of the sweep kernels (hipEvents on ctx->stream)
     bool timing = false;
     int timing_mode = 0;  // 1: events around each batch of launches, 2: around every launch

@@ -707,6 +707,40 @@ AbortInfo read_abort(sv_ctx *ctx) {
     return a;
 }
 
+// The batch tail in one synchronization: abort flag, report count and the batch's statistics land in a pinned
+// host block (DMA copies); the stats are kept only when no rejection aborted the batch.
+AbortInfo read_abort_stats(sv_ctx *ctx, int count, sv_stats *stats) {
+    const size_t bytes = 64 + (size_t)count * sizeof(sv_stats);
+    if (bytes > ctx->tail_cap) {
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+        if (ctx->h_tail) SV_HIP(hipHostFree(ctx->h_tail));
+        ctx->tail_cap = std::max<size_t>(bytes, 64 + 64 * sizeof(sv_stats));
+        SV_HIP(hipHostMalloc((void **)&ctx->h_tail, ctx->tail_cap, hipHostMallocDefault));
+    }
+    int32_t *h_ab = (int32_t *)ctx->h_tail;
+    uint32_t *h_nrep = (uint32_t *)(ctx->h_tail + 4);
+    sv_stats *h_st = (sv_stats *)(ctx->h_tail + 64);
+    SV_HIP(hipMemcpyAsync(h_ab, ctx->d_abort, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    SV_HIP(hipMemcpyAsync(h_nrep, ctx->d_nreport, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    SV_HIP(hipMemcpyAsync(h_st, ctx->d_stats, count * sizeof(sv_stats), hipMemcpyDeviceToHost, ctx->stream));
+    SV_HIP(hipStreamSynchronize(ctx->stream));
+    AbortInfo a;
+    a.abort = *h_ab;
+    uint32_t nrep = *h_nrep;
+    if (!a.abort) {
+        std::memcpy(stats, h_st, count * sizeof(sv_stats));
+        return a;
+    }
+    if (nrep > (uint32_t)MAX_REPORTS) nrep = MAX_REPORTS;
+    a.reports.resize(nrep);
+    if (nrep) {
+        SV_HIP(hipMemcpyAsync(a.reports.data(), ctx->d_reports, nrep * sizeof(Report), hipMemcpyDeviceToHost,
+                              ctx->stream));
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    return a;
+}
+
 void clear_abort(sv_ctx *ctx) {
     SV_HIP(hipMemsetAsync(ctx->d_abort, 0, sizeof(int32_t), ctx->stream));
     SV_HIP(hipMemsetAsync(ctx->d_nreport, 0, sizeof(uint32_t), ctx->stream));
@@ -890,17 +924,14 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         if (!per_launch) ctx->time_end(ev, count);
         SV_HIP(hipGetLastError());
         auto tp2 = std::chrono::steady_clock::now();
-        AbortInfo a = read_abort(ctx);
+        AbortInfo a = read_abort_stats(ctx, count, stats + sw);
         auto tp3 = std::chrono::steady_clock::now();
         if (dbg)
             fprintf(stderr, "[sv] launch %.1f us, wait %.1f us\n", std::chrono::duration<double, std::micro>(tp2 - tp1).count(),
                     std::chrono::duration<double, std::micro>(tp3 - tp2).count());
         if (a.abort) ctx->time_discard();  // aborted launches exit early: keep the average honest
         ctx->time_collect();
-        if (!a.abort) {
-            SV_HIP(hipMemcpyAsync(stats + sw, ctx->d_stats, count * sizeof(sv_stats), hipMemcpyDeviceToHost,
-                                  ctx->stream));
-            SV_HIP(hipStreamSynchronize(ctx->stream));
+        if (!a.abort) {  // the stats already landed with the abort flag
             for (int k = 0; k < count; k++) {
                 stats[sw + k].proposed = V;
                 int64_t rj = 0;
