@@ -18,6 +18,7 @@
 #include <chrono>
 #include <cstdio>
 #include <algorithm>
+#include <array>
 #include <cstring>
 
 #include "villain.h"
@@ -97,6 +98,11 @@ struct sv_replicas {
     sv_stats *d_stats = nullptr;
     double *d_obs = nullptr;
     std::vector<std::pair<uint64_t, uint64_t>> incs;  // current per-replica increments
+    // pinned batch tail: abort flag, report count, then the batch's statistics and observables (one DMA each,
+    // one synchronization)
+    char *h_tail = nullptr;
+    size_t tail_cap = 0;
+    int32_t *d_map = nullptr;  // replica maps of the split launches of a batch (R * REP_BATCH slots)
 };
 
 namespace {
@@ -139,10 +145,11 @@ bool has_skips(const SkipMap &m, int first, int count) {
     return it != m.end() && it->first.first < first + count;
 }
 
-// advance a no-skip replica's cursor by `sweeps` sweeps (closed form, see the file header)
-void advance_closed(Cursor &c, u128 inc, uint64_t V, int sweeps) {
-    if (sweeps <= 0) return;
-    c.s = host_jump(c.s, inc, (uint64_t)sweeps * 4 * V);
+// advance a no-skip replica's cursor by a whole number of sweeps (closed form, see the file header).  k PCG64
+// steps map s to M^k s + inc (M^(k-1) + ... + 1): `unit` = the map of k steps with increment 1, (M^k, sum M^i), is
+// shared by every replica, so each one costs two 128-bit products instead of its own power of its step map.
+void advance_closed(Cursor &c, u128 inc, const Affine &unit) {
+    c.s = add(mul(unit.A, c.s), mul(inc, unit.C));
     c.buf = (uint32_t)(xsl_rr(c.s) >> 32);
 }
 
@@ -169,8 +176,6 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
     std::vector<PlanIn> pin(R);
     std::vector<std::vector<Block>> hb;  // host-planned descriptors, alive until the batch's stream sync
     std::vector<uint32_t> hskip, sk;
-    std::vector<sv_stats> hst;
-    std::vector<double> hobs;
     int sw = 0;
     const bool dbg = getenv("SV_DEBUG_TIMING") != nullptr;
     using clk = std::chrono::steady_clock;
@@ -209,7 +214,53 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         SV_HIP(hipMemsetAsync(ctx->d_nreport, 0, sizeof(uint32_t), ctx->stream));
         SV_HIP(hipMemsetAsync(b->d_stats, 0, (size_t)R * count * sizeof(sv_stats), ctx->stream));
         if (obs) SV_HIP(hipMemsetAsync(b->d_obs, 0, (size_t)R * count * 4 * sizeof(double), ctx->stream));
-        // --- sweeps
+        // --- sweeps.  A sweep runs on the fast-draw kernel (villain_sweep_hot_fr) when no replica's choice blocks
+        // of that sweep carry a skip (the closed-form replicas have none; the host-planned ones are checked), else
+        // on the general fused kernel.  Within a skip-free sweep a replica's four choice blocks start on the same
+        // half-word parity (they draw V/2, an even count), which is all the fast kernel's two draw forms need.
+        const bool fr_hot = hot_fr_ok(b->N) && nsx == 1 && hot_params_ok(P);
+        std::vector<char> hot_k(count, fr_hot);
+        std::vector<std::vector<int32_t>> skipped(count);  // per sweep: replicas whose choice blocks carry skips
+        if (fr_hot) {
+            size_t hi = 0;
+            for (int r = 0; r < R; r++) {
+                if (!hosted[r]) continue;
+                const std::vector<Block> &blk = hb[hi++];
+                for (int k = 0; k < count; k++) {
+                    bool sk_k = false;
+                    for (int bi = 2; bi < NB; bi++) sk_k |= bi != 6 && blk[(size_t)k * NB + bi].nskip != 0;
+                    if (sk_k) {
+                        hot_k[k] = 0;
+                        skipped[k].push_back(r);
+                    }
+                }
+            }
+        }
+        // a sweep with skips in a few replicas runs as two launches over replica maps: the fast kernel for the
+        // others, the general kernel for those (so a NumPy Lemire rejection slows one replica's replay, not all)
+        std::vector<int32_t> hmap;
+        std::vector<std::array<int64_t, 4>> split(count, {0, 0, 0, 0});  // hot offset, hot count, general offset, count
+        for (int k = 0; k < count; k++) {
+            if (!fr_hot || hot_k[k]) continue;
+            split[k][0] = (int64_t)hmap.size();
+            size_t j = 0;
+            for (int r = 0; r < R; r++) {
+                if (j < skipped[k].size() && skipped[k][j] == r) {
+                    j++;
+                    continue;
+                }
+                hmap.push_back(r);
+            }
+            split[k][1] = (int64_t)hmap.size() - split[k][0];
+            split[k][2] = (int64_t)hmap.size();
+            hmap.insert(hmap.end(), skipped[k].begin(), skipped[k].end());
+            split[k][3] = (int64_t)skipped[k].size();
+        }
+        if (!hmap.empty()) {
+            if (!b->d_map) SV_HIP(hipMalloc(&b->d_map, (size_t)R * REP_BATCH * sizeof(int32_t)));
+            SV_HIP(hipMemcpyAsync(b->d_map, hmap.data(), hmap.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                                  ctx->stream));
+        }
         const auto t_b = clk::now();
         const int cur0 = b->cur;
         hipEvent_t ev;
@@ -239,19 +290,45 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
             A.Trep = b->d_Trep;
             A.advrep = b->d_adv;
             A.obs = obs ? b->d_obs + 4 * k : nullptr;
-            launch_fused_batch(A, R * tiles, obs != nullptr, ctx->stream);
+            if (hot_k[k]) {
+                launch_hot_fr(A, R * tiles, obs != nullptr, ctx->stream);
+            } else if (split[k][3] > 0) {
+                FArgs Ah = A, Ag = A;
+                Ah.rep_map = b->d_map + split[k][0];
+                Ag.rep_map = b->d_map + split[k][2];
+                // the few replaying replicas: 8-row strips, so that their launch is not one long strip per
+                // workgroup serialized behind the fast launch
+                Ag.TH = 8;
+                Ag.nsy = (b->N + 7) / 8;
+                Ag.tiles_per_rep = nsx * Ag.nsy;
+                if (split[k][1] > 0) launch_hot_fr(Ah, (int)split[k][1] * tiles, obs != nullptr, ctx->stream);
+                launch_fused_batch(Ag, (int)split[k][3] * Ag.tiles_per_rep, obs != nullptr, ctx->stream);
+            } else {
+                launch_fused_batch(A, R * tiles, obs != nullptr, ctx->stream);
+            }
             b->cur ^= 1;
         }
         ctx->time_end(ev, count);
         SV_HIP(hipGetLastError());
-        // --- outcome
-        int32_t ab = 0;
-        uint32_t nrep = 0;
-        SV_HIP(hipMemcpyAsync(&ab, ctx->d_abort, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
-        SV_HIP(hipMemcpyAsync(&nrep, ctx->d_nreport, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+        // --- outcome: abort flag, report count, statistics and observables land in one pinned block
+        const size_t st_bytes = (size_t)R * count * sizeof(sv_stats), ob_bytes = obs ? (size_t)R * count * 4 * sizeof(double) : 0;
+        if (64 + st_bytes + ob_bytes > b->tail_cap) {
+            SV_HIP(hipStreamSynchronize(ctx->stream));
+            if (b->h_tail) SV_HIP(hipHostFree(b->h_tail));
+            b->tail_cap = 64 + (size_t)R * REP_BATCH * (sizeof(sv_stats) + 4 * sizeof(double));
+            SV_HIP(hipHostMalloc((void **)&b->h_tail, b->tail_cap, hipHostMallocDefault));
+        }
+        sv_stats *h_st = (sv_stats *)(b->h_tail + 64);
+        double *h_ob = (double *)(b->h_tail + 64 + st_bytes);
+        SV_HIP(hipMemcpyAsync(b->h_tail, ctx->d_abort, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipMemcpyAsync(b->h_tail + 4, ctx->d_nreport, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipMemcpyAsync(h_st, b->d_stats, st_bytes, hipMemcpyDeviceToHost, ctx->stream));
+        if (obs) SV_HIP(hipMemcpyAsync(h_ob, b->d_obs, ob_bytes, hipMemcpyDeviceToHost, ctx->stream));
         const auto t_c = clk::now();
         SV_HIP(hipStreamSynchronize(ctx->stream));
         const auto t_d = clk::now();
+        const int32_t ab = *(int32_t *)b->h_tail;
+        uint32_t nrep = *(uint32_t *)(b->h_tail + 4);
         int good = count;
         if (ab) {
             ctx->time_discard();
@@ -277,23 +354,18 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         ctx->time_collect();
         // --- keep sweeps [sw, sw + good): stats, observables, cursors
         if (good > 0) {
-            hst.resize((size_t)R * count);
-            SV_HIP(hipMemcpy(hst.data(), b->d_stats, hst.size() * sizeof(sv_stats), hipMemcpyDeviceToHost));
-            if (obs) {
-                hobs.resize((size_t)R * count * 4);
-                SV_HIP(hipMemcpy(hobs.data(), b->d_obs, hobs.size() * sizeof(double), hipMemcpyDeviceToHost));
-            }
             for (int r = 0; r < R; r++)
                 for (int k = 0; k < good; k++) {
-                    sv_stats s = hst[(size_t)r * count + k];
+                    sv_stats s = h_st[(size_t)r * count + k];
                     s.proposed = V;
                     s.rejections = skips[r].empty() ? 0 : rejections_in(skips[r], sw + k, NB);
                     stats[(size_t)r * sweeps + sw + k] = s;
                     if (obs)
-                        std::memcpy(obs + ((size_t)r * sweeps + sw + k) * 4, &hobs[((size_t)r * count + k) * 4],
+                        std::memcpy(obs + ((size_t)r * sweeps + sw + k) * 4, &h_ob[((size_t)r * count + k) * 4],
                                     4 * sizeof(double));
                 }
         }
+        const Affine unit = good > 0 ? host_power(u128{1, 0}, (uint64_t)good * 4 * V) : Affine{};
         for (int r = 0; r < R; r++) {
             if (good == count && hosted[r]) {
                 cur[r] = end_host[r];
@@ -302,8 +374,8 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
                 std::vector<Block> blk;
                 plan_sweeps(ctx, c, inc[r], specs, sw, good, skips[r], blk, sk);
                 cur[r] = c;
-            } else {
-                advance_closed(cur[r], inc[r], (uint64_t)V, good);
+            } else if (good > 0) {
+                advance_closed(cur[r], inc[r], unit);
             }
         }
         b->cur = cur0 ^ (good & 1);
@@ -375,6 +447,8 @@ int sv_replicas_destroy(sv_replicas *b) {
     (void)hipFree(b->d_blocks);
     (void)hipFree(b->d_stats);
     (void)hipFree(b->d_obs);
+    if (b->h_tail) (void)hipHostFree(b->h_tail);
+    if (b->d_map) (void)hipFree(b->d_map);
     delete b;
     return 0;
 }

@@ -58,6 +58,7 @@ struct FArgs {
     const Affine *advrep;           // per-replica adv[3], or nullptr (all use adv)
     double *obs;                    // OBS kernels: per replica {sum (d phi - 2 pi n)^2, sum (dn)^2, sum n0, sum n1}
     const int32_t *strip_map = nullptr;  // TILE: launch index -> strip index (interior / boundary launches)
+    const int32_t *rep_map = nullptr;    // replica batches: launch's replica slot -> replica (a subset launch), or identity
 };
 
 }  // namespace sv
@@ -96,6 +97,11 @@ void launch_fused_batch(const FArgs &A, int grid, bool obs, hipStream_t stream);
 // and its launch (periodic single lattice or a domain tile, from the geometry)
 bool hot_ok(const VParams &P, const Block *blocks);
 void launch_hot(const FArgs &A, int grid, hipStream_t stream);
+// full-row replica batches (config 5) on the fast-draw kernel: whether N qualifies, and the launch (the sweep must
+// pass hot_ok for every replica: no skips, no buffered half-word, choice values in range)
+bool hot_fr_ok(int32_t N);
+bool hot_params_ok(const VParams &P);  // the parameter part of hot_ok
+void launch_hot_fr(const FArgs &A, int grid, bool obs, hipStream_t stream);
 // plain single-lattice FArgs defaults (one replica, no observables)
 void farg_single(FArgs &A, int nsx, int nsy);
 

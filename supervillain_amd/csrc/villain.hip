@@ -169,8 +169,9 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     // domain tiles: the launch covers a subset of the strips (interior ones while the halos travel)
     if (TILE && A.strip_map) b = __builtin_amdgcn_readfirstlane(A.strip_map[b]);
     // replica of this workgroup (replica batches; 0 otherwise)
-    const int rep = REPS ? __builtin_amdgcn_readfirstlane(b / A.tiles_per_rep) : 0;  // uniform: keep it scalar
-    if (REPS) b = __builtin_amdgcn_readfirstlane(b - rep * A.tiles_per_rep);
+    const int slot = REPS ? __builtin_amdgcn_readfirstlane(b / A.tiles_per_rep) : 0;  // uniform: keep it scalar
+    if (REPS) b = __builtin_amdgcn_readfirstlane(b - slot * A.tiles_per_rep);
+    const int rep = REPS && A.rep_map ? __builtin_amdgcn_readfirstlane(A.rep_map[slot]) : slot;
     const Rep RP{REPS ? A.blocks + (int64_t)rep * A.rep_blocks : A.blocks, REPS ? A.Trep[rep] : A.T, (uint32_t)rep};
     const double *phi_in = REPS ? A.phi_in + rep * A.rep_field : A.phi_in;
     const int64_t *n_in = REPS ? A.n_in + 2 * rep * A.rep_field : A.n_in;
@@ -647,6 +648,7 @@ void farg_single(FArgs &A, int nsx, int nsy) {
     A.advrep = nullptr;
     A.obs = nullptr;
     A.strip_map = nullptr;
+    A.rep_map = nullptr;
 }
 
 // plan `count` sweeps starting at sweep `first`, writing descriptors to ctx host staging

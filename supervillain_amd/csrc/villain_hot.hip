@@ -106,12 +106,20 @@ struct HotLDS {
     Affine adv[3];
     u128 base[4][32];  // per wave: [8c + ty] block ty's base for the colour-c row at xb; [16 + ..] at xw
     int32_t bad;
+    double obs[4];     // OBS: the workgroup's sums of the inline observables
 };
 
 // EDGE: the strip's region wraps around the lattice rows (or sits within 4 columns of an edge); a
-// template parameter so that the two draw forms are two code paths, not one if-converted stream
-template <bool TILE, bool EDGE>
+// template parameter so that the two draw forms are two code paths, not one if-converted stream.
+// FR: replica batches of full-row lattices (Nx <= 128, Nx % 4 == 0): consecutive runs of
+// tiles_per_rep workgroups serve one replica (its fields, descriptors, tables and statistics), one strip spans
+// the whole row, its LDS columns ARE the lattice columns and neighbours wrap inside LDS; the paired draws hold
+// because a row's first rank N/2 q is even -- unless the replica's choice blocks start on a buffered half-word
+// (after an odd number of NumPy Lemire rejections in its chain): then the pairs would straddle rows and the
+// replica draws unpaired (the EDGE form).  OBS: the inline observables fused into the row stores.
+template <bool TILE, bool EDGE, bool FR = false, bool OBS = false>
 __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
+    static_assert(!(FR && TILE), "full-row replica strips are periodic");
     constexpr int NW = 4;
     constexpr int R = HotLDS::R, RR = HotLDS::RR;
     constexpr int PF = RW / 64;
@@ -143,32 +151,41 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
         b = xcd * per + (xcd < rem ? xcd : rem) + k;
     }
     if (TILE && A.strip_map) b = __builtin_amdgcn_readfirstlane(A.strip_map[b]);
-    const double *phi_in = A.phi_in;
-    const int64_t *n_in = A.n_in;
-    double *phi_out = A.phi_out;
-    int64_t *n_out = A.n_out;
+    const int slot = FR ? __builtin_amdgcn_readfirstlane(b / A.tiles_per_rep) : 0;  // uniform: keep it scalar
+    if (FR) b = __builtin_amdgcn_readfirstlane(b - slot * A.tiles_per_rep);
+    const int rep = FR && A.rep_map ? __builtin_amdgcn_readfirstlane(A.rep_map[slot]) : slot;
+    const Block *blocks = FR ? A.blocks + (int64_t)rep * A.rep_blocks : A.blocks;
+    const JumpTables *Tb = FR ? A.Trep[rep] : A.T;
+    const double *phi_in = FR ? A.phi_in + rep * A.rep_field : A.phi_in;
+    const int64_t *n_in = FR ? A.n_in + 2 * rep * A.rep_field : A.n_in;
+    double *phi_out = FR ? A.phi_out + rep * A.rep_field : A.phi_out;
+    int64_t *n_out = FR ? A.n_out + 2 * rep * A.rep_field : A.n_out;
     const int ix = b % A.nsx, iy = b / A.nsx;
     const int32_t x0 = (int32_t)((int64_t)ix * Gm.Wt / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * Gm.Wt / A.nsx);
     const int32_t w = x1 - x0;
     const int32_t t0 = iy * A.TH;
     const int32_t t1 = t0 + A.TH < Gm.Ht ? t0 + A.TH : Gm.Ht;
     const int32_t rbase = t0 - 2;  // local row 0
-    const int32_t cols = w + 5;
-    const int32_t cofs = x0 - 2;   // LDS column of local column x is x - cofs
+    const int32_t cols = FR ? w : w + 5;
+    const int32_t cofs = FR ? 0 : x0 - 2;   // LDS column of local column x is x - cofs
+    // LDS neighbour columns (full rows wrap inside the row)
+    auto cxp = [&](int cx) { return FR ? (cx + 1 == w ? 0 : cx + 1) : cx + 1; };
+    auto cxm = [&](int cx) { return FR ? (cx == 0 ? w - 1 : cx - 1) : cx - 1; };
     const int32_t gx0 = Gm.X0 + x0;
     const bool interior = gx0 >= 4 && gx0 + w + 2 < Nx;
-    const int32_t xb = ((Nx <= SMALL_LDS && !interior) || gx0 - 2 < 0) ? 0 : gx0 - 2;
+    const int32_t xb = (FR || (Nx <= SMALL_LDS && !interior) || gx0 - 2 < 0) ? 0 : gx0 - 2;
     constexpr bool edge = EDGE;
     (void)interior;
     const bool two_sets = edge && Nx > SMALL_LDS;   // wrapped columns need the second base set
     const int32_t xw = gx0 - 2 < 0 ? Nx - 2 : 0;
 
     for (int e = threadIdx.x; e < SMALL_LDS; e += NW * 64) {
-        s_small.A[e] = A.T->small[e].A;
-        s_small.C[e] = A.T->small[e].C;
+        s_small.A[e] = Tb->small[e].A;
+        s_small.C[e] = Tb->small[e].C;
     }
-    if (threadIdx.x < 3) s_adv[threadIdx.x] = A.adv[threadIdx.x];
+    if (threadIdx.x < 3) s_adv[threadIdx.x] = FR ? A.advrep[3 * rep + threadIdx.x] : A.adv[threadIdx.x];
     if (threadIdx.x == 0) s_bad = 0;
+    if (OBS && threadIdx.x < 4) Ls.obs[threadIdx.x] = 0.0;
 
     // per colour: the buffered-half flags and words of the choice blocks (equal within each fwd/bwd pair on
     // this kernel), uniform
@@ -177,10 +194,10 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
     for (int c = 0; c < 2; c++) {
 #pragma unroll
         for (int mu = 0; mu < 2; mu++)
-            has_c[c][mu] = (uint32_t)__builtin_amdgcn_readfirstlane(A.blocks[2 + 5 * c + 2 * mu].has);
+            has_c[c][mu] = (uint32_t)__builtin_amdgcn_readfirstlane(blocks[2 + 5 * c + 2 * mu].has);
         if (edge) {
 #pragma unroll
-            for (int j = 0; j < 4; j++) buf_c[c][j] = (uint32_t)__builtin_amdgcn_readfirstlane(A.blocks[2 + 5 * c + j].buf);
+            for (int j = 0; j < 4; j++) buf_c[c][j] = (uint32_t)__builtin_amdgcn_readfirstlane(blocks[2 + 5 * c + j].buf);
         }
     }
     const VParams P = A.P;
@@ -192,7 +209,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
     int64_t pf_n0[PF], pf_n1[PF];
     int pf_gx[PF];
 #pragma unroll
-    for (int k = 0; k < PF; k++) pf_gx[k] = mcol(x0 - 2 + lane + 64 * k);
+    for (int k = 0; k < PF; k++) pf_gx[k] = FR ? lane + 64 * k : mcol(x0 - 2 + lane + 64 * k);
     if (SV_ABLATE & 16) {
 #pragma unroll
         for (int k = 0; k < PF; k++) pf_phi[k] = 0.0, pf_n0[k] = pf_n1[k] = 0;
@@ -243,13 +260,13 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
     const int bc = (lane >> 3) & 1, bty = lane & 7;
     const int32_t bx = lane >= 16 ? xw : xb;
     const int bblk = bty == 0 ? 0 : 1 + 5 * bc + bty - 1;
-    const uint32_t bhas = (base_lane && bty >= 2) ? A.blocks[bblk].has : 0u;
+    const uint32_t bhas = (base_lane && bty >= 2) ? blocks[bblk].has : 0u;
     const int32_t tfirst = t0 - 3;
     int32_t brow = tfirst + 2 - bc + wave;  // colour 0 row t+2+wave, colour 1 row t+1+wave
     int32_t brow1 = tfirst + 1 + wave;      // the colour-1 row, wave-uniform
     {  // (the running bases live in LDS only: the advance reads them back, no registers held across the loop)
         u128 bases{0, 0};
-        if (base_lane) bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)base_pos(bty, grow(brow), Nx, bx, bhas));
+        if (base_lane) bases = full_jump(Tb, &blocks[bblk], (uint32_t)base_pos(bty, grow(brow), Nx, bx, bhas));
         __builtin_amdgcn_s_waitcnt(0);
         if (base_lane) s_base[wave][lane] = bases;
     }
@@ -259,13 +276,13 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
     if constexpr (!edge) {
         {
             const int32_t q = tfirst + 2 + wave;
-            const int32_t xs = (x0 - 1) + ((par0 + q + x0 - 1) & 1);
+            const int32_t xs = FR ? ((par0 + q) & 1) : (x0 - 1) + ((par0 + q + x0 - 1) & 1);
             pk0 = fast_pack(has_c[0], lane, (uint32_t)grow(q) * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
                             (uint32_t)(Gm.X0 + xs + 2 * lane), (uint32_t)xb);
         }
         {
             const int32_t q = tfirst + 1 + wave;
-            const int32_t xs = x0 + ((par0 + q + x0 + 1) & 1);
+            const int32_t xs = FR ? ((par0 + q + 1) & 1) : x0 + ((par0 + q + x0 + 1) & 1);
             pk1 = fast_pack(has_c[1], lane, (uint32_t)grow(q) * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
                             (uint32_t)(Gm.X0 + xs + 2 * lane), (uint32_t)xb);
         }
@@ -277,6 +294,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
     auto store_rows = [&](int32_t ra) {
         if (SV_ABLATE & 8) return;
         const int32_t q = ra + wave;
+        double o_act = 0.0, o_w2 = 0.0, o_n0 = 0.0, o_n1 = 0.0;  // OBS partials (integers exact in f64)
         if (q >= t0 && q < t1) {
             const int slot = (q - rbase) % R;
             const int64_t g0 = mrow(q) + x0;
@@ -284,11 +302,38 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
             for (int k = 0; k < PF; k++) {
                 const int cc = lane + 64 * k;
                 if (cc < w) {
+                    const int cx = FR ? cc : cc + 2;
                     const int64_t g = g0 + cc;
-                    phi_out[g] = s_phi[slot][cc + 2];
-                    n_out[g] = (int64_t)s_n0[slot][cc + 2];
-                    n_out[V + g] = (int64_t)s_n1[slot][cc + 2];
+                    phi_out[g] = s_phi[slot][cx];
+                    n_out[g] = (int64_t)s_n0[slot][cx];
+                    n_out[V + g] = (int64_t)s_n1[slot][cx];
+                    if (OBS) {
+                        // rows <= q+1 and columns <= x+1 are final here (villain.py:51-66, winding.py:30-37,
+                        // wrapping.py:17-25): link residuals, plaquette winding dn, holonomy sums
+                        const int slot1 = (q + 1 - rbase) % R;
+                        const double ph = s_phi[slot][cx];
+                        const double l0 = (0.0 + (s_phi[slot1][cx] - ph)) - TWO_PI * (double)s_n0[slot][cx];
+                        const double l1 = (0.0 + (s_phi[slot][cxp(cx)] - ph)) - TWO_PI * (double)s_n1[slot][cx];
+                        o_act += l0 * l0 + l1 * l1;
+                        const int64_t dn = ((int64_t)s_n1[slot1][cx] - s_n1[slot][cx]) -
+                                           ((int64_t)s_n0[slot][cxp(cx)] - s_n0[slot][cx]);
+                        o_w2 += (double)(dn * dn);
+                        o_n0 += (double)s_n0[slot][cx];
+                        o_n1 += (double)s_n1[slot][cx];
+                    }
                 }
+            }
+        }
+        if (OBS) {
+            o_act = wave_sum(o_act);
+            o_w2 = wave_sum(o_w2);
+            o_n0 = wave_sum(o_n0);
+            o_n1 = wave_sum(o_n1);
+            if (lane == 0) {
+                atomicAdd(&Ls.obs[0], o_act);
+                atomicAdd(&Ls.obs[1], o_w2);
+                atomicAdd(&Ls.obs[2], o_n0);
+                atomicAdd(&Ls.obs[3], o_n1);
             }
         }
     };
@@ -317,7 +362,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
             const uint32_t rank = (uint32_t)(((int64_t)gq * Nx + wrapN(Gm.X0 + x, Nx)) >> 1);
 #pragma unroll
             for (int j = 0; j < 4; j++)
-                if ((uint32_t)((uint64_t)D.w[j] * kc) < thr) report(A.S, A.sweep, (uint32_t)(1 + 5 * c + 1 + j), rank);
+                if ((uint32_t)((uint64_t)D.w[j] * kc) < thr) report(A.S, A.sweep, (uint32_t)(1 + 5 * c + 1 + j), rank, (uint32_t)rep);
         }
     };
 
@@ -335,16 +380,16 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
         {
             const int32_t q = t + 2 + wave;
             const bool row_ok = (q >= t0 - 1) && (q <= t1 + 1);
-            const int32_t xs = (x0 - 1) + ((par0 + q + x0 - 1) & 1);
+            const int32_t xs = FR ? ((par0 + q) & 1) : (x0 - 1) + ((par0 + q + x0 - 1) & 1);
             const int32_t x = xs + 2 * lane;
-            const bool active = row_ok && x <= x1 + 1;
+            const bool active = row_ok && (FR ? x < w : x <= x1 + 1);
             HotDraws D;
             int32_t cn[4];
             draw(0, q, x, active, D, cn);
             if (active) {
                 const int lr = q - rbase;
                 const int sm = (lr - 1) % R, s0 = lr % R, sp = (lr + 1) % R;
-                const int cx = x - cofs, cp = cx + 1, cm = cx - 1;
+                const int cx = x - cofs, cp = cxp(cx), cm = cxm(cx);
                 const double ph = s_phi[s0][cx];
                 const int32_t n_f0 = s_n0[s0][cx], n_b0 = s_n0[sm][cx], n_f1 = s_n1[s0][cx], n_b1 = s_n1[s0][cm];
                 // r on the four links f0=(0,q,x), b0=(0,q-1,x), f1=(1,q,x), b1=(1,q,x-1) (neighborhood.py:91)
@@ -367,7 +412,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
                 double p = sv_exp(-dS);
                 p = p > 1.0 ? 1.0 : p;
                 const bool acc = D.u < p;
-                if (q >= t0 && q < t1 && x >= x0 && x < x1) {
+                if (q >= t0 && q < t1 && (FR || (x >= x0 && x < x1))) {
                     acc_count += acc;
                     psum += p;
                 }
@@ -398,16 +443,16 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
         {
             const int32_t q = t + 1 + wave;
             const bool row_ok = (q >= t0) && (q <= t1);
-            const int32_t xs = x0 + ((par0 + q + x0 + 1) & 1);
+            const int32_t xs = FR ? ((par0 + q + 1) & 1) : x0 + ((par0 + q + x0 + 1) & 1);
             const int32_t x = xs + 2 * lane;
-            const bool active = row_ok && x <= x1;
+            const bool active = row_ok && (FR ? x < w : x <= x1);
             HotDraws D;
             int32_t cn[4];
             draw(1, q, x, active, D, cn);
             if (active) {
                 const int lr = q - rbase;
                 const int sm = (lr - 1) % R, s0 = lr % R;
-                const int cx = x - cofs, cm = cx - 1;
+                const int cx = x - cofs, cm = cxm(cx);
                 double ri[4];
                 const int r0s = lr % RR, rms = (lr - 1) % RR;
                 ri[0] = s_r0[r0s][cx];
@@ -426,7 +471,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
                 double p = sv_exp(-dS);
                 p = p > 1.0 ? 1.0 : p;
                 const bool acc = D.u < p;
-                if (q >= t0 && q < t1 && x >= x0 && x < x1) {
+                if (q >= t0 && q < t1 && (FR || (x >= x0 && x < x1))) {
                     acc_count += acc;
                     psum += p;
                 }
@@ -461,7 +506,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
             const int64_t step = bty == 0 ? (int64_t)NW * Nx : (bty == 1 ? (int64_t)NW * Nx / 2 : (int64_t)NW * Nx / 4);
             u128 bases = s_base[wave][lane];
             if (p_new - p_old == step) bases = apply(s_adv[ai], bases);
-            else bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)p_new);
+            else bases = full_jump(Tb, &blocks[bblk], (uint32_t)p_new);
             brow += NW;
             s_base[wave][lane] = bases;
         } else {
@@ -474,8 +519,12 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
         while (tl + NW < t1) tl += NW;
         store_rows(tl);
     }
-    if (s_bad && threadIdx.x == 0) report(A.S, A.sweep, OVERFLOW_BLOCK, 0, 0);
-    flush_stats(A.stat, acc_count, psum);
+    if (s_bad && threadIdx.x == 0) report(A.S, A.sweep, OVERFLOW_BLOCK, 0, (uint32_t)rep);
+    flush_stats(FR ? A.stat + (int64_t)rep * A.rep_stat : A.stat, acc_count, psum);
+    if (OBS) {
+        __syncthreads();
+        if (threadIdx.x < 4) unsafeAtomicAdd(&A.obs[(int64_t)rep * A.rep_obs + threadIdx.x], Ls.obs[threadIdx.x]);
+    }
 }
 
 template <bool TILE>
@@ -500,22 +549,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4
 template __global__ void villain_sweep_hot<false>(FArgs);
 template __global__ void villain_sweep_hot<true>(FArgs);
 
+// replica batches of full-row lattices (config 5), with or without the inline observables
+template <bool OBS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4 ? 4 : 3))) void villain_sweep_hot_fr(FArgs A) {
+    __shared__ HotLDS Ls;
+    // the replica this workgroup serves (the mapping hot_body makes), to pick the draw form
+    int b = blockIdx.x;
+    {
+        const int G = gridDim.x, per = G / 8, rem = G % 8;
+        const int xcd = b & 7, k = b >> 3;
+        b = xcd * per + (xcd < rem ? xcd : rem) + k;
+    }
+    const int slot = b / A.tiles_per_rep;
+    const Block *blk = A.blocks + (int64_t)(A.rep_map ? A.rep_map[slot] : slot) * A.rep_blocks;
+    if (__builtin_amdgcn_readfirstlane((int)(blk[2].has | blk[4].has | blk[7].has | blk[9].has)))
+        hot_body<false, true, true, OBS>(A, Ls);
+    else
+        hot_body<false, false, true, OBS>(A, Ls);
+}
+template __global__ void villain_sweep_hot_fr<false>(FArgs);
+template __global__ void villain_sweep_hot_fr<true>(FArgs);
+
 }  // namespace sv
 
 namespace svh {
 
 // The hot kernel covers a sweep when its choice blocks carry no skip list and each fwd/bwd pair has equal
 // buffered-half flags, and the choice values W (index - interval_n) fit int32
-bool hot_ok(const VParams &P, const Block *blocks) {
+bool hot_params_ok(const VParams &P) {
     const int64_t aw = P.W < 0 ? -P.W : P.W;
     if (P.k <= 1 || P.k > (1u << 20) || aw > (1 << 20) || aw * (int64_t)P.k >= (1 << 28)) return false;  // int32 values
     if (SV_HOT_OCC4 && aw > (1 << 12)) return false;  // the int16 n image: |n| < 2^14 plus 2|W| per sweep
+    return true;
+}
+
+bool hot_ok(const VParams &P, const Block *blocks) {
+    if (!hot_params_ok(P)) return false;
     for (int c = 0; c < 2; c++) {
         const Block *B = blocks + 2 + 5 * c;
         if (B[0].nskip || B[1].nskip || B[2].nskip || B[3].nskip) return false;
         if (B[0].has != B[1].has || B[2].has != B[3].has) return false;
     }
     return true;
+}
+
+// replica batch of full-row lattices: N <= 128 columns (one strip), N % 4 == 0 (row ranks start on whole words)
+bool hot_fr_ok(int32_t N) { return hot_enabled() && N <= RW && N % 4 == 0 && N >= 8; }
+
+void launch_hot_fr(const FArgs &A, int grid, bool obs, hipStream_t stream) {
+    if (obs) villain_sweep_hot_fr<true><<<grid, 4 * 64, 0, stream>>>(A);
+    else villain_sweep_hot_fr<false><<<grid, 4 * 64, 0, stream>>>(A);
 }
 
 void launch_hot(const FArgs &A, int grid, hipStream_t stream) {

@@ -139,3 +139,33 @@ def test_one_shot_entry_point(oracle_lib):
         assert g.bit_generator.state == gens[i].bit_generator.state
         assert [s.accepted for s in ref] == [st[i * sweeps + k].accepted for k in range(sweeps)]
         np.testing.assert_allclose(obs[i, -1, 0], offline(p, m)[0], rtol=1e-12)
+
+
+@pytest.mark.parametrize('inline', [False, True])
+def test_replicas_starting_on_a_buffered_half_word(oracle_lib, inline):
+    """Replicas whose generators hold NumPy's buffered uint32 (has_uint32 = 1, as after an odd number of bounded
+    draws or Lemire rejections) run the fast replica kernel's unpaired draw form; the others the paired one; every
+    replica equals its own chain and, with inline observables, its offline measurement."""
+    R, N, W, sweeps = 6, 64, 2, 4
+    phi0, n0 = hot(R, N, W, 21)
+
+    def gens_():
+        gs = [np.random.default_rng(300 + r) for r in range(R)]
+        for r in (1, 4):
+            gs[r].integers(0, 3)  # leaves has_uint32 = 1
+        return gs
+    gens = gens_()
+    assert gens[1].bit_generator.state['has_uint32'] == 1
+    phi, n, stats, obs = run_batch(R, N, 0.5, W, phi0, n0, sweeps, gens, inline=inline)
+    ref = gens_()
+    for r in range(R):
+        p, m = phi0[r].copy(), n0[r].copy()
+        for s in range(sweeps):
+            oracle_lib.villain_neighborhood(N, 0.5, W, p, m, 1, ref[r])
+            if inline:
+                act, w2, s0, s1 = offline(p, m)
+                np.testing.assert_allclose(obs['ActionDensity'][r, s], 0.5 / 2 * act / (N * N), rtol=1e-12)
+                assert obs['WindingSquared'][r, s] == w2 / (N * N)
+                assert list(obs['TorusWrapping'][r, s]) == [s0, s1]
+        assert (phi[r] == p).all() and (n[r] == m).all(), r
+        assert gens[r].bit_generator.state == ref[r].bit_generator.state
