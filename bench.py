@@ -73,6 +73,9 @@ def parse():
     ap.add_argument('--kappa', type=float, default=0.5)
     ap.add_argument('--W', type=int, default=1)
     ap.add_argument('--path', type=int, default=2, help='0 auto, 1 per-colour kernels, 2 fused sweep kernel')
+    ap.add_argument('--rng', default='pcg64', choices=['pcg64', 'philox'],
+                    help='villain workload: pcg64 = the reference chain (NumPy stream replay, the headline); philox = '
+                         'the optional counter-based mode (SURVEY.md 8(b) sv_rng mode 1, a different chain)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-sweeps', type=int, default=5)
     ap.add_argument('--weak', action='store_true', help='N>1: an L x L tile per GPU (weak scaling) instead of one '
@@ -691,11 +694,17 @@ def main():
     n = np.zeros((2, L, L), dtype=np.int64)
     ctx.check(Lib.sv_villain_upload(h, _native.ptr(phi), _native.ptr(n)), 'upload')
     r = rng_from_numpy(np.random.default_rng(0))
+    from supervillain_amd._abi import SvPhilox
+    ph = SvPhilox(0x5eed, 0, 0)
 
     def run(k):
         st = _native.stats_array(k)
-        ctx.check(Lib.sv_villain_run(h, args.kappa, args.W, float(np.pi), 1, k, ctypes.byref(r), st, args.path),
-                  'sv_villain_run')
+        if args.rng == 'philox':
+            ctx.check(Lib.sv_villain_run_philox(h, args.kappa, args.W, float(np.pi), 1, k, ctypes.byref(ph), st),
+                      'sv_villain_run_philox')
+        else:
+            ctx.check(Lib.sv_villain_run(h, args.kappa, args.W, float(np.pi), 1, k, ctypes.byref(r), st, args.path),
+                      'sv_villain_run')
         return st
 
     warm_up(run, args)
@@ -706,11 +715,15 @@ def main():
     avg_launch_s = kernel_time(Lib, ctx)
     acc = sum(st[i].accepted for i in range(args.steps)) / (args.steps * L * L)
     rej = sum(st[i].rejections for i in range(args.steps))
-    config = {'workload': f'L={L} Villain NeighborhoodUpdate sweep, kappa={args.kappa}, W={args.W}, '
-                          'bit-exact reference chain (PCG64 replay), fused two-colour sweep kernel (villain_sweep_hot)',
+    chain = ('bit-exact reference chain (PCG64 replay), fused two-colour sweep kernel (villain_sweep_hot)'
+             if args.rng == 'pcg64' else 'counter-based Philox4x32-10 mode (a different chain from the reference\'s), '
+             'fused two-colour sweep kernel (villain_sweep_hot_ph)')
+    config = {'workload': f'L={L} Villain NeighborhoodUpdate sweep, kappa={args.kappa}, W={args.W}, ' + chain,
+              'rng': args.rng,
               'L': L, 'lattice': [L, L], 'path': args.path, 'parallelism': 'single GPU',
               'lemire_rejections_in_timed_steps': int(rej)}
-    report(args, 1, L * L, L * L, t1 - t0, acc, avg_launch_s, config, L, ctx=ctx)
+    report(args, 1, L * L, L * L, t1 - t0, acc, avg_launch_s, config, L, ctx=ctx,
+           kernel='villain_sweep_hot' if args.rng == 'pcg64' else 'villain_sweep_hot_ph')
     Lib.sv_villain_destroy(h)
 
 

@@ -88,6 +88,21 @@ int sv_villain_create(sv_ctx *ctx, int32_t N, sv_villain **out);
 int sv_villain_destroy(sv_villain *st);
 int sv_villain_upload(sv_villain *st, const double *phi, const int64_t *n);
 int sv_villain_download(sv_villain *st, double *phi, int64_t *n);
+/* The optional counter-based mode (sv_rng mode 1, "Philox fast").  The same NeighborhoodUpdate
+ * sweep (neighborhood.py:59-137, operation order and acceptance as above) with every draw from Philox4x32-10:
+ * site s of sweep number c (rng->counter counts the sweeps done) draws u and dphi from call (s, c, 0) and its four
+ * choice words from call (s, c, 1) under key rng->key; a word NumPy's bounded Lemire sampler would reject is
+ * redrawn in place (call (s, c, 2 + j + 4 t)).  A different Markov chain from the reference's (NumPy PCG64),
+ * statistically equivalent; no replays.  Even N, |W| <= 2^12, |n| < 2^14.  test_threshold (tests
+ * only, 0 = Lemire's) replaces the rejection threshold to exercise the redraws.  Returns -2 with the fields
+ * unspecified if |n| outgrows the int16 image (re-upload); rng->counter then is not advanced. */
+typedef struct sv_philox {
+    uint64_t key, counter;
+    uint32_t test_threshold;
+} sv_philox;
+int sv_villain_run_philox(sv_villain *st, double kappa, int64_t W, double interval_phi, int64_t interval_n,
+                          int32_t sweeps, sv_philox *rng, sv_stats *stats);
+
 /* Asynchronous emission of the resident configuration into host storage (the D2H of
  * Ensemble.generate's kept configurations, ensemble.py:89-92, overlapped with the sweeps that follow).
  * sv_villain_emit returns at once: the state as of every sweep queued so far is snapshotted on the device

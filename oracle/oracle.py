@@ -44,6 +44,9 @@ def lib():
         L.sv_o_villain_neighborhood_mt.argtypes = [i32, f64, i64, f64, i64, vp, vp, i32, P(SvRng), vp, i32]
         L.sv_o_villain_worm.argtypes = [i32, f64, i64, vp, vp, i32, P(SvRng), vp, vp]
         L.sv_o_worldline_worm.argtypes = [i32, f64, f64, vp, vp, i32, i32, P(SvRng), vp, vp]
+        u32, u64 = ctypes.c_uint32, ctypes.c_uint64
+        L.sv_o_philox4x32_10.argtypes = [vp, vp, vp]
+        L.sv_o_villain_neighborhood_philox.argtypes = [i32, f64, i64, f64, i64, vp, vp, i32, u64, u64, u32, vp]
         _LIB = L
     return _LIB
 
@@ -97,6 +100,28 @@ def villain_neighborhood(N, kappa, W, phi, n, sweeps, gen, interval_phi=np.pi, i
     if rc != 0:
         raise ValueError('oracle rejected the arguments')
     rng_to_numpy(r, gen)
+    return [st[i] for i in range(sweeps)]
+
+
+def philox4x32_10(ctr, key):
+    """Philox4x32-10 of a 4-word counter under a 2-word key (the optional fast mode's generator)."""
+    c = np.ascontiguousarray(ctr, dtype=np.uint32)
+    k = np.ascontiguousarray(key, dtype=np.uint32)
+    out = np.empty(4, dtype=np.uint32)
+    lib().sv_o_philox4x32_10(_ptr(c), _ptr(k), _ptr(out))
+    return out
+
+
+def villain_neighborhood_philox(N, kappa, W, phi, n, sweeps, key, counter, interval_phi=np.pi, interval_n=1,
+                                thr_override=0):
+    """NeighborhoodUpdate sweeps with the counter-based Philox draws (sv_oracle.c's header of that section)."""
+    assert phi.dtype == np.float64 and n.dtype == np.int64
+    assert phi.flags.c_contiguous and n.flags.c_contiguous
+    st = _stats_array(sweeps)
+    rc = lib().sv_o_villain_neighborhood_philox(N, kappa, int(W), interval_phi, int(interval_n), _ptr(phi), _ptr(n),
+                                                sweeps, key, counter, thr_override, st)
+    if rc != 0:
+        raise ValueError('oracle rejected the arguments')
     return [st[i] for i in range(sweeps)]
 
 

@@ -338,6 +338,148 @@ int sv_o_villain_neighborhood_rect(int32_t Nt, int32_t Nx, double kappa, int64_t
     return 0;
 }
 
+/* ---------------------------------------------------------------- optional counter-based mode (Philox) */
+/* SURVEY.md 8(b) sv_rng mode 1: the same NeighborhoodUpdate sweep (neighborhood.py:59-137, the operation order of
+ * villain_sweep above) with its draws from Philox4x32-10 by counter instead of NumPy's PCG64 stream.  For colour
+ * site s (row-major index) in sweep number `sweep` (a 64-bit count kept by the caller):
+ *   call (s, sweep_lo, sweep_hi, 0) -> words w0..w3: metropolis u = next_double(w1:w0), dphi = uniform(w3:w2);
+ *   call (s, sweep_lo, sweep_hi, 1) -> the 4 choice words: [2 mu] the forward link (mu, s), [2 mu + 1] the
+ *   backward link (mu, s - e_mu);
+ *   choice j is Lemire's bounded draw on its word; a rejected word is replaced by word 0 of call
+ *   (s, sweep_lo, sweep_hi, 2 + j + 4 t) at retry t (in place: nothing else shifts).
+ * Every site draws u (the reference draws it for all sites, :87), only colour sites use it.  `thr_override`
+ * (tests only) replaces Lemire's threshold to exercise the retry path. */
+static inline void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+    for (int i = 0; i < 10; i++) {
+        if (i) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n1 = (uint32_t)p1, n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1,
+                 n3 = (uint32_t)p0;
+        c[0] = n0;
+        c[1] = n1;
+        c[2] = n2;
+        c[3] = n3;
+    }
+}
+
+int sv_o_philox4x32_10(const uint32_t *ctr, const uint32_t *key, uint32_t *out) {
+    uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]};
+    philox4x32_10(c, key[0], key[1]);
+    for (int i = 0; i < 4; i++) out[i] = c[i];
+    return 0;
+}
+
+static inline double u53_of(uint32_t lo, uint32_t hi) {
+    return (double)((((uint64_t)hi << 32) | lo) >> 11) * (1.0 / 9007199254740992.0);
+}
+
+static uint32_t philox_choice(uint32_t s, uint64_t sweep, uint64_t key, uint32_t word, int j, uint32_t k, uint32_t thr,
+                              int64_t *retries) {
+    uint64_t m = (uint64_t)word * k;
+    for (uint32_t t = 0; (uint32_t)m < thr; t++) {
+        uint32_t c[4] = {s, (uint32_t)sweep, (uint32_t)(sweep >> 32), 2u + (uint32_t)j + 4u * t};
+        philox4x32_10(c, (uint32_t)key, (uint32_t)(key >> 32));
+        m = (uint64_t)c[0] * k;
+        if (retries) (*retries)++;
+    }
+    return (uint32_t)(m >> 32);
+}
+
+int sv_o_villain_neighborhood_philox(int32_t N, double kappa, int64_t W, double interval_phi, int64_t interval_n,
+                                     double *phi, int64_t *n, int32_t sweeps, uint64_t key, uint64_t counter,
+                                     uint32_t thr_override, sv_stats *stats) {
+    if (N < 2 || (N % 2) || sweeps < 0) return -1;
+    const int64_t Nt = N, Nx = N, V = (int64_t)N * N;
+    colors_t C = colors_make(N);
+    double *metro = (double *)malloc(sizeof(double) * 6 * V + sizeof(int64_t) * 3 * V);
+    double *r = metro + V, *cphi = r + 2 * V, *dSl = cphi + V;
+    int64_t *cn = (int64_t *)(dSl + 2 * V), *acc = cn + 2 * V;
+    const double half_kappa = kappa / 2.0, range_phi = interval_phi - (-interval_phi);
+    const uint32_t k = (uint32_t)(2 * interval_n + 1);
+    const uint32_t thr = thr_override ? thr_override : (k > 1 ? (uint32_t)((0u - k) % k) : 0u);
+    for (int32_t sw = 0; sw < sweeps; sw++) {
+        const uint64_t sweep = counter + (uint64_t)sw;
+        sv_stats *st = &stats[sw];
+        memset(st, 0, sizeof(*st));
+        double *dphi_all = dSl; /* scratch: the dphi of every site (used by colour sites only) */
+        for (int64_t s = 0; s < V; s++) {
+            uint32_t c[4] = {(uint32_t)s, (uint32_t)sweep, (uint32_t)(sweep >> 32), 0u};
+            philox4x32_10(c, (uint32_t)key, (uint32_t)(key >> 32));
+            metro[s] = 0.0 + 1.0 * u53_of(c[0], c[1]);
+            dphi_all[s] = -interval_phi + range_phi * u53_of(c[2], c[3]);
+        }
+        for (int mu = 0; mu < 2; mu++)
+            for (int64_t s = 0; s < V; s++)
+                r[mu * V + s] = (0.0 + (phi[fwd2(s, mu, Nt, Nx)] - phi[s])) - TWO_PI * (double)n[mu * V + s];
+        for (int col = 0; col < C.ncol; col++) {
+            const int64_t nc = C.count[col];
+            const int64_t *sites = C.sites[col];
+            for (int64_t s = 0; s < V; s++) cphi[s] = 0.0;
+            for (int64_t l = 0; l < 2 * V; l++) cn[l] = 0;
+            for (int64_t i = 0; i < nc; i++) {
+                const int64_t s = sites[i];
+                cphi[s] = dphi_all[s];
+                uint32_t c[4] = {(uint32_t)s, (uint32_t)sweep, (uint32_t)(sweep >> 32), 1u};
+                philox4x32_10(c, (uint32_t)key, (uint32_t)(key >> 32));
+                for (int mu = 0; mu < 2; mu++) {
+                    uint32_t f = philox_choice((uint32_t)s, sweep, key, c[2 * mu], 2 * mu, k, thr, &st->rejections);
+                    uint32_t b = philox_choice((uint32_t)s, sweep, key, c[2 * mu + 1], 2 * mu + 1, k, thr, &st->rejections);
+                    cn[mu * V + s] = W * ((int64_t)f - interval_n);
+                    cn[mu * V + bwd2(s, mu, Nt, Nx)] = W * ((int64_t)b - interval_n);
+                }
+            }
+            /* from here on exactly villain_sweep's :110-129 */
+            double *dS_l = (double *)malloc(sizeof(double) * 2 * V);
+            for (int mu = 0; mu < 2; mu++)
+                for (int64_t s = 0; s < V; s++) {
+                    double cr = (0.0 + (cphi[fwd2(s, mu, Nt, Nx)] - cphi[s])) - TWO_PI * (double)cn[mu * V + s];
+                    double a = half_kappa * cr;
+                    double b = (2.0 * r[mu * V + s]) + cr;
+                    dS_l[mu * V + s] = a * b;
+                }
+            for (int64_t i = 0; i < nc; i++) {
+                int64_t s = sites[i];
+                double dS = 0.0;
+                dS += dS_l[0 * V + s];
+                dS += dS_l[0 * V + bwd2(s, 0, Nt, Nx)];
+                dS += dS_l[1 * V + s];
+                dS += dS_l[1 * V + bwd2(s, 1, Nt, Nx)];
+                double p = exp(-dS);
+                p = p < 0.0 ? 0.0 : p;
+                p = p > 1.0 ? 1.0 : p;
+                int a = metro[s] < p;
+                acc[s] = a;
+                st->accepted += a;
+                st->acceptance_sum += p;
+            }
+            free(dS_l);
+            for (int64_t i = 0; i < nc; i++) {
+                int64_t s = sites[i];
+                double a = (double)acc[s];
+                cphi[s] = cphi[s] * a;
+                for (int mu = 0; mu < 2; mu++) {
+                    cn[mu * V + s] *= acc[s];
+                    cn[mu * V + bwd2(s, mu, Nt, Nx)] *= acc[s];
+                }
+            }
+            for (int64_t s = 0; s < V; s++) phi[s] = phi[s] + cphi[s];
+            for (int64_t l = 0; l < 2 * V; l++) n[l] = n[l] + cn[l];
+            for (int mu = 0; mu < 2; mu++)
+                for (int64_t s = 0; s < V; s++) {
+                    double dcp = 0.0 + (cphi[fwd2(s, mu, Nt, Nx)] - cphi[s]);
+                    r[mu * V + s] = (r[mu * V + s] + dcp) - TWO_PI * (double)cn[mu * V + s];
+                }
+        }
+        st->proposed = V;
+    }
+    free(metro);
+    colors_free(&C);
+    return 0;
+}
+
 /* Villain action, villain.py:51-66 (sequential sum; the reference uses NumPy pairwise). */
 double sv_o_villain_action(int32_t N, double kappa, const double *phi, const int64_t *n) {
     int64_t V = (int64_t)N * N;

@@ -21,6 +21,11 @@ class SvRng(ctypes.Structure):
     ]
 
 
+class SvPhilox(ctypes.Structure):
+    """sv_philox: the optional counter-based mode's key, sweeps done, and a test-only rejection threshold."""
+    _fields_ = [('key', ctypes.c_uint64), ('counter', ctypes.c_uint64), ('test_threshold', ctypes.c_uint32)]
+
+
 class SvStats(ctypes.Structure):
     _fields_ = [
         ('accepted', ctypes.c_int64),

@@ -6,7 +6,7 @@ import ctypes
 import os
 import threading
 
-from supervillain_amd._abi import SvRng, SvStats
+from supervillain_amd._abi import SvPhilox, SvRng, SvStats
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('SV_LIB_OVERRIDE') or os.path.join(_HERE, 'libsvhip.so')  # override: timing experiments
@@ -49,6 +49,7 @@ def lib():
         L.sv_villain_destroy.argtypes = [vp]
         L.sv_villain_upload.argtypes = [vp, vp, vp]
         L.sv_villain_download.argtypes = [vp, vp, vp]
+        L.sv_villain_run_philox.argtypes = [vp, f64, i64, f64, i64, i32, P(SvPhilox), P(SvStats)]
         L.sv_villain_emit.argtypes = [vp, vp, vp]
         L.sv_villain_emit_wait.argtypes = [vp]
         L.sv_worldline_emit.argtypes = [vp, vp, vp]
@@ -106,7 +107,7 @@ def lib():
 EXPORTED = ('sv_ctx_create', 'sv_ctx_destroy', 'sv_last_error', 'sv_device_count', 'sv_build_info',
             'sv_ctx_set_timing', 'sv_ctx_kernel_time', 'sv_hbm_copy', 'sv_rng_gather', 'sv_rng_scatter',
             'sv_villain_neighborhood', 'sv_villain_create', 'sv_villain_destroy', 'sv_villain_upload',
-            'sv_villain_download', 'sv_villain_run', 'sv_villain_observables', 'sv_villain_emit', 'sv_villain_emit_wait',
+            'sv_villain_download', 'sv_villain_run', 'sv_villain_observables', 'sv_villain_emit', 'sv_villain_emit_wait', 'sv_villain_run_philox',
             'sv_worldline_emit', 'sv_worldline_emit_wait', 'sv_host_register', 'sv_host_unregister',
             'sv_ctx_set_deferred', 'sv_ctx_sync',
             'sv_villain_site_run', 'sv_villain_link_run', 'sv_villain_exact_run', 'sv_villain_cohomology_run', 'sv_worldline_create',

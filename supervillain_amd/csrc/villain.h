@@ -48,6 +48,7 @@ struct FArgs {
     sv_stats *stat;
     DevScratch S;
     uint32_t sweep;
+    uint64_t ph_key = 0, ph_sweep = 0;  // counter-based mode: Philox key, this launch's global sweep number
     // replica batch (periodic mode): consecutive runs of tiles_per_rep workgroups serve one replica
     int32_t tiles_per_rep;          // nsx * nsy
     int32_t rep_blocks;             // descriptors per replica (0: shared)
@@ -101,6 +102,7 @@ void launch_hot(const FArgs &A, int grid, hipStream_t stream);
 // pass hot_ok for every replica: no skips, no buffered half-word, choice values in range)
 bool hot_fr_ok(int32_t N);
 bool hot_params_ok(const VParams &P);  // the parameter part of hot_ok
+void launch_hot_ph(const FArgs &A, int grid, hipStream_t stream);  // counter-based (Philox) mode
 void launch_hot_fr(const FArgs &A, int grid, bool obs, hipStream_t stream);
 // plain single-lattice FArgs defaults (one replica, no observables)
 void farg_single(FArgs &A, int nsx, int nsy);

@@ -1130,6 +1130,85 @@ int sv_villain_run(sv_villain *st, double kappa, int64_t W, double interval_phi,
     }
 }
 
+// The optional counter-based mode (SURVEY.md 8(b) sv_rng mode 1): the same fused sweep with Philox draws by
+// (site, sweep, slot).  Nothing to plan and no NumPy Lemire rejection to replay (a rejected choice word is
+// redrawn in place), so a batch of sweeps is launched back to back with one synchronization at its end.
+int sv_villain_run_philox(sv_villain *st, double kappa, int64_t W, double interval_phi, int64_t interval_n,
+                          int32_t sweeps, sv_philox *rng, sv_stats *stats) {
+    if (!st || !rng || (sweeps > 0 && !stats)) return -1;
+    sv_ctx *ctx = st->ctx;
+    try {
+        if (sweeps < 0) throw std::invalid_argument("sweeps must be >= 0");
+        if (interval_n < 0 || interval_n > (1 << 20)) throw std::invalid_argument("interval_n out of range");
+        const int32_t N = st->N;
+        const int64_t V = (int64_t)N * N;
+        if (!fused_ok(N)) throw std::invalid_argument("the counter-based mode needs an even N >= 4");
+        if (V >= (int64_t(1) << 32)) throw std::invalid_argument("the counter-based mode addresses sites by 32 bits");
+        VParams P = make_params(N, kappa, W, interval_phi, interval_n);
+        if (rng->test_threshold) P.thr = rng->test_threshold;
+        if (P.k < 2 || !hot_params_ok(P))
+            throw std::invalid_argument("the counter-based mode needs interval_n >= 1, |W| <= 2^12 and W (2 interval_n + 1) < 2^28");
+        SV_HIP(hipSetDevice(ctx->device));
+        const int nsx = (N + FW_MAX - 1) / FW_MAX;
+        const int TH = fused_th(N, nsx);
+        const int nsy = (N + TH - 1) / TH;
+        const int grid = nsx * nsy;
+        const int BATCH = 64;
+        for (int sw = 0; sw < sweeps;) {
+            const int count = std::min(BATCH, sweeps - sw);
+            clear_abort(ctx);
+            ctx->ensure_stats(count);
+            SV_HIP(hipMemsetAsync(ctx->d_stats, 0, count * sizeof(sv_stats), ctx->stream));
+            hipEvent_t ev;
+            ctx->time_begin(&ev);
+            for (int k = 0; k < count; k++) {
+                FArgs A;
+                A.P = P;
+                A.G = FGeom{N, N, 0, 0, N, N, N, V, 0};
+                A.phi_in = st->phi[st->cur];
+                A.n_in = st->n[st->cur];
+                A.phi_out = st->phi[st->cur ^ 1];
+                A.n_out = st->n[st->cur ^ 1];
+                A.nsx = nsx;
+                A.TH = TH;
+                A.nsy = nsy;
+                A.blocks = nullptr;
+                A.skips = nullptr;
+                A.T = nullptr;
+                A.stat = ctx->d_stats + k;
+                A.S = scratch(ctx);
+                A.sweep = (uint32_t)k;
+                A.ph_key = rng->key;
+                A.ph_sweep = rng->counter + (uint64_t)(sw + k);
+                farg_single(A, nsx, nsy);
+                launch_hot_ph(A, grid, ctx->stream);
+                st->cur ^= 1;
+            }
+            ctx->time_end(ev, count);
+            SV_HIP(hipGetLastError());
+            AbortInfo a = read_abort_stats(ctx, count, stats + sw);
+            ctx->time_collect();
+            if (a.abort) {
+                // the only report this kernel makes: |n| beyond its int16 image (|n| >= 2^14).  The ping-pong
+                // buffers have been overwritten by the batch, so the fields are unspecified after this error
+                // (re-upload before the next call); the counter is not advanced.
+                throw std::runtime_error("|n| exceeds the counter-based mode's int16 image (|n| < 2^14 required); "
+                                         "fields unspecified, re-upload");
+            }
+            for (int k = 0; k < count; k++) {
+                stats[sw + k].proposed = V;
+                stats[sw + k].rejections = 0;
+            }
+            sw += count;
+        }
+        rng->counter += (uint64_t)sweeps;
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
 int sv_villain_neighborhood(sv_ctx *ctx, int32_t N, double kappa, int64_t W, double interval_phi, int64_t interval_n,
                             double *phi, int64_t *n, int32_t sweeps, sv_rng *rng, sv_stats *stats) {
     sv_villain *st = nullptr;

@@ -26,6 +26,7 @@
 #define SV_EXP_SCOEF 1  // exp coefficients as SGPR operands (18 VGPRs fewer)
 #endif
 #include "fused.h"
+#include "philox.h"
 
 #ifndef SV_HOT_ADV
 #define SV_HOT_ADV 1  // row bases advanced by the precomputed maps behind a wave-uniform test (r3xx A/B)
@@ -117,7 +118,9 @@ struct HotLDS {
 // because a row's first rank N/2 q is even -- unless the replica's choice blocks start on a buffered half-word
 // (after an odd number of NumPy Lemire rejections in its chain): then the pairs would straddle rows and the
 // replica draws unpaired (the EDGE form).  OBS: the inline observables fused into the row stores.
-template <bool TILE, bool EDGE, bool FR = false, bool OBS = false>
+// PH: the optional counter-based mode (SURVEY.md 8(b) sv_rng mode 1): every draw is Philox4x32-10 of (global site,
+// sweep, slot) -- no stream positions, row bases, jump tables or replays
+template <bool TILE, bool EDGE, bool FR = false, bool OBS = false, bool PH = false>
 __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
     static_assert(!(FR && TILE), "full-row replica strips are periodic");
     constexpr int NW = 4;
@@ -179,11 +182,13 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
     const bool two_sets = edge && Nx > SMALL_LDS;   // wrapped columns need the second base set
     const int32_t xw = gx0 - 2 < 0 ? Nx - 2 : 0;
 
-    for (int e = threadIdx.x; e < SMALL_LDS; e += NW * 64) {
-        s_small.A[e] = Tb->small[e].A;
-        s_small.C[e] = Tb->small[e].C;
+    if constexpr (!PH) {
+        for (int e = threadIdx.x; e < SMALL_LDS; e += NW * 64) {
+            s_small.A[e] = Tb->small[e].A;
+            s_small.C[e] = Tb->small[e].C;
+        }
+        if (threadIdx.x < 3) s_adv[threadIdx.x] = FR ? A.advrep[3 * rep + threadIdx.x] : A.adv[threadIdx.x];
     }
-    if (threadIdx.x < 3) s_adv[threadIdx.x] = FR ? A.advrep[3 * rep + threadIdx.x] : A.adv[threadIdx.x];
     if (threadIdx.x == 0) s_bad = 0;
     if (OBS && threadIdx.x < 4) Ls.obs[threadIdx.x] = 0.0;
 
@@ -194,7 +199,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
     for (int c = 0; c < 2; c++) {
 #pragma unroll
         for (int mu = 0; mu < 2; mu++)
-            has_c[c][mu] = (uint32_t)__builtin_amdgcn_readfirstlane(blocks[2 + 5 * c + 2 * mu].has);
+            has_c[c][mu] = PH ? 0u : (uint32_t)__builtin_amdgcn_readfirstlane(blocks[2 + 5 * c + 2 * mu].has);
         if (edge) {
 #pragma unroll
             for (int j = 0; j < 4; j++) buf_c[c][j] = (uint32_t)__builtin_amdgcn_readfirstlane(blocks[2 + 5 * c + j].buf);
@@ -256,15 +261,15 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
 
     // ---- per-wave running row bases: lane 8c+ty holds block ty's base for this wave's colour-c row
     // (at column xb); lanes 16 + 8c + ty the same at column xw (edge strips of rows longer than SMALL_LDS)
-    const bool base_lane = (lane & 7) < 6 && (lane < 16 || (two_sets && lane < 32));
+    const bool base_lane = !PH && (lane & 7) < 6 && (lane < 16 || (two_sets && lane < 32));
     const int bc = (lane >> 3) & 1, bty = lane & 7;
     const int32_t bx = lane >= 16 ? xw : xb;
     const int bblk = bty == 0 ? 0 : 1 + 5 * bc + bty - 1;
-    const uint32_t bhas = (base_lane && bty >= 2) ? blocks[bblk].has : 0u;
+    const uint32_t bhas = (!PH && base_lane && bty >= 2) ? blocks[bblk].has : 0u;
     const int32_t tfirst = t0 - 3;
     int32_t brow = tfirst + 2 - bc + wave;  // colour 0 row t+2+wave, colour 1 row t+1+wave
     int32_t brow1 = tfirst + 1 + wave;      // the colour-1 row, wave-uniform
-    {  // (the running bases live in LDS only: the advance reads them back, no registers held across the loop)
+    if constexpr (!PH) {  // (the running bases live in LDS only: the advance reads them back)
         u128 bases{0, 0};
         if (base_lane) bases = full_jump(Tb, &blocks[bblk], (uint32_t)base_pos(bty, grow(brow), Nx, bx, bhas));
         __builtin_amdgcn_s_waitcnt(0);
@@ -273,7 +278,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
 
     // paired-draw lane constants per colour (interior strips; valid for every row of this wave)
     uint32_t pk0 = 0, pk1 = 0;
-    if constexpr (!edge) {
+    if constexpr (!edge && !PH) {
         {
             const int32_t q = tfirst + 2 + wave;
             const int32_t xs = FR ? ((par0 + q) & 1) : (x0 - 1) + ((par0 + q + x0 - 1) & 1);
@@ -341,7 +346,26 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
     // draws of colour c for global row gq, local column x; the 4 choice values; a rejected word is reported
     auto draw = [&](int c, int32_t q, int32_t x, bool active, HotDraws &D, int32_t cn[4]) {
         const int32_t gq = grow(q);
-        if constexpr (!edge) {
+        if constexpr (PH) {
+            // site s of sweep `ph_sweep`: call (s, sweep, 0) -> u, dphi; call (s, sweep, 1) -> the four choice words; a
+            // word Lemire rejects is replaced in place by word 0 of call (s, sweep, 2 + j + 4 t) (sv_oracle.c, philox)
+            const uint32_t site = (uint32_t)gq * (uint32_t)Nx + (uint32_t)wrapN(Gm.X0 + x, Nx);
+            const uint32_t s0 = (uint32_t)A.ph_sweep, s1 = (uint32_t)(A.ph_sweep >> 32);
+            const uint32_t k0 = (uint32_t)A.ph_key, k1 = (uint32_t)(A.ph_key >> 32);
+            const P4 a = philox4x32_10(P4{{site, s0, s1, 0u}}, k0, k1);
+            const P4 b = philox4x32_10(P4{{site, s0, s1, 1u}}, k0, k1);
+            D.u = u53(((uint64_t)a.v[1] << 32) | a.v[0]);
+            D.dphi = A.P.lo_phi + A.P.range_phi * u53(((uint64_t)a.v[3] << 32) | a.v[2]);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                uint64_t m = (uint64_t)b.v[j] * kc;
+                for (uint32_t t = 0; __builtin_expect((uint32_t)m < thr, 0) && t < 64; t++)
+                    m = (uint64_t)philox4x32_10(P4{{site, s0, s1, 2u + (uint32_t)j + 4u * t}}, k0, k1).v[0] * kc;
+                cn[j] = (int32_t)(m >> 32) * Wn - nW;
+            }
+            (void)active;
+            return;
+        } else if constexpr (!edge) {
             u128 bs[6];
 #pragma unroll
             for (int k = 0; k < 6; k++) bs[k] = s_base[wave][8 * c + k];
@@ -493,7 +517,9 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
         // wave-uniform test keeps the position arithmetic (64-bit, on every lane) off the common path.
         const int32_t glo = grow(brow1);
         brow1 += NW;
-        if (SV_HOT_ADV && glo >= 1 && glo + NW + 1 < Nt) {
+        if (PH) {
+            // no row bases
+        } else if (SV_HOT_ADV && glo >= 1 && glo + NW + 1 < Nt) {
             if (base_lane) {
                 const int ai = bty == 0 ? 0 : (bty == 1 ? 1 : 2);
                 s_base[wave][lane] = mad128c(s_adv[ai].A, s_base[wave][lane], s_adv[ai].C);
@@ -570,6 +596,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4
 template __global__ void villain_sweep_hot_fr<false>(FArgs);
 template __global__ void villain_sweep_hot_fr<true>(FArgs);
 
+// the counter-based mode on a periodic single lattice (every strip draws the same way)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4 ? 4 : 3))) void villain_sweep_hot_ph(FArgs A) {
+    __shared__ HotLDS Ls;
+    hot_body<false, false, false, false, true>(A, Ls);
+}
+
 }  // namespace sv
 
 namespace svh {
@@ -600,6 +632,8 @@ void launch_hot_fr(const FArgs &A, int grid, bool obs, hipStream_t stream) {
     if (obs) villain_sweep_hot_fr<true><<<grid, 4 * 64, 0, stream>>>(A);
     else villain_sweep_hot_fr<false><<<grid, 4 * 64, 0, stream>>>(A);
 }
+
+void launch_hot_ph(const FArgs &A, int grid, hipStream_t stream) { villain_sweep_hot_ph<<<grid, 4 * 64, 0, stream>>>(A); }
 
 void launch_hot(const FArgs &A, int grid, hipStream_t stream) {
     if (A.G.org == 0 && A.G.pitch == A.G.Nx && A.G.T0 == 0 && A.G.X0 == 0 && A.G.Ht == A.G.Nt && A.G.Wt == A.G.Nx)

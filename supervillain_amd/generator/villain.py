@@ -28,11 +28,15 @@ class NeighborhoodUpdate(DeviceState, Generator):
       inline: also return ActionDensity, InternalEnergyDensity, WindingSquared and TorusWrapping of
               each new configuration, reduced on the device (measured inline, observable.py:50-54).
       path:   0 auto (fused sweep kernel for even N), 1 per-colour kernels, 2 fused only.
+      philox: an integer seed selects the optional counter-based mode (SURVEY.md 8(b) sv_rng mode 1): every draw
+              comes from Philox4x32-10 by (site, sweep, slot) under that key instead of from `rng` -- a different,
+              statistically equivalent chain with no NumPy-rejection replays (sv_villain_run_philox).  The sweep
+              counter is `philox_counter`.
     '''
 
     INLINE = ('ActionDensity', 'InternalEnergyDensity', 'WindingSquared', 'TorusWrapping')
 
-    def __init__(self, action, interval_phi=np.pi, interval_n=1, *, device=None, inline=False, path=0):
+    def __init__(self, action, interval_phi=np.pi, interval_n=1, *, device=None, inline=False, path=0, philox=None):
         if not _is_villain(action):
             raise ValueError('The Neighborhood Metropolis update requires the Villain action.')
         self.Action = action
@@ -49,6 +53,8 @@ class NeighborhoodUpdate(DeviceState, Generator):
         self.device = device
         self.inline = inline
         self.path = path
+        self.philox = philox
+        self.philox_counter = 0
 
     def __str__(self):
         return 'NeighborhoodUpdate'
@@ -85,11 +91,19 @@ class NeighborhoodUpdate(DeviceState, Generator):
         neighborhood.py:131-135 and returns the inline observables of the new state (or None)."""
         L = _native.lib()
         st = _native.stats_array(sweeps)
-        r = rng_from_numpy(self.rng)
-        ctx.check(L.sv_villain_run(h, float(self.kappa), int(self.Action.W), float(self.interval_phi),
-                                   int(self.interval_n), sweeps, ctypes.byref(r), st, int(self.path)),
-                  'sv_villain_run')
-        rng_to_numpy(r, self.rng)
+        if self.__dict__.get('philox') is not None:
+            from supervillain_amd._abi import SvPhilox
+            ph = SvPhilox(int(self.philox) & ((1 << 64) - 1), int(self.philox_counter), 0)
+            ctx.check(L.sv_villain_run_philox(h, float(self.kappa), int(self.Action.W), float(self.interval_phi),
+                                              int(self.interval_n), sweeps, ctypes.byref(ph), st),
+                      'sv_villain_run_philox')
+            self.philox_counter = int(ph.counter)
+        else:
+            r = rng_from_numpy(self.rng)
+            ctx.check(L.sv_villain_run(h, float(self.kappa), int(self.Action.W), float(self.interval_phi),
+                                       int(self.interval_n), sweeps, ctypes.byref(r), st, int(self.path)),
+                      'sv_villain_run')
+            rng_to_numpy(r, self.rng)
         V = self.Lattice.sites
 
         def fold():
