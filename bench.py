@@ -260,12 +260,13 @@ def run_replicas(args, world, rank, dist):
     if rank == 0:
         config = {'workload': f'{Rt} independent L={L} Villain NeighborhoodUpdate replica chains (W={args.W}), '
                               'inline ActionDensity/InternalEnergyDensity/WindingSquared/TorusWrapping, '
-                              f'{per} replicas per GPU, one launch per sweep for all of them',
+                              f'{per} replicas per GPU, one full-row villain_sweep_hot_fr launch per sweep for all of them (two when a '
+                              'known NumPy Lemire rejection splits off the replicas that replay it)',
                   'L': L, 'replicas': Rt, 'replicas_per_gpu': per, 'path': 'replicas',
                   'parallelism': f'{world} GPU(s), replicas sharded, no collectives'}
         report(args, world, Rt * L * L, per * L * L, elapsed, acc, launches_s, config, L,
                metric=f'replica-site updates/sec, {Rt} x L={L} Villain replicas, W={args.W}, inline observables',
-               unit='replica-site updates/s', kernel='villain_sweep_fused_obs', baseline=baseline, ctx=B.ctx,
+               unit='replica-site updates/s', kernel='villain_sweep_hot_fr (obs)', baseline=baseline, ctx=B.ctx,
                scaling='strong')
     B.close()
 
