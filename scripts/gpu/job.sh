@@ -1,10 +1,8 @@
 source scripts/gpu/guard.sh
-T=${1:-r331}
+T=${1:-r336}
 O=gpurun_out/$T
 mkdir -p $O
 export TMPDIR=/tmp
-step brep timeout -k 10 300 python bench.py --workload replicas > $O/b_replicas.log 2>&1
-grep '^{' $O/b_replicas.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('rep', round(d['value']/1e9,2), d['ms_per_step'], round(d['roofline']['avg_launch_us'],2), round(d['roofline']['frac'],3))"
-step prep timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_rep -o rep -- python bench.py --workload replicas --no-cpu-baseline --no-copy-ceiling > $O/prof_rep.log 2>&1
-step pph timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_ph -o ph -- python bench.py --rng philox --no-cpu-baseline --no-copy-ceiling > $O/prof_ph.log 2>&1
-find $O -name '*kernel_stats.csv'
+step tests timeout -k 10 600 python -u -m pytest tests/test_gpu_philox.py tests/test_gpu_replicas.py tests/test_gpu_pipeline.py -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1
+tail -3 $O/tests.log
+REPS="1 2" bash scripts/gpu/job_ab.sh $T "p4 p5 p6" --rng philox

@@ -153,6 +153,16 @@ void advance_closed(Cursor &c, u128 inc, const Affine &unit) {
     c.buf = (uint32_t)(xsl_rr(c.s) >> 32);
 }
 
+// One batch of sweeps in flight: what its enqueue planned and where its outcome lands.
+struct RepBatch {
+    int sw = 0, count = 0, cur0 = 0, slot = 0;
+    std::vector<char> hosted;          // replicas planned on the host (known skips in the batch)
+    std::vector<Cursor> end_host;      // their cursors after the whole batch
+    std::vector<std::vector<Block>> hb;  // host-planned descriptors, alive until the batch's stream sync
+    std::vector<uint32_t> hskip;
+    std::vector<int32_t> hmap;
+};
+
 void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs, sv_stats *stats, double *obs) {
     sv_ctx *ctx = b->ctx;
     const int R = b->R;
@@ -173,59 +183,73 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
     const int TH = getenv("SV_FUSED_TH") ? fused_th(b->N, nsx) : ((int64_t)R * nsx * ((b->N + 63) / 64) < 768 ? 32 : 64);
     const int nsy = (b->N + TH - 1) / TH;
     const int tiles = nsx * nsy;
-    std::vector<PlanIn> pin(R);
-    std::vector<std::vector<Block>> hb;  // host-planned descriptors, alive until the batch's stream sync
-    std::vector<uint32_t> hskip, sk;
-    int sw = 0;
+    const bool fr_hot = hot_fr_ok(b->N) && nsx == 1 && hot_params_ok(P);
+    // pinned batch tails, two slots: batch k+1 is enqueued before batch k's statistics are copied out
+    const size_t slot_bytes = 64 + (size_t)R * REP_BATCH * (sizeof(sv_stats) + 4 * sizeof(double));
+    if (b->tail_cap < 2 * slot_bytes) {
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+        if (b->h_tail) SV_HIP(hipHostFree(b->h_tail));
+        b->h_tail = nullptr;
+        b->tail_cap = 0;
+        SV_HIP(hipHostMalloc((void **)&b->h_tail, 2 * slot_bytes, hipHostMallocDefault));
+        b->tail_cap = 2 * slot_bytes;
+    }
+    if (!b->d_map) SV_HIP(hipMalloc(&b->d_map, (size_t)R * REP_BATCH * sizeof(int32_t)));
     const bool dbg = getenv("SV_DEBUG_TIMING") != nullptr;
     using clk = std::chrono::steady_clock;
     auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-    while (sw < sweeps) {
-        const int count = std::min(REP_BATCH, sweeps - sw);
-        const auto t_a = clk::now();
-        // --- plan: device closed form for every replica, host planner for replicas with skips
+    std::vector<PlanIn> pin(R);
+    std::vector<uint32_t> sk;
+
+    // --- enqueue the batch [sw, sw + count) from the cursors `cur`: plan (device closed form for every replica,
+    // host planner for replicas with known skips), the sweeps, and the tail copies into pinned slot `slot`
+    auto enqueue = [&](RepBatch &B, int sw, int count, int slot) {
+        B.sw = sw;
+        B.count = count;
+        B.slot = slot;
+        B.cur0 = b->cur;
         for (int r = 0; r < R; r++) pin[r] = PlanIn{cur[r].s.lo, cur[r].s.hi, cur[r].has, cur[r].buf};
         SV_HIP(hipMemcpyAsync(b->d_plan, pin.data(), R * sizeof(PlanIn), hipMemcpyHostToDevice, ctx->stream));
         const int64_t nplan = (int64_t)R * count * NB;
         plan_replicas<<<(unsigned)((nplan + 255) / 256), 256, 0, ctx->stream>>>(b->d_plan, b->d_Trep, b->d_blocks, R,
                                                                                   count, (uint64_t)V);
-        hskip.clear();
-        hb.clear();
-        std::vector<Cursor> end_host(R);
-        std::vector<char> hosted(R, 0);
+        B.hskip.clear();
+        B.hb.clear();
+        B.hmap.clear();
+        B.end_host.assign(R, Cursor{});
+        B.hosted.assign(R, 0);
         for (int r = 0; r < R; r++) {
             if (!has_skips(skips[r], sw, count)) continue;
-            hosted[r] = 1;
+            B.hosted[r] = 1;
             Cursor c = cur[r];
-            hb.emplace_back();
-            std::vector<Block> &blk = hb.back();
+            B.hb.emplace_back();
+            std::vector<Block> &blk = B.hb.back();
             plan_sweeps(ctx, c, inc[r], specs, sw, count, skips[r], blk, sk);
-            for (Block &x : blk) x.skip0 += (int32_t)hskip.size();
-            hskip.insert(hskip.end(), sk.begin(), sk.end());
-            end_host[r] = c;
+            for (Block &x : blk) x.skip0 += (int32_t)B.hskip.size();
+            B.hskip.insert(B.hskip.end(), sk.begin(), sk.end());
+            B.end_host[r] = c;
             SV_HIP(hipMemcpyAsync(b->d_blocks + (size_t)r * count * NB, blk.data(), blk.size() * sizeof(Block),
                                   hipMemcpyHostToDevice, ctx->stream));
         }
-        ctx->ensure_skips(hskip.size() + 1);
-        if (!hskip.empty())
-            SV_HIP(hipMemcpyAsync(ctx->d_skips, hskip.data(), hskip.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+        ctx->ensure_skips(B.hskip.size() + 1);
+        if (!B.hskip.empty())
+            SV_HIP(hipMemcpyAsync(ctx->d_skips, B.hskip.data(), B.hskip.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
                                   ctx->stream));
         SV_HIP(hipMemsetAsync(ctx->d_abort, 0, sizeof(int32_t), ctx->stream));
         SV_HIP(hipMemsetAsync(ctx->d_nreport, 0, sizeof(uint32_t), ctx->stream));
         SV_HIP(hipMemsetAsync(b->d_stats, 0, (size_t)R * count * sizeof(sv_stats), ctx->stream));
         if (obs) SV_HIP(hipMemsetAsync(b->d_obs, 0, (size_t)R * count * 4 * sizeof(double), ctx->stream));
-        // --- sweeps.  A sweep runs on the fast-draw kernel (villain_sweep_hot_fr) when no replica's choice blocks
-        // of that sweep carry a skip (the closed-form replicas have none; the host-planned ones are checked), else
-        // on the general fused kernel.  Within a skip-free sweep a replica's four choice blocks start on the same
-        // half-word parity (they draw V/2, an even count), which is all the fast kernel's two draw forms need.
-        const bool fr_hot = hot_fr_ok(b->N) && nsx == 1 && hot_params_ok(P);
+        // A sweep runs on the fast-draw kernel (villain_sweep_hot_fr) when no replica's choice blocks of that sweep
+        // carry a skip (the closed-form replicas have none; the host-planned ones are checked), else on the general
+        // fused kernel.  Within a skip-free sweep a replica's four choice blocks start on the same half-word parity
+        // (they draw V/2, an even count), which is all the fast kernel's two draw forms need.
         std::vector<char> hot_k(count, fr_hot);
         std::vector<std::vector<int32_t>> skipped(count);  // per sweep: replicas whose choice blocks carry skips
         if (fr_hot) {
             size_t hi = 0;
             for (int r = 0; r < R; r++) {
-                if (!hosted[r]) continue;
-                const std::vector<Block> &blk = hb[hi++];
+                if (!B.hosted[r]) continue;
+                const std::vector<Block> &blk = B.hb[hi++];
                 for (int k = 0; k < count; k++) {
                     bool sk_k = false;
                     for (int bi = 2; bi < NB; bi++) sk_k |= bi != 6 && blk[(size_t)k * NB + bi].nskip != 0;
@@ -238,31 +262,26 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         }
         // a sweep with skips in a few replicas runs as two launches over replica maps: the fast kernel for the
         // others, the general kernel for those (so a NumPy Lemire rejection slows one replica's replay, not all)
-        std::vector<int32_t> hmap;
         std::vector<std::array<int64_t, 4>> split(count, {0, 0, 0, 0});  // hot offset, hot count, general offset, count
         for (int k = 0; k < count; k++) {
             if (!fr_hot || hot_k[k]) continue;
-            split[k][0] = (int64_t)hmap.size();
+            split[k][0] = (int64_t)B.hmap.size();
             size_t j = 0;
             for (int r = 0; r < R; r++) {
                 if (j < skipped[k].size() && skipped[k][j] == r) {
                     j++;
                     continue;
                 }
-                hmap.push_back(r);
+                B.hmap.push_back(r);
             }
-            split[k][1] = (int64_t)hmap.size() - split[k][0];
-            split[k][2] = (int64_t)hmap.size();
-            hmap.insert(hmap.end(), skipped[k].begin(), skipped[k].end());
+            split[k][1] = (int64_t)B.hmap.size() - split[k][0];
+            split[k][2] = (int64_t)B.hmap.size();
+            B.hmap.insert(B.hmap.end(), skipped[k].begin(), skipped[k].end());
             split[k][3] = (int64_t)skipped[k].size();
         }
-        if (!hmap.empty()) {
-            if (!b->d_map) SV_HIP(hipMalloc(&b->d_map, (size_t)R * REP_BATCH * sizeof(int32_t)));
-            SV_HIP(hipMemcpyAsync(b->d_map, hmap.data(), hmap.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+        if (!B.hmap.empty())
+            SV_HIP(hipMemcpyAsync(b->d_map, B.hmap.data(), B.hmap.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                                   ctx->stream));
-        }
-        const auto t_b = clk::now();
-        const int cur0 = b->cur;
         hipEvent_t ev;
         ctx->time_begin(&ev);
         for (int k = 0; k < count; k++) {
@@ -310,79 +329,110 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         }
         ctx->time_end(ev, count);
         SV_HIP(hipGetLastError());
-        // --- outcome: abort flag, report count, statistics and observables land in one pinned block
-        const size_t st_bytes = (size_t)R * count * sizeof(sv_stats), ob_bytes = obs ? (size_t)R * count * 4 * sizeof(double) : 0;
-        if (64 + st_bytes + ob_bytes > b->tail_cap) {
-            SV_HIP(hipStreamSynchronize(ctx->stream));
-            if (b->h_tail) SV_HIP(hipHostFree(b->h_tail));
-            b->tail_cap = 64 + (size_t)R * REP_BATCH * (sizeof(sv_stats) + 4 * sizeof(double));
-            SV_HIP(hipHostMalloc((void **)&b->h_tail, b->tail_cap, hipHostMallocDefault));
+        // outcome: abort flag, report count, statistics and observables land in the pinned slot
+        char *tail = b->h_tail + slot * slot_bytes;
+        const size_t st_bytes = (size_t)R * count * sizeof(sv_stats);
+        SV_HIP(hipMemcpyAsync(tail, ctx->d_abort, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipMemcpyAsync(tail + 4, ctx->d_nreport, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipMemcpyAsync(tail + 64, b->d_stats, st_bytes, hipMemcpyDeviceToHost, ctx->stream));
+        if (obs)
+            SV_HIP(hipMemcpyAsync(tail + 64 + st_bytes, b->d_obs, (size_t)R * count * 4 * sizeof(double),
+                                  hipMemcpyDeviceToHost, ctx->stream));
+    };
+    // --- keep sweeps [B.sw, B.sw + good) of a finished batch: statistics and observables into the caller's arrays
+    auto keep = [&](const RepBatch &B, int good) {
+        const char *tail = b->h_tail + B.slot * slot_bytes;
+        const sv_stats *h_st = (const sv_stats *)(tail + 64);
+        const double *h_ob = (const double *)(tail + 64 + (size_t)R * B.count * sizeof(sv_stats));
+        for (int r = 0; r < R; r++) {
+            const bool none = skips[r].empty();
+            sv_stats *dst = stats + (size_t)r * sweeps + B.sw;
+            const sv_stats *src = h_st + (size_t)r * B.count;
+            for (int k = 0; k < good; k++) {
+                dst[k] = src[k];
+                dst[k].proposed = V;
+                dst[k].rejections = none ? 0 : rejections_in(skips[r], B.sw + k, NB);
+            }
+            if (obs)
+                std::memcpy(obs + ((size_t)r * sweeps + B.sw) * 4, h_ob + (size_t)r * B.count * 4,
+                            (size_t)good * 4 * sizeof(double));
         }
-        sv_stats *h_st = (sv_stats *)(b->h_tail + 64);
-        double *h_ob = (double *)(b->h_tail + 64 + st_bytes);
-        SV_HIP(hipMemcpyAsync(b->h_tail, ctx->d_abort, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
-        SV_HIP(hipMemcpyAsync(b->h_tail + 4, ctx->d_nreport, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-        SV_HIP(hipMemcpyAsync(h_st, b->d_stats, st_bytes, hipMemcpyDeviceToHost, ctx->stream));
-        if (obs) SV_HIP(hipMemcpyAsync(h_ob, b->d_obs, ob_bytes, hipMemcpyDeviceToHost, ctx->stream));
-        const auto t_c = clk::now();
+    };
+
+    RepBatch batch[2];
+    int cb = 0;  // batch[cb] is in flight
+    int sw = 0;
+    if (sweeps > 0) enqueue(batch[cb], 0, std::min(REP_BATCH, sweeps), 0);
+    while (sw < sweeps) {
+        RepBatch &B = batch[cb];
+        const auto t_a = clk::now();
         SV_HIP(hipStreamSynchronize(ctx->stream));
-        const auto t_d = clk::now();
-        const int32_t ab = *(int32_t *)b->h_tail;
-        uint32_t nrep = *(uint32_t *)(b->h_tail + 4);
-        int good = count;
+        const auto t_b = clk::now();
+        const char *tail = b->h_tail + B.slot * slot_bytes;
+        const int32_t ab = *(const int32_t *)tail;
         if (ab) {
+            // a NumPy Lemire rejection (or |n| overflow): keep the sweeps before the failing one, absorb the
+            // rejected positions into the failing replicas' skip lists, replay from there
             ctx->time_discard();
-            nrep = std::min<uint32_t>(nrep, MAX_REPORTS);
+            uint32_t nrep = std::min<uint32_t>(*(const uint32_t *)(tail + 4), MAX_REPORTS);
             std::vector<Report> reps(nrep);
-            if (nrep)
-                SV_HIP(hipMemcpy(reps.data(), ctx->d_reports, nrep * sizeof(Report), hipMemcpyDeviceToHost));
+            if (nrep) SV_HIP(hipMemcpy(reps.data(), ctx->d_reports, nrep * sizeof(Report), hipMemcpyDeviceToHost));
             if (reps.empty()) throw std::runtime_error("device aborted without a rejection report");
             uint32_t bad = ~0u;
             for (const Report &x : reps) {
                 if (x.block == OVERFLOW_BLOCK) throw std::runtime_error("|n| exceeds the fused path's int32 LDS image");
                 bad = std::min(bad, x.sweep);
             }
-            // each replica that failed in sweep `bad`: absorb its earliest block's rejected positions
             for (int r = 0; r < R; r++) {
                 AbortInfo a{1, {}};
                 for (const Report &x : reps)
                     if ((int)x.pad == r && x.sweep == bad) a.reports.push_back(x);
-                if (!a.reports.empty()) absorb_reports(a, sw, skips[r]);
+                if (!a.reports.empty()) absorb_reports(a, B.sw, skips[r]);
             }
-            good = (int)bad;
+            const int good = (int)bad;
+            const Affine unit = good > 0 ? host_power(u128{1, 0}, (uint64_t)good * 4 * V) : Affine{};
+            for (int r = 0; r < R; r++) {
+                if (has_skips(skips[r], B.sw, good)) {
+                    Cursor c = cur[r];
+                    std::vector<Block> blk;
+                    plan_sweeps(ctx, c, inc[r], specs, B.sw, good, skips[r], blk, sk);
+                    cur[r] = c;
+                } else if (good > 0) {
+                    advance_closed(cur[r], inc[r], unit);
+                }
+            }
+            b->cur = B.cur0 ^ (good & 1);
+            sw = B.sw + good;
+            const auto t_c = clk::now();
+            // the replay goes out first (into the other slot), the kept sweeps are copied out while it runs
+            if (sw < sweeps) enqueue(batch[cb ^ 1], sw, std::min(REP_BATCH, sweeps - sw), B.slot ^ 1);
+            const auto t_d = clk::now();
+            keep(B, good);
+            if (dbg)
+                fprintf(stderr, "[sv replicas] wait %.1f us, abort at %d/%d, replan %.1f us, enqueue %.1f us, keep %.1f us\n",
+                        us(t_a, t_b), good, B.count, us(t_b, t_c), us(t_c, t_d), us(t_d, clk::now()));
+            cb ^= 1;
+            continue;
         }
         ctx->time_collect();
-        // --- keep sweeps [sw, sw + good): stats, observables, cursors
-        if (good > 0) {
-            for (int r = 0; r < R; r++)
-                for (int k = 0; k < good; k++) {
-                    sv_stats s = h_st[(size_t)r * count + k];
-                    s.proposed = V;
-                    s.rejections = skips[r].empty() ? 0 : rejections_in(skips[r], sw + k, NB);
-                    stats[(size_t)r * sweeps + sw + k] = s;
-                    if (obs)
-                        std::memcpy(obs + ((size_t)r * sweeps + sw + k) * 4, &h_ob[((size_t)r * count + k) * 4],
-                                    4 * sizeof(double));
-                }
-        }
-        const Affine unit = good > 0 ? host_power(u128{1, 0}, (uint64_t)good * 4 * V) : Affine{};
+        // clean batch: advance the cursors past it, enqueue the next batch, and copy this one's statistics out
+        // while the next one runs
+        const Affine unit = host_power(u128{1, 0}, (uint64_t)B.count * 4 * V);
         for (int r = 0; r < R; r++) {
-            if (good == count && hosted[r]) {
-                cur[r] = end_host[r];
-            } else if (has_skips(skips[r], sw, good)) {
-                Cursor c = cur[r];
-                std::vector<Block> blk;
-                plan_sweeps(ctx, c, inc[r], specs, sw, good, skips[r], blk, sk);
-                cur[r] = c;
-            } else if (good > 0) {
+            if (B.hosted[r])
+                cur[r] = B.end_host[r];
+            else
                 advance_closed(cur[r], inc[r], unit);
-            }
         }
-        b->cur = cur0 ^ (good & 1);
-        sw += good;
+        sw = B.sw + B.count;
+        const auto t_c = clk::now();
+        if (sw < sweeps) enqueue(batch[cb ^ 1], sw, std::min(REP_BATCH, sweeps - sw), B.slot ^ 1);
+        const auto t_d = clk::now();
+        keep(B, B.count);
         if (dbg)
-            fprintf(stderr, "[sv replicas] plan %.1f us, launch %.1f us, wait %.1f us, post %.1f us, good %d/%d\n",
-                    us(t_a, t_b), us(t_b, t_c), us(t_c, t_d), us(t_d, clk::now()), good, count);
+            fprintf(stderr, "[sv replicas] wait %.1f us, advance %.1f us, enqueue next %.1f us, keep %.1f us, %d sweeps\n",
+                    us(t_a, t_b), us(t_b, t_c), us(t_c, t_d), us(t_d, clk::now()), B.count);
+        cb ^= 1;
     }
     for (int r = 0; r < R; r++) {
         rngs[r].state_hi = cur[r].s.hi;

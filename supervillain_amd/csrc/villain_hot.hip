@@ -31,6 +31,9 @@
 #ifndef SV_HOT_ADV
 #define SV_HOT_ADV 1  // row bases advanced by the precomputed maps behind a wave-uniform test (r3xx A/B)
 #endif
+#ifndef SV_HOT_PH_OCC
+#define SV_HOT_PH_OCC 4  // the counter-based kernel (29.5 KB of LDS, 81 VGPRs): 4, 5 and 6 waves/SIMD measured flat (r336)
+#endif
 
 namespace sv {
 
@@ -92,7 +95,11 @@ __device__ __forceinline__ HotDraws hot_draws_edge(const FArgs &A, int64_t gq, i
 }
 
 // The workgroup's LDS (one allocation shared by the two bodies below)
-struct HotLDS {
+struct HotEmpty {};
+// PH (counter-based mode) keeps no small-offset maps, row-advance maps or row bases: its LDS is 6 KB smaller, which
+// lets a fifth workgroup onto a CU
+template <bool PH>
+struct HotLDST {
     static constexpr int R = FusedGeom<4>::R;
     // the residuals r live from the colour-0 pass of step t (rows t+1..t+5) to the colour-1 pass of step t+4
     // (which reads row t+4 again): NW + 2 rows
@@ -103,12 +110,13 @@ struct HotLDS {
     double r1[RR][RW];
     nint n0[R][RW];
     nint n1[R][RW];
-    SmallTab small;
-    Affine adv[3];
-    u128 base[4][32];  // per wave: [8c + ty] block ty's base for the colour-c row at xb; [16 + ..] at xw
+    std::conditional_t<PH, HotEmpty, SmallTab> small;
+    std::conditional_t<PH, HotEmpty, Affine[3]> adv;
+    std::conditional_t<PH, HotEmpty, u128[4][32]> base;  // per wave: [8c + ty] block ty's base for the colour-c row at xb; [16 + ..] at xw
     int32_t bad;
     double obs[4];     // OBS: the workgroup's sums of the inline observables
 };
+using HotLDS = HotLDST<false>;
 
 // EDGE: the strip's region wraps around the lattice rows (or sits within 4 columns of an edge); a
 // template parameter so that the two draw forms are two code paths, not one if-converted stream.
@@ -119,9 +127,9 @@ struct HotLDS {
 // (after an odd number of NumPy Lemire rejections in its chain): then the pairs would straddle rows and the
 // replica draws unpaired (the EDGE form).  OBS: the inline observables fused into the row stores.
 // PH: the optional counter-based mode (SURVEY.md 8(b) sv_rng mode 1): every draw is Philox4x32-10 of (global site,
-// sweep, slot) -- no stream positions, row bases, jump tables or replays (DESIGN.md 5.8)
+// sweep, slot) -- no stream positions, row bases, jump tables or replays (DESIGN.md 5.7)
 template <bool TILE, bool EDGE, bool FR = false, bool OBS = false, bool PH = false>
-__device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
+__device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH> &Ls) {
     static_assert(!(FR && TILE), "full-row replica strips are periodic");
     constexpr int NW = 4;
     constexpr int R = HotLDS::R, RR = HotLDS::RR;
@@ -517,7 +525,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDS &Ls) {
         // wave-uniform test keeps the position arithmetic (64-bit, on every lane) off the common path.
         const int32_t glo = grow(brow1);
         brow1 += NW;
-        if (PH) {
+        if constexpr (PH) {
             // no row bases
         } else if (SV_HOT_ADV && glo >= 1 && glo + NW + 1 < Nt) {
             if (base_lane) {
@@ -597,8 +605,8 @@ template __global__ void villain_sweep_hot_fr<false>(FArgs);
 template __global__ void villain_sweep_hot_fr<true>(FArgs);
 
 // the counter-based mode on a periodic single lattice (every strip draws the same way)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4 ? 4 : 3))) void villain_sweep_hot_ph(FArgs A) {
-    __shared__ HotLDS Ls;
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_PH_OCC))) void villain_sweep_hot_ph(FArgs A) {
+    __shared__ HotLDST<true> Ls;
     hot_body<false, false, false, false, true>(A, Ls);
 }
 
