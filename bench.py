@@ -566,7 +566,7 @@ def run_local(args, world, rank, dist):
 def run_domain(args, world, rank, local, dist):
     """N > 1 (or --tiles on one GPU): BASELINE config 4, one lattice domain-decomposed, RCCL halos."""
     from supervillain_amd import _native
-    from supervillain_amd.domain import VillainDomain, tile_grid
+    from supervillain_amd.domain import VillainDomain, ghost_frame, tile_grid
     L = args.L
     if args.tiles:
         ty, tx = (int(v) for v in args.tiles.lower().split('x'))
@@ -615,6 +615,8 @@ def run_domain(args, world, rank, local, dist):
                               f'domain-decomposed into {ty}x{tx} tiles of {Ht}x{Wt} (one per GPU), RCCL halo '
                               'exchange, bit-exact reference chain (PCG64 replay)',
                   'L': L, 'lattice': [Nt, Nx], 'tiles': [ty, tx], 'path': 'domain',
+                  # deep halos: K sweeps per halo exchange, ghost frame 2K / 3K deep
+                  'sweeps_per_halo_exchange': ghost_frame(Nt, Nx, (ty, tx))[0] // 2,
                   'parallelism': f'{ty}x{tx} domain decomposition over {world} GPU(s)',
                   'weak_scaling': {'tile': [Ht, Wt], 'R1': r1_mean,
                                    'E_N': value / (world * r1_mean),

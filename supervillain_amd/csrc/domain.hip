@@ -185,6 +185,7 @@ struct sv_domain {
     int nranks = 1, rank = 0;
     int64_t pitch = 0, plane = 0, org = 0;
     int R = 2, cur = 0;
+    int depth = 1;                  // Villain: sweeps per halo exchange (deep halos, see villain_depth)
     HaloTable H{};
     int64_t msg_words = 0;
     std::vector<sv_domain_tile> tiles;  // local tiles (all tiles when nranks == 1)
@@ -215,12 +216,37 @@ int tile_index(const sv_domain *d, int iy, int ix) {
     return iy * d->tx + ix;
 }
 
+// Deep halos (Villain).  One sweep reads a 2/3/2/3 ring around the sites it decides, so K sweeps can run between two
+// halo exchanges when the ghost frame is K times as deep (2K above, 3K below, 2K left, 3K right) and sweep j of a
+// group of K decides the tile extended by 2(K-1-j) rows / columns above and left and 3(K-1-j) below and right: each
+// sweep recomputes, bit for bit, the ring its successor reads (every draw is addressed by its global stream
+// position), counts only the tile's own sites, and the group's last sweep decides exactly the tile.  The
+// redundant ring costs ~5(K-1)/2 rows and columns per sweep (0.6% of a 2048 x 1024 tile at K = 4) and saves K-1
+// of every K exchanges -- on the strong-scaled config 4 the RCCL exchange is a large part of a tile sweep.  The
+// frame must come from the adjacent tiles only (3K <= tile extents) and the extended rows must stay within the
+// kernels' single wrap of the torus (5K - 2 <= lattice extents).  SV_DOMAIN_DEPTH sets K (default 4, at most 8:
+// the interior's 16-column left pad); the opt-in split sweeps keep K = 1.
+int villain_depth(int32_t Ht, int32_t Wt, int32_t Nt, int32_t Nx) {
+    const char *sp = getenv("SV_DOMAIN_SPLIT");
+    if (sp && sp[0] == '1') return 1;
+    const char *e = getenv("SV_DOMAIN_DEPTH");
+    int K = e ? atoi(e) : 4;
+    K = std::max(1, std::min(8, K));
+    while (K > 1 && (3 * K > std::min(Ht, Wt) || 5 * K - 2 > std::min(Nt, Nx))) K--;
+    return K;
+}
+
 void geometry(sv_domain *d) {
     if (d->Nt % d->ty || d->Nx % d->tx) throw std::invalid_argument("the lattice must divide evenly into tiles");
     d->Ht = d->Nt / d->ty;
     d->Wt = d->Nx / d->tx;
     if (d->Ht % 2 || d->Wt % 2 || d->Ht < 4 || d->Wt < 4)
         throw std::invalid_argument("tiles must be at least 4 x 4 with even extents");
+    if (d->model == 0) {
+        d->depth = villain_depth(d->Ht, d->Wt, d->Nt, d->Nx);
+        const int K = d->depth;
+        d->ghost = Ghost{VILLAIN_GHOST.top * K, VILLAIN_GHOST.bottom * K, VILLAIN_GHOST.left * K, VILLAIN_GHOST.right * K};
+    }
     if ((int64_t)d->Nt * d->Nx >= (1LL << 32)) throw std::invalid_argument("lattice too large for 32-bit stream positions");
     const Ghost &g = d->ghost;
     if (d->Ht < std::max(g.top, g.bottom) || d->Wt < std::max(g.left, g.right))
@@ -228,10 +254,11 @@ void geometry(sv_domain *d) {
     d->pitch = ((LEFT_PAD + d->Wt + g.right + 15) / 16) * 16;
     d->plane = (int64_t)(d->Ht + g.top + g.bottom) * d->pitch;
     d->org = (int64_t)g.top * d->pitch + LEFT_PAD;
-    // ring depth: an abort travels one tile-hop (8-neighbour torus) per sweep; with split sweeps the
-    // interior launch of the sweep that receives the abort still runs, so one more buffer
+    // ring depth: an abort travels one tile-hop (8-neighbour torus) per exchange, i.e. per K sweeps, so a tile
+    // D hops away runs at most D K sweeps past the failing one; with split sweeps (K = 1) the interior launch of
+    // the sweep that receives the abort still runs, so one more buffer
     const int D = std::max(d->ty / 2, d->tx / 2);
-    d->R = std::max(2, D + 2);
+    d->R = std::max(2, D * d->depth + 2);
     int64_t off = 0;
     for (int s = 0; s < NDIR; s++) {
         d->H.rect[s] = send_rect(s, d->Ht, d->Wt, d->ghost);
@@ -392,9 +419,34 @@ int domain_batch_q(const sv_domain *d, double q) {
     const int B = (int)std::lround(std::sqrt(2.0 * o / (q * r)));
     return std::max(4, std::min(DOMAIN_BATCH, B));
 }
+// Rows per strip of a Villain tile.  A tile of a strong-scaled lattice is small for one GPU (2048 x 1024 per GPU at
+// L=4096 on 8): with 52-row strips its 9 x 40 workgroups fill a third of the chip's 1024 slots (4 per CU) and the
+// sweep takes one strip's time.  When 52-row strips need at most two rounds of the slots, the strips are cut to
+// the shortest height (>= 20 rows, a multiple of 4) that keeps the same number of rounds.  Measured (r343, one
+// MI355X, one periodic tile): 2048 x 1024 at 52 / 36 (the single-lattice rule) / 20 rows 72.2 / 65.0 / 55.9 us per
+// sweep; 4096 x 2048 at 52 / 36 152.8 / 144.9 us; 4096^2 (three rounds) keeps 52.  SV_FUSED_TH overrides.
+int domain_th(const sv_domain *d, int nsx) {
+    if (getenv("SV_FUSED_TH")) return fused_th(d->Ht, nsx);
+    static const int slots = [] {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 1024;
+        return 4 * prop.multiProcessorCount;
+    }();
+    auto wgs = [&](int th) { return (int64_t)nsx * ((d->Ht + th - 1) / th); };
+    const int64_t rounds = (wgs(52) + slots - 1) / slots;
+    if (rounds > 2) return fused_th(d->Ht, nsx);
+    int th = 52;
+    while (th > 20 && wgs(th - 4) <= rounds * slots) th -= 4;
+    return th;
+}
+
 int domain_batch(const sv_domain *d, const VParams &P) {
     const double V = (double)d->Nt * d->Nx;
-    return domain_batch_q(d, P.k > 1 ? 4.0 * V * (double)P.thr / 4294967296.0 : 0.0);
+    const int B = domain_batch_q(d, P.k > 1 ? 4.0 * V * (double)P.thr / 4294967296.0 : 0.0);
+    if (getenv("SV_DOMAIN_BATCH")) return B;  // as given (tests: batches shorter than a group)
+    const int K = d->depth;  // whole groups of K sweeps per exchange where the batch allows
+    return std::min(DOMAIN_BATCH, std::max(K, (B + K / 2) / K * K));
 }
 
 void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u128 inc, sv_stats *stats) {
@@ -406,7 +458,7 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
     const int nb = (int)specs.size();
     constexpr int NWv = 4;
     const int nsx = (d->Wt + FW_MAX - 1) / FW_MAX;
-    const int TH = fused_th(d->Ht, nsx);
+    const int TH = domain_th(d, nsx);
     const int nsy = (d->Ht + TH - 1) / TH;
     const Affine adv[3] = {host_power(inc, (uint64_t)NWv * d->Nx), host_power(inc, (uint64_t)NWv * d->Nx / 2),
                            host_power(inc, (uint64_t)NWv * d->Nx / 4)};
@@ -460,8 +512,29 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
         for (int k = 0; k < count; k++) {
             const int in = d->cur, out = (d->cur + 1) % d->R;
             if (!d->split) {
-                exchange(d, ctx->stream);
-                for (auto &Tl : d->tiles) launch_fused_tile(fargs(Tl, k, in, out), nsx * nsy, ctx->stream, hot[k]);
+                // deep halos: one exchange per group of K sweeps; sweep j of a group of g decides the tile extended
+                // by e = g-1-j rings of (2 above, 3 below, 2 left, 3 right), counting only the tile's own sites
+                const int K = d->depth, g0 = k - k % K, e = std::min(K, count - g0) - 1 - (k - g0);
+                if (k == g0) exchange(d, ctx->stream);
+                for (auto &Tl : d->tiles) {
+                    FArgs A = fargs(Tl, k, in, out);
+                    if (e > 0) {
+                        const int32_t up = 2 * e, left = 2 * e;
+                        A.G.T0 = (Tl.T0 - up + d->Nt) % d->Nt;
+                        A.G.X0 = (Tl.X0 - left + d->Nx) % d->Nx;
+                        A.G.Ht = d->Ht + 5 * e;
+                        A.G.Wt = d->Wt + 5 * e;
+                        A.G.org = d->org - (int64_t)up * d->pitch - left;
+                        A.nsx = (A.G.Wt + FW_MAX - 1) / FW_MAX;
+                        A.nsy = (A.G.Ht + TH - 1) / TH;
+                        A.tiles_per_rep = A.nsx * A.nsy;
+                        A.own_r0 = up;
+                        A.own_r1 = up + d->Ht;
+                        A.own_c0 = left;
+                        A.own_c1 = left + d->Wt;
+                    }
+                    launch_fused_tile(A, A.nsx * A.nsy, ctx->stream, hot[k]);
+                }
             } else {
                 // A: interior strips of sweep k need the boundary strips of sweep k-1 (their input rows)
                 SV_HIP(hipStreamWaitEvent(A_, d->ev_boundary, 0));
@@ -637,6 +710,7 @@ static int exchange_plan_impl(int model, int32_t Nt, int32_t Nx, int32_t tiles_t
     try {
         if (!out || tiles_t < 1 || tiles_x < 1 || rank < 0 || rank >= tiles_t * tiles_x) return -1;
         sv_domain d;
+        d.model = model;
         d.ghost = model == 1 ? WORLDLINE_GHOST : VILLAIN_GHOST;
         d.Nt = Nt;
         d.Nx = Nx;
@@ -671,6 +745,7 @@ static int message_layout_impl(int model, int32_t Nt, int32_t Nx, int32_t tiles_
     try {
         if (!out || tiles_t < 1 || tiles_x < 1 || rank < 0 || rank >= tiles_t * tiles_x) return -1;
         sv_domain d;
+        d.model = model;
         d.ghost = model == 1 ? WORLDLINE_GHOST : VILLAIN_GHOST;
         d.Nt = Nt;
         d.Nx = Nx;
@@ -757,7 +832,7 @@ static int domain_create(sv_ctx *ctx, int model, int32_t Nt, int32_t Nx, int32_t
         // split sweeps (Villain): strips whose stencil stays inside the tile run while the halos travel
         if (model == 0) {
             const int nsx = (d->Wt + FW_MAX - 1) / FW_MAX;
-            const int TH = fused_th(d->Ht, nsx), nsy = (d->Ht + TH - 1) / TH;
+            const int TH = domain_th(d, nsx), nsy = (d->Ht + TH - 1) / TH;
             std::vector<int32_t> inner, outer;
             for (int iy = 0; iy < nsy; iy++)
                 for (int ix = 0; ix < nsx; ix++) {

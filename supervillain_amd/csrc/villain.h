@@ -60,6 +60,9 @@ struct FArgs {
     double *obs;                    // OBS kernels: per replica {sum (d phi - 2 pi n)^2, sum (dn)^2, sum n0, sum n1}
     const int32_t *strip_map = nullptr;  // TILE: launch index -> strip index (interior / boundary launches)
     const int32_t *rep_map = nullptr;    // replica batches: launch's replica slot -> replica (a subset launch), or identity
+    // TILE: the window of the launch's region whose sites are counted in the statistics, [r0, r1) x [c0, c1) in
+    // region coordinates (domain.hip's deep halos run sweeps over a tile extended by a ring it does not own)
+    int32_t own_r0 = -(1 << 30), own_r1 = 1 << 30, own_c0 = -(1 << 30), own_c1 = 1 << 30;
 };
 
 }  // namespace sv

@@ -188,7 +188,12 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     // LDS neighbour columns (full rows wrap inside the row)
     auto cxp = [&](int cx) { return FR ? (cx + 1 == w ? 0 : cx + 1) : cx + 1; };
     auto cxm = [&](int cx) { return FR ? (cx == 0 ? w - 1 : cx - 1) : cx - 1; };
-    const int32_t gx0 = Gm.X0 + x0;                  // global column of the strip's first site
+    // global column origin of this strip (its first column wrapped onto the torus: deep-halo regions start
+    // anywhere), and the sites it counts in the statistics (its own, within the launch's owned window)
+    const int32_t X0s = TILE ? wrapN(Gm.X0 + x0, Nx) - x0 : Gm.X0;
+    const int32_t q_lo = TILE && A.own_r0 > t0 ? A.own_r0 : t0, q_hi = TILE && A.own_r1 < t1 ? A.own_r1 : t1;
+    const int32_t c_lo = TILE && A.own_c0 > x0 ? A.own_c0 : x0, c_hi = TILE && A.own_c1 < x1 ? A.own_c1 : x1;
+    const int32_t gx0 = X0s + x0;                    // global column of the strip's first site
     const bool interior = !FR && gx0 >= 4 && gx0 + w + 2 < Nx;
     // row bases at the first non-wrapped region column (global); on rows of <= 128 sites at the row
     // start, so that every column -- wrapped halo columns included -- is a small-table offset away
@@ -292,14 +297,14 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     if (fast[0]) {
         const int32_t q = tfirst + 2 + wave;
         const int32_t xs = (x0 - 1) + ((par0 + q + x0 - 1) & 1);
-        pk0 = fast_pack(has_c0, lane, (uint32_t)grow(q) * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
-                        (uint32_t)(Gm.X0 + xs + 2 * lane), (uint32_t)xb);
+        pk0 = fast_pack(has_c0, lane, (uint32_t)grow(q) * (uint32_t)Nx, (uint32_t)(X0s + xs),
+                        (uint32_t)(X0s + xs + 2 * lane), (uint32_t)xb);
     }
     if (fast[1]) {
         const int32_t q = tfirst + 1 + wave;
         const int32_t xs = x0 + ((par0 + q + x0 + 1) & 1);
-        pk1 = fast_pack(has_c1, lane, (uint32_t)grow(q) * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
-                        (uint32_t)(Gm.X0 + xs + 2 * lane), (uint32_t)xb);
+        pk1 = fast_pack(has_c1, lane, (uint32_t)grow(q) * (uint32_t)Nx, (uint32_t)(X0s + xs),
+                        (uint32_t)(X0s + xs + 2 * lane), (uint32_t)xb);
     }
 
     int64_t acc_count = 0;
@@ -377,13 +382,13 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             for (int k = 0; k < 6; k++) bs[k] = wave_uniform(s_base[wave][k]);
             Draws D;
             if (fast[0])
-                D = draws_fastp<K3>(A, RL, 0, active, lane, pk0, ((uint32_t)gq * (uint32_t)Nx + (uint32_t)(Gm.X0 + x)) >> 1,
+                D = draws_fastp<K3>(A, RL, 0, active, lane, pk0, ((uint32_t)gq * (uint32_t)Nx + (uint32_t)(X0s + x)) >> 1,
                                 bs, s_small);
             else if (fastfr[0])
                 D = draws_fast<K3>(A, RL, 0, has_c0, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)xs, (uint32_t)x, 0u,
                                bs, s_small);
             else
-                D = draws_general<K3>(A, RL, 0, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small, edge, xw,
+                D = draws_general<K3>(A, RL, 0, active, gq, wrapN(X0s + x, Nx), xb, bs, s_small, edge, xw,
                                   &s_base[wave][16]);
             if (active) {
                 const int lr = q - rbase;
@@ -417,7 +422,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
                 p = p < 0.0 ? 0.0 : p;
                 p = p > 1.0 ? 1.0 : p;
                 const int acc = D.u < p;
-                const bool own = q >= t0 && q < t1 && (FR || (x >= x0 && x < x1));
+                const bool own = q >= q_lo && q < q_hi && (FR || (x >= c_lo && x < c_hi));
                 if (own) {  // count each site once; colour-0 phi is final after this pass
                     acc_count += acc;
                     psum += p;
@@ -452,13 +457,13 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             for (int k = 0; k < 6; k++) bs[k] = wave_uniform(s_base[wave][8 + k]);
             Draws D;
             if (fast[1])
-                D = draws_fastp<K3>(A, RL, 1, active, lane, pk1, ((uint32_t)gq * (uint32_t)Nx + (uint32_t)(Gm.X0 + x)) >> 1,
+                D = draws_fastp<K3>(A, RL, 1, active, lane, pk1, ((uint32_t)gq * (uint32_t)Nx + (uint32_t)(X0s + x)) >> 1,
                                 bs, s_small);
             else if (fastfr[1])
                 D = draws_fast<K3>(A, RL, 1, has_c1, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)xs, (uint32_t)x, 0u,
                                bs, s_small);
             else
-                D = draws_general<K3>(A, RL, 1, active, gq, wrapN(Gm.X0 + x, Nx), xb, bs, s_small, edge, xw,
+                D = draws_general<K3>(A, RL, 1, active, gq, wrapN(X0s + x, Nx), xb, bs, s_small, edge, xw,
                                   &s_base[wave][24]);
             if (active) {
                 const int lr = q - rbase;
@@ -486,7 +491,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
                 p = p < 0.0 ? 0.0 : p;
                 p = p > 1.0 ? 1.0 : p;
                 const int acc = D.u < p;
-                if (q >= t0 && q < t1 && (FR || (x >= x0 && x < x1))) {
+                if (q >= q_lo && q < q_hi && (FR || (x >= c_lo && x < c_hi))) {
                     acc_count += acc;
                     psum += p;
                 }

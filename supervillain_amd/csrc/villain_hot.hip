@@ -176,13 +176,19 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH> &Ls) {
     const int32_t w = x1 - x0;
     const int32_t t0 = iy * A.TH;
     const int32_t t1 = t0 + A.TH < Gm.Ht ? t0 + A.TH : Gm.Ht;
+    // the sites this strip counts in the statistics (its own, within the launch's owned window)
+    const int32_t q_lo = TILE && A.own_r0 > t0 ? A.own_r0 : t0, q_hi = TILE && A.own_r1 < t1 ? A.own_r1 : t1;
+    const int32_t c_lo = TILE && A.own_c0 > x0 ? A.own_c0 : x0, c_hi = TILE && A.own_c1 < x1 ? A.own_c1 : x1;
+    // global column origin of this strip: its first column wrapped onto the torus, so that X0s + x stays within
+    // [-2, Nx + 126) on the strip wherever the launch's region starts (deep-halo regions start anywhere)
+    const int32_t X0s = TILE ? wrapN(Gm.X0 + x0, Nx) - x0 : Gm.X0;
     const int32_t rbase = t0 - 2;  // local row 0
     const int32_t cols = FR ? w : w + 5;
     const int32_t cofs = FR ? 0 : x0 - 2;   // LDS column of local column x is x - cofs
     // LDS neighbour columns (full rows wrap inside the row)
     auto cxp = [&](int cx) { return FR ? (cx + 1 == w ? 0 : cx + 1) : cx + 1; };
     auto cxm = [&](int cx) { return FR ? (cx == 0 ? w - 1 : cx - 1) : cx - 1; };
-    const int32_t gx0 = Gm.X0 + x0;
+    const int32_t gx0 = X0s + x0;
     const bool interior = gx0 >= 4 && gx0 + w + 2 < Nx;
     const int32_t xb = (FR || (Nx <= SMALL_LDS && !interior) || gx0 - 2 < 0) ? 0 : gx0 - 2;
     constexpr bool edge = EDGE;
@@ -237,8 +243,16 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH> &Ls) {
                 if (lane + 64 * k < cols) {
                     const int64_t g = g0 + pf_gx[k];
                     pf_phi[k] = phi_in[g];
-                    pf_n0[k] = n_in[g];
-                    pf_n1[k] = n_in[V + g];
+                    if (SV_ABLATE & 256) {  // timing experiment: a compact int32 n layout (cold start only)
+                        pf_n0[k] = ((const int32_t *)n_in)[g];
+                        pf_n1[k] = ((const int32_t *)n_in)[V + g];
+                    } else if (SV_ABLATE & 512) {  // the same with int16
+                        pf_n0[k] = ((const int16_t *)n_in)[g];
+                        pf_n1[k] = ((const int16_t *)n_in)[V + g];
+                    } else {
+                        pf_n0[k] = n_in[g];
+                        pf_n1[k] = n_in[V + g];
+                    }
                 }
             }
         }
@@ -290,14 +304,14 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH> &Ls) {
         {
             const int32_t q = tfirst + 2 + wave;
             const int32_t xs = FR ? ((par0 + q) & 1) : (x0 - 1) + ((par0 + q + x0 - 1) & 1);
-            pk0 = fast_pack(has_c[0], lane, (uint32_t)grow(q) * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
-                            (uint32_t)(Gm.X0 + xs + 2 * lane), (uint32_t)xb);
+            pk0 = fast_pack(has_c[0], lane, (uint32_t)grow(q) * (uint32_t)Nx, (uint32_t)(X0s + xs),
+                            (uint32_t)(X0s + xs + 2 * lane), (uint32_t)xb);
         }
         {
             const int32_t q = tfirst + 1 + wave;
             const int32_t xs = FR ? ((par0 + q + 1) & 1) : x0 + ((par0 + q + x0 + 1) & 1);
-            pk1 = fast_pack(has_c[1], lane, (uint32_t)grow(q) * (uint32_t)Nx, (uint32_t)(Gm.X0 + xs),
-                            (uint32_t)(Gm.X0 + xs + 2 * lane), (uint32_t)xb);
+            pk1 = fast_pack(has_c[1], lane, (uint32_t)grow(q) * (uint32_t)Nx, (uint32_t)(X0s + xs),
+                            (uint32_t)(X0s + xs + 2 * lane), (uint32_t)xb);
         }
     }
 
@@ -318,8 +332,16 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH> &Ls) {
                     const int cx = FR ? cc : cc + 2;
                     const int64_t g = g0 + cc;
                     phi_out[g] = s_phi[slot][cx];
-                    n_out[g] = (int64_t)s_n0[slot][cx];
-                    n_out[V + g] = (int64_t)s_n1[slot][cx];
+                    if (SV_ABLATE & 256) {
+                        ((int32_t *)n_out)[g] = s_n0[slot][cx];
+                        ((int32_t *)n_out)[V + g] = s_n1[slot][cx];
+                    } else if (SV_ABLATE & 512) {
+                        ((int16_t *)n_out)[g] = s_n0[slot][cx];
+                        ((int16_t *)n_out)[V + g] = s_n1[slot][cx];
+                    } else {
+                        n_out[g] = (int64_t)s_n0[slot][cx];
+                        n_out[V + g] = (int64_t)s_n1[slot][cx];
+                    }
                     if (OBS) {
                         // rows <= q+1 and columns <= x+1 are final here (villain.py:51-66, winding.py:30-37,
                         // wrapping.py:17-25): link residuals, plaquette winding dn, holonomy sums
@@ -357,7 +379,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH> &Ls) {
         if constexpr (PH) {
             // site s of sweep `ph_sweep`: call (s, sweep, 0) -> u, dphi; call (s, sweep, 1) -> the four choice words; a
             // word Lemire rejects is replaced in place by word 0 of call (s, sweep, 2 + j + 4 t) (sv_oracle.c, philox)
-            const uint32_t site = (uint32_t)gq * (uint32_t)Nx + (uint32_t)wrapN(Gm.X0 + x, Nx);
+            const uint32_t site = (uint32_t)gq * (uint32_t)Nx + (uint32_t)wrapN(X0s + x, Nx);
             const uint32_t s0 = (uint32_t)A.ph_sweep, s1 = (uint32_t)(A.ph_sweep >> 32);
             const uint32_t k0 = (uint32_t)A.ph_key, k1 = (uint32_t)(A.ph_key >> 32);
             const P4 a = philox4x32_10(P4{{site, s0, s1, 0u}}, k0, k1);
@@ -379,7 +401,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH> &Ls) {
             for (int k = 0; k < 6; k++) bs[k] = s_base[wave][8 * c + k];
             D = hot_draws_paired(A, lane, c == 0 ? pk0 : pk1, bs, s_small);
         } else {
-            D = hot_draws_edge(A, gq, wrapN(Gm.X0 + x, Nx), xb, two_sets ? xw : xb, &s_base[wave][8 * c],
+            D = hot_draws_edge(A, gq, wrapN(X0s + x, Nx), xb, two_sets ? xw : xb, &s_base[wave][8 * c],
                                &s_base[wave][(two_sets ? 16 : 0) + 8 * c], s_small, has_c[c], buf_c[c]);
         }
         bool rej = false;
@@ -391,7 +413,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH> &Ls) {
             cn[j] = SV_HOT_MUL24 ? __mul24((int32_t)(m >> 32), Wn) - nW : (int32_t)(m >> 32) * Wn - nW;
         }
         if (__builtin_expect(rej && active && !(SV_ABLATE & 2), 0)) {
-            const uint32_t rank = (uint32_t)(((int64_t)gq * Nx + wrapN(Gm.X0 + x, Nx)) >> 1);
+            const uint32_t rank = (uint32_t)(((int64_t)gq * Nx + wrapN(X0s + x, Nx)) >> 1);
 #pragma unroll
             for (int j = 0; j < 4; j++)
                 if ((uint32_t)((uint64_t)D.w[j] * kc) < thr) report(A.S, A.sweep, (uint32_t)(1 + 5 * c + 1 + j), rank, (uint32_t)rep);
@@ -444,7 +466,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH> &Ls) {
                 double p = sv_exp(-dS);
                 p = p > 1.0 ? 1.0 : p;
                 const bool acc = D.u < p;
-                if (q >= t0 && q < t1 && (FR || (x >= x0 && x < x1))) {
+                if (q >= q_lo && q < q_hi && (FR || (x >= c_lo && x < c_hi))) {
                     acc_count += acc;
                     psum += p;
                 }
@@ -503,7 +525,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH> &Ls) {
                 double p = sv_exp(-dS);
                 p = p > 1.0 ? 1.0 : p;
                 const bool acc = D.u < p;
-                if (q >= t0 && q < t1 && (FR || (x >= x0 && x < x1))) {
+                if (q >= q_lo && q < q_hi && (FR || (x >= c_lo && x < c_hi))) {
                     acc_count += acc;
                     psum += p;
                 }
@@ -574,7 +596,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4
     if (TILE && A.strip_map) b = A.strip_map[b];
     const int ix = b % A.nsx;
     const int32_t x0 = (int32_t)((int64_t)ix * A.G.Wt / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * A.G.Wt / A.nsx);
-    const int32_t gx0 = A.G.X0 + x0;
+    const int32_t gx0 = wrapN(A.G.X0 + x0, A.G.Nx);
     const bool interior = gx0 >= 4 && gx0 + (x1 - x0) + 2 < A.G.Nx;
     if (__builtin_amdgcn_readfirstlane((int)interior)) hot_body<TILE, false>(A, Ls);
     else hot_body<TILE, true>(A, Ls);

@@ -53,6 +53,16 @@ def exchange_plan(Nt, Nx, tiles, rank, model='villain'):
     return plan
 
 
+def ghost_frame(Nt, Nx, tiles, model='villain'):
+    """(rows above, below, columns left, right) of the ghost frame libsvhip.so gives this decomposition: GHOSTS for
+    the Worldline and for Villain at depth 1, K times the Villain frame when K sweeps run per halo exchange (deep
+    halos, SV_DOMAIN_DEPTH).  Read off the exchange plan: the message toward (dy, dx) = (1, 0) fills
+    the receiver's rows above, and so on."""
+    plan = exchange_plan(Nt, Nx, tiles, 0, model)
+    shape = {(m['dy'], m['dx']): m['shape'] for m in plan}
+    return shape[(1, 0)][0], shape[(-1, 0)][0], shape[(0, 1)][1], shape[(0, -1)][1]
+
+
 def message_layout(Nt, Nx, tiles, rank, model='villain'):
     """The RCCL message layout libsvhip.so uses for `rank` when every tile is a rank (host-only).
 

@@ -9,7 +9,7 @@ import socket
 import numpy as np
 import pytest
 
-from supervillain_amd.domain import GHOSTS, exchange_plan, message_layout, tile_grid
+from supervillain_amd.domain import GHOSTS, exchange_plan, ghost_frame, message_layout, tile_grid
 
 MODELS = list(GHOSTS)
 
@@ -20,7 +20,7 @@ def test_tile_grid():
 
 def padded_tile(G, tiles, rank, model):
     """Tile `rank` of global array G with an unfilled (NaN) ghost frame."""
-    GT, GB, GL, GR = GHOSTS[model]
+    GT, GB, GL, GR = ghost_frame(*G.shape, tiles, model)
     Nt, Nx = G.shape
     ty, tx = tiles
     Ht, Wt = Nt // ty, Nx // tx
@@ -31,7 +31,7 @@ def padded_tile(G, tiles, rank, model):
 
 
 def expected_frame(G, tiles, rank, model):
-    GT, GB, GL, GR = GHOSTS[model]
+    GT, GB, GL, GR = ghost_frame(*G.shape, tiles, model)
     Nt, Nx = G.shape
     ty, tx = tiles
     Ht, Wt = Nt // ty, Nx // tx
@@ -41,14 +41,14 @@ def expected_frame(G, tiles, rank, model):
     return G[np.ix_(rows, cols)]
 
 
-def message(P, m, model):
-    GT, GB, GL, GR = GHOSTS[model]
+def message(P, m, model, ghost):
+    GT, GB, GL, GR = ghost
     (r0, c0), (h, w) = m['src'], m['shape']
     return P[GT + r0:GT + r0 + h, GL + c0:GL + c0 + w].copy()
 
 
-def place(P, m, block, model):
-    GT, GB, GL, GR = GHOSTS[model]
+def place(P, m, block, model, ghost):
+    GT, GB, GL, GR = ghost
     (r0, c0), (h, w) = m['dst'], m['shape']
     P[GT + r0:GT + r0 + h, GL + c0:GL + c0 + w] = block
 
@@ -58,20 +58,22 @@ GRIDS = [(1, 1), (1, 2), (2, 1), (2, 2), (2, 4), (3, 2), (1, 8), (4, 4)]
 
 @pytest.mark.parametrize('model', MODELS)
 @pytest.mark.parametrize('tiles', GRIDS)
-def test_plan_fills_every_ghost(tiles, model):
+@pytest.mark.parametrize('size', [(8, 6), (24, 24)])  # small tiles clamp the Villain depth, 24 x 24 tiles take K = 4
+def test_plan_fills_every_ghost(tiles, model, size):
     ty, tx = tiles
-    Nt, Nx = 8 * ty, 6 * tx
+    Nt, Nx = size[0] * ty, size[1] * tx
     G = np.random.default_rng(0).normal(size=(Nt, Nx))
+    gh = ghost_frame(Nt, Nx, tiles, model)
     ntiles = ty * tx
     plans = [exchange_plan(Nt, Nx, tiles, r, model) for r in range(ntiles)]
     P = [padded_tile(G, tiles, r, model) for r in range(ntiles)]
     sent = {}
     for r in range(ntiles):
         for s, m in enumerate(plans[r]):
-            sent[(r, m['send_to'], s)] = message(P[r], m, model)
+            sent[(r, m['send_to'], s)] = message(P[r], m, model, gh)
     for r in range(ntiles):
         for s, m in enumerate(plans[r]):
-            place(P[r], m, sent[(m['recv_from'], r, s)], model)
+            place(P[r], m, sent[(m['recv_from'], r, s)], model, gh)
     for r in range(ntiles):
         np.testing.assert_array_equal(P[r], expected_frame(G, tiles, r, model))
 
@@ -121,6 +123,7 @@ def _exchange_worker(rank, world, port, tiles, Nt, Nx, errfile, model):
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
         G = np.random.default_rng(1).normal(size=(Nt, Nx))
+        gh = ghost_frame(Nt, Nx, tiles, model)
         plan = exchange_plan(Nt, Nx, tiles, rank, model)
         lay = message_layout(Nt, Nx, tiles, rank, model)
         P = padded_tile(G, tiles, rank, model)
@@ -128,7 +131,7 @@ def _exchange_worker(rank, world, port, tiles, Nt, Nx, errfile, model):
         # one send per distinct peer, one receive per distinct source; self messages stay local
         send = np.zeros(lay['msg_words'])
         for s, m in enumerate(plan):
-            blk = message(P, m, model).ravel()
+            blk = message(P, m, model, gh).ravel()
             o = lay['soff'][s]
             assert lay['words'][s] == 2 + 3 * blk.size
             send[o + 2:o + 2 + blk.size] = blk
@@ -145,8 +148,8 @@ def _exchange_worker(rank, world, port, tiles, Nt, Nx, errfile, model):
                 o = lay['roff'][s]
                 block = recvbuf.numpy()[o + 2:o + 2 + cnt].reshape(m['shape'])
             else:
-                block = message(P, plan[s], model)
-            place(P, m, block, model)
+                block = message(P, plan[s], model, gh)
+            place(P, m, block, model, gh)
         np.testing.assert_array_equal(P, expected_frame(G, tiles, rank, model))
     except Exception as e:  # report to the parent
         with open(errfile, 'a') as f:
@@ -161,7 +164,7 @@ def _exchange_worker(rank, world, port, tiles, Nt, Nx, errfile, model):
 def test_two_rank_gloo_exchange(tiles, model, tmp_path):
     import torch.multiprocessing as mp
     errfile = str(tmp_path / 'err.txt')
-    Nt, Nx = 8 * tiles[0], 6 * tiles[1]
+    Nt, Nx = 24 * tiles[0], 24 * tiles[1]  # Villain tiles of 24 x 24: depth 4, the 8 / 12-deep frame
     world = tiles[0] * tiles[1]
     mp.start_processes(_exchange_worker, args=(world, _free_port(), tiles, Nt, Nx, errfile, model), nprocs=world,
                        join=True, start_method='spawn')
@@ -170,13 +173,14 @@ def test_two_rank_gloo_exchange(tiles, model, tmp_path):
 
 @pytest.mark.parametrize('model', MODELS)
 @pytest.mark.parametrize('tiles', GRIDS)
-def test_rccl_blocks_line_up(tiles, model):
+@pytest.mark.parametrize('size', [(8, 6), (24, 24)])
+def test_rccl_blocks_line_up(tiles, model, size):
     """The per-peer message blocks libsvhip.so sends (one ncclSend / ncclRecv per distinct peer): rank a's block
     for b and rank b's block from a have the same size, and every message s sits at the same offset inside
     both blocks, so the receiver's ghost block s gets exactly the sender's message s."""
     from supervillain_amd.domain import exchange_plan, message_layout
     ty, tx = tiles
-    Nt, Nx = 8 * ty, 6 * tx
+    Nt, Nx = size[0] * ty, size[1] * tx
     ntiles = ty * tx
     lay = [message_layout(Nt, Nx, tiles, r, model) for r in range(ntiles)]
     plans = [exchange_plan(Nt, Nx, tiles, r, model) for r in range(ntiles)]

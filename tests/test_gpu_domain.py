@@ -114,6 +114,27 @@ def test_forced_rejections(tiles, batch, oracle_lib, monkeypatch):
         assert [s.rejections for s in st] == [s.rejections for s in st_ref]
 
 
+@pytest.mark.parametrize('depth', ['1', '2', '3', '5', '8'])
+@pytest.mark.parametrize('tiles', [(2, 2), (1, 4), (2, 4)])
+def test_deep_halo_depths(depth, tiles, oracle_lib, monkeypatch):
+    """K sweeps per halo exchange (SV_DOMAIN_DEPTH; the default is 4): every depth, with groups cut short by the
+    call's sweep count (11 = 2K + 3 at K = 4) and a forced NumPy Lemire rejection whose abort spreads one tile-hop
+    per exchange, equals the oracle's single-lattice chain."""
+    monkeypatch.setenv('SV_DOMAIN_DEPTH', depth)
+    N = 128
+    V = N * N
+    pos, half = 4 * V + V + V // 2 + 11, 0  # sweep 1, a colour-0 choice block
+    phi0, n0 = hot(N, N, 1, 99)
+    gen = crafted_generator(5, pos, half)
+    phi, n, st = run_domain(N, N, tiles, 0.45, 1, phi0, n0, 11, gen)
+    g = crafted_generator(5, pos, half)
+    p, m = phi0.copy(), n0.copy()
+    st_ref = oracle_lib.villain_neighborhood(N, 0.45, 1, p, m, 11, g)
+    assert sum(s.rejections for s in st_ref) >= 1
+    assert_same(phi, n, st, gen, p, m, st_ref, g)
+    assert [s.rejections for s in st] == [s.rejections for s in st_ref]
+
+
 def test_chunked_calls_continue_the_chain(oracle_lib):
     """Calls of 3 + 1 + 4 sweeps (ring index carried across calls) equal one call of 8."""
     N = 64
