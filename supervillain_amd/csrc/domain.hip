@@ -137,13 +137,74 @@ __global__ void halo_unpack(double *phi, int64_t *n, int64_t pitch, int64_t plan
 }
 
 // Per-tile batch summary, contiguous so that ranks can all-gather it in one collective.
+static constexpr int MAX_CAND = 64;
 struct Summary {
     int32_t abort;
     uint32_t nreport;
-    uint64_t pad;
+    uint32_t ncand;      // rejection prediction: words of the NEXT batch NumPy's Lemire sampler would reject
+    uint32_t pad;
     Report reports[MAX_REPORTS];
     sv_stats stats[2 * DOMAIN_BATCH];  // Villain: one per sweep; Worldline: (Plaquette, Coexact) per step
+    uint64_t cand[MAX_CAND];           // half-word indices (2 u64 + high) counted from the next batch's start state
 };
+
+// Rejection prediction.  A NumPy Lemire rejection aborts a decomposed batch from its sweep on, and with small tiles
+// (the strong-scaled config 4) the drained sweeps and the host round trip of the replay cost several sweep times;
+// so the batch size was kept short, and with it every batch pays an all-gather and a synchronization.  Whether a
+// word is rejected depends only on the stream, not on the lattice, so the words the NEXT batch's choice blocks will
+// draw can be tested while this batch runs: sweep k of a batch draws its bounded words from u64 [1.5V, 2.5V) and
+// [3V, 4V) after its nominal start (4V u64 per sweep; skips shift that by a few half-words, covered by a margin of
+// SCAN_MARGIN u64 on each side).  The ranks split the scan, and the words found travel in the batch summaries the
+// ranks all-gather anyway; the host turns them into skip lists before planning the batch (add_predicted).  The
+// abort / replay protocol stays as the safety net (a word outside the scanned ranges, the first batch of a call).
+static constexpr uint64_t SCAN_MARGIN = 32;
+static constexpr int SCAN_CHUNK = 64;  // u64 per lane: one table jump, then single steps
+
+struct ScanArgs {
+    const u128 *s_k;      // per sweep of the scanned batch: the state after k 4V steps from the batch start
+    const JumpTables *T;
+    uint64_t V, lo, hi;   // this rank's slice [lo, hi) of the batch's scan index space (2 (V + 2 M) per sweep)
+    uint32_t k, thr;      // bounded draws over k values; NumPy's rejection threshold
+    uint32_t *ncand;
+    uint64_t *cand;
+};
+
+__global__ __launch_bounds__(256) void scan_rejections(ScanArgs a) {
+    const uint64_t seg = a.V + 2 * SCAN_MARGIN, per = 2 * seg;
+    uint64_t v = a.lo + (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) * SCAN_CHUNK;
+    if (v >= a.hi) return;
+    const uint64_t v1 = v + SCAN_CHUNK < a.hi ? v + SCAN_CHUNK : a.hi;
+    uint32_t k = (uint32_t)(v / per);
+    uint64_t r = v - (uint64_t)k * per;
+    const Affine one = a.T->small[1];
+    while (v < v1) {
+        // a run of consecutive u64 within sweep k: the colour-0 choice run or the colour-1 one (with margins)
+        const bool first = r < seg;
+        uint64_t j = first ? a.V + a.V / 2 - SCAN_MARGIN + r : 3 * a.V - SCAN_MARGIN + (r - seg);
+        const uint64_t left = (first ? seg - r : per - r), n = left < v1 - v ? left : v1 - v;
+        u128 st = jump(a.T, a.s_k[k], (uint32_t)(j + 1));  // the state whose output is u64 j
+        for (uint64_t e = 0; e < n; e++, j++) {
+            const uint64_t x = xsl_rr(st);
+            const bool rl = (uint32_t)((uint64_t)(uint32_t)x * a.k) < a.thr;
+            const bool rh = (uint32_t)((uint64_t)(uint32_t)(x >> 32) * a.k) < a.thr;
+            if (__builtin_expect(rl | rh, 0)) {
+                const uint64_t h = 2 * ((uint64_t)k * 4 * a.V + j);
+                for (int half = 0; half < 2; half++)
+                    if (half ? rh : rl) {
+                        const uint32_t i = atomicAdd(a.ncand, 1u);
+                        if (i < MAX_CAND) a.cand[i] = h + half;
+                    }
+            }
+            st = mad128c(one.A, st, one.C);
+        }
+        v += n;
+        r += n;
+        if (r == per) {
+            r = 0;
+            k++;
+        }
+    }
+}
 
 // Worldline tiles: the per-step StatStripes of worldline_step_fused folded into the tile's Summary
 __global__ void wd_fold(const StatStripe *ss, sv_stats *out, int count) {
@@ -186,6 +247,16 @@ struct sv_domain {
     int64_t pitch = 0, plane = 0, org = 0;
     int R = 2, cur = 0;
     int depth = 1;                  // Villain: sweeps per halo exchange (deep halos, see villain_depth)
+    u128 *d_scan = nullptr;         // rejection prediction: per-sweep start states of the scanned batch
+    hipStream_t scan_stream = nullptr;  // lowest priority: the scan fills the slots the sweeps leave free
+    hipEvent_t ev_sum = nullptr, ev_scan = nullptr;
+    struct Pred {                   // the scanned words of the batch starting at cursor c (kept across calls)
+        bool valid = false;
+        int sw = 0, count = 0;
+        Cursor c{};
+        u128 inc{0, 0};
+        std::vector<uint64_t> cand;
+    } pred;
     HaloTable H{};
     int64_t msg_words = 0;
     std::vector<sv_domain_tile> tiles;  // local tiles (all tiles when nranks == 1)
@@ -391,6 +462,52 @@ void gather(sv_domain *d) {
     SV_HIP(hipStreamSynchronize(ctx->stream));
 }
 
+// Skip lists of the batch [sw, sw + count) from cursor c0 given the rejected words found by the scan (half-word
+// indices from c0's state, sorted): walk the blocks as plan_block does, mapping each bounded block's draw positions
+// to half-word indices -- position 0 is the buffered half (from the last u64 of an earlier bounded block) when
+// `has`, then the halves of the block's own u64s in order.
+void add_predicted(SkipMap &skips, const Cursor &c0, const std::vector<BlockSpec> &specs, int sw, int count,
+                   const std::vector<uint64_t> &cand) {
+    int64_t j = 0, buf = -1;  // u64 drawn so far; half-word index of the buffered word (-1: before the batch)
+    uint32_t has = c0.has;
+    const int nb = (int)specs.size();
+    for (int k = 0; k < count; k++)
+        for (int b = 0; b < nb; b++) {
+            const BlockSpec &sp = specs[b];
+            if (sp.kind == UNIFORM) {
+                j += sp.count;
+                continue;
+            }
+            if (sp.count == 0) continue;
+            const auto key = std::make_pair(sw + k, b);
+            auto it = skips.find(key);
+            std::vector<uint32_t> S = it == skips.end() ? std::vector<uint32_t>{} : it->second;
+            std::vector<uint32_t> Pd;
+            for (uint64_t c : cand) {
+                int64_t p = -1;
+                if (has && (int64_t)c == buf) p = 0;
+                else if ((int64_t)c >= 2 * j) p = (int64_t)c - 2 * j + has;
+                if (p >= 0 && p < (int64_t)sp.count + 2 * MAX_CAND) Pd.push_back((uint32_t)p);
+            }
+            std::vector<uint32_t> all = S;
+            all.insert(all.end(), Pd.begin(), Pd.end());
+            std::sort(all.begin(), all.end());
+            all.erase(std::unique(all.begin(), all.end()), all.end());
+            uint64_t u = sp.count;
+            for (;;) {  // words consumed: the draws plus every rejected position met on the way
+                const uint64_t z = (uint64_t)std::count_if(all.begin(), all.end(), [&](uint32_t p) { return p < u; });
+                if (sp.count + z == u) break;
+                u = sp.count + z;
+            }
+            all.erase(std::remove_if(all.begin(), all.end(), [&](uint32_t p) { return p >= u; }), all.end());
+            if (all.size() != S.size()) skips[key] = all;
+            const uint64_t rest = u - (has ? 1 : 0), words = (rest + 1) / 2;
+            if (rest & 1) buf = 2 * (j + (int64_t)words - 1) + 1;
+            j += (int64_t)words;
+            has = (uint32_t)(rest & 1);
+        }
+}
+
 void fill_stats(const sv_domain *d, const SkipMap &skips, int nb, int sw, int count, sv_stats *stats) {
     const int64_t V = (int64_t)d->Nt * d->Nx;
     for (int k = 0; k < count; k++) {
@@ -465,16 +582,47 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
     SkipMap skips;
     std::vector<Block> blocks;
     std::vector<uint32_t> skipvec;
-    const int batch = domain_batch(d, P);
+    // rejection prediction (see scan_rejections): the scan of batch b+1 runs behind batch b's sweeps
+    // On by default where the ranks split the scan (several RCCL ranks: each scans 1/N of the batch's words, ~3 us
+    // per sweep and rank at L=4096 on 8 GPUs, against all-gathers every ~16 sweeps and aborts that drain the rest
+    // of a batch); one process scanning a whole lattice pays ~20 us per L=4096 sweep (r348), more than the ~3% the
+    // rejections cost there.  SV_DOMAIN_PREDICT=1 / 0 forces it on / off.
+    const char *np_env = getenv("SV_DOMAIN_PREDICT");
+    const bool predict = P.k > 1 && P.thr > 0 && V >= 256 &&
+                         (np_env ? np_env[0] == '1' : (d->comm != nullptr && d->nranks > 1));
+    // unpredicted batches stay short (an abort drains the rest of the batch); predicted ones run the full 64
+    const int batch = domain_batch(d, P), full = predict && !getenv("SV_DOMAIN_BATCH") ? DOMAIN_BATCH : batch;
+    auto &pred = d->pred;
+    sv_domain::Pred next;
+    if (pred.valid && pred.sw != 0) pred.valid = false;  // a scan is for the batch a call starts with, or its own
+    const Affine per_sweep = host_power(inc, 4 * (uint64_t)V);
+    if (predict && !d->d_scan) {
+        SV_HIP(hipMalloc(&d->d_scan, DOMAIN_BATCH * sizeof(u128)));
+        int least = 0, greatest = 0;
+        SV_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        SV_HIP(hipStreamCreateWithPriority(&d->scan_stream, hipStreamNonBlocking, least));
+        SV_HIP(hipEventCreateWithFlags(&d->ev_sum, hipEventDisableTiming));
+        SV_HIP(hipEventCreateWithFlags(&d->ev_scan, hipEventDisableTiming));
+    }
+    std::vector<u128> h_scan(DOMAIN_BATCH);
+    int predicted_batches = 0, aborts = 0;
     int sw = 0;
     while (sw < sweeps) {
-        const int count = std::min(batch, sweeps - sw);
+        int count = std::min(batch, sweeps - sw);
+        if (pred.valid && pred.sw == sw && pred.c.s.lo == cur.s.lo && pred.c.s.hi == cur.s.hi && pred.c.has == cur.has &&
+            pred.inc.lo == inc.lo && pred.inc.hi == inc.hi) {
+            count = std::min(sweeps - sw, pred.count);
+            add_predicted(skips, cur, specs, sw, count, pred.cand);
+            predicted_batches++;
+        }
+        pred.valid = false;
         Cursor c = cur;
         plan_sweeps(ctx, c, inc, specs, sw, count, skips, blocks, skipvec);
         upload_plan(ctx, blocks, skipvec);
         std::vector<char> hot(count);
         for (int k = 0; k < count; k++) hot[k] = hot_enabled() && hot_ok(P, &blocks[(size_t)k * nb]);
         for (auto &Tl : d->tiles) SV_HIP(hipMemsetAsync(Tl.sum, 0, sizeof(Summary), ctx->stream));
+        if (predict) SV_HIP(hipEventRecord(d->ev_sum, ctx->stream));
         const int cur0 = d->cur;
         auto fargs = [&](sv_domain_tile &Tl, int k, int in, int out) {
             FArgs A;
@@ -562,6 +710,41 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
             SV_HIP(hipStreamWaitEvent(ctx->stream, d->ev_interior, 0));
         }
         ctx->time_end(ev, count);
+        // scan the words of the next batch (from this batch's end cursor c) for NumPy rejections; this rank's share
+        // (past the end of the call: as many sweeps as this batch, for the batch the next call starts with)
+        next.valid = false;
+        const int ncount = sweeps - sw - count > 0 ? std::min(full, sweeps - sw - count) : std::min(full, count);
+        if (predict && ncount > 0) {
+            u128 sk = c.s;
+            for (int k = 0; k < ncount; k++) {
+                h_scan[k] = sk;
+                sk = apply(per_sweep, sk);
+            }
+            // on the low-priority stream, after this batch's summary was cleared; the gather waits for it
+            SV_HIP(hipStreamWaitEvent(d->scan_stream, d->ev_sum, 0));
+            SV_HIP(hipMemcpyAsync(d->d_scan, h_scan.data(), ncount * sizeof(u128), hipMemcpyHostToDevice, d->scan_stream));
+            const uint64_t total = (uint64_t)ncount * 2 * ((uint64_t)V + 2 * SCAN_MARGIN);
+            const int parts = d->comm ? d->nranks : 1, me = d->comm ? d->rank : 0;
+            ScanArgs a;
+            a.s_k = d->d_scan;
+            a.T = T;
+            a.V = (uint64_t)V;
+            a.lo = total * me / parts;
+            a.hi = total * (me + 1) / parts;
+            a.k = P.k;
+            a.thr = P.thr;
+            a.ncand = &d->tiles[0].sum->ncand;
+            a.cand = d->tiles[0].sum->cand;
+            const uint64_t lanes = (a.hi - a.lo + SCAN_CHUNK - 1) / SCAN_CHUNK;
+            if (lanes) scan_rejections<<<(unsigned)((lanes + 255) / 256), 256, 0, d->scan_stream>>>(a);
+            SV_HIP(hipEventRecord(d->ev_scan, d->scan_stream));
+            SV_HIP(hipStreamWaitEvent(ctx->stream, d->ev_scan, 0));
+            next.valid = true;
+            next.sw = sw + count < sweeps ? sw + count : 0;
+            next.count = ncount;
+            next.c = c;
+            next.inc = inc;
+        }
         SV_HIP(hipGetLastError());
         gather(d);
         AbortInfo a{0, {}};
@@ -576,8 +759,20 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
             fill_stats(d, skips, nb, sw, count, stats);
             cur = c;
             sw += count;
+            if (next.valid) {
+                next.cand.clear();
+                bool over = false;
+                for (const Summary &S : d->host_sum) {
+                    over |= S.ncand > (uint32_t)MAX_CAND;
+                    next.cand.insert(next.cand.end(), S.cand, S.cand + std::min<uint32_t>(S.ncand, MAX_CAND));
+                }
+                std::sort(next.cand.begin(), next.cand.end());
+                next.cand.erase(std::unique(next.cand.begin(), next.cand.end()), next.cand.end());
+                if (!over) pred = next;  // (an overflowing scan leaves the batch to the abort protocol)
+            }
             continue;
         }
+        aborts++;
         for (const Report &r : a.reports)
             if (r.block == OVERFLOW_BLOCK)
                 throw std::runtime_error("|n| exceeds the fused path's int32 LDS image (domain mode has no fallback)");
@@ -593,6 +788,9 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
         d->cur = (cur0 + bad) % d->R;
         sw += bad;
     }
+    if (getenv("SV_DEBUG_TIMING"))
+        fprintf(stderr, "[sv domain] %d sweeps, batch %d, depth %d, predicted batches %d, aborts %d\n", sweeps, batch,
+                d->depth, predicted_batches, aborts);
 }
 
 // Worldline (config 3 decomposed): one step = checkerboard PlaquetteUpdate sweep + CoexactUpdate
@@ -923,6 +1121,13 @@ int sv_domain_destroy(sv_domain *d) {
     if (d->halo_stream) (void)hipStreamSynchronize(d->halo_stream);
     if (d->comm) (void)ncclCommDestroy(d->comm);
     (void)hipFree(d->gathered);
+    (void)hipFree(d->d_scan);
+    if (d->scan_stream) {
+        (void)hipStreamSynchronize(d->scan_stream);
+        (void)hipStreamDestroy(d->scan_stream);
+    }
+    if (d->ev_sum) (void)hipEventDestroy(d->ev_sum);
+    if (d->ev_scan) (void)hipEventDestroy(d->ev_scan);
     (void)hipFree(d->d_strips);
     if (d->ev_interior) (void)hipEventDestroy(d->ev_interior);
     if (d->ev_boundary) (void)hipEventDestroy(d->ev_boundary);

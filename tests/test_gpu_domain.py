@@ -135,6 +135,31 @@ def test_deep_halo_depths(depth, tiles, oracle_lib, monkeypatch):
     assert [s.rejections for s in st] == [s.rejections for s in st_ref]
 
 
+@pytest.mark.parametrize('tiles', [(2, 2), (2, 4)])
+@pytest.mark.parametrize('pos_half', [(8 * 128 * 128 + 3 * 128 * 128 // 2 + 7, 0), (12 * 128 * 128 + 3 * 128 * 128 + 5, 1),
+                                      (16 * 128 * 128 + 2 * 128 * 128 + 128 * 128 // 4 - 1, 1)])
+def test_predicted_rejections(tiles, pos_half, oracle_lib, monkeypatch, capfd):
+    """Rejection prediction: the words of the next batch are scanned while a batch runs, so a NumPy Lemire rejection
+    in sweep 2, 3 or 4 (a colour-0 choice block, a colour-1 one, the last word of a colour-0 block) becomes a skip
+    list before its batch is planned and nothing aborts; the chain equals the oracle's."""
+    monkeypatch.setenv('SV_DOMAIN_BATCH', '2')
+    monkeypatch.setenv('SV_DOMAIN_PREDICT', '1')  # (on by default only with several RCCL ranks)
+    monkeypatch.setenv('SV_DEBUG_TIMING', '1')
+    N = 128
+    pos, half = pos_half
+    phi0, n0 = hot(N, N, 1, 5)
+    gen = crafted_generator(3, pos, half)
+    phi, n, st = run_domain(N, N, tiles, 0.4, 1, phi0, n0, 7, gen)
+    g = crafted_generator(3, pos, half)
+    p, m = phi0.copy(), n0.copy()
+    st_ref = oracle_lib.villain_neighborhood(N, 0.4, 1, p, m, 7, g)
+    assert sum(s.rejections for s in st_ref) >= 1
+    assert_same(phi, n, st, gen, p, m, st_ref, g)
+    assert [s.rejections for s in st] == [s.rejections for s in st_ref]
+    err = capfd.readouterr().err
+    assert '[sv domain] 7 sweeps' in err and 'aborts 0' in err, err
+
+
 def test_chunked_calls_continue_the_chain(oracle_lib):
     """Calls of 3 + 1 + 4 sweeps (ring index carried across calls) equal one call of 8."""
     N = 64
@@ -170,11 +195,13 @@ def test_equals_single_lattice_at_scale(tiles):
     assert sum(s.accepted for s in st) == G.accepted
 
 
-@pytest.mark.parametrize('batch', ['', '5'])
+@pytest.mark.parametrize('batch', ['', '5', 'predict'])
 def test_natural_rejections_bench_size(batch, monkeypatch):
     """L=4096 in 2 x 4 tiles for 96 sweeps: NumPy rejects ~1.6% of sweeps' draws somewhere, so the
     abort / replay protocol runs on real data; the chain equals the single-lattice one.  batch: as above."""
-    if batch:
+    if batch == 'predict':
+        monkeypatch.setenv('SV_DOMAIN_PREDICT', '1')  # the first batch aborts at sweep 3, later ones are predicted
+    elif batch:
         monkeypatch.setenv('SV_DOMAIN_BATCH', batch)
     N = 4096
     phi0, n0 = np.zeros((N, N)), np.zeros((2, N, N), dtype=np.int64)
@@ -187,10 +214,15 @@ def test_natural_rejections_bench_size(batch, monkeypatch):
     assert sum(s.accepted for s in st) == G.accepted
 
 
-@pytest.mark.parametrize('N,sweeps', [(64, 5), (1024, 3)])
-def test_rccl_loopback(N, sweeps, oracle_lib):
+@pytest.mark.parametrize('predict', ['0', '1'])
+@pytest.mark.parametrize('N,sweeps', [(64, 5), (1024, 3), (256, 40)])
+def test_rccl_loopback(N, sweeps, predict, oracle_lib, monkeypatch):
     """One rank, one tile, every halo message through ncclSend/ncclRecv to itself and the batch
-    summary through ncclAllGather: the RCCL code path of the multi-GPU run, on one GPU."""
+    summary (with the rejection scan's words) through ncclAllGather: the RCCL code path of the multi-GPU run, on one
+    GPU; N=256 over 40 sweeps in batches of 8 runs predicted batches."""
+    monkeypatch.setenv('SV_DOMAIN_PREDICT', predict)
+    if N == 256:
+        monkeypatch.setenv('SV_DOMAIN_BATCH', '8')
     phi0, n0 = hot(N, N, 1, N)
     gen = np.random.default_rng(N)
     phi, n, st = run_domain(N, N, (1, 1), 0.5, 1, phi0, n0, sweeps, gen, rccl=True)
