@@ -6,9 +6,10 @@
 //
 //     pack (8 halo messages) -> exchange -> unpack into the ghost frame -> fused sweep kernel.
 //
-// Because both colours are decided inside one launch there is ONE exchange per sweep.  Every draw is
-// addressed by its global NumPy stream position and the colouring by global coordinates, so the
-// decomposed chain is bit-identical to the single-lattice chain (and to the reference's).
+// Because both colours are decided inside one launch there is ONE exchange per sweep -- or one per K sweeps with
+// deep halos (villain_depth: a K-times deeper frame, each sweep of a group deciding the tile plus the ring its
+// successor reads).  Every draw is addressed by its global NumPy stream position and the colouring by global
+// coordinates, so the decomposed chain is bit-identical to the single-lattice chain (and to the reference's).
 //
 // Transport: tiles in the same process (one GPU emulating any tile grid -- the parity tests -- or a
 // tile grid dimension of 1) read each other's send buffers directly; tiles on other ranks exchange
@@ -16,9 +17,9 @@
 //
 // Rejections (NumPy's Lemire sampler rejecting a uint32, which shifts the rest of its block) are
 // found by whichever tile draws the position.  Each halo message carries its sender's abort flag,
-// so an abort spreads one tile-hop per sweep and every tile stops within D sweeps (D = tile-torus
-// radius); the tile states are kept in a ring of R = D + 2 buffers (one more for the opt-in split sweeps) so the input of the failing sweep
-// survives everywhere.  After each batch the ranks all-gather their reports (one collective per
+// so an abort spreads one tile-hop per exchange and every tile stops within D K sweeps (D = tile-torus
+// radius); the tile states are kept in a ring of R = D K + 2 buffers so the input of the failing sweep
+// survives everywhere.  With several ranks the rejections are mostly predicted (scan_rejections) and no abort happens.  After each batch the ranks all-gather their reports (one collective per
 // batch) and take the same replay decision as the single-lattice driver.
 #include <rccl/rccl.h>
 
