@@ -98,7 +98,16 @@ __device__ __forceinline__ HotDraws hot_draws_edge(const FArgs &A, int64_t gq, i
 struct HotEmpty {};
 // PH (counter-based mode) keeps no small-offset maps, row-advance maps or row bases: its LDS is 6 KB smaller, which
 // lets a fifth workgroup onto a CU
-template <bool PH>
+// OBSL (replica batches with inline observables): each lane's running sums over the strip live in LDS, added to by
+// no-return LDS atomics at every row store -- a wave reduction per row step cost ~25% of the sweep (r352), and the
+// same sums held in registers spilled (r353); full-row strips never need the second set of row bases, which makes
+// the room.  n0 and n1 sums share one 64-bit word (n0 + 2^32 n1, two's complement).
+struct ObsLane {
+    double act[256];
+    unsigned long long w2[256];
+    unsigned long long npk[256];
+};
+template <bool PH, bool OBSL = false>
 struct HotLDST {
     static constexpr int R = FusedGeom<4>::R;
     // the residuals r live from the colour-0 pass of step t (rows t+1..t+5) to the colour-1 pass of step t+4
@@ -112,9 +121,11 @@ struct HotLDST {
     nint n1[R][RW];
     std::conditional_t<PH, HotEmpty, SmallTab> small;
     std::conditional_t<PH, HotEmpty, Affine[3]> adv;
-    std::conditional_t<PH, HotEmpty, u128[4][32]> base;  // per wave: [8c + ty] block ty's base for the colour-c row at xb; [16 + ..] at xw
+    // per wave: [8c + ty] block ty's base for the colour-c row at xb; [16 + ..] at xw (edge strips of rows > SMALL_LDS)
+    std::conditional_t<PH, HotEmpty, std::conditional_t<OBSL, u128[4][16], u128[4][32]>> base;
     int32_t bad;
     double obs[4];     // OBS: the workgroup's sums of the inline observables
+    std::conditional_t<OBSL, ObsLane, HotEmpty> ol;
 };
 using HotLDS = HotLDST<false>;
 
@@ -129,7 +140,7 @@ using HotLDS = HotLDST<false>;
 // PH: the optional counter-based mode (SURVEY.md 8(b) sv_rng mode 1): every draw is Philox4x32-10 of (global site,
 // sweep, slot) -- no stream positions, row bases, jump tables or replays
 template <bool TILE, bool EDGE, bool FR = false, bool OBS = false, bool PH = false>
-__device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH> &Ls) {
+__device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS> &Ls) {
     static_assert(!(FR && TILE), "full-row replica strips are periodic");
     constexpr int NW = 4;
     constexpr int R = HotLDS::R, RR = HotLDS::RR;
@@ -205,6 +216,11 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH> &Ls) {
     }
     if (threadIdx.x == 0) s_bad = 0;
     if (OBS && threadIdx.x < 4) Ls.obs[threadIdx.x] = 0.0;
+    if constexpr (FR && OBS) {  // this lane's running sums (only this lane touches its slots)
+        Ls.ol.act[threadIdx.x] = 0.0;
+        Ls.ol.w2[threadIdx.x] = 0;
+        Ls.ol.npk[threadIdx.x] = 0;
+    }
 
     // per colour: the buffered-half flags and words of the choice blocks (equal within each fwd/bwd pair on
     // this kernel), uniform
@@ -321,7 +337,9 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH> &Ls) {
     auto store_rows = [&](int32_t ra) {
         if (SV_ABLATE & 8) return;
         const int32_t q = ra + wave;
-        double o_act = 0.0, o_w2 = 0.0, o_n0 = 0.0, o_n1 = 0.0;  // OBS partials (integers exact in f64)
+        double o_act = 0.0;  // OBS partials of this row step
+        int64_t o_w2 = 0;
+        int32_t o_n0 = 0, o_n1 = 0;
         if (q >= t0 && q < t1) {
             const int slot = (q - rbase) % R;
             const int64_t g0 = mrow(q) + x0;
@@ -350,25 +368,23 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH> &Ls) {
                         const double l0 = (0.0 + (s_phi[slot1][cx] - ph)) - TWO_PI * (double)s_n0[slot][cx];
                         const double l1 = (0.0 + (s_phi[slot][cxp(cx)] - ph)) - TWO_PI * (double)s_n1[slot][cx];
                         o_act += l0 * l0 + l1 * l1;
-                        const int64_t dn = ((int64_t)s_n1[slot1][cx] - s_n1[slot][cx]) -
-                                           ((int64_t)s_n0[slot][cxp(cx)] - s_n0[slot][cx]);
-                        o_w2 += (double)(dn * dn);
-                        o_n0 += (double)s_n0[slot][cx];
-                        o_n1 += (double)s_n1[slot][cx];
+                        // with the int16 image |n| < 2^14, so |dn| < 2^16 and dn^2 fits uint32
+                        using dint = std::conditional_t<SV_HOT_OCC4, int32_t, int64_t>;
+                        const dint dn = ((dint)s_n1[slot1][cx] - s_n1[slot][cx]) - ((dint)s_n0[slot][cxp(cx)] - s_n0[slot][cx]);
+                        o_w2 += SV_HOT_OCC4 ? (int64_t)(uint32_t)(dn * dn) : (int64_t)(dn * dn);
+                        o_n0 += s_n0[slot][cx];
+                        o_n1 += s_n1[slot][cx];
                     }
                 }
             }
         }
         if (OBS) {
-            o_act = wave_sum(o_act);
-            o_w2 = wave_sum(o_w2);
-            o_n0 = wave_sum(o_n0);
-            o_n1 = wave_sum(o_n1);
-            if (lane == 0) {
-                atomicAdd(&Ls.obs[0], o_act);
-                atomicAdd(&Ls.obs[1], o_w2);
-                atomicAdd(&Ls.obs[2], o_n0);
-                atomicAdd(&Ls.obs[3], o_n1);
+            // this lane's running sums over the strip (LDS, no-return atomics; reduced once at the strip's end)
+            if constexpr (FR && OBS) {
+                atomicAdd(&Ls.ol.act[threadIdx.x], o_act);
+                atomicAdd(&Ls.ol.w2[threadIdx.x], (unsigned long long)o_w2);
+                atomicAdd(&Ls.ol.npk[threadIdx.x],
+                          (unsigned long long)((int64_t)o_n0 + (int64_t)((uint64_t)(int64_t)o_n1 << 32)));
             }
         }
     };
@@ -577,7 +593,19 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH> &Ls) {
     }
     if (s_bad && threadIdx.x == 0) report(A.S, A.sweep, OVERFLOW_BLOCK, 0, (uint32_t)rep);
     flush_stats(FR ? A.stat + (int64_t)rep * A.rep_stat : A.stat, acc_count, psum);
-    if (OBS) {
+    if constexpr (FR && OBS) {
+        // |sum n0|, |sum n1| <= 2 sites x 2^14 x strip rows < 2^31: the packed halves decode exactly
+        const uint64_t pk = Ls.ol.npk[threadIdx.x];
+        const int32_t a_n0 = (int32_t)(uint32_t)pk;
+        const int64_t a_n1 = (int64_t)(pk - (uint64_t)(int64_t)a_n0) >> 32;
+        const double w_act = wave_sum(Ls.ol.act[threadIdx.x]), w_w2 = wave_sum((double)Ls.ol.w2[threadIdx.x]);
+        const double w_n0 = wave_sum((double)a_n0), w_n1 = wave_sum((double)a_n1);
+        if (lane == 0) {
+            atomicAdd(&Ls.obs[0], w_act);
+            atomicAdd(&Ls.obs[1], w_w2);
+            atomicAdd(&Ls.obs[2], w_n0);
+            atomicAdd(&Ls.obs[3], w_n1);
+        }
         __syncthreads();
         if (threadIdx.x < 4) unsafeAtomicAdd(&A.obs[(int64_t)rep * A.rep_obs + threadIdx.x], Ls.obs[threadIdx.x]);
     }
@@ -608,7 +636,7 @@ template __global__ void villain_sweep_hot<true>(FArgs);
 // replica batches of full-row lattices (config 5), with or without the inline observables
 template <bool OBS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4 ? 4 : 3))) void villain_sweep_hot_fr(FArgs A) {
-    __shared__ HotLDS Ls;
+    __shared__ HotLDST<false, OBS> Ls;
     // the replica this workgroup serves (the mapping hot_body makes), to pick the draw form
     int b = blockIdx.x;
     {
