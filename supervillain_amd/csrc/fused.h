@@ -299,6 +299,25 @@ __device__ __forceinline__ Draws draws_general(const FArgs &A, const Rep &RP, in
     return D;
 }
 
+// The paired draws swap one 32-bit half with the neighbouring lane: `send` of lane - 1 (half = 1) or lane + 1
+// (half = 0), wrapping around the wave.  DPP wave rotates are one VALU move each (on gfx950 wave_ror:1 reads lane
+// i - 1 and wave_rol:1 lane i + 1, scripts/perf/dpp_check.hip) where ds_bpermute is an LDS round trip the draw
+// waits on.  All 64 lanes execute the draws (inactive sites only discard their results).
+#ifndef SV_DPP_PAIR
+#define SV_DPP_PAIR 1
+#endif
+__device__ __forceinline__ uint32_t pair_exchange(uint32_t send, uint32_t half, int lane) {
+#if SV_DPP_PAIR
+    (void)lane;
+    const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, 0x13C /* wave_ror:1 */, 0xF, 0xF, false);
+    const uint32_t next = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, 0x134 /* wave_rol:1 */, 0xF, 0xF, false);
+    return half ? prev : next;
+#else
+    const int partner = half ? ((lane - 1) & 63) : lane + 1;
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(partner << 2, (int)send);
+#endif
+}
+
 // Fast draws for interior strips (no wrapped columns, no skips, equal buffers within each
 // forward/backward pair).  4 compositions per site: the fwd and bwd choice blocks of a direction
 // read the SAME u64 word for two adjacent lanes (its two 32-bit halves), so each lane of a pair
@@ -373,8 +392,7 @@ __device__ __forceinline__ Draws draws_fastp(const FArgs &A, const Rep &RP, int 
             const uint64_t X = xsl_rr(st);
             // lo lanes computed the fwd word (send its high half), hi lanes the bwd word (send its low half)
             const uint32_t send = half ? (uint32_t)X : (uint32_t)(X >> 32);
-            const int partner = half ? ((lane - 1) & 63) : lane + 1;
-            const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute(partner << 2, (int)send);
+            const uint32_t got = pair_exchange(send, half, lane);
             const uint32_t wf = half ? got : (uint32_t)X;
             const uint32_t wb = half ? (uint32_t)(X >> 32) : got;
             if (active) {
@@ -419,8 +437,7 @@ __device__ __forceinline__ Draws draws_fast(const FArgs &A, const Rep &RP, int c
             const uint64_t X = xsl_rr(st);
             // lo lanes computed the fwd word (send its high half), hi lanes the bwd word (send its low half)
             const uint32_t send = half ? (uint32_t)X : (uint32_t)(X >> 32);
-            const int partner = half ? (lane == 0 ? 63 : lane - 1) : lane + 1;
-            const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute(partner << 2, (int)send);
+            const uint32_t got = pair_exchange(send, half, lane);
             const uint32_t wf = half ? got : (uint32_t)X;
             const uint32_t wb = half ? (uint32_t)(X >> 32) : got;
             if (active) {

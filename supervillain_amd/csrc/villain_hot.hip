@@ -55,8 +55,7 @@ __device__ __forceinline__ HotDraws hot_draws_paired(const FArgs &A, int32_t lan
         const uint64_t X = xsl_rr(hot_apply(sm, (pk >> (14 + 7 * mu)) & (SMALL_LDS - 1), half ? bs[3 + 2 * mu] : bs[2 + 2 * mu]));
         // lo lanes computed the fwd word (send its high half), hi lanes the bwd word (send its low half)
         const uint32_t send = half ? (uint32_t)X : (uint32_t)(X >> 32);
-        const int partner = half ? ((lane - 1) & 63) : lane + 1;
-        const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute(partner << 2, (int)send);
+        const uint32_t got = pair_exchange(send, half, lane);
         D.w[2 * mu] = half ? got : (uint32_t)X;
         D.w[2 * mu + 1] = half ? (uint32_t)(X >> 32) : got;
     }

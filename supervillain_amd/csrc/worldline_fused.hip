@@ -271,8 +271,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS &Ls) {
             const uint64_t X = xsl_rr(hot_apply(s_small, (pk[p] >> 7) & (SMALL_LDS - 1), half ? bs[2] : bs[1]));
             // lo lanes computed the change_m word (send its high half), hi lanes the change_v word
             const uint32_t send = half ? (uint32_t)X : (uint32_t)(X >> 32);
-            const int partner = half ? ((lane - 1) & 63) : lane + 1;
-            const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute(partner << 2, (int)send);
+            const uint32_t got = pair_exchange(send, half, lane);
             wm = half ? got : (uint32_t)X;
             wv = half ? (uint32_t)(X >> 32) : got;
         } else {
