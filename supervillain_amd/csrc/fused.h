@@ -103,7 +103,8 @@ __device__ __forceinline__ int32_t wrapN(int32_t v, int32_t N) {
 #endif
 #ifndef SV_ABLATE
 #define SV_ABLATE 0  // timing experiments only: 1 = no exp, 2 = no RNG compositions, 4 = no wrapped-column jumps,
-                     // 8 = no HBM stores, 16 = no HBM loads, 64 = no choice draws
+                     // 8 = no HBM stores, 16 = no HBM loads, 32 = no barriers, 64 = no choice draws,
+                     // 256 / 512 = n kept in HBM as int32 / int16 (villain_sweep_hot; valid from a cold start only)
 #endif
 #ifndef SV_EXP_OCML
 #define SV_EXP_OCML 1
