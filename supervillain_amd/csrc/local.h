@@ -197,9 +197,8 @@ static inline void run_batches(sv_ctx *ctx, const std::vector<BlockSpec> &specs,
             Cursor c = cur;
             plan_sweeps(ctx, c, inc, specs, sw, count, skips, blocks, skipvec);
             upload_plan(ctx, blocks, skipvec);
-            clear_abort(ctx);
             ctx->ensure_stats(count);
-            SV_HIP(hipMemsetAsync(ctx->d_stats, 0, count * sizeof(sv_stats), ctx->stream));
+            reset_batch(ctx, ctx->d_stats, count * sizeof(sv_stats));
             hipEvent_t ev;
             ctx->time_begin(&ev);
             for (int k = 0; k < count; k++) launch_sweep(k, ctx->d_blocks + (size_t)k * nb, ctx->d_stats + k);

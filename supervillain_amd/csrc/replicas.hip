@@ -235,10 +235,8 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         if (!B.hskip.empty())
             SV_HIP(hipMemcpyAsync(ctx->d_skips, B.hskip.data(), B.hskip.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
                                   ctx->stream));
-        SV_HIP(hipMemsetAsync(ctx->d_abort, 0, sizeof(int32_t), ctx->stream));
-        SV_HIP(hipMemsetAsync(ctx->d_nreport, 0, sizeof(uint32_t), ctx->stream));
-        SV_HIP(hipMemsetAsync(b->d_stats, 0, (size_t)R * count * sizeof(sv_stats), ctx->stream));
-        if (obs) SV_HIP(hipMemsetAsync(b->d_obs, 0, (size_t)R * count * 4 * sizeof(double), ctx->stream));
+        reset_batch(ctx, b->d_stats, (size_t)R * count * sizeof(sv_stats), obs ? b->d_obs : nullptr,
+                    obs ? (size_t)R * count * 4 * sizeof(double) : 0);
         // A sweep runs on the fast-draw kernel (villain_sweep_hot_fr) when no replica's choice blocks of that sweep
         // carry a skip (the closed-form replicas have none; the host-planned ones are checked), else on the general
         // fused kernel.  Within a skip-free sweep a replica's four choice blocks start on the same half-word parity

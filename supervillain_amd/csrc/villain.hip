@@ -748,6 +748,24 @@ AbortInfo read_abort_stats(sv_ctx *ctx, int count, sv_stats *stats) {
     return a;
 }
 
+__global__ __launch_bounds__(256) void reset_batch_kernel(int32_t *abort, uint32_t *nreport, uint64_t *a, int64_t na,
+                                                         uint64_t *b, int64_t nb) {
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
+    if (t == 0) {
+        *abort = 0;
+        *nreport = 0;
+    }
+    for (int64_t i = t; i < na; i += stride) a[i] = 0;
+    for (int64_t i = t; i < nb; i += stride) b[i] = 0;
+}
+
+void reset_batch(sv_ctx *ctx, void *a, size_t a_bytes, void *b, size_t b_bytes) {
+    if (a_bytes % 8 || b_bytes % 8) throw std::logic_error("reset_batch: sizes must be multiples of 8 bytes");
+    const int64_t na = (int64_t)(a_bytes / 8), nb = (int64_t)(b_bytes / 8), n = std::max(na, nb);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 256));
+    reset_batch_kernel<<<grid, 256, 0, ctx->stream>>>(ctx->d_abort, ctx->d_nreport, (uint64_t *)a, na, (uint64_t *)b, nb);
+}
+
 void clear_abort(sv_ctx *ctx) {
     SV_HIP(hipMemsetAsync(ctx->d_abort, 0, sizeof(int32_t), ctx->stream));
     SV_HIP(hipMemsetAsync(ctx->d_nreport, 0, sizeof(uint32_t), ctx->stream));
@@ -817,8 +835,7 @@ void run_generic(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, 
             Cursor c = cur;
             plan_sweeps(ctx, c, inc, specs, sw, 1, skips, blocks, skipvec);
             upload_plan(ctx, blocks, skipvec);
-            clear_abort(ctx);
-            SV_HIP(hipMemsetAsync(ctx->d_stats, 0, sizeof(sv_stats), ctx->stream));
+            reset_batch(ctx, ctx->d_stats, sizeof(sv_stats));
             const int grid = (int)std::min<int64_t>((V + 255) / 256, 4096);
             villain_phi_normalize<<<grid, 256, 0, ctx->stream>>>(st->N, phi, ctx->d_abort);
             villain_r_init<<<grid, 256, 0, ctx->stream>>>(st->N, phi, n, st->r, ctx->d_abort);
@@ -889,9 +906,8 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         auto tp1 = std::chrono::steady_clock::now();
         if (dbg) fprintf(stderr, "[sv] plan %d sweeps: %.1f us\n", count, std::chrono::duration<double, std::micro>(tp1 - tp0).count());
         upload_plan(ctx, blocks, skipvec);
-        clear_abort(ctx);
         ctx->ensure_stats(count);
-        SV_HIP(hipMemsetAsync(ctx->d_stats, 0, count * sizeof(sv_stats), ctx->stream));
+        reset_batch(ctx, ctx->d_stats, count * sizeof(sv_stats));
         const int cur0 = st->cur;
         hipEvent_t ev;
         const bool per_launch = ctx->timing_mode == 2;  // events around every launch, else around the batch
@@ -1161,9 +1177,8 @@ int sv_villain_run_philox(sv_villain *st, double kappa, int64_t W, double interv
         const int BATCH = 64;
         for (int sw = 0; sw < sweeps;) {
             const int count = std::min(BATCH, sweeps - sw);
-            clear_abort(ctx);
             ctx->ensure_stats(count);
-            SV_HIP(hipMemsetAsync(ctx->d_stats, 0, count * sizeof(sv_stats), ctx->stream));
+            reset_batch(ctx, ctx->d_stats, count * sizeof(sv_stats));
             hipEvent_t ev;
             ctx->time_begin(&ev);
             for (int k = 0; k < count; k++) {

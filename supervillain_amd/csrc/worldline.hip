@@ -425,11 +425,6 @@ void wupload(sv_ctx *ctx, const std::vector<Block> &blocks, const std::vector<ui
                               ctx->stream));
 }
 
-void wclear(sv_ctx *ctx) {
-    SV_HIP(hipMemsetAsync(ctx->d_abort, 0, sizeof(int32_t), ctx->stream));
-    SV_HIP(hipMemsetAsync(ctx->d_nreport, 0, sizeof(uint32_t), ctx->stream));
-}
-
 bool wcheck(sv_ctx *ctx, std::vector<Report> &reps) {
     int32_t ab = 0;
     uint32_t nrep = 0;
@@ -528,11 +523,10 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
             Cursor c = cur;
             wplan(c, inc, specs, sw, count, skips, blocks, skipvec);
             wupload(ctx, blocks, skipvec);
-            wclear(ctx);
             ctx->ensure_stats((size_t)count * nstat);
-            SV_HIP(hipMemsetAsync(ctx->d_stats, 0, (size_t)count * nstat * sizeof(sv_stats), ctx->stream));
             StatStripe *ss = (StatStripe *)st->stripes;
-            SV_HIP(hipMemsetAsync(ss, 0, (size_t)count * nstat * NSTRIPE * sizeof(StatStripe), ctx->stream));
+            svh::reset_batch(ctx, ctx->d_stats, (size_t)count * nstat * sizeof(sv_stats), ss,
+                        (size_t)count * nstat * NSTRIPE * sizeof(StatStripe));
             hipEvent_t ev;
             ctx->time_begin(&ev);
             for (int k = 0; k < count; k++)
@@ -920,10 +914,8 @@ int sv_worldline_plaquette_ordered_run(sv_worldline *st, double kappa, double W_
             Cursor c = cur;
             wplan(c, inc, specs, 0, 1, skips, blocks, skipvec);
             wupload(ctx, blocks, skipvec);
-            wclear(ctx);
-            SV_HIP(hipMemsetAsync(ctx->d_stats, 0, sizeof(sv_stats), ctx->stream));
             StatStripe *ss = (StatStripe *)st->stripes;
-            SV_HIP(hipMemsetAsync(ss, 0, NSTRIPE * sizeof(StatStripe), ctx->stream));
+            svh::reset_batch(ctx, ctx->d_stats, sizeof(sv_stats), ss, NSTRIPE * sizeof(StatStripe));
             if (st->v_is_float)
                 plaquette_f_init<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f);
             else
