@@ -160,6 +160,30 @@ def test_predicted_rejections(tiles, pos_half, oracle_lib, monkeypatch, capfd):
     assert '[sv domain] 7 sweeps' in err and 'aborts 0' in err, err
 
 
+@pytest.mark.parametrize('interval_n,W,depth', [(2, 1, '4'), (6, 2, '3'), (6, 1, '8')])
+def test_predicted_rejections_other_choice_counts(interval_n, W, depth, oracle_lib, monkeypatch, capfd):
+    """Choice over 5 or 13 values (NumPy thresholds 1 and 9), W = 2, depths 3 / 4 / 8: a forced rejection in sweep 3
+    is predicted (no abort) and the decomposed chain equals the oracle's."""
+    monkeypatch.setenv('SV_DOMAIN_BATCH', '2')
+    monkeypatch.setenv('SV_DOMAIN_PREDICT', '1')
+    monkeypatch.setenv('SV_DOMAIN_DEPTH', depth)
+    monkeypatch.setenv('SV_DEBUG_TIMING', '1')
+    N = 128
+    V = N * N
+    pos = 12 * V + 3 * V + V // 3
+    phi0, n0 = hot(N, N, W, 17)
+    gen = crafted_generator(11, pos, 1)
+    phi, n, st = run_domain(N, N, (2, 4), 0.35, W, phi0, n0, 6, gen, interval_n=interval_n)
+    g = crafted_generator(11, pos, 1)
+    p, m = phi0.copy(), n0.copy()
+    st_ref = oracle_lib.villain_neighborhood(N, 0.35, W, p, m, 6, g, interval_n=interval_n)
+    assert sum(s.rejections for s in st_ref) >= 1
+    assert_same(phi, n, st, gen, p, m, st_ref, g)
+    assert [s.rejections for s in st] == [s.rejections for s in st_ref]
+    err = capfd.readouterr().err
+    assert '[sv domain] 6 sweeps' in err and 'aborts 0' in err, err
+
+
 def test_chunked_calls_continue_the_chain(oracle_lib):
     """Calls of 3 + 1 + 4 sweeps (ring index carried across calls) equal one call of 8."""
     N = 64
