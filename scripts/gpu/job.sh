@@ -1,7 +1,11 @@
 source scripts/gpu/guard.sh
-T=${1:-r363}
+T=${1:-r367}
 O=gpurun_out/$T
 mkdir -p $O
 export TMPDIR=/tmp
-step tests timeout -k 10 600 python -u -m pytest tests/test_gpu_domain.py -x -q -k "other_choice or predicted" --timeout 300 --timeout-method thread > $O/tests.log 2>&1
-tail -15 $O/tests.log
+for rep in 1 2 3; do
+for nw in 4 8; do
+SV_SIZES=2048x1024 SV_HOT_NW=$nw step d$nw timeout -k 10 300 python scripts/perf/deep_halo.py 4 > $O/d${nw}_$rep.log 2>&1
+grep us/sweep $O/d${nw}_$rep.log | sed "s/^/nw$nw /"
+done
+done

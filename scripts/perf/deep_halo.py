@@ -12,7 +12,8 @@ sys.path.insert(0, '.')
 from supervillain_amd.domain import VillainDomain, ghost_frame, unique_id  # noqa: E402
 
 depths = sys.argv[1:] or ['1', '2', '4', '8']
-for Nt, Nx in [(2048, 1024), (4096, 2048), (4096, 4096)]:
+for Nt, Nx in ([tuple(int(v) for v in os.environ['SV_SIZES'].split('x'))] if os.environ.get('SV_SIZES') else
+               [(2048, 1024), (4096, 2048), (4096, 4096)]):
     for loop in (True, False):
         for K in depths:
             os.environ['SV_DOMAIN_DEPTH'] = K

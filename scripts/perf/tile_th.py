@@ -9,7 +9,7 @@ import numpy as np
 sys.path.insert(0, '.')
 from supervillain_amd.domain import VillainDomain  # noqa: E402
 
-sizes = [(2048, 1024), (4096, 2048), (4096, 4096)]
+sizes = [tuple(int(v) for v in os.environ['SV_SIZES'].split('x')) ] if os.environ.get('SV_SIZES') else [(2048, 1024), (4096, 2048), (4096, 4096)]
 warm = VillainDomain(4096, 4096, (1, 1), kappa=0.5, W=1)  # clocks to steady state before the first timing
 warm.cold()
 warm.run(2000, np.random.default_rng(9))

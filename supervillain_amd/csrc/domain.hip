@@ -543,7 +543,15 @@ int domain_batch_q(const sv_domain *d, double q) {
 // the shortest height (>= 20 rows, a multiple of 4) that keeps the same number of rounds.  Measured (r343, one
 // MI355X, one periodic tile): 2048 x 1024 at 52 / 36 (the single-lattice rule) / 20 rows 72.2 / 65.0 / 55.9 us per
 // sweep; 4096 x 2048 at 52 / 36 152.8 / 144.9 us; 4096^2 (three rounds) keeps 52.  SV_FUSED_TH overrides.
-int domain_th(const sv_domain *d, int nsx) {
+//
+// 8-wave strips.  When even 52-row strips leave the tile short of one round and 40-row strips of 8 waves (8 rows per
+// step, 2 workgroups per CU) fill at most one round of those slots, the tile runs villain_sweep_hot with 8 waves and
+// 40-row strips: half the halo rows per row decided.  Measured (r365, one periodic tile): 2048 x 1024 (the per-GPU
+// tile at N = 8) 56.0 us with 4 waves x 20 rows, 52.7-52.9 us with 8 waves x 40 rows; 2048 x 2048 75.9 us with 4
+// waves x 36 rows, 78.1-99.6 us with 8 waves (kept at 4); the L=4096 single lattice 240 us with 4 waves, 260-279 us
+// with 8 (r364).  *nw8 is set when the 8-wave form is chosen.
+int domain_th(const sv_domain *d, int nsx, int *nw8 = nullptr) {
+    if (nw8) *nw8 = 0;
     if (getenv("SV_FUSED_TH")) return fused_th(d->Ht, nsx);
     static const int slots = [] {
         int dev = 0;
@@ -553,6 +561,11 @@ int domain_th(const sv_domain *d, int nsx) {
     }();
     auto wgs = [&](int th) { return (int64_t)nsx * ((d->Ht + th - 1) / th); };
     const int64_t rounds = (wgs(52) + slots - 1) / slots;
+    const char *nwe = getenv("SV_HOT_NW");
+    if (nw8 && !(nwe && atoi(nwe) == 4) && hot_enabled() && rounds == 1 && wgs(40) <= slots / 2) {
+        *nw8 = 1;
+        return 40;
+    }
     if (rounds > 2) return fused_th(d->Ht, nsx);
     int th = 52;
     while (th > 20 && wgs(th - 4) <= rounds * slots) th -= 4;
@@ -576,10 +589,14 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
     const int nb = (int)specs.size();
     constexpr int NWv = 4;
     const int nsx = (d->Wt + FW_MAX - 1) / FW_MAX;
-    const int TH = domain_th(d, nsx);
+    int nw8 = 0;
+    const int TH = domain_th(d, nsx, &nw8);
     const int nsy = (d->Ht + TH - 1) / TH;
     const Affine adv[3] = {host_power(inc, (uint64_t)NWv * d->Nx), host_power(inc, (uint64_t)NWv * d->Nx / 2),
                            host_power(inc, (uint64_t)NWv * d->Nx / 4)};
+    const int hot_nw = nw8 ? 8 : hot_waves(TH);  // villain_sweep_hot with 8 rows per step (domain_th)
+    const Affine adv8[3] = {host_power(inc, 8 * (uint64_t)d->Nx), host_power(inc, 8 * (uint64_t)d->Nx / 2),
+                            host_power(inc, 8 * (uint64_t)d->Nx / 4)};
     SkipMap skips;
     std::vector<Block> blocks;
     std::vector<uint32_t> skipvec;
@@ -646,6 +663,12 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
             A.S = DevScratch{&Tl.sum->abort, &Tl.sum->nreport, Tl.sum->reports};
             A.sweep = (uint32_t)k;
             farg_single(A, nsx, nsy);
+            if (hot[k] && hot_nw == 8) {
+                A.hot_nw = 8;
+                A.adv[0] = adv8[0];
+                A.adv[1] = adv8[1];
+                A.adv[2] = adv8[2];
+            }
             return A;
         };
         hipEvent_t ev;

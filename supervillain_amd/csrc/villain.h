@@ -63,6 +63,8 @@ struct FArgs {
     // TILE: the window of the launch's region whose sites are counted in the statistics, [r0, r1) x [c0, c1) in
     // region coordinates (domain.hip's deep halos run sweeps over a tile extended by a ring it does not own)
     int32_t own_r0 = -(1 << 30), own_r1 = 1 << 30, own_c0 = -(1 << 30), own_c1 = 1 << 30;
+    // villain_sweep_hot: waves (rows per step) of a workgroup, 4 or 8 (adv must then advance 8 rows; TH % 8 == 0)
+    int32_t hot_nw = 4;
 };
 
 }  // namespace sv
@@ -98,6 +100,7 @@ int fused_th(int32_t N, int nsx);  // rows per strip (SV_FUSED_TH overrides)
 // villain_sweep_fused<4, true> otherwise
 void launch_fused_tile(const FArgs &A, int grid, hipStream_t stream, bool hot);
 bool hot_enabled();  // false when SV_HOT=0
+int hot_waves(int TH);  // waves per workgroup of villain_sweep_hot for strips of TH rows (4, or 8)
 // launch villain_sweep_fused<4, false, obs> over a replica batch (grid = replicas * tiles_per_rep)
 void launch_fused_batch(const FArgs &A, int grid, bool obs, hipStream_t stream);
 // villain_hot.hip: whether the fast-draw kernel covers the sweep whose 11 descriptors start at `blocks`,

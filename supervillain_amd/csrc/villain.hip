@@ -627,6 +627,15 @@ void launch_fused_tile(const FArgs &A, int grid, hipStream_t stream, bool hot) {
     else villain_sweep_fused<4, true, false, false><<<grid, 4 * 64, 0, stream>>>(A);
 }
 
+// Waves per workgroup of villain_sweep_hot for strips of TH rows: SV_HOT_NW=8 (experiments) takes 8 when TH allows
+int hot_waves(int TH) {
+    static const int nw = [] {
+        const char *e = getenv("SV_HOT_NW");
+        return e && atoi(e) == 8 ? 8 : 4;
+    }();
+    return nw == 8 && TH % 8 == 0 ? 8 : 4;
+}
+
 bool hot_enabled() {  // SV_HOT=0: every sweep on villain_sweep_fused (A/B measurements)
     static const bool on = [] {
         const char *e = getenv("SV_HOT");
@@ -892,6 +901,10 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     if ((int64_t)NWv * N % 4) throw std::invalid_argument("fused path needs NW*N divisible by 4");
     const Affine adv[3] = {host_power(inc, (uint64_t)NWv * N), host_power(inc, (uint64_t)NWv * N / 2),
                            host_power(inc, (uint64_t)NWv * N / 4)};
+    // villain_sweep_hot with 8 waves per workgroup (8 rows per step) when the strips allow it
+    const int hot_nw = hot_waves(TH);
+    const Affine adv8[3] = {host_power(inc, 8 * (uint64_t)N), host_power(inc, 8 * (uint64_t)N / 2),
+                            host_power(inc, 8 * (uint64_t)N / 4)};
     SkipMap skips;
     std::vector<Block> blocks;
     std::vector<uint32_t> skipvec;
@@ -935,7 +948,15 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             A.S = scratch(ctx);
             A.sweep = (uint32_t)k;
             farg_single(A, nsx, nsy);
-            if (use_hot && NWv == 4 && hot_ok(P, &blocks[(size_t)k * nb])) launch_hot(A, grid, ctx->stream);
+            if (use_hot && NWv == 4 && hot_ok(P, &blocks[(size_t)k * nb])) {
+                if (hot_nw == 8) {
+                    A.hot_nw = 8;
+                    A.adv[0] = adv8[0];
+                    A.adv[1] = adv8[1];
+                    A.adv[2] = adv8[2];
+                }
+                launch_hot(A, grid, ctx->stream);
+            }
             else if (NWv == 6) villain_sweep_fused<6, false, false, false><<<grid, 6 * 64, 0, ctx->stream>>>(A);
 #if SV_K3
             else if (P.k == 3) villain_sweep_fused<4, false, false, false, true><<<grid, 4 * 64, 0, ctx->stream>>>(A);

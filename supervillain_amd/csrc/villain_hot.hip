@@ -106,12 +106,12 @@ struct ObsLane {
     unsigned long long w2[256];
     unsigned long long npk[256];
 };
-template <bool PH, bool OBSL = false>
+template <bool PH, bool OBSL = false, int NWL = 4>
 struct HotLDST {
-    static constexpr int R = FusedGeom<4>::R;
+    static constexpr int R = FusedGeom<NWL>::R;
     // the residuals r live from the colour-0 pass of step t (rows t+1..t+5) to the colour-1 pass of step t+4
     // (which reads row t+4 again): NW + 2 rows
-    static constexpr int RR = SV_HOT_OCC4 ? 4 + 2 : R;
+    static constexpr int RR = SV_HOT_OCC4 ? NWL + 2 : R;
     using nint = std::conditional_t<SV_HOT_OCC4, int16_t, int32_t>;  // hot_ok / commit bound |n|
     double phi[R][RW];
     double r0[RR][RW];
@@ -121,7 +121,7 @@ struct HotLDST {
     std::conditional_t<PH, HotEmpty, SmallTab> small;
     std::conditional_t<PH, HotEmpty, Affine[3]> adv;
     // per wave: [8c + ty] block ty's base for the colour-c row at xb; [16 + ..] at xw (edge strips of rows > SMALL_LDS)
-    std::conditional_t<PH, HotEmpty, std::conditional_t<OBSL, u128[4][16], u128[4][32]>> base;
+    std::conditional_t<PH, HotEmpty, std::conditional_t<OBSL, u128[NWL][16], u128[NWL][32]>> base;
     int32_t bad;
     double obs[4];     // OBS: the workgroup's sums of the inline observables
     std::conditional_t<OBSL, ObsLane, HotEmpty> ol;
@@ -138,11 +138,12 @@ using HotLDS = HotLDST<false>;
 // replica draws unpaired (the EDGE form).  OBS: the inline observables fused into the row stores.
 // PH: the optional counter-based mode (SURVEY.md 8(b) sv_rng mode 1): every draw is Philox4x32-10 of (global site,
 // sweep, slot) -- no stream positions, row bases, jump tables or replays
-template <bool TILE, bool EDGE, bool FR = false, bool OBS = false, bool PH = false>
-__device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS> &Ls) {
+template <bool TILE, bool EDGE, bool FR = false, bool OBS = false, bool PH = false, int NWT = 4>
+__device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, NWT> &Ls) {
     static_assert(!(FR && TILE), "full-row replica strips are periodic");
-    constexpr int NW = 4;
-    constexpr int R = HotLDS::R, RR = HotLDS::RR;
+    static_assert(NWT == 4 || (NWT == 8 && !FR && !PH), "8-wave strips: single lattices and tiles");
+    constexpr int NW = NWT;
+    constexpr int R = HotLDST<PH, FR && OBS, NWT>::R, RR = HotLDST<PH, FR && OBS, NWT>::RR;
     constexpr int PF = RW / 64;
     auto &s_phi = Ls.phi;
     auto &s_r0 = Ls.r0;
@@ -610,9 +611,9 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS> 
     }
 }
 
-template <bool TILE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4 ? 4 : 3))) void villain_sweep_hot(FArgs A) {
-    __shared__ HotLDS Ls;
+template <bool TILE, int NWT>
+__global__ __launch_bounds__(NWT * 64) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4 ? 4 : 3))) void villain_sweep_hot(FArgs A) {
+    __shared__ HotLDST<false, false, NWT> Ls;
     // the strip this workgroup owns (the same mapping hot_body makes), to pick the body
     int b = blockIdx.x;
     {
@@ -625,12 +626,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4
     const int32_t x0 = (int32_t)((int64_t)ix * A.G.Wt / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * A.G.Wt / A.nsx);
     const int32_t gx0 = wrapN(A.G.X0 + x0, A.G.Nx);
     const bool interior = gx0 >= 4 && gx0 + (x1 - x0) + 2 < A.G.Nx;
-    if (__builtin_amdgcn_readfirstlane((int)interior)) hot_body<TILE, false>(A, Ls);
-    else hot_body<TILE, true>(A, Ls);
+    if (__builtin_amdgcn_readfirstlane((int)interior)) hot_body<TILE, false, false, false, false, NWT>(A, Ls);
+    else hot_body<TILE, true, false, false, false, NWT>(A, Ls);
 }
 
-template __global__ void villain_sweep_hot<false>(FArgs);
-template __global__ void villain_sweep_hot<true>(FArgs);
+template __global__ void villain_sweep_hot<false, 4>(FArgs);
+template __global__ void villain_sweep_hot<true, 4>(FArgs);
+template __global__ void villain_sweep_hot<false, 8>(FArgs);
+template __global__ void villain_sweep_hot<true, 8>(FArgs);
 
 // replica batches of full-row lattices (config 5), with or without the inline observables
 template <bool OBS>
@@ -693,10 +696,17 @@ void launch_hot_fr(const FArgs &A, int grid, bool obs, hipStream_t stream) {
 void launch_hot_ph(const FArgs &A, int grid, hipStream_t stream) { villain_sweep_hot_ph<<<grid, 4 * 64, 0, stream>>>(A); }
 
 void launch_hot(const FArgs &A, int grid, hipStream_t stream) {
-    if (A.G.org == 0 && A.G.pitch == A.G.Nx && A.G.T0 == 0 && A.G.X0 == 0 && A.G.Ht == A.G.Nt && A.G.Wt == A.G.Nx)
-        villain_sweep_hot<false><<<grid, 4 * 64, 0, stream>>>(A);
-    else
-        villain_sweep_hot<true><<<grid, 4 * 64, 0, stream>>>(A);
+    const bool periodic =
+        A.G.org == 0 && A.G.pitch == A.G.Nx && A.G.T0 == 0 && A.G.X0 == 0 && A.G.Ht == A.G.Nt && A.G.Wt == A.G.Nx;
+    if (A.hot_nw == 8) {
+        if (A.TH % 8) throw std::logic_error("8-wave strips need a multiple of 8 rows");
+        if (periodic) villain_sweep_hot<false, 8><<<grid, 8 * 64, 0, stream>>>(A);
+        else villain_sweep_hot<true, 8><<<grid, 8 * 64, 0, stream>>>(A);
+    } else if (periodic) {
+        villain_sweep_hot<false, 4><<<grid, 4 * 64, 0, stream>>>(A);
+    } else {
+        villain_sweep_hot<true, 4><<<grid, 4 * 64, 0, stream>>>(A);
+    }
 }
 
 }  // namespace svh
