@@ -272,6 +272,9 @@ struct PairwisePlan {
     int32_t nleaf, nprog;
 };
 static constexpr int MAX_LEAVES = 2048;
+// slices up to this length have all their terms formed at once by every thread into LDS (the loads of a mu = 1
+// slice, one row apart each, then overlap); the leaves' sums then read LDS in NumPy's order
+static constexpr int COHO_LDS_TERMS = 4096;
 
 __device__ __forceinline__ uint64_t coho_u64(u128 &s, const u128 &inc) {
     s = add(mul(s, mult()), inc);
@@ -284,12 +287,19 @@ __global__ __launch_bounds__(256) void cohomology_run(int32_t N, double half_kap
                                                       const int32_t *leaves /* 2 per leaf */,
                                                       const uint8_t *prog, PairwisePlan plan) {
     __shared__ double leafv[MAX_LEAVES];
+    __shared__ double s_terms[COHO_LDS_TERMS];
+    __shared__ uint8_t s_prog[2 * MAX_LEAVES];
+    __shared__ double s_stk[64];
     __shared__ double s_dS;
     __shared__ int64_t s_h;
     __shared__ int s_acc;
     const int64_t V = (int64_t)N * N;
     u128 st{rng->s_lo, rng->s_hi}, inc{rng->inc_lo, rng->inc_hi};
     uint32_t has = rng->has, buf = rng->buf;
+    // the postfix program in LDS: thread 0 walks it once per direction and sweep (from global memory every step
+    // of the walk waited on a load)
+    for (int pc = threadIdx.x; pc < plan.nprog; pc += blockDim.x) s_prog[pc] = prog[pc];
+    __syncthreads();
     for (int32_t sw = 0; sw < sweeps; sw++) {
         int64_t accepted = 0, rejections = 0;
         double psum = 0.0;
@@ -319,14 +329,21 @@ __global__ __launch_bounds__(256) void cohomology_run(int32_t N, double half_kap
             const double change_r = -LTWO_PI * (double)h;  // cohomology.py:94
             const double a = half_kappa * change_r;
             // leaves: slice x_mu = 0 is n[0, 0, i] (mu = 0) or n[1, i, 0] (mu = 1)
+            auto term_at = [&](int64_t i) {
+                const int64_t s = mu == 0 ? i : i * N;
+                const int64_t fs = mu == 0 ? N + i : i * N + 1;  // s + e_mu (N >= 2: no wrap)
+                const double r = (0.0 + (phi[fs] - phi[s])) - LTWO_PI * (double)n[(int64_t)mu * V + s];
+                return a * ((2.0 * r) + change_r);
+            };
+            const bool in_lds = N <= COHO_LDS_TERMS;
+            if (in_lds) {
+#pragma unroll 8
+                for (int64_t i = threadIdx.x; i < N; i += blockDim.x) s_terms[i] = term_at(i);
+                __syncthreads();
+            }
             for (int j = threadIdx.x; j < plan.nleaf; j += blockDim.x) {
                 const int32_t i0 = leaves[2 * j], len = leaves[2 * j + 1];
-                auto term = [&](int64_t i) {
-                    const int64_t s = mu == 0 ? i : i * N;
-                    const int64_t fs = mu == 0 ? N + i : i * N + 1;  // s + e_mu (N >= 2: no wrap)
-                    const double r = (0.0 + (phi[fs] - phi[s])) - LTWO_PI * (double)n[(int64_t)mu * V + s];
-                    return a * ((2.0 * r) + change_r);
-                };
+                auto term = [&](int64_t i) { return in_lds ? s_terms[i] : term_at(i); };
                 double res;
                 if (len < 8) {
                     res = 0.0;
@@ -346,16 +363,16 @@ __global__ __launch_bounds__(256) void cohomology_run(int32_t N, double half_kap
             }
             __syncthreads();
             if (threadIdx.x == 0) {
-                double stk[40];
+                // (the stack in LDS: a private array indexed at run time lives in scratch memory)
                 int top = 0, nl = 0;
                 for (int pc = 0; pc < plan.nprog; pc++) {
-                    if (prog[pc] == 0) stk[top++] = leafv[nl++];
+                    if (s_prog[pc] == 0) s_stk[top++] = leafv[nl++];
                     else {
-                        const double b = stk[--top];
-                        stk[top - 1] = stk[top - 1] + b;
+                        const double b = s_stk[--top];
+                        s_stk[top - 1] = s_stk[top - 1] + b;
                     }
                 }
-                const double dS = stk[0];
+                const double dS = s_stk[0];
                 const double p = clip01(exp(-dS));
                 const double u = 0.0 + 1.0 * to_double(coho_u64(st, inc));  // cohomology.py:100
                 s_acc = u < p;
