@@ -15,6 +15,15 @@ struct VParams {
 };
 
 static constexpr uint32_t OVERFLOW_BLOCK = 0xFFFFu;  // report tag: state not representable on this path
+
+// (t, x) = (s / N, s mod N) for a site index s of a lattice of fewer than 2^32 sites (every device path addresses
+// stream positions with 32 bits): one 32-bit unsigned division instead of the 64-bit one (a long emulated
+// sequence on the GPU) the grid-stride kernels paid per element
+__device__ __forceinline__ void divmod_site(int64_t s, int64_t N, int64_t &t, int64_t &x) {
+    const uint32_t q = (uint32_t)s / (uint32_t)N;
+    t = q;
+    x = s - (int64_t)q * N;
+}
 static constexpr int FW_MAX = 123;     // colour-0 sites per region row <= 63, so lane 63 is always spare
 static constexpr int RW = FW_MAX + 5;  // 128 region columns: x0-2 .. x1+2
 static constexpr int SMALL_LDS = 128;  // small-offset maps cached in LDS (in-row offsets are <= w+4)

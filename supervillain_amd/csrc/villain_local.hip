@@ -50,7 +50,8 @@ __global__ void local_dphi_init(int32_t N, double *phi, double *D, int normalize
     if (*(volatile const int32_t *)abort) return;
     const int64_t V = (int64_t)N * N;
     for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < V; s += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t t = s / N, x = s - t * N;
+        int64_t t, x;
+        divmod_site(s, N, t, x);
         const double p = phi[s];
         D[s] = 0.0 + (phi[((t + 1 == N) ? 0 : t + 1) * N + x] - p);
         D[V + s] = 0.0 + (phi[t * N + ((x + 1 == N) ? 0 : x + 1)] - p);
@@ -78,7 +79,8 @@ __global__ __launch_bounds__(256) void site_pass(LParams P, double *phi, const i
         if (!EVEN) um.init = ud.init = false;
         const double u = 0.0 + 1.0 * to_double(um.next(T, BM, (uint32_t)s, adv_m));
         const double dph = P.lo + P.range * to_double(ud.next(T, BD, (uint32_t)e, adv_e));
-        const int64_t t = s / N, x = s - t * N;
+        int64_t t, x;
+        divmod_site(s, N, t, x);
         const int64_t L[4] = {s, ((t == 0) ? N - 1 : t - 1) * N + x, V + s, V + t * N + ((x == 0) ? N - 1 : x - 1)};
         const double cd_f = 0.0 + (0.0 - dph), cd_b = 0.0 + (dph - 0.0);
         double dv[4];
@@ -127,7 +129,8 @@ __global__ __launch_bounds__(256) void site_pp(LParams P, const double *phi_in, 
         const int64_t s = even_site(e, N, PASS);
         const double u = 0.0 + 1.0 * to_double(um.next(T, BM, (uint32_t)s, adv_m));
         const double dph = P.lo + P.range * to_double(ud.next(T, BD, (uint32_t)e, adv_e));
-        const int64_t t = s / N, x = s - t * N;
+        int64_t t, x;
+        divmod_site(s, N, t, x);
         const int64_t f0 = ((t + 1 == N) ? 0 : t + 1) * N + x, b0 = ((t == 0) ? N - 1 : t - 1) * N + x;
         const int64_t f1 = t * N + ((x + 1 == N) ? 0 : x + 1), b1 = t * N + ((x == 0) ? N - 1 : x - 1);
         const double ps = phi_in[s];
@@ -190,7 +193,8 @@ __global__ __launch_bounds__(256) void exact_pass(LParams P, int64_t *n, const d
         const uint32_t idx = lemire(w, P.k, P.thr, &rej);
         if (rej) lreport(Sx, sweep, 1u + (uint32_t)color, q);
         const int64_t z = nonzero_value(idx, P.iv);
-        const int64_t t = s / N, x = s - t * N;
+        int64_t t, x;
+        divmod_site(s, N, t, x);
         const int64_t L[4] = {s, ((t == 0) ? N - 1 : t - 1) * N + x, V + s, V + t * N + ((x == 0) ? N - 1 : x - 1)};
         const int64_t cn_f = 0 + (0 - z), cn_b = 0 + (z - 0);
         // d(phi) on the four links, exactly as d() forms it (phi is fixed during the update, exact.py:71)
@@ -241,7 +245,8 @@ __global__ __launch_bounds__(256) void link_sweep(LParams P, const double *phi, 
         const int64_t cn = P.W * nonzero_value(idx, P.iv);
         const int mu = l >= V;
         const int64_t s = l - (mu ? V : 0);
-        const int64_t t = s / N, x = s - t * N;
+        int64_t t, x;
+        divmod_site(s, N, t, x);
         const int64_t f = mu ? t * N + ((x + 1 == N) ? 0 : x + 1) : ((t + 1 == N) ? 0 : t + 1) * N + x;
         const double dphi = 0.0 + (phi[f] - phi[s]);
         const int64_t nl = n[l];

@@ -91,7 +91,8 @@ __device__ __forceinline__ double dvw_at(const void *v, int64_t N, int mu, int64
 }
 template <bool VF>
 __device__ __forceinline__ double dvw_link(const void *v, int64_t N, int mu, int64_t s, double Weff) {
-    const int64_t t = s / N, x = s - t * N;
+    int64_t t, x;
+    divmod_site(s, N, t, x);
     return dvw_at<VF>(v, N, mu, s, t, x, Weff);
 }
 
@@ -140,7 +141,8 @@ __global__ __launch_bounds__(256) void coexact_pass(WParams P, int64_t *m, const
     double psum = 0.0;
     if (i < nc) {
         const int64_t x = sites[i];
-        const int64_t tt = x / N, xx = x - tt * N;
+        int64_t tt, xx;
+        divmod_site(x, N, tt, xx);
         const int64_t xe0 = ((tt + 1 == N) ? 0 : tt + 1) * N + xx;
         const int64_t xe1 = tt * N + ((xx + 1 == N) ? 0 : xx + 1);
         const double u = 0.0 + 1.0 * to_double(xsl_rr(jump(T, wbase(blocks[0]), (uint32_t)x)));
@@ -190,7 +192,8 @@ __global__ __launch_bounds__(256) void plaquette_cb_pass(WParams P, int64_t *m, 
     double psum = 0.0;
     if (i < nc) {
         const int64_t x = sites[i];
-        const int64_t tt = x / N, xx = x - tt * N;
+        int64_t tt, xx;
+        divmod_site(x, N, tt, xx);
         const int64_t xm = ((tt + 1 == N) ? 0 : tt + 1) * N + xx;  // here + e_mu (mu = 0)
         const int64_t xn = tt * N + ((xx + 1 == N) ? 0 : xx + 1);  // here + e_nu (nu = 1)
         const double u = 0.0 + 1.0 * to_double(xsl_rr(jump(T, wbase(blocks[0]), (uint32_t)x)));
@@ -240,7 +243,8 @@ __global__ __launch_bounds__(256) void coexact_gs(WParams P, int64_t *m, const v
     double psum = 0.0;
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nc; e += G) {
         const int64_t x = loc::even_site(e, N, color);
-        const int64_t tt = x / N, xx = x - tt * N;
+        int64_t tt, xx;
+        divmod_site(x, N, tt, xx);
         const double u = 0.0 + 1.0 * to_double(um.next(T, BM, (uint32_t)x, P.adv_m));
         uint32_t q = (uint32_t)e, w;
         if (slow) w = loc::bnd_word_slow(T, BT, skips, (uint32_t)e, &q);
@@ -295,7 +299,8 @@ __global__ __launch_bounds__(256) void plaquette_cb_gs(WParams P, int64_t *m, vo
     double psum = 0.0;
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nc; e += G) {
         const int64_t x = loc::even_site(e, N, color);
-        const int64_t tt = x / N, xx = x - tt * N;
+        int64_t tt, xx;
+        divmod_site(x, N, tt, xx);
         const double u = 0.0 + 1.0 * to_double(um.next(T, BM, (uint32_t)x, P.adv_m));
         uint32_t qm = (uint32_t)e, qv = (uint32_t)e, wm, wv;
         if (slow) {
@@ -361,7 +366,8 @@ __global__ __launch_bounds__(256) void plaquette_level(WParams P, int64_t *m, vo
     double psum = 0.0;
     if (i < count) {
         const int64_t x = list[i];
-        const int64_t tt = x / N, xx = x - tt * N;
+        int64_t tt, xx;
+        divmod_site(x, N, tt, xx);
         const int64_t xm = ((tt + 1 == N) ? 0 : tt + 1) * N + xx;
         const int64_t xn = tt * N + ((xx + 1 == N) ? 0 : xx + 1);
         const uint32_t idx = (uint32_t)pos[x];

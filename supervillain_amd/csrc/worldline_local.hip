@@ -53,7 +53,8 @@ __global__ void vortex_dv_init(int32_t N, const double *v, double *dv, const int
     if (*(volatile const int32_t *)abort) return;
     const int64_t V = (int64_t)N * N;
     for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < V; s += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t t = s / N, x = s - t * N;
+        int64_t t, x;
+        divmod_site(s, N, t, x);
         const double vs = v[s];
         dv[s] = 0.0 - (-(vs - v[t * N + (x == 0 ? N - 1 : x - 1)]));
         dv[V + s] = 0.0 - (vs - v[(t == 0 ? N - 1 : t - 1) * N + x]);
@@ -80,7 +81,8 @@ __global__ __launch_bounds__(256) void vortex_pass(VxParams P, const int64_t *m,
         const int64_t s = EVEN ? wl_site(e, N, color) : sites[e];
         if (!EVEN) um.init = up.init = bp.init = false;
         const double u = 0.0 + 1.0 * to_double(um.next(T, BM, (uint32_t)s, adv_m));
-        const int64_t t = s / N, x = s - t * N;
+        int64_t t, x;
+        divmod_site(s, N, t, x);
         const int64_t f0 = ((t + 1 == N) ? 0 : t + 1) * N + x, f1 = t * N + ((x + 1 == N) ? 0 : x + 1);
         const int64_t L0 = s, L0f = f1, L1 = V + s, L1f = V + f0;
         double a, c0, c0f, c1, c1f, d0, d0f, d1, d1f;
@@ -314,7 +316,9 @@ __global__ void wrap_apply(WrParams P, int64_t *m, const int64_t *cprop, const i
     const int64_t N = P.N, V = P.V;
     for (int64_t l = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; l < 2 * V; l += (int64_t)gridDim.x * blockDim.x) {
         const int mu = l >= V;
-        const int64_t s = l - (mu ? V : 0), t = s / N, x = s - t * N;
+        const int64_t s = l - (mu ? V : 0);
+        int64_t t, x;
+        divmod_site(s, N, t, x);
         const int64_t j = mu ? N + t : x;
         if (accf[j]) m[l] += cprop[j];
     }
