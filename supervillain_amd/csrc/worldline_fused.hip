@@ -448,7 +448,9 @@ template __global__ void worldline_step_fused<true>(WFArgs);
 namespace svh {
 using namespace sv;
 
-// rows per strip (SV_WF_TH overrides): as fused_th, cut down until the grid has `fill` workgroups
+// rows per strip (SV_WF_TH overrides): as fused_th, cut down until the grid has `fill` workgroups.  448: at L=1024
+// (9 column strips) that stops at 20 rows, 468 workgroups for the 768 slots of 3 per CU (r381: 16 / 20 / 24 / 28 rows
+// 47.9 / 46.1 / 51.3 / 56.5 us per step; 512 stopped at 16)
 static int wf_th(int32_t N, int nsx) {
     const char *e = getenv("SV_WF_TH");
     if (e) {
@@ -457,8 +459,8 @@ static int wf_th(int32_t N, int nsx) {
     }
     static const int fill = [] {
         const char *f = getenv("SV_WF_FILL");
-        const int v = f ? atoi(f) : 512;
-        return v > 0 ? v : 512;
+        const int v = f ? atoi(f) : 448;
+        return v > 0 ? v : 448;
     }();
     int th = 64;
     while (th > 4 && (int64_t)nsx * ((N + th - 1) / th) < fill) th -= 4;
