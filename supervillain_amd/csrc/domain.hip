@@ -37,7 +37,7 @@ bool wf_usable(int32_t N, bool v_is_float, double W_eff, int64_t it);
 bool wf_fast(const sv::Block *blocks);
 void launch_wf(const sv::FGeom &G, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in,
                int64_t *m_out, int64_t *v_out, const sv::Block *blocks, const uint32_t *skips, bool general,
-               const sv::JumpTables *T, const sv::Affine adv[3], void *pstat, void *cstat, sv::DevScratch S,
+               const sv::JumpTables *T, const sv::Affine adv[6], void *pstat, void *cstat, sv::DevScratch S,
                uint32_t sweep, hipStream_t stream);
 }  // namespace svh
 
@@ -830,8 +830,9 @@ void run_wdomain(sv_domain *d, double kappa, double W_eff, int64_t it, int32_t s
     const std::vector<BlockSpec> specs = {{UNIFORM, (uint32_t)V}, {BOUNDED, half}, {BOUNDED, half}, {BOUNDED, half},
                                           {BOUNDED, half}, {UNIFORM, (uint32_t)V}, {BOUNDED, half}, {BOUNDED, half}};
     const int nb = (int)specs.size();
-    const Affine adv[3] = {host_power(inc, 4 * (uint64_t)d->Nx), host_power(inc, 2 * (uint64_t)d->Nx),
-                           host_power(inc, (uint64_t)d->Nx)};
+    const Affine adv[6] = {host_power(inc, 4 * (uint64_t)d->Nx), host_power(inc, 2 * (uint64_t)d->Nx),
+                           host_power(inc, (uint64_t)d->Nx), host_power(inc, 8 * (uint64_t)d->Nx),
+                           host_power(inc, 4 * (uint64_t)d->Nx), host_power(inc, 2 * (uint64_t)d->Nx)};
     // rejections possible in the change_v blocks (threshold 1) and, for interval_t > 2, the t blocks
     const uint32_t kt = (uint32_t)(2 * it), thrt = (0u - kt) % kt;
     const double q = (double)V * (1.0 + (double)thrt) / 4294967296.0;

@@ -23,7 +23,7 @@ bool wf_usable(int32_t N, bool v_is_float, double W_eff, int64_t it);
 bool wf_fast(const sv::Block *blocks);
 void launch_wf(const sv::FGeom &G, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in,
                int64_t *m_out, int64_t *v_out, const sv::Block *blocks, const uint32_t *skips, bool general,
-               const sv::JumpTables *T, const sv::Affine adv[3], void *pstat, void *cstat, sv::DevScratch S,
+               const sv::JumpTables *T, const sv::Affine adv[6], void *pstat, void *cstat, sv::DevScratch S,
                uint32_t sweep, hipStream_t stream);
 }  // namespace svh
 
@@ -824,8 +824,9 @@ int sv_worldline_plaquette_coexact_run(sv_worldline *st, double kappa, double W_
         const char *wf_env = getenv("SV_WF");  // SV_WF=0: the four pass kernels only (A/B measurements)
         const bool use_wf = !(wf_env && atoi(wf_env) == 0);
         const int64_t N = st->N;
-        const Affine adv[3] = {host_power(inc, 4 * (uint64_t)N), host_power(inc, 2 * (uint64_t)N),
-                               host_power(inc, (uint64_t)N)};
+        // row-base advance maps of worldline_step_fused for 4 and 8 waves (rows per step NW: NW N draws, NW N / 4 words)
+        const Affine adv[6] = {host_power(inc, 4 * (uint64_t)N), host_power(inc, 2 * (uint64_t)N), host_power(inc, (uint64_t)N),
+                               host_power(inc, 8 * (uint64_t)N), host_power(inc, 4 * (uint64_t)N), host_power(inc, 2 * (uint64_t)N)};
         if (use_wf && N % 2 == 0 && !st->v_is_float && !st->m_alt) {
             SV_HIP(hipMalloc(&st->m_alt, 2 * (size_t)N * N * sizeof(int64_t)));
             SV_HIP(hipMalloc(&st->v_alt, (size_t)N * N * sizeof(int64_t)));

@@ -22,10 +22,15 @@
 namespace sv {
 
 static constexpr int WF_W = 119;          // output columns per strip: region = WF_W + 9 <= RW
-static constexpr int WF_NW = 4;
-// ring rows: at the end of step t the ring holds rows t-5..t+7 (P0 reads up to v[t+7]; C1 still reads
-// v[t-1]); the next rows t+8..t+11 go into the slots of t-5..t-2, stored at the start of steps t-4 and t
-static constexpr int WF_R = 3 * WF_NW + 1;
+// NW waves = NW rows per step.  Ring rows: during step t the passes read rows t-1..t+NW+3 (C1 reads v[t-1], P0
+// up to v[t+NW+3]) and the rows t+NW+4..t+2NW+3 that step t+NW's P0 needs are committed at its end, after C1,
+// with no barrier between: 2 NW + 5 slots (NW = 4: the ring holds rows t-5..t+7, the next rows t+8..t+11 go
+// into the slots of t-5..t-2, stored at the start of steps t-4 and t)
+template <int NW>
+struct WFGeom {
+    static constexpr int R = 2 * NW + 5;
+    static constexpr int AHEAD = NW + 4;  // step t prefetches (and commits) rows t + AHEAD ..
+};
 
 struct WFArgs {
     FGeom G;  // the periodic Nt x Nx lattice, or one domain tile with its ghost frame (villain.h)
@@ -49,13 +54,15 @@ struct WFArgs {
     int32_t general;       // MODE 2 for every strip (wf_body)
 };
 
+template <int NW>
 struct WFLDS {
-    int32_t m0[WF_R][RW];
-    int32_t m1[WF_R][RW];
-    int32_t v[WF_R][RW];
+    static constexpr int R = WFGeom<NW>::R;
+    int32_t m0[R][RW];
+    int32_t m1[R][RW];
+    int32_t v[R][RW];
     SmallTab small;
     Affine adv[3];
-    u128 base[WF_NW][64];  // per wave: lane 8p + ty = block ty's base for pass p's row at xb; 32 + .. at xw
+    u128 base[NW][64];  // per wave: lane 8p + ty = block ty's base for pass p's row at xb; 32 + .. at xw
     double df[6], dfk[6];
     int32_t bad;
 };
@@ -76,10 +83,10 @@ __device__ __forceinline__ double wf_dv1(int32_t vs, int32_t vn, double Winv) { 
 // MODE 0: interior strip, paired plaquette words; 1: edge strip (rows wrap), unpaired words from two base sets;
 // 2: GENERAL, a step with known Lemire rejections (skip lists) or unequal buffered-half flags: bounded words by
 // a full table jump at their skip-adjusted stream position (the rare replay of a rejected step)
-template <bool TILE, int MODE>
-__device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS &Ls) {
+template <bool TILE, int MODE, int NW>
+__device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     constexpr bool EDGE = MODE != 0;
-    constexpr int NW = WF_NW, R = WF_R, PF = RW / 64;
+    constexpr int R = WFGeom<NW>::R, AH = WFGeom<NW>::AHEAD, PF = RW / 64;
     auto &s_m0 = Ls.m0;
     auto &s_m1 = Ls.m1;
     auto &s_v = Ls.v;
@@ -385,14 +392,14 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS &Ls) {
         }
     };
 
-    for (int32_t ra = t0 - 5; ra < tfirst + 8; ra += NW) {
+    for (int32_t ra = t0 - 5; ra < tfirst + AH; ra += NW) {
         prefetch(ra);
         commit(ra);
     }
     __syncthreads();
 
     for (int32_t t = tfirst; t < t1; t += NW) {
-        prefetch(t + 8);
+        prefetch(t + AH);
         store_rows(t - NW);
         plaquette(0, t + 3 + wave);
         __syncthreads();
@@ -401,7 +408,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS &Ls) {
         coexact(2, t + 1 + wave);
         __syncthreads();
         coexact(3, t + wave);
-        commit(t + 8);
+        commit(t + AH);
         if (base_lane) {
             const int64_t p_old = wf_base_pos(bbnd, grow(brow), N, bx, bhas);
             const int64_t p_new = wf_base_pos(bbnd, grow(brow + NW), N, bx, bhas);
@@ -423,9 +430,12 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS &Ls) {
     wflush(A.cstat, cacc, cpsum);
 }
 
-template <bool TILE>
-__global__ __launch_bounds__(256) void worldline_step_fused(WFArgs A) {
-    __shared__ WFLDS Ls;
+#ifndef SV_WF_OCC8
+#define SV_WF_OCC8 2  // waves per SIMD the 8-wave kernel is compiled for (4: two workgroups per CU, <= 128 VGPRs)
+#endif
+template <bool TILE, int NW>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 8 ? SV_WF_OCC8 : 1))) void worldline_step_fused(WFArgs A) {
+    __shared__ WFLDS<NW> Ls;
     int b = blockIdx.x;
     {
         const int G = gridDim.x, per = G / 8, rem = G % 8;
@@ -436,26 +446,48 @@ __global__ __launch_bounds__(256) void worldline_step_fused(WFArgs A) {
     const int32_t x0 = (int32_t)((int64_t)ix * A.G.Wt / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * A.G.Wt / A.nsx);
     const int32_t gx0 = A.G.X0 + x0;
     const bool interior = gx0 - 5 >= 0 && gx0 + (x1 - x0) + 4 <= A.G.Nx && A.G.Nx > SMALL_LDS;
-    if (A.general) wf_body<TILE, 2>(A, Ls);
-    else if (__builtin_amdgcn_readfirstlane((int)interior)) wf_body<TILE, 0>(A, Ls);
-    else wf_body<TILE, 1>(A, Ls);
+    if (A.general) wf_body<TILE, 2, NW>(A, Ls);
+    else if (__builtin_amdgcn_readfirstlane((int)interior)) wf_body<TILE, 0, NW>(A, Ls);
+    else wf_body<TILE, 1, NW>(A, Ls);
 }
-template __global__ void worldline_step_fused<false>(WFArgs);
-template __global__ void worldline_step_fused<true>(WFArgs);
+template __global__ void worldline_step_fused<false, 4>(WFArgs);
+template __global__ void worldline_step_fused<true, 4>(WFArgs);
+template __global__ void worldline_step_fused<false, 8>(WFArgs);
+template __global__ void worldline_step_fused<true, 8>(WFArgs);
 
 }  // namespace sv
 
 namespace svh {
 using namespace sv;
 
-// rows per strip (SV_WF_TH overrides): as fused_th, cut down until the grid has `fill` workgroups.  448: at L=1024
-// (9 column strips) that stops at 20 rows, 468 workgroups for the 768 slots of 3 per CU (r381: 16 / 20 / 24 / 28 rows
-// 47.9 / 46.1 / 51.3 / 56.5 us per step; 512 stopped at 16)
-static int wf_th(int32_t N, int nsx) {
+static int wf_th(int32_t N, int nsx, int nw);
+
+// waves per workgroup (SV_WF_NW = 4 or 8 overrides).  8-wave workgroups recompute the 7 halo rows a strip's passes
+// need for more rows each, at one workgroup per CU (r386 at L=1024: 46.0 -> 43.4 us per step, 8 x 40-row strips; with
+// two 8-wave workgroups per CU at <= 128 VGPRs 44.1 us over 24-row strips, 51 us over 16 or 32); used when one round
+// of them covers at least 3/4 of the CUs, else 4 waves
+static int wf_nw(int32_t Ht, int nsx) {
+    const char *e = getenv("SV_WF_NW");
+    if (e) return atoi(e) == 8 ? 8 : 4;
+    const int th = wf_th(Ht, nsx, 8);
+    return (int64_t)nsx * ((Ht + th - 1) / th) >= 192 ? 8 : 4;
+}
+
+// rows per strip (SV_WF_TH overrides).  4 waves: as fused_th, cut down until the grid has `fill` workgroups.  448: at
+// L=1024 (9 column strips) that stops at 20 rows, 468 workgroups for the 768 slots of 3 per CU (r381: 16 / 20 / 24 /
+// 28 rows 47.9 / 46.1 / 51.3 / 56.5 us per step; 512 stopped at 16).  8 waves: the fewest row steps per strip with
+// at most one workgroup per CU (L=1024: 40 rows; r386: 32 / 40 / 48 rows 68.7 / 43.4 / 49.1 us, 32 needing two rounds)
+static int wf_th(int32_t N, int nsx, int nw) {
     const char *e = getenv("SV_WF_TH");
     if (e) {
         const int v = atoi(e);
         if (v >= 4 && v % 4 == 0) return v;
+    }
+    if (nw == 8) {
+        const int slots = 256 * (SV_WF_OCC8 >= 4 ? 2 : 1);
+        int th = 8;
+        while (th < N && (int64_t)nsx * ((N + th - 1) / th) > slots) th += 8;
+        return th;
     }
     static const int fill = [] {
         const char *f = getenv("SV_WF_FILL");
@@ -485,14 +517,15 @@ bool wf_fast(const Block *blocks) {
 
 void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in,
                int64_t *m_out, int64_t *v_out, const Block *blocks, const uint32_t *skips, bool general,
-               const JumpTables *T, const Affine adv[3], void *pstat, void *cstat, DevScratch S, uint32_t sweep,
+               const JumpTables *T, const Affine adv[6], void *pstat, void *cstat, DevScratch S, uint32_t sweep,
                hipStream_t stream) {
     WFArgs A{};
     A.skips = skips;
     A.general = general ? 1 : 0;
     A.G = G;
     A.nsx = (G.Wt + WF_W - 1) / WF_W;
-    A.TH = wf_th(G.Ht, A.nsx);
+    const int nw = wf_nw(G.Ht, A.nsx);
+    A.TH = wf_th(G.Ht, A.nsx, nw);
     A.nsy = (G.Ht + A.TH - 1) / A.TH;
     A.m_in = m_in;
     A.v_in = v_in;
@@ -500,7 +533,7 @@ void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
     A.v_out = v_out;
     A.blocks = blocks;
     A.T = T;
-    for (int i = 0; i < 3; i++) A.adv[i] = adv[i];
+    for (int i = 0; i < 3; i++) A.adv[i] = adv[(nw == 8 ? 3 : 0) + i];
     A.pstat = (StatStripe *)pstat;
     A.cstat = (StatStripe *)cstat;
     A.S = S;
@@ -518,8 +551,13 @@ void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
     A.kt = (uint32_t)(2 * it);
     A.thrt = (uint32_t)((0u - A.kt) % A.kt);
     const bool tile = !(G.T0 == 0 && G.X0 == 0 && G.Ht == G.Nt && G.Wt == G.Nx && G.pitch == G.Nx && G.org == 0);
-    if (tile) worldline_step_fused<true><<<A.nsx * A.nsy, WF_NW * 64, 0, stream>>>(A);
-    else worldline_step_fused<false><<<A.nsx * A.nsy, WF_NW * 64, 0, stream>>>(A);
+    if (nw == 8) {
+        if (tile) worldline_step_fused<true, 8><<<A.nsx * A.nsy, 8 * 64, 0, stream>>>(A);
+        else worldline_step_fused<false, 8><<<A.nsx * A.nsy, 8 * 64, 0, stream>>>(A);
+    } else {
+        if (tile) worldline_step_fused<true, 4><<<A.nsx * A.nsy, 4 * 64, 0, stream>>>(A);
+        else worldline_step_fused<false, 4><<<A.nsx * A.nsy, 4 * 64, 0, stream>>>(A);
+    }
 }
 
 }  // namespace svh
