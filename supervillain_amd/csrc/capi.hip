@@ -209,6 +209,17 @@ int sv_ctx_set_timing(sv_ctx *ctx, int32_t enable) {
     if (!ctx) return -1;
     ctx->timing = enable != 0;
     ctx->timing_mode = enable;
+    try {  // the first timed batch should not pay for creating its events
+        SV_HIP(hipSetDevice(ctx->device));
+        while (enable && ctx->ev_pool.size() < 4) {
+            hipEvent_t e;
+            SV_HIP(hipEventCreate(&e));
+            ctx->ev_pool.push_back(e);
+        }
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
     ctx->timed_ms = 0.0;
     ctx->timed_launches = 0;
     return 0;
@@ -392,8 +403,9 @@ int sv_ctx_create(int device, sv_ctx **out) {
         ctx->device = device;
         SV_HIP(hipSetDevice(device));
         SV_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-        SV_HIP(hipMalloc(&ctx->d_abort, sizeof(int32_t)));
-        SV_HIP(hipMalloc(&ctx->d_nreport, sizeof(uint32_t)));
+        // abort flag and report count side by side: a batch tail reads both with one copy
+        SV_HIP(hipMalloc(&ctx->d_abort, 2 * sizeof(int32_t)));
+        ctx->d_nreport = reinterpret_cast<uint32_t *>(ctx->d_abort + 1);
         SV_HIP(hipMalloc(&ctx->d_reports, sv::MAX_REPORTS * sizeof(sv::Report)));
         SV_HIP(hipMemset(ctx->d_abort, 0, sizeof(int32_t)));
         SV_HIP(hipMemset(ctx->d_nreport, 0, sizeof(uint32_t)));
@@ -425,7 +437,6 @@ int sv_ctx_destroy(sv_ctx *ctx) {
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
     if (ctx->h_tail) (void)hipHostFree(ctx->h_tail);
     if (ctx->h_stage_abort) (void)hipHostFree(ctx->h_stage_abort);
-    (void)hipFree(ctx->d_nreport);
     (void)hipFree(ctx->d_reports);
     (void)hipFree(ctx->d_blocks);
     (void)hipFree(ctx->d_skips);

@@ -330,8 +330,7 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         // outcome: abort flag, report count, statistics and observables land in the pinned slot
         char *tail = b->h_tail + slot * slot_bytes;
         const size_t st_bytes = (size_t)R * count * sizeof(sv_stats);
-        SV_HIP(hipMemcpyAsync(tail, ctx->d_abort, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
-        SV_HIP(hipMemcpyAsync(tail + 4, ctx->d_nreport, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipMemcpyAsync(tail, ctx->d_abort, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));  // + d_nreport
         SV_HIP(hipMemcpyAsync(tail + 64, b->d_stats, st_bytes, hipMemcpyDeviceToHost, ctx->stream));
         if (obs)
             SV_HIP(hipMemcpyAsync(tail + 64 + st_bytes, b->d_obs, (size_t)R * count * 4 * sizeof(double),

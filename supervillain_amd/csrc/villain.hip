@@ -710,9 +710,11 @@ DevScratch scratch(sv_ctx *ctx) { return DevScratch{ctx->d_abort, ctx->d_nreport
 AbortInfo read_abort(sv_ctx *ctx) {
     AbortInfo a;
     uint32_t nrep = 0;
-    SV_HIP(hipMemcpyAsync(&a.abort, ctx->d_abort, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
-    SV_HIP(hipMemcpyAsync(&nrep, ctx->d_nreport, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    int32_t both[2];  // d_abort, d_nreport are adjacent (capi.hip)
+    SV_HIP(hipMemcpyAsync(both, ctx->d_abort, sizeof(both), hipMemcpyDeviceToHost, ctx->stream));
     SV_HIP(hipStreamSynchronize(ctx->stream));
+    a.abort = both[0];
+    nrep = (uint32_t)both[1];
     if (nrep > (uint32_t)MAX_REPORTS) nrep = MAX_REPORTS;
     a.reports.resize(nrep);
     if (nrep) {
@@ -736,8 +738,7 @@ AbortInfo read_abort_stats(sv_ctx *ctx, int count, sv_stats *stats) {
     int32_t *h_ab = (int32_t *)ctx->h_tail;
     uint32_t *h_nrep = (uint32_t *)(ctx->h_tail + 4);
     sv_stats *h_st = (sv_stats *)(ctx->h_tail + 64);
-    SV_HIP(hipMemcpyAsync(h_ab, ctx->d_abort, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
-    SV_HIP(hipMemcpyAsync(h_nrep, ctx->d_nreport, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    SV_HIP(hipMemcpyAsync(h_ab, ctx->d_abort, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));  // + d_nreport
     SV_HIP(hipMemcpyAsync(h_st, ctx->d_stats, count * sizeof(sv_stats), hipMemcpyDeviceToHost, ctx->stream));
     SV_HIP(hipStreamSynchronize(ctx->stream));
     AbortInfo a;
@@ -917,13 +918,14 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     while (sw < sweeps) {
         const int count = std::min(BATCH, sweeps - sw);
         Cursor c = cur;
+        // the batch reset first: the device clears the flags and statistics while the host plans
+        ctx->ensure_stats(count);
+        reset_batch(ctx, ctx->d_stats, count * sizeof(sv_stats));
         auto tp0 = std::chrono::steady_clock::now();
         plan_sweeps(ctx, c, inc, specs, sw, count, skips, blocks, skipvec);
         auto tp1 = std::chrono::steady_clock::now();
         if (dbg) fprintf(stderr, "[sv] plan %d sweeps: %.1f us\n", count, std::chrono::duration<double, std::micro>(tp1 - tp0).count());
         upload_plan(ctx, blocks, skipvec);
-        ctx->ensure_stats(count);
-        reset_batch(ctx, ctx->d_stats, count * sizeof(sv_stats));
         const int cur0 = st->cur;
         hipEvent_t ev;
         const bool per_launch = ctx->timing_mode == 2;  // events around every launch, else around the batch

@@ -432,11 +432,11 @@ void wupload(sv_ctx *ctx, const std::vector<Block> &blocks, const std::vector<ui
 }
 
 bool wcheck(sv_ctx *ctx, std::vector<Report> &reps) {
-    int32_t ab = 0;
-    uint32_t nrep = 0;
-    SV_HIP(hipMemcpyAsync(&ab, ctx->d_abort, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
-    SV_HIP(hipMemcpyAsync(&nrep, ctx->d_nreport, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    int32_t both[2];  // d_abort, d_nreport are adjacent (capi.hip)
+    SV_HIP(hipMemcpyAsync(both, ctx->d_abort, sizeof(both), hipMemcpyDeviceToHost, ctx->stream));
     SV_HIP(hipStreamSynchronize(ctx->stream));
+    const int32_t ab = both[0];
+    uint32_t nrep = (uint32_t)both[1];
     reps.clear();
     if (!ab) return false;
     if (nrep > (uint32_t)MAX_REPORTS) nrep = MAX_REPORTS;
