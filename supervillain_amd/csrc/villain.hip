@@ -914,7 +914,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     std::vector<uint32_t> skipvec;
     int sw = 0;
     const bool dbg = getenv("SV_DEBUG_TIMING") != nullptr;
-    const bool use_hot = hot_enabled();
+    const bool use_hot = hot_enabled() && V < (int64_t(1) << 28);  // villain_sweep_hot's 32-bit row offsets
     while (sw < sweeps) {
         const int count = std::min(BATCH, sweeps - sw);
         Cursor c = cur;

@@ -28,6 +28,9 @@
 #include "fused.h"
 #include "philox.h"
 
+#ifndef SV_HOT_OFF32
+#define SV_HOT_OFF32 1  // periodic lattices: row loads / stores by 32-bit byte offsets from the SGPR bases
+#endif
 #ifndef SV_HOT_ADV
 #define SV_HOT_ADV 1  // row bases advanced by the precomputed maps behind a wave-uniform test (r3xx A/B)
 #endif
@@ -144,6 +147,9 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     static_assert(NWT == 4 || (NWT == 8 && !FR && !PH), "8-wave strips: single lattices and tiles");
     constexpr int NW = NWT;
     constexpr int R = HotLDST<PH, FR && OBS, NWT>::R, RR = HotLDST<PH, FR && OBS, NWT>::RR;
+    // periodic lattices address rows by 32-bit byte offsets (run_fused keeps 16 V < 2^32 on this kernel; replica
+    // batches address within one replica of N <= 128)
+    constexpr bool OFF32 = SV_HOT_OFF32 && !TILE && !PH && !(SV_ABLATE & (16 | 256 | 512 | 8));
     constexpr int PF = RW / 64;
     auto &s_phi = Ls.phi;
     auto &s_r0 = Ls.r0;
@@ -258,6 +264,13 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
             for (int k = 0; k < PF; k++) {
                 if (lane + 64 * k < cols) {
                     const int64_t g = g0 + pf_gx[k];
+                    if (OFF32) {  // 32-bit byte offsets from the uniform bases (global_load's SGPR-base form)
+                        const uint32_t o = ((uint32_t)g0 + (uint32_t)pf_gx[k]) * 8u;
+                        pf_phi[k] = *(const double *)((const char *)phi_in + o);
+                        pf_n0[k] = *(const int64_t *)((const char *)n_in + o);
+                        pf_n1[k] = *(const int64_t *)((const char *)n_in + (o + (uint32_t)V * 8u));
+                        continue;
+                    }
                     pf_phi[k] = phi_in[g];
                     if (SV_ABLATE & 256) {  // timing experiment: a compact int32 n layout (cold start only)
                         pf_n0[k] = ((const int32_t *)n_in)[g];
@@ -349,6 +362,12 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
                 if (cc < w) {
                     const int cx = FR ? cc : cc + 2;
                     const int64_t g = g0 + cc;
+                    if (OFF32) {
+                        const uint32_t o = ((uint32_t)g0 + (uint32_t)cc) * 8u;
+                        *(double *)((char *)phi_out + o) = s_phi[slot][cx];
+                        *(int64_t *)((char *)n_out + o) = (int64_t)s_n0[slot][cx];
+                        *(int64_t *)((char *)n_out + (o + (uint32_t)V * 8u)) = (int64_t)s_n1[slot][cx];
+                    } else {
                     phi_out[g] = s_phi[slot][cx];
                     if (SV_ABLATE & 256) {
                         ((int32_t *)n_out)[g] = s_n0[slot][cx];
@@ -359,6 +378,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
                     } else {
                         n_out[g] = (int64_t)s_n0[slot][cx];
                         n_out[V + g] = (int64_t)s_n1[slot][cx];
+                    }
                     }
                     if (OBS) {
                         // rows <= q+1 and columns <= x+1 are final here (villain.py:51-66, winding.py:30-37,
