@@ -638,7 +638,9 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
         plan_sweeps(ctx, c, inc, specs, sw, count, skips, blocks, skipvec);
         upload_plan(ctx, blocks, skipvec);
         std::vector<char> hot(count);
-        for (int k = 0; k < count; k++) hot[k] = hot_enabled() && hot_ok(P, &blocks[(size_t)k * nb]);
+        // (villain_sweep_hot's 32-bit row offsets: 16 plane < 2^32)
+        for (int k = 0; k < count; k++)
+            hot[k] = hot_enabled() && d->plane < (int64_t(1) << 28) && hot_ok(P, &blocks[(size_t)k * nb]);
         for (auto &Tl : d->tiles) SV_HIP(hipMemsetAsync(Tl.sum, 0, sizeof(Summary), ctx->stream));
         if (predict) SV_HIP(hipEventRecord(d->ev_sum, ctx->stream));
         const int cur0 = d->cur;

@@ -29,7 +29,7 @@
 #include "philox.h"
 
 #ifndef SV_HOT_OFF32
-#define SV_HOT_OFF32 1  // periodic lattices: row loads / stores by 32-bit byte offsets from the SGPR bases
+#define SV_HOT_OFF32 1  // row loads / stores by 32-bit byte offsets from the SGPR bases
 #endif
 #ifndef SV_HOT_ADV
 #define SV_HOT_ADV 1  // row bases advanced by the precomputed maps behind a wave-uniform test (r3xx A/B)
@@ -147,9 +147,9 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     static_assert(NWT == 4 || (NWT == 8 && !FR && !PH), "8-wave strips: single lattices and tiles");
     constexpr int NW = NWT;
     constexpr int R = HotLDST<PH, FR && OBS, NWT>::R, RR = HotLDST<PH, FR && OBS, NWT>::RR;
-    // periodic lattices address rows by 32-bit byte offsets (run_fused keeps 16 V < 2^32 on this kernel; replica
-    // batches address within one replica of N <= 128)
-    constexpr bool OFF32 = SV_HOT_OFF32 && !TILE && !PH && !(SV_ABLATE & (16 | 256 | 512 | 8));
+    // rows move by 32-bit byte offsets from the uniform bases: the hosts keep every offset below 2^32 on this kernel
+    // (run_fused: 16 V < 2^32; domain tiles: 16 plane < 2^32; replica batches address within one replica of N <= 128)
+    constexpr bool OFF32 = SV_HOT_OFF32 && !PH && !(SV_ABLATE & (16 | 256 | 512 | 8));
     constexpr int PF = RW / 64;
     auto &s_phi = Ls.phi;
     auto &s_r0 = Ls.r0;
