@@ -62,6 +62,11 @@ int sv_device_count(void);
  * (batches that hit a Lemire rejection are not counted). */
 int sv_ctx_set_timing(sv_ctx *ctx, int32_t enable);
 int sv_ctx_kernel_time(sv_ctx *ctx, double *ms_total, int64_t *launches);
+/* Diagnostic: Villain NeighborhoodUpdate sweep launches since the last call (then reset), by kernel -- hot: the
+ * fast-draw kernel (int16 n image, no skip lists); fused: the general fused kernel (int32 n image, skip lists,
+ * replays); generic: the per-colour int64 path.  A domain counts one launch per tile, a replica batch one per
+ * launch.  Lets tests prove which kernel ran (e.g. the int32 fallback after |n| >= 2^14). */
+int sv_ctx_sweep_counts(sv_ctx *ctx, int64_t *hot, int64_t *fused, int64_t *generic);
 /* Host-only: copy R NumPy PCG64 bit-generator states into (gather) or out of (scatter) sv_rng records, given
  * each generator's `bit_generator.ctypes.state_address` (NumPy's pcg64_state, numpy/random/src/pcg64/pcg64.h,
  * native 128-bit layout; the Python wrapper verifies it against the public state dict first).  Lets a

@@ -41,6 +41,7 @@ def lib():
         L.sv_build_info.restype = ctypes.c_char_p
         L.sv_ctx_set_timing.argtypes = [vp, i32]
         L.sv_ctx_kernel_time.argtypes = [vp, P(f64), P(i64)]
+        L.sv_ctx_sweep_counts.argtypes = [vp, P(i64), P(i64), P(i64)]
         L.sv_hbm_copy.argtypes = [vp, i64, i32, i32, P(f64)]
         L.sv_rng_gather.argtypes = [vp, i32, vp]
         L.sv_rng_scatter.argtypes = [vp, i32, vp]
@@ -105,7 +106,7 @@ def lib():
 
 
 EXPORTED = ('sv_ctx_create', 'sv_ctx_destroy', 'sv_last_error', 'sv_device_count', 'sv_build_info',
-            'sv_ctx_set_timing', 'sv_ctx_kernel_time', 'sv_hbm_copy', 'sv_rng_gather', 'sv_rng_scatter',
+            'sv_ctx_set_timing', 'sv_ctx_kernel_time', 'sv_ctx_sweep_counts', 'sv_hbm_copy', 'sv_rng_gather', 'sv_rng_scatter',
             'sv_villain_neighborhood', 'sv_villain_create', 'sv_villain_destroy', 'sv_villain_upload',
             'sv_villain_download', 'sv_villain_run', 'sv_villain_observables', 'sv_villain_emit', 'sv_villain_emit_wait', 'sv_villain_run_philox',
             'sv_worldline_emit', 'sv_worldline_emit_wait', 'sv_host_register', 'sv_host_unregister',
@@ -153,9 +154,12 @@ class Context:
     def end_deferred(self):
         """One synchronization lands every deferred statistic; then the folds run in call order."""
         folds, self.folds = self.folds, None
-        self.check(lib().sv_ctx_set_deferred(self.handle, 0), 'sv_ctx_set_deferred')
-        for f in folds or ():
-            f()
+        try:
+            self.check(lib().sv_ctx_set_deferred(self.handle, 0), 'sv_ctx_set_deferred')
+        finally:
+            # the statistics landed even when a member aborted: fold them, so that the counters match the device
+            for f in folds or ():
+                f()
 
     def fold_later(self, fold):
         """Run a counter fold that reads sv_stats now, or at end_deferred inside a deferred step."""
@@ -163,6 +167,12 @@ class Context:
             fold()
         else:
             self.folds.append(fold)
+
+    def sweep_counts(self):
+        """Villain sweep launches by kernel since the last call: {'hot', 'fused', 'generic'} (sv_ctx_sweep_counts)."""
+        c = [ctypes.c_int64() for _ in range(3)]
+        self.check(lib().sv_ctx_sweep_counts(self.handle, *[ctypes.byref(x) for x in c]), 'sv_ctx_sweep_counts')
+        return dict(zip(('hot', 'fused', 'generic'), (x.value for x in c)))
 
     def check(self, rc, what):
         if rc != 0:

@@ -76,7 +76,13 @@ void sv_ctx::land() {
     }
     landings.clear();
     stage_used = abort_used = 0;
-    if (bad) throw std::runtime_error("unexpected NumPy Lemire rejection report");
+    // deferred runs draw only power-of-two ranges, so NumPy's Lemire sampler cannot reject there: an abort is a
+    // kernel's OVERFLOW report (a field beyond the kernel's LDS image).  The statistics above landed; the device
+    // state of the aborting run is past its failing sweep and unspecified.
+    if (bad)
+        throw std::runtime_error("a deferred run aborted on the device (a field beyond a kernel's LDS image: OVERFLOW; "
+                                 "deferred runs cannot meet NumPy Lemire rejections); the device state is unspecified: "
+                                 "re-upload the configuration");
 }
 
 void sv::Emitter::emit(hipStream_t compute, const void *a, size_t bytes0, const void *b, size_t bytes1, void *ha,
@@ -222,6 +228,15 @@ int sv_ctx_set_timing(sv_ctx *ctx, int32_t enable) {
     }
     ctx->timed_ms = 0.0;
     ctx->timed_launches = 0;
+    return 0;
+}
+
+int sv_ctx_sweep_counts(sv_ctx *ctx, int64_t *hot, int64_t *fused, int64_t *generic) {
+    if (!ctx) return -1;
+    if (hot) *hot = ctx->sweeps_hot;
+    if (fused) *fused = ctx->sweeps_fused;
+    if (generic) *generic = ctx->sweeps_generic;
+    ctx->sweeps_hot = ctx->sweeps_fused = ctx->sweeps_generic = 0;
     return 0;
 }
 

@@ -112,6 +112,9 @@ struct sv_ctx {
     std::vector<int64_t> ev_launches;
     double timed_ms = 0.0;
     int64_t timed_launches = 0;
+    // Villain NeighborhoodUpdate sweeps by kernel (sv_ctx_sweep_counts): villain_sweep_hot (+ _fr), the general
+    // fused kernel (villain_sweep_fused: int32 n image, skip lists), the per-colour int64 path (villain_pass_generic)
+    int64_t sweeps_hot = 0, sweeps_fused = 0, sweeps_generic = 0;
     void time_begin(hipEvent_t *a);
     void time_end(hipEvent_t a, int64_t launches = 1);
     void time_collect();  // after a stream sync

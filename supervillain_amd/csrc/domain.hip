@@ -256,6 +256,7 @@ struct sv_domain {
         int sw = 0, count = 0;
         Cursor c{};
         u128 inc{0, 0};
+        uint32_t k = 0, thr = 0;    // the bounded draws the words were tested for (from interval_n)
         std::vector<uint64_t> cand;
     } pred;
     HaloTable H{};
@@ -266,14 +267,6 @@ struct sv_domain {
     bool loopback = false;              // 1 rank, 1 tile, halos through RCCL to itself (tests the RCCL path)
     Summary *gathered = nullptr;        // device, nranks summaries (RCCL mode)
     std::vector<Summary> host_sum;
-    // split sweeps: interior strips on ctx->stream while the halos travel on `halo_stream` (high
-    // priority), then the boundary strips there; events order the two streams
-    bool split = true;
-    hipStream_t halo_stream = nullptr;
-    hipStream_t interior_stream = nullptr;  // CU-masked: a few CUs stay free for the halo path (RCCL's kernel)
-    hipEvent_t ev_interior = nullptr, ev_boundary = nullptr;
-    int32_t *d_strips = nullptr;        // interior strip indices, then boundary strip indices
-    int n_interior = 0, n_boundary = 0;
 };
 
 namespace {
@@ -297,10 +290,8 @@ int tile_index(const sv_domain *d, int iy, int ix) {
 // of every K exchanges -- on the strong-scaled config 4 the RCCL exchange is a large part of a tile sweep.  The
 // frame must come from the adjacent tiles only (3K <= tile extents) and the extended rows must stay within the
 // kernels' single wrap of the torus (5K - 2 <= lattice extents).  SV_DOMAIN_DEPTH sets K (default 4, at most 8:
-// the interior's 16-column left pad); the opt-in split sweeps keep K = 1.
+// the interior's 16-column left pad).
 int villain_depth(int32_t Ht, int32_t Wt, int32_t Nt, int32_t Nx) {
-    const char *sp = getenv("SV_DOMAIN_SPLIT");
-    if (sp && sp[0] == '1') return 1;
     const char *e = getenv("SV_DOMAIN_DEPTH");
     int K = e ? atoi(e) : 4;
     K = std::max(1, std::min(8, K));
@@ -327,8 +318,7 @@ void geometry(sv_domain *d) {
     d->plane = (int64_t)(d->Ht + g.top + g.bottom) * d->pitch;
     d->org = (int64_t)g.top * d->pitch + LEFT_PAD;
     // ring depth: an abort travels one tile-hop (8-neighbour torus) per exchange, i.e. per K sweeps, so a tile
-    // D hops away runs at most D K sweeps past the failing one; with split sweeps (K = 1) the interior launch of
-    // the sweep that receives the abort still runs, so one more buffer
+    // D hops away runs at most D K sweeps past the failing one
     const int D = std::max(d->ty / 2, d->tx / 2);
     d->R = std::max(2, D * d->depth + 2);
     int64_t off = 0;
@@ -623,15 +613,77 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
         SV_HIP(hipEventCreateWithFlags(&d->ev_scan, hipEventDisableTiming));
     }
     std::vector<u128> h_scan(DOMAIN_BATCH);
-    int predicted_batches = 0, aborts = 0;
+    // scan the choice words of n sweeps from cursor `from` on `stream`: the scan is split into one part per tile --
+    // each rank scans its own share into its summary (the words found travel in the summaries the ranks all-gather),
+    // and one process emulating a tile grid runs every tile's share into that tile's summary: the same partition
+    // and merge as several ranks
+    auto launch_scan = [&](const Cursor &from, int n, hipStream_t stream) {
+        u128 sk = from.s;
+        for (int k = 0; k < n; k++) {
+            h_scan[k] = sk;
+            sk = apply(per_sweep, sk);
+        }
+        SV_HIP(hipMemcpyAsync(d->d_scan, h_scan.data(), n * sizeof(u128), hipMemcpyHostToDevice, stream));
+        const uint64_t total = (uint64_t)n * 2 * ((uint64_t)V + 2 * SCAN_MARGIN);
+        const int parts = d->comm ? d->nranks : (int)d->tiles.size();
+        for (size_t li = 0; li < d->tiles.size(); li++) {
+            const int me = d->comm ? d->rank : (int)li;
+            ScanArgs a;
+            a.s_k = d->d_scan;
+            a.T = T;
+            a.V = (uint64_t)V;
+            a.lo = total * me / parts;
+            a.hi = total * (me + 1) / parts;
+            a.k = P.k;
+            a.thr = P.thr;
+            a.ncand = &d->tiles[li].sum->ncand;
+            a.cand = d->tiles[li].sum->cand;
+            const uint64_t lanes = (a.hi - a.lo + SCAN_CHUNK - 1) / SCAN_CHUNK;
+            if (lanes) scan_rejections<<<(unsigned)((lanes + 255) / 256), 256, 0, stream>>>(a);
+        }
+    };
+    // the finds of every part (gathered summaries, global tile order), sorted; false if a part overflowed
+    auto merge_cand = [&](std::vector<uint64_t> &cand) {
+        cand.clear();
+        bool over = false;
+        for (const Summary &S : d->host_sum) {
+            over |= S.ncand > (uint32_t)MAX_CAND;
+            cand.insert(cand.end(), S.cand, S.cand + std::min<uint32_t>(S.ncand, MAX_CAND));
+        }
+        std::sort(cand.begin(), cand.end());
+        cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
+        return !over;
+    };
+    int predicted_batches = 0, prescanned = 0, aborts = 0, predicted_aborts = 0;
+    // |n| beyond villain_sweep_hot's int16 image (|n| >= 2^14): the failing sweep is replayed, and the rest of the
+    // call runs, on villain_sweep_fused's int32 image -- the single-lattice driver's fallback (run_fused)
+    bool no_hot = false;
     int sw = 0;
     while (sw < sweeps) {
         int count = std::min(batch, sweeps - sw);
+        bool predicted = false;
         if (pred.valid && pred.sw == sw && pred.c.s.lo == cur.s.lo && pred.c.s.hi == cur.s.hi && pred.c.has == cur.has &&
-            pred.inc.lo == inc.lo && pred.inc.hi == inc.hi) {
+            pred.inc.lo == inc.lo && pred.inc.hi == inc.hi && pred.k == P.k && pred.thr == P.thr) {
             count = std::min(sweeps - sw, pred.count);
             add_predicted(skips, cur, specs, sw, count, pred.cand);
             predicted_batches++;
+            predicted = true;
+        } else if (predict) {
+            // no scan ran ahead of this batch (a call's first batch, or the replay after an abort): scan it now, in
+            // front of it (one more scan and all-gather), so that it runs predicted and full-length too
+            const int n = std::min(full, sweeps - sw);
+            for (auto &Tl : d->tiles) SV_HIP(hipMemsetAsync(Tl.sum, 0, sizeof(Summary), ctx->stream));
+            launch_scan(cur, n, ctx->stream);
+            SV_HIP(hipGetLastError());
+            gather(d);
+            std::vector<uint64_t> cand;
+            if (merge_cand(cand)) {
+                count = n;
+                add_predicted(skips, cur, specs, sw, count, cand);
+                predicted_batches++;
+                prescanned++;
+                predicted = true;
+            }
         }
         pred.valid = false;
         Cursor c = cur;
@@ -640,7 +692,7 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
         std::vector<char> hot(count);
         // (villain_sweep_hot's 32-bit row offsets: 16 plane < 2^32)
         for (int k = 0; k < count; k++)
-            hot[k] = hot_enabled() && d->plane < (int64_t(1) << 28) && hot_ok(P, &blocks[(size_t)k * nb]);
+            hot[k] = !no_hot && hot_enabled() && d->plane < (int64_t(1) << 28) && hot_ok(P, &blocks[(size_t)k * nb]);
         for (auto &Tl : d->tiles) SV_HIP(hipMemsetAsync(Tl.sum, 0, sizeof(Summary), ctx->stream));
         if (predict) SV_HIP(hipEventRecord(d->ev_sum, ctx->stream));
         const int cur0 = d->cur;
@@ -675,65 +727,33 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
         };
         hipEvent_t ev;
         ctx->time_begin(&ev);
-        hipStream_t A_ = d->interior_stream ? d->interior_stream : ctx->stream;
-        if (d->split) {
-            // A (interior) and C (halo_stream) start after everything queued so far on ctx->stream
-            SV_HIP(hipEventRecord(d->ev_interior, ctx->stream));
-            SV_HIP(hipStreamWaitEvent(d->halo_stream, d->ev_interior, 0));
-            SV_HIP(hipStreamWaitEvent(A_, d->ev_interior, 0));
-            SV_HIP(hipEventRecord(d->ev_boundary, d->halo_stream));
-        }
         for (int k = 0; k < count; k++) {
             const int in = d->cur, out = (d->cur + 1) % d->R;
-            if (!d->split) {
-                // deep halos: one exchange per group of K sweeps; sweep j of a group of g decides the tile extended
-                // by e = g-1-j rings of (2 above, 3 below, 2 left, 3 right), counting only the tile's own sites
-                const int K = d->depth, g0 = k - k % K, e = std::min(K, count - g0) - 1 - (k - g0);
-                if (k == g0) exchange(d, ctx->stream);
-                for (auto &Tl : d->tiles) {
-                    FArgs A = fargs(Tl, k, in, out);
-                    if (e > 0) {
-                        const int32_t up = 2 * e, left = 2 * e;
-                        A.G.T0 = (Tl.T0 - up + d->Nt) % d->Nt;
-                        A.G.X0 = (Tl.X0 - left + d->Nx) % d->Nx;
-                        A.G.Ht = d->Ht + 5 * e;
-                        A.G.Wt = d->Wt + 5 * e;
-                        A.G.org = d->org - (int64_t)up * d->pitch - left;
-                        A.nsx = (A.G.Wt + FW_MAX - 1) / FW_MAX;
-                        A.nsy = (A.G.Ht + TH - 1) / TH;
-                        A.tiles_per_rep = A.nsx * A.nsy;
-                        A.own_r0 = up;
-                        A.own_r1 = up + d->Ht;
-                        A.own_c0 = left;
-                        A.own_c1 = left + d->Wt;
-                    }
-                    launch_fused_tile(A, A.nsx * A.nsy, ctx->stream, hot[k]);
+            // deep halos: one exchange per group of K sweeps; sweep j of a group of g decides the tile extended
+            // by e = g-1-j rings of (2 above, 3 below, 2 left, 3 right), counting only the tile's own sites
+            const int K = d->depth, g0 = k - k % K, e = std::min(K, count - g0) - 1 - (k - g0);
+            if (k == g0) exchange(d, ctx->stream);
+            for (auto &Tl : d->tiles) {
+                FArgs A = fargs(Tl, k, in, out);
+                if (e > 0) {
+                    const int32_t up = 2 * e, left = 2 * e;
+                    A.G.T0 = (Tl.T0 - up + d->Nt) % d->Nt;
+                    A.G.X0 = (Tl.X0 - left + d->Nx) % d->Nx;
+                    A.G.Ht = d->Ht + 5 * e;
+                    A.G.Wt = d->Wt + 5 * e;
+                    A.G.org = d->org - (int64_t)up * d->pitch - left;
+                    A.nsx = (A.G.Wt + FW_MAX - 1) / FW_MAX;
+                    A.nsy = (A.G.Ht + TH - 1) / TH;
+                    A.tiles_per_rep = A.nsx * A.nsy;
+                    A.own_r0 = up;
+                    A.own_r1 = up + d->Ht;
+                    A.own_c0 = left;
+                    A.own_c1 = left + d->Wt;
                 }
-            } else {
-                // A: interior strips of sweep k need the boundary strips of sweep k-1 (their input rows)
-                SV_HIP(hipStreamWaitEvent(A_, d->ev_boundary, 0));
-                // C: the halos of sweep k are read from the full output of sweep k-1
-                SV_HIP(hipStreamWaitEvent(d->halo_stream, d->ev_interior, 0));
-                if (d->n_interior)
-                    for (auto &Tl : d->tiles) {
-                        FArgs A = fargs(Tl, k, in, out);
-                        A.strip_map = d->d_strips;
-                        launch_fused_tile(A, d->n_interior, A_, hot[k]);
-                    }
-                SV_HIP(hipEventRecord(d->ev_interior, A_));
-                exchange(d, d->halo_stream);
-                for (auto &Tl : d->tiles) {
-                    FArgs A = fargs(Tl, k, in, out);
-                    A.strip_map = d->d_strips + d->n_interior;
-                    launch_fused_tile(A, d->n_boundary, d->halo_stream, hot[k]);
-                }
-                SV_HIP(hipEventRecord(d->ev_boundary, d->halo_stream));
+                launch_fused_tile(A, A.nsx * A.nsy, ctx->stream, hot[k]);
+                (hot[k] ? ctx->sweeps_hot : ctx->sweeps_fused)++;
             }
             d->cur = out;
-        }
-        if (d->split) {
-            SV_HIP(hipStreamWaitEvent(ctx->stream, d->ev_boundary, 0));
-            SV_HIP(hipStreamWaitEvent(ctx->stream, d->ev_interior, 0));
         }
         ctx->time_end(ev, count);
         // scan the words of the next batch (from this batch's end cursor c) for NumPy rejections; this rank's share
@@ -741,28 +761,9 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
         next.valid = false;
         const int ncount = sweeps - sw - count > 0 ? std::min(full, sweeps - sw - count) : std::min(full, count);
         if (predict && ncount > 0) {
-            u128 sk = c.s;
-            for (int k = 0; k < ncount; k++) {
-                h_scan[k] = sk;
-                sk = apply(per_sweep, sk);
-            }
             // on the low-priority stream, after this batch's summary was cleared; the gather waits for it
             SV_HIP(hipStreamWaitEvent(d->scan_stream, d->ev_sum, 0));
-            SV_HIP(hipMemcpyAsync(d->d_scan, h_scan.data(), ncount * sizeof(u128), hipMemcpyHostToDevice, d->scan_stream));
-            const uint64_t total = (uint64_t)ncount * 2 * ((uint64_t)V + 2 * SCAN_MARGIN);
-            const int parts = d->comm ? d->nranks : 1, me = d->comm ? d->rank : 0;
-            ScanArgs a;
-            a.s_k = d->d_scan;
-            a.T = T;
-            a.V = (uint64_t)V;
-            a.lo = total * me / parts;
-            a.hi = total * (me + 1) / parts;
-            a.k = P.k;
-            a.thr = P.thr;
-            a.ncand = &d->tiles[0].sum->ncand;
-            a.cand = d->tiles[0].sum->cand;
-            const uint64_t lanes = (a.hi - a.lo + SCAN_CHUNK - 1) / SCAN_CHUNK;
-            if (lanes) scan_rejections<<<(unsigned)((lanes + 255) / 256), 256, 0, d->scan_stream>>>(a);
+            launch_scan(c, ncount, d->scan_stream);
             SV_HIP(hipEventRecord(d->ev_scan, d->scan_stream));
             SV_HIP(hipStreamWaitEvent(ctx->stream, d->ev_scan, 0));
             next.valid = true;
@@ -770,6 +771,8 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
             next.count = ncount;
             next.c = c;
             next.inc = inc;
+            next.k = P.k;
+            next.thr = P.thr;
         }
         SV_HIP(hipGetLastError());
         gather(d);
@@ -785,24 +788,24 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
             fill_stats(d, skips, nb, sw, count, stats);
             cur = c;
             sw += count;
-            if (next.valid) {
-                next.cand.clear();
-                bool over = false;
-                for (const Summary &S : d->host_sum) {
-                    over |= S.ncand > (uint32_t)MAX_CAND;
-                    next.cand.insert(next.cand.end(), S.cand, S.cand + std::min<uint32_t>(S.ncand, MAX_CAND));
-                }
-                std::sort(next.cand.begin(), next.cand.end());
-                next.cand.erase(std::unique(next.cand.begin(), next.cand.end()), next.cand.end());
-                if (!over) pred = next;  // (an overflowing scan leaves the batch to the abort protocol)
-            }
+            if (next.valid && merge_cand(next.cand)) pred = next;  // (an overflowing scan: abort protocol)
             continue;
         }
         aborts++;
+        predicted_aborts += predicted;
+        // an overflow report: the sweeps before it stand, the failing one is replayed on the int32 kernel (a
+        // rejection report of an earlier sweep, or of the same sweep, is absorbed first as usual)
+        uint32_t ovf = ~0u;
         for (const Report &r : a.reports)
-            if (r.block == OVERFLOW_BLOCK)
-                throw std::runtime_error("|n| exceeds the fused path's int32 LDS image (domain mode has no fallback)");
-        const int bad = absorb_reports(a, sw, skips);
+            if (r.block == OVERFLOW_BLOCK) ovf = std::min(ovf, r.sweep);
+        if (ovf != ~0u) {
+            if (no_hot) throw std::runtime_error("|n| exceeds villain_sweep_fused's int32 LDS image (|n| < 2^30 required)");
+            no_hot = true;
+            a.reports.erase(std::remove_if(a.reports.begin(), a.reports.end(),
+                                           [&](const Report &r) { return r.block == OVERFLOW_BLOCK || r.sweep > ovf; }),
+                            a.reports.end());
+        }
+        const int bad = a.reports.empty() ? (int)ovf : absorb_reports(a, sw, skips);
         if (bad > 0) {
             Cursor c2 = cur;
             std::vector<Block> b2;
@@ -815,8 +818,8 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
         sw += bad;
     }
     if (getenv("SV_DEBUG_TIMING"))
-        fprintf(stderr, "[sv domain] %d sweeps, batch %d, depth %d, predicted batches %d, aborts %d\n", sweeps, batch,
-                d->depth, predicted_batches, aborts);
+        fprintf(stderr, "[sv domain] %d sweeps, batch %d, depth %d, predicted batches %d (%d pre-scanned), aborts %d (%d in "
+                "predicted batches)\n", sweeps, batch, d->depth, predicted_batches, prescanned, aborts, predicted_aborts);
 }
 
 // Worldline (config 3 decomposed): one step = checkerboard PlaquetteUpdate sweep + CoexactUpdate
@@ -1054,53 +1057,6 @@ static int domain_create(sv_ctx *ctx, int model, int32_t Nt, int32_t Nx, int32_t
             SV_HIP(hipMemset(T.sum, 0, sizeof(Summary)));
             if (model == 1) SV_HIP(hipMalloc(&T.stripes, (size_t)DOMAIN_BATCH * 2 * NSTRIPE * sizeof(StatStripe)));
         }
-        // split sweeps (Villain): strips whose stencil stays inside the tile run while the halos travel
-        if (model == 0) {
-            const int nsx = (d->Wt + FW_MAX - 1) / FW_MAX;
-            const int TH = domain_th(d, nsx), nsy = (d->Ht + TH - 1) / TH;
-            std::vector<int32_t> inner, outer;
-            for (int iy = 0; iy < nsy; iy++)
-                for (int ix = 0; ix < nsx; ix++) {
-                    const int64_t x0 = (int64_t)ix * d->Wt / nsx, x1 = (int64_t)(ix + 1) * d->Wt / nsx;
-                    const int64_t t0 = (int64_t)iy * TH, t1 = std::min<int64_t>(t0 + TH, d->Ht);
-                    const bool in = x0 >= 3 && x1 + 3 <= d->Wt && t0 >= 3 && t1 + 3 <= d->Ht;
-                    (in ? inner : outer).push_back(iy * nsx + ix);
-                }
-            // measured on one MI355X (RCCL loopback, 4096^2 tile): sequential 390 us/sweep, split 406-418 us
-            // (RCCL's kernel waits for CU slots behind the interior launch; CU-masking the interior stream
-            // was slower still), so the split is opt-in: SV_DOMAIN_SPLIT=1
-            const char *env = getenv("SV_DOMAIN_SPLIT");
-            d->split = !inner.empty() && env && env[0] == '1';
-            if (d->split) {
-                d->n_interior = (int)inner.size();
-                d->n_boundary = (int)outer.size();
-                inner.insert(inner.end(), outer.begin(), outer.end());
-                SV_HIP(hipMalloc(&d->d_strips, inner.size() * sizeof(int32_t)));
-                SV_HIP(hipMemcpy(d->d_strips, inner.data(), inner.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-                int lo = 0, hi = 0;
-                SV_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-                SV_HIP(hipStreamCreateWithPriority(&d->halo_stream, hipStreamNonBlocking, hi));
-                // the interior launch would otherwise take every CU slot before RCCL's kernel is queued,
-                // and its workgroups run ~100 us each: keep `reserve` CUs (spread over the XCDs) for the halos
-                const char *re = getenv("SV_DOMAIN_RESERVE");
-                const int reserve = re ? atoi(re) : 0;
-                hipDeviceProp_t prop;
-                SV_HIP(hipGetDeviceProperties(&prop, ctx->device));
-                const int ncu = prop.multiProcessorCount;
-                if (reserve > 0 && reserve < ncu) {
-                    std::vector<uint32_t> mask((ncu + 31) / 32, 0);
-                    for (int c = 0; c < ncu; c++) mask[c / 32] |= 1u << (c % 32);
-                    const int stride = ncu / reserve;
-                    for (int i = 0; i < reserve; i++) {
-                        const int c = i * stride + stride - 1;
-                        mask[c / 32] &= ~(1u << (c % 32));
-                    }
-                    SV_HIP(hipExtStreamCreateWithCUMask(&d->interior_stream, (uint32_t)mask.size(), mask.data()));
-                }
-                SV_HIP(hipEventCreateWithFlags(&d->ev_interior, hipEventDisableTiming));
-                SV_HIP(hipEventCreateWithFlags(&d->ev_boundary, hipEventDisableTiming));
-            }
-        }
         if (nranks > 1 || d->loopback) {
             ncclUniqueId u;
             std::memcpy(u.internal, unique_id, NCCL_UNIQUE_ID_BYTES);
@@ -1145,7 +1101,6 @@ int sv_domain_destroy(sv_domain *d) {
         (void)hipFree(T.sum);
         (void)hipFree(T.stripes);
     }
-    if (d->halo_stream) (void)hipStreamSynchronize(d->halo_stream);
     if (d->comm) (void)ncclCommDestroy(d->comm);
     (void)hipFree(d->gathered);
     (void)hipFree(d->d_scan);
@@ -1155,11 +1110,6 @@ int sv_domain_destroy(sv_domain *d) {
     }
     if (d->ev_sum) (void)hipEventDestroy(d->ev_sum);
     if (d->ev_scan) (void)hipEventDestroy(d->ev_scan);
-    (void)hipFree(d->d_strips);
-    if (d->ev_interior) (void)hipEventDestroy(d->ev_interior);
-    if (d->ev_boundary) (void)hipEventDestroy(d->ev_boundary);
-    if (d->halo_stream) (void)hipStreamDestroy(d->halo_stream);
-    if (d->interior_stream) (void)hipStreamDestroy(d->interior_stream);
     delete d;
     return 0;
 }

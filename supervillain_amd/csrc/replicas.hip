@@ -184,6 +184,9 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
     const int nsy = (b->N + TH - 1) / TH;
     const int tiles = nsx * nsy;
     const bool fr_hot = hot_fr_ok(b->N) && nsx == 1 && hot_params_ok(P);
+    // replicas whose |n| left villain_sweep_hot_fr's int16 image (|n| >= 2^14) in this call: from the failing sweep
+    // on they run on the general fused kernel's int32 image, beside the others (the split launches below)
+    std::vector<char> big(R, 0);
     // pinned batch tails, two slots: batch k+1 is enqueued before batch k's statistics are copied out
     const size_t slot_bytes = 64 + (size_t)R * REP_BATCH * (sizeof(sv_stats) + 4 * sizeof(double));
     if (b->tail_cap < 2 * slot_bytes) {
@@ -242,21 +245,22 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         // fused kernel.  Within a skip-free sweep a replica's four choice blocks start on the same half-word parity
         // (they draw V/2, an even count), which is all the fast kernel's two draw forms need.
         std::vector<char> hot_k(count, fr_hot);
-        std::vector<std::vector<int32_t>> skipped(count);  // per sweep: replicas whose choice blocks carry skips
+        std::vector<std::vector<int32_t>> skipped(count);  // per sweep: replicas on the general kernel (ascending)
         if (fr_hot) {
+            std::vector<const std::vector<Block> *> hbr(R, nullptr);
             size_t hi = 0;
-            for (int r = 0; r < R; r++) {
-                if (!B.hosted[r]) continue;
-                const std::vector<Block> &blk = B.hb[hi++];
-                for (int k = 0; k < count; k++) {
-                    bool sk_k = false;
-                    for (int bi = 2; bi < NB; bi++) sk_k |= bi != 6 && blk[(size_t)k * NB + bi].nskip != 0;
-                    if (sk_k) {
+            for (int r = 0; r < R; r++)
+                if (B.hosted[r]) hbr[r] = &B.hb[hi++];
+            for (int k = 0; k < count; k++)
+                for (int r = 0; r < R; r++) {
+                    bool gen = big[r] != 0;
+                    if (hbr[r])
+                        for (int bi = 2; bi < NB; bi++) gen |= bi != 6 && (*hbr[r])[(size_t)k * NB + bi].nskip != 0;
+                    if (gen) {
                         hot_k[k] = 0;
                         skipped[k].push_back(r);
                     }
                 }
-            }
         }
         // a sweep with skips in a few replicas runs as two launches over replica maps: the fast kernel for the
         // others, the general kernel for those (so a NumPy Lemire rejection slows one replica's replay, not all)
@@ -309,6 +313,7 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
             A.obs = obs ? b->d_obs + 4 * k : nullptr;
             if (hot_k[k]) {
                 launch_hot_fr(A, R * tiles, obs != nullptr, ctx->stream);
+                ctx->sweeps_hot++;
             } else if (split[k][3] > 0) {
                 FArgs Ah = A, Ag = A;
                 Ah.rep_map = b->d_map + split[k][0];
@@ -320,8 +325,11 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
                 Ag.tiles_per_rep = nsx * Ag.nsy;
                 if (split[k][1] > 0) launch_hot_fr(Ah, (int)split[k][1] * tiles, obs != nullptr, ctx->stream);
                 launch_fused_batch(Ag, (int)split[k][3] * Ag.tiles_per_rep, obs != nullptr, ctx->stream);
+                ctx->sweeps_hot += split[k][1] > 0;
+                ctx->sweeps_fused++;
             } else {
                 launch_fused_batch(A, R * tiles, obs != nullptr, ctx->stream);
+                ctx->sweeps_fused++;
             }
             b->cur ^= 1;
         }
@@ -376,14 +384,17 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
             if (nrep) SV_HIP(hipMemcpy(reps.data(), ctx->d_reports, nrep * sizeof(Report), hipMemcpyDeviceToHost));
             if (reps.empty()) throw std::runtime_error("device aborted without a rejection report");
             uint32_t bad = ~0u;
-            for (const Report &x : reps) {
-                if (x.block == OVERFLOW_BLOCK) throw std::runtime_error("|n| exceeds the fused path's int32 LDS image");
-                bad = std::min(bad, x.sweep);
-            }
+            for (const Report &x : reps) bad = std::min(bad, x.sweep);
+            for (const Report &x : reps)
+                if (x.block == OVERFLOW_BLOCK && x.sweep == bad) {
+                    // int16 image of the fast kernel: replay this replica on the general kernel's int32 image
+                    if (!fr_hot || big[x.pad]) throw std::runtime_error("|n| exceeds the general fused kernel's int32 LDS image (|n| < 2^30 required)");
+                    big[x.pad] = 1;
+                }
             for (int r = 0; r < R; r++) {
                 AbortInfo a{1, {}};
                 for (const Report &x : reps)
-                    if ((int)x.pad == r && x.sweep == bad) a.reports.push_back(x);
+                    if ((int)x.pad == r && x.sweep == bad && x.block != OVERFLOW_BLOCK) a.reports.push_back(x);
                 if (!a.reports.empty()) absorb_reports(a, B.sw, skips[r]);
             }
             const int good = (int)bad;

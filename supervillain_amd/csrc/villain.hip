@@ -849,6 +849,7 @@ void run_generic(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, 
             const int grid = (int)std::min<int64_t>((V + 255) / 256, 4096);
             villain_phi_normalize<<<grid, 256, 0, ctx->stream>>>(st->N, phi, ctx->d_abort);
             villain_r_init<<<grid, 256, 0, ctx->stream>>>(st->N, phi, n, st->r, ctx->d_abort);
+            ctx->sweeps_generic++;
             for (int col = 0; col < st->ncol; col++) {
                 int64_t nc = st->count[col];
                 if (!nc) continue;
@@ -915,6 +916,9 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     int sw = 0;
     const bool dbg = getenv("SV_DEBUG_TIMING") != nullptr;
     const bool use_hot = hot_enabled() && V < (int64_t(1) << 28);  // villain_sweep_hot's 32-bit row offsets
+    // |n| beyond villain_sweep_hot's int16 image: the failing sweep is replayed, and the rest of the call runs, on
+    // villain_sweep_fused's int32 image; only an overflow of that one falls back to the per-colour int64 path
+    bool hot_off = false;
     while (sw < sweeps) {
         const int count = std::min(BATCH, sweeps - sw);
         Cursor c = cur;
@@ -953,7 +957,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             A.S = scratch(ctx);
             A.sweep = (uint32_t)k;
             farg_single(A, nsx, nsy);
-            if (use_hot && NWv == 4 && hot_ok(P, &blocks[(size_t)k * nb])) {
+            if (use_hot && !hot_off && NWv == 4 && hot_ok(P, &blocks[(size_t)k * nb])) {
                 if (hot_nw == 8) {
                     A.hot_nw = 8;
                     A.adv[0] = adv8[0];
@@ -961,12 +965,15 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                     A.adv[2] = adv8[2];
                 }
                 launch_hot(A, grid, ctx->stream);
-            }
-            else if (NWv == 6) villain_sweep_fused<6, false, false, false><<<grid, 6 * 64, 0, ctx->stream>>>(A);
+                ctx->sweeps_hot++;
+            } else {
+                ctx->sweeps_fused++;
+                if (NWv == 6) villain_sweep_fused<6, false, false, false><<<grid, 6 * 64, 0, ctx->stream>>>(A);
 #if SV_K3
-            else if (P.k == 3) villain_sweep_fused<4, false, false, false, true><<<grid, 4 * 64, 0, ctx->stream>>>(A);
+                else if (P.k == 3) villain_sweep_fused<4, false, false, false, true><<<grid, 4 * 64, 0, ctx->stream>>>(A);
 #endif
-            else villain_sweep_fused<4, false, false, false><<<grid, 4 * 64, 0, ctx->stream>>>(A);
+                else villain_sweep_fused<4, false, false, false><<<grid, 4 * 64, 0, ctx->stream>>>(A);
+            }
             if (per_launch) ctx->time_end(ev1, 1);
             st->cur ^= 1;
         }
@@ -1006,6 +1013,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         }
         if (overflow) {
             const int bad = (int)first_bad;
+            const bool to_int32 = use_hot && !hot_off && NWv == 4;  // the failing sweep may have run on the int16 image
             if (bad > 0) {
                 Cursor c2 = cur;
                 std::vector<Block> b2;
@@ -1026,6 +1034,11 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                 cur = c2;
             }
             st->cur = cur0 ^ (bad & 1);
+            if (to_int32) {
+                hot_off = true;
+                sw += bad;
+                continue;
+            }
             done_sweeps = sw + bad;
             return false;
         }
@@ -1160,7 +1173,7 @@ int sv_villain_run(sv_villain *st, double kappa, int64_t W, double interval_phi,
         if (use_fused && sweeps > 0) {
             // run as many sweeps as possible fused; on int32 overflow fall back for the rest
             bool all = run_fused(st, P, sweeps, cur, inc, stats, done);
-            if (!all && path == 2) throw std::runtime_error("|n| exceeds the fused path's int32 LDS image");
+            if (!all && path == 2) throw std::runtime_error("|n| exceeds the fused path's int32 LDS image (|n| < 2^30 required)");
         }
         if (done < sweeps) {
             // generic path works on phi[cur], n[cur] in place
@@ -1194,7 +1207,7 @@ int sv_villain_run_philox(sv_villain *st, double kappa, int64_t W, double interv
         VParams P = make_params(N, kappa, W, interval_phi, interval_n);
         if (rng->test_threshold) P.thr = rng->test_threshold;
         if (P.k < 2 || !hot_params_ok(P))
-            throw std::invalid_argument("the counter-based mode needs interval_n >= 1, |W| <= 2^12 and W (2 interval_n + 1) < 2^28");
+            throw std::invalid_argument("the counter-based mode needs interval_n >= 1, |W| <= 2^12 and |W| interval_n <= 2^13");
         SV_HIP(hipSetDevice(ctx->device));
         const int nsx = (N + FW_MAX - 1) / FW_MAX;
         const int TH = fused_th(N, nsx);

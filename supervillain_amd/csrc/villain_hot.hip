@@ -388,10 +388,9 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
                         const double l0 = (0.0 + (s_phi[slot1][cx] - ph)) - TWO_PI * (double)s_n0[slot][cx];
                         const double l1 = (0.0 + (s_phi[slot][cxp(cx)] - ph)) - TWO_PI * (double)s_n1[slot][cx];
                         o_act += l0 * l0 + l1 * l1;
-                        // with the int16 image |n| < 2^14, so |dn| < 2^16 and dn^2 fits uint32
-                        using dint = std::conditional_t<SV_HOT_OCC4, int32_t, int64_t>;
-                        const dint dn = ((dint)s_n1[slot1][cx] - s_n1[slot][cx]) - ((dint)s_n0[slot][cxp(cx)] - s_n0[slot][cx]);
-                        o_w2 += SV_HOT_OCC4 ? (int64_t)(uint32_t)(dn * dn) : (int64_t)(dn * dn);
+                        // |n| <= 2^15 on the int16 image, so |dn| < 2^17 fits int32 and dn^2 needs 64 bits
+                        const int32_t dn = ((int32_t)s_n1[slot1][cx] - s_n1[slot][cx]) - ((int32_t)s_n0[slot][cxp(cx)] - s_n0[slot][cx]);
+                        o_w2 += (int64_t)dn * dn;
                         o_n0 += s_n0[slot][cx];
                         o_n1 += s_n1[slot][cx];
                     }
@@ -691,7 +690,10 @@ namespace svh {
 bool hot_params_ok(const VParams &P) {
     const int64_t aw = P.W < 0 ? -P.W : P.W;
     if (P.k <= 1 || P.k > (1u << 20) || aw > (1 << 20) || aw * (int64_t)P.k >= (1 << 28)) return false;  // int32 values
-    if (SV_HOT_OCC4 && aw > (1 << 12)) return false;  // the int16 n image: |n| < 2^14 plus 2|W| per sweep
+    // the int16 n image: a row enters LDS with |n| < 2^14 (else OVERFLOW is reported) and each link changes at most
+    // twice per sweep (once per colour) by |W (index - interval_n)| <= |W| interval_n, so |W| interval_n <= 2^13 keeps
+    // every value within int16
+    if (SV_HOT_OCC4 && (aw > (1 << 12) || aw * P.interval_n > (1 << 13))) return false;
     return true;
 }
 

@@ -116,7 +116,8 @@ class Ensemble:
         return cols
 
     def to_store(self, path):
-        """Write the ensemble as a new ExtendableStore (an existing one at `path` is replaced)."""
+        """Write the ensemble as a new ExtendableStore at `path`; a store there that already holds draws is refused
+        (FileExistsError: append with extend_store)."""
         store = ExtendableStore(path)
         if len(store):
             raise FileExistsError(f'{path} already holds {len(store)} draws; use extend_store')

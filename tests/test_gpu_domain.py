@@ -184,6 +184,55 @@ def test_predicted_rejections_other_choice_counts(interval_n, W, depth, oracle_l
     assert '[sv domain] 6 sweeps' in err and 'aborts 0' in err, err
 
 
+@pytest.mark.parametrize('tiles', [(2, 4), (2, 2), (1, 8)])
+def test_prediction_partitioned_over_tiles(tiles, oracle_lib, monkeypatch, capfd):
+    """The rejection scan split into one part per tile -- the partition several RCCL ranks use, each scanning its
+    share into its own batch summary -- and the merge of every summary's finds into the next batch's skip lists.
+    interval_n = 125576 gives NumPy's Lemire sampler the threshold 250996 (~4 rejected words per N=128 sweep, ~2 per
+    part and batch of 4 sweeps).  The call's first batch is scanned in front of it (no scan ran ahead of it), every
+    later one behind its predecessor; no batch may abort, and the chain equals the oracle's."""
+    monkeypatch.setenv('SV_DOMAIN_BATCH', '4')
+    monkeypatch.setenv('SV_DOMAIN_PREDICT', '1')
+    monkeypatch.setenv('SV_DEBUG_TIMING', '1')
+    N, sweeps, interval_n = 128, 16, 125576
+    phi0, n0 = hot(N, N, 1, 31)
+    gen = np.random.default_rng(12)
+    phi, n, st = run_domain(N, N, tiles, 0.5, 1, phi0, n0, sweeps, gen, interval_n=interval_n)
+    g = np.random.default_rng(12)
+    p, m = phi0.copy(), n0.copy()
+    st_ref = oracle_lib.villain_neighborhood(N, 0.5, 1, p, m, sweeps, g, interval_n=interval_n)
+    assert sum(s.rejections for s in st_ref) >= 2 * sweeps
+    assert_same(phi, n, st, gen, p, m, st_ref, g)
+    assert [s.rejections for s in st] == [s.rejections for s in st_ref]
+    err = capfd.readouterr().err
+    line = [x for x in err.splitlines() if x.startswith(f'[sv domain] {sweeps} sweeps')]
+    assert line and 'predicted batches 4 (1 pre-scanned), aborts 0' in line[0], err
+
+
+def test_prediction_not_reused_across_interval_n(oracle_lib, monkeypatch):
+    """A scan kept for the batch the next call starts with is tied to the draw parameters it tested: a next call
+    with another interval_n (other Lemire threshold) must not take its finds as skip positions."""
+    monkeypatch.setenv('SV_DOMAIN_PREDICT', '1')
+    monkeypatch.setenv('SV_DOMAIN_BATCH', '2')
+    N = 128
+    phi0, n0 = hot(N, N, 1, 41)
+    dom_gen = np.random.default_rng(13)
+    dom = VillainDomain(N, N, (2, 2), 0.5, 1, interval_n=1048064)
+    try:
+        dom.upload(phi0, n0)
+        dom.run(2, dom_gen)  # leaves a scan for the next call's first batch (threshold 2095104)
+        dom.interval_n = 1
+        st = dom.run(2, dom_gen)  # threshold 1: those words are not rejected
+        phi, n = dom.download()
+    finally:
+        dom.close()
+    g = np.random.default_rng(13)
+    p, m = phi0.copy(), n0.copy()
+    oracle_lib.villain_neighborhood(N, 0.5, 1, p, m, 2, g, interval_n=1048064)
+    ref = oracle_lib.villain_neighborhood(N, 0.5, 1, p, m, 2, g, interval_n=1)
+    assert_same(phi, n, st, dom_gen, p, m, ref, g)
+
+
 def test_chunked_calls_continue_the_chain(oracle_lib):
     """Calls of 3 + 1 + 4 sweeps (ring index carried across calls) equal one call of 8."""
     N = 64
