@@ -160,12 +160,13 @@ void sv_ctx::time_begin(hipEvent_t *a) {
     SV_HIP(hipEventRecord(*a, stream));
 }
 
-void sv_ctx::time_end(hipEvent_t a, int64_t launches) {
+void sv_ctx::time_end(hipEvent_t a, int64_t launches, int64_t first) {
     if (!timing || !a) return;
     hipEvent_t b = take_event(ev_pool);
     SV_HIP(hipEventRecord(b, stream));
     ev_pending.push_back({a, b});
     ev_launches.push_back(launches);
+    ev_first.push_back(first);
 }
 
 void sv_ctx::time_collect() {
@@ -181,6 +182,7 @@ void sv_ctx::time_collect() {
     }
     ev_pending.clear();
     ev_launches.clear();
+    ev_first.clear();
 }
 
 void sv_ctx::time_discard() {
@@ -190,6 +192,25 @@ void sv_ctx::time_discard() {
     }
     ev_pending.clear();
     ev_launches.clear();
+    ev_first.clear();
+}
+
+void sv_ctx::time_keep_before(int64_t bad) {
+    size_t j = 0;
+    for (size_t i = 0; i < ev_pending.size(); i++) {
+        if (ev_first[i] + ev_launches[i] <= bad) {
+            ev_pending[j] = ev_pending[i];
+            ev_launches[j] = ev_launches[i];
+            ev_first[j] = ev_first[i];
+            j++;
+        } else {
+            ev_pool.push_back(ev_pending[i].first);
+            ev_pool.push_back(ev_pending[i].second);
+        }
+    }
+    ev_pending.resize(j);
+    ev_launches.resize(j);
+    ev_first.resize(j);
 }
 
 // Streaming copy b[i] = a[i] with W-byte lanes (16: dwordx4, 8: dwordx2): the measured HBM ceiling the
@@ -424,6 +445,10 @@ int sv_ctx_create(int device, sv_ctx **out) {
         SV_HIP(hipMalloc(&ctx->d_reports, sv::MAX_REPORTS * sizeof(sv::Report)));
         SV_HIP(hipMemset(ctx->d_abort, 0, sizeof(int32_t)));
         SV_HIP(hipMemset(ctx->d_nreport, 0, sizeof(uint32_t)));
+        SV_HIP(hipHostMalloc((void **)&ctx->h_flag, sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent));
+        SV_HIP(hipHostGetDevicePointer((void **)&ctx->d_flag, ctx->h_flag, 0));
+        *ctx->h_flag = 0;
+        for (auto &e : ctx->ev_chunk) SV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         ctx->ensure_blocks(64);
         ctx->ensure_skips(64);
         ctx->ensure_stats(64);
@@ -449,6 +474,9 @@ int sv_ctx_destroy(sv_ctx *ctx) {
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
     (void)hipFree(ctx->d_abort);
     if (ctx->h_abort) (void)hipHostFree(ctx->h_abort);
+    if (ctx->h_flag) (void)hipHostFree(ctx->h_flag);
+    for (auto &e : ctx->ev_chunk)
+        if (e) (void)hipEventDestroy(e);
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
     if (ctx->h_tail) (void)hipHostFree(ctx->h_tail);
     if (ctx->h_stage_abort) (void)hipHostFree(ctx->h_stage_abort);

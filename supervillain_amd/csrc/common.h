@@ -60,6 +60,7 @@ struct DevScratch {
     int32_t *abort;     // nonzero: a rejection (or overflow) was met; later sweeps exit immediately
     uint32_t *nreport;  // count of reports
     Report *reports;
+    int32_t *hflag = nullptr;  // optional host-mapped copy of the abort flag (the host polls it between chunks)
 };
 
 // Asynchronous emission of a resident state: the state is snapshotted on the compute
@@ -101,6 +102,10 @@ struct sv_ctx {
     size_t stats_cap = 0;
     // pinned host image of d_abort: batches that cannot meet a rejection copy it with their stats (one sync)
     int32_t *h_abort = nullptr;
+    // host-mapped abort flag (fine-grained pinned memory: h_flag for the host, d_flag for kernels), written by a
+    // kernel's rejection report so that the host can stop enqueueing a batch that has failed (run_fused)
+    int32_t *h_flag = nullptr, *d_flag = nullptr;
+    hipEvent_t ev_chunk[2] = {nullptr, nullptr};
     // pinned batch tail (abort flag, report count, statistics) of the single-lattice Villain run: one sync
     char *h_tail = nullptr;
     size_t tail_cap = 0;
@@ -110,15 +115,17 @@ struct sv_ctx {
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
     std::vector<int64_t> ev_launches;
+    std::vector<int64_t> ev_first;  // index of the segment's first launch within its batch
     double timed_ms = 0.0;
     int64_t timed_launches = 0;
     // Villain NeighborhoodUpdate sweeps by kernel (sv_ctx_sweep_counts): villain_sweep_hot (+ _fr), the general
     // fused kernel (villain_sweep_fused: int32 n image, skip lists), the per-colour int64 path (villain_pass_generic)
     int64_t sweeps_hot = 0, sweeps_fused = 0, sweeps_generic = 0;
     void time_begin(hipEvent_t *a);
-    void time_end(hipEvent_t a, int64_t launches = 1);
+    void time_end(hipEvent_t a, int64_t launches = 1, int64_t first = 0);
     void time_collect();  // after a stream sync
     void time_discard();  // drop pending (unsynchronized-safe: after a stream sync)
+    void time_keep_before(int64_t bad);  // an aborted batch: keep the segments that ended before launch `bad`
 
     // deferred statistics (sv_ctx_set_deferred): a run whose sweeps cannot meet a NumPy Lemire rejection leaves
     // its statistics (and abort flag) in a pinned staging area and returns without synchronizing; sv_ctx_sync

@@ -20,6 +20,7 @@ __device__ __forceinline__ void report(const DevScratch &S, uint32_t sweep, uint
     uint32_t i = atomicAdd(S.nreport, 1u);
     if (i < (uint32_t)MAX_REPORTS) S.reports[i] = Report{sweep, block, pos, rep};
     __hip_atomic_store(S.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (S.hflag) __hip_atomic_store(S.hflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     // drain here, on the rare path: a result still pending at the join would make the compiler wait
     // for every outstanding load and store (the row prefetch, the finished-row stores) on the common path
     __builtin_amdgcn_s_waitcnt(0);
@@ -98,6 +99,9 @@ __device__ __forceinline__ int32_t wrapN(int32_t v, int32_t N) {
     return v;
 }
 
+#ifndef SV_SKIP_FULLJUMP
+#define SV_SKIP_FULLJUMP 0
+#endif
 #ifndef SV_SCALAR_WAVE
 #define SV_SCALAR_WAVE 1
 #endif
@@ -283,16 +287,23 @@ __device__ __forceinline__ Draws draws_general(const FArgs &A, const Rep &RP, in
         for (int q = 0; q < 4; q++) {
             const Block *B = &RP.blocks[bb + 1 + q];
             uint32_t word, spos = (uint32_t)rank;
-            if (B->nskip == 0) {
-                const int64_t qq = rank - (int64_t)B->has;
+#if SV_SKIP_FULLJUMP  // (timing experiments: the round-2 form, a full table jump per draw of a block with skips)
+            if (B->nskip) {
+                spos = skip_pos(*B, A.skips, (uint32_t)rank);
+                word = bounded_word(T, *B, spos);
+                __builtin_amdgcn_s_waitcnt(0);
+            } else
+#endif
+            {
+                // known rejected positions push this draw's stream position forward (skip_pos); the row base sits
+                // at the unshifted position of column xr, so the shifted word is still a small offset ahead of it
+                // (from_base falls back to a full jump otherwise)
+                if (B->nskip) spos = skip_pos(*B, A.skips, (uint32_t)rank);
+                const int64_t qq = (int64_t)spos - (int64_t)B->has;
                 const int64_t wi = qq < 0 ? 0 : (qq >> 1);
                 const uint64_t X = xsl_rr(from_base(T, B, sm, wr ? wb[2 + q] : bases[2 + q], base_pos(2, gq, N, xr, B->has), wi));
                 word = (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
                 if (qq < 0) word = B->buf;  // has && rank == 0: the buffered half-word
-            } else {
-                spos = skip_pos(*B, A.skips, (uint32_t)rank);
-                word = bounded_word(T, *B, spos);
-                __builtin_amdgcn_s_waitcnt(0);
             }
             D.cn[q] = choice_value<K3>(A, RP, word, (uint32_t)(bb + 1 + q), spos);
         }

@@ -931,12 +931,32 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         if (dbg) fprintf(stderr, "[sv] plan %d sweeps: %.1f us\n", count, std::chrono::duration<double, std::micro>(tp1 - tp0).count());
         upload_plan(ctx, blocks, skipvec);
         const int cur0 = st->cur;
-        hipEvent_t ev;
-        const bool per_launch = ctx->timing_mode == 2;  // events around every launch, else around the batch
-        if (!per_launch) ctx->time_begin(&ev);
+        // Timing (sv_ctx_set_timing) measures villain_sweep_hot only: events around each run of consecutive hot
+        // launches (mode 1) or around every hot launch (mode 2); the general kernel's replays are not counted
+        hipEvent_t seg = nullptr;
+        int seg_k0 = 0;
+        const bool per_launch = ctx->timing_mode == 2;
+        // Large lattices enqueue a batch in chunks of CH sweeps and, after enqueueing chunk j, wait for chunk j-1 and
+        // read the host-mapped abort flag: a sweep that meets a NumPy Lemire rejection then leaves at most ~2 CH
+        // launches queued behind it (each an early exit over every workgroup, ~5 us at L=4096) instead of the rest of
+        // a 64-sweep batch.  The GPU always has a chunk queued (CH sweeps >> the host's enqueue time).
+        static const int CH_env = [] {  // SV_CHUNK overrides the chunk (0: the whole batch)
+            const char *e = getenv("SV_CHUNK");
+            return e ? atoi(e) : -1;
+        }();
+        const int CH = CH_env > 0 ? CH_env : (CH_env == 0 || V < (int64_t(1) << 20) ? count : 4);
+        int launched = count;
+        *ctx->h_flag = 0;
         for (int k = 0; k < count; k++) {
-            hipEvent_t ev1;
-            if (per_launch) ctx->time_begin(&ev1);
+            const bool hot_k = use_hot && !hot_off && NWv == 4 && hot_ok(P, &blocks[(size_t)k * nb]);
+            if (!hot_k && seg) {
+                ctx->time_end(seg, k - seg_k0, seg_k0);
+                seg = nullptr;
+            }
+            if (hot_k && !seg) {
+                ctx->time_begin(&seg);
+                seg_k0 = k;
+            }
             FArgs A;
             A.P = P;
             A.G = FGeom{N, N, 0, 0, N, N, N, V, 0};
@@ -955,9 +975,10 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             A.adv[2] = adv[2];
             A.stat = ctx->d_stats + k;
             A.S = scratch(ctx);
+            A.S.hflag = ctx->d_flag;
             A.sweep = (uint32_t)k;
             farg_single(A, nsx, nsy);
-            if (use_hot && !hot_off && NWv == 4 && hot_ok(P, &blocks[(size_t)k * nb])) {
+            if (hot_k) {
                 if (hot_nw == 8) {
                     A.hot_nw = 8;
                     A.adv[0] = adv8[0];
@@ -974,10 +995,24 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
 #endif
                 else villain_sweep_fused<4, false, false, false><<<grid, 4 * 64, 0, ctx->stream>>>(A);
             }
-            if (per_launch) ctx->time_end(ev1, 1);
+            if (per_launch && seg) {
+                ctx->time_end(seg, 1, k);
+                seg = nullptr;
+            }
             st->cur ^= 1;
+            if ((k + 1) % CH == 0 && k + 1 < count) {
+                const int j = (k + 1) / CH - 1;  // chunk j is enqueued
+                SV_HIP(hipEventRecord(ctx->ev_chunk[j & 1], ctx->stream));
+                if (j >= 1) {
+                    SV_HIP(hipEventSynchronize(ctx->ev_chunk[(j - 1) & 1]));
+                    if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE)) {
+                        launched = k + 1;  // the rest of the batch is not enqueued
+                        break;
+                    }
+                }
+            }
         }
-        if (!per_launch) ctx->time_end(ev, count);
+        if (seg) ctx->time_end(seg, launched - seg_k0, seg_k0);
         SV_HIP(hipGetLastError());
         auto tp2 = std::chrono::steady_clock::now();
         AbortInfo a = read_abort_stats(ctx, count, stats + sw);
@@ -985,7 +1020,12 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         if (dbg)
             fprintf(stderr, "[sv] launch %.1f us, wait %.1f us\n", std::chrono::duration<double, std::micro>(tp2 - tp1).count(),
                     std::chrono::duration<double, std::micro>(tp3 - tp2).count());
-        if (a.abort) ctx->time_discard();  // aborted launches exit early: keep the average honest
+        // aborted launches exit early: only the timed segments that ended before the first failing sweep count
+        if (a.abort) {
+            uint32_t first = ~0u;
+            for (const Report &r : a.reports) first = std::min(first, r.sweep);
+            ctx->time_keep_before(first == ~0u ? 0 : first);
+        }
         ctx->time_collect();
         if (!a.abort) {  // the stats already landed with the abort flag
             for (int k = 0; k < count; k++) {

@@ -1,0 +1,143 @@
+"""Statistical parity of the GPU-native chains with the reference's chains, set up the way the reference compares its
+own algorithms (example/worldline-algorithm-comparison.py:22-25,37-42 and example/villain-algorithm-comparison.py:
+22-26,40-60): an ergodic combination of updates per chain, cold start, the reference's observable set measured on
+every configuration, thermalization cut, blocked-bootstrap means compared within 4 standard errors.
+
+* Worldline: checkerboard PlaquetteUpdate (mode='checkerboard', the chain config 3 benches) + Vortex + Coexact +
+  Wrapping against the reference-order PlaquetteUpdate (plaquette.py:35-104, bit-exact with the reference) + Vortex +
+  Coexact + Wrapping, both on the GPU; ActionDensity, InternalEnergyDensity, InternalEnergyDensitySquared,
+  WindingSquared, WrappingSquared (observable/action.py:35-47, energy.py:34-47,84-100, winding.py:40-52,
+  wrapping.py:28-59) at N = 8, 16 and kappa = 0.3, 0.5, 1.0.
+* Villain: the counter-based NeighborhoodUpdate (Philox mode) against the reference's comparison
+  suite Link + Site + Exact + Cohomology (villain-algorithm-comparison.py:52-60) on the PCG64 replay; ActionDensity,
+  InternalEnergyDensity, InternalEnergyDensitySquared, WindingSquared (observable/action.py:25-31, energy.py:25-30,
+  70-80, winding.py:30-37) at N = 8, 16 and kappa = 0.25, 0.5, 1.0.
+
+The power of the comparison is checked too: the same chains at kappa = 0.45 against 0.5 must differ by more than
+4 standard errors in some observable."""
+import numpy as np
+import pytest
+
+import supervillain_amd as sv
+from supervillain_amd.generator import Sequentially
+from supervillain_amd.generator import villain as V
+from supervillain_amd.generator import worldline as WL
+from tests.statparity import blocked_bootstrap, delta_v
+
+pytestmark = pytest.mark.gpu
+
+WORLDLINE_NAMES = ('ActionDensity', 'InternalEnergyDensity', 'InternalEnergyDensitySquared', 'WindingSquared',
+                   'WrappingSquared')
+VILLAIN_NAMES = ('ActionDensity', 'InternalEnergyDensity', 'InternalEnergyDensitySquared', 'WindingSquared')
+
+
+def worldline_observables(m, v, kappa, W):
+    """The reference's Worldline observables per configuration; m (steps, 2, N, N), v (steps, 1, N, N)."""
+    steps, _, N, _ = m.shape
+    links, sites = 2 * N * N, N * N
+    f = m.astype(np.float64) - np.stack([delta_v(v[i, 0], W) for i in range(steps)])  # Links = m - delta v / W
+    S2 = (f ** 2).sum(axis=(1, 2, 3))
+    act = (links / 2 - 0.5 / kappa * S2) / sites
+    U = act / kappa
+    pk = (links / 2 - 0.5 / kappa * S2) / kappa
+    p2k = (S2 / kappa - links / 2) / kappa ** 2
+    U2 = (pk ** 2 - p2k) / sites ** 2
+    # d of the 1-form Links (D=2): (dL)[x] = (L1[x + e0] - L1[x]) - (L0[x + e1] - L0[x])
+    dL = (np.roll(f[:, 1], -1, axis=1) - f[:, 1]) - (np.roll(f[:, 0], -1, axis=2) - f[:, 0])
+    w2 = 1 / (np.pi ** 2 * kappa) - (dL ** 2).mean(axis=(1, 2)) / (2 * np.pi * kappa) ** 2
+    tw = m.sum(axis=(2, 3)) / N
+    return np.stack([act, U, U2, w2, (tw ** 2).sum(axis=1)], axis=1)
+
+
+def villain_observables(phi, n, kappa):
+    """The reference's Villain observables per configuration; phi (steps, 1, N, N), n (steps, 2, N, N)."""
+    N = phi.shape[-1]
+    p = phi[:, 0]
+    l0 = (np.roll(p, -1, axis=1) - p) - 2 * np.pi * n[:, 0]
+    l1 = (np.roll(p, -1, axis=2) - p) - 2 * np.pi * n[:, 1]
+    S = kappa / 2 * ((l0 ** 2).sum(axis=(1, 2)) + (l1 ** 2).sum(axis=(1, 2)))
+    U = S / (N * N * kappa)
+    dn = (np.roll(n[:, 1], -1, axis=1) - n[:, 1]) - (np.roll(n[:, 0], -1, axis=2) - n[:, 0])
+    return np.stack([S / (N * N), U, U ** 2, (dn.astype(np.float64) ** 2).mean(axis=(1, 2))], axis=1)
+
+
+def worldline_chain(N, kappa, mode, steps, seed, measure_kappa=None):
+    L = sv.Lattice2D(N)
+    S = sv.Worldline(L, kappa, 1)
+    gens = [WL.PlaquetteUpdate(S, mode=mode), WL.VortexUpdate(S), WL.CoexactUpdate(S), WL.WrappingUpdate(S)]
+    for i, g in enumerate(gens):
+        g.rng = np.random.default_rng(1000 * seed + i)
+    np.random.seed(seed)  # the reference-order Plaquette's global-RandomState permutation (plaquette.py:63)
+    E = sv.Ensemble(S).generate(steps, Sequentially(gens))
+    return worldline_observables(np.asarray(E.configuration.m.array), np.asarray(E.configuration.v.array),
+                                 measure_kappa or kappa, 1)
+
+
+def villain_chain(N, kappa, suite, steps, seed, measure_kappa=None):
+    L = sv.Lattice2D(N)
+    S = sv.Villain(L, kappa, 1)
+    if suite == 'philox':
+        gens = [V.NeighborhoodUpdate(S, philox=0x5EED0000 + seed)]
+    else:
+        gens = [V.LinkUpdate(S), V.SiteUpdate(S), V.ExactUpdate(S), V.CohomologyUpdate(S)]
+        for i, g in enumerate(gens):
+            g.rng = np.random.default_rng(1000 * seed + i)
+    E = sv.Ensemble(S).generate(steps, Sequentially(gens))
+    return villain_observables(np.asarray(E.configuration.phi.array), np.asarray(E.configuration.n.array),
+                               measure_kappa or kappa)
+
+
+def zscores(a, b, names, cut, blocks=100):
+    out = {}
+    for k, name in enumerate(names):
+        ma, ea = blocked_bootstrap(a[cut:, k], blocks)
+        mb, eb = blocked_bootstrap(b[cut:, k], blocks)
+        out[name] = ((ma - mb) / np.hypot(ea, eb) if ea + eb > 0 else 0.0, ma, ea, mb, eb)
+    return out
+
+
+def assert_agree(zs, label):
+    print(label, ' '.join(f'{k}: z={v[0]:+.2f}' for k, v in zs.items()))
+    for name, (z, ma, ea, mb, eb) in zs.items():
+        if ea == 0 and eb == 0:
+            # a sector neither chain leaves at this kappa and volume (no torus wrapping is ever accepted at N=16,
+            # kappa=0.3): the constant values must be equal
+            assert ma == mb, f'{label} {name}: constant {ma} vs {mb}'
+            continue
+        assert abs(z) < 4.0, f'{label} {name}: {ma:.6g} +- {ea:.2g} vs {mb:.6g} +- {eb:.2g} (z = {z:.2f})'
+
+
+WL_STEPS = {8: 16000, 16: 8000}
+
+
+@pytest.mark.parametrize('kappa', [0.3, 0.5, 1.0])
+@pytest.mark.parametrize('N', [8, 16])
+def test_worldline_checkerboard_vs_reference_order(N, kappa):
+    steps = WL_STEPS[N]
+    cb = worldline_chain(N, kappa, 'checkerboard', steps, 1)
+    ref = worldline_chain(N, kappa, 'reference', steps, 2)
+    assert_agree(zscores(cb, ref, WORLDLINE_NAMES, steps // 10), f'Worldline N={N} kappa={kappa}')
+
+
+VL_STEPS = {8: 40000, 16: 20000}
+
+
+@pytest.mark.parametrize('kappa', [0.25, 0.5, 1.0])
+@pytest.mark.parametrize('N', [8, 16])
+def test_villain_philox_vs_reference_suite(N, kappa):
+    steps = VL_STEPS[N]
+    ph = villain_chain(N, kappa, 'philox', steps, 1)
+    ref = villain_chain(N, kappa, 'pcg64', steps, 2)
+    assert_agree(zscores(ph, ref, VILLAIN_NAMES, steps // 10), f'Villain N={N} kappa={kappa}')
+
+
+def test_comparison_has_power():
+    """A chain that samples kappa = 0.45, measured as if it were kappa = 0.5, must fail the same comparison against
+    a kappa = 0.5 chain: the tests above can see a shifted distribution, not only a broken chain."""
+    N, steps = 8, WL_STEPS[8]
+    a = worldline_chain(N, 0.45, 'checkerboard', steps, 3, measure_kappa=0.5)
+    b = worldline_chain(N, 0.5, 'reference', steps, 4)
+    assert max(abs(z[0]) for z in zscores(a, b, WORLDLINE_NAMES, steps // 10).values()) > 4.0
+    a = villain_chain(N, 0.45, 'philox', steps, 3, measure_kappa=0.5)
+    b = villain_chain(N, 0.5, 'pcg64', steps, 4)
+    assert max(abs(z[0]) for z in zscores(a, b, VILLAIN_NAMES, steps // 10).values()) > 4.0
