@@ -1,0 +1,84 @@
+"""Per-workgroup timeline of villain_sweep_hot (variant built with -DSV_WGTIME=1: entry / loop start / loop end / exit
+timestamps from s_memrealtime, 100 MHz, and the hardware ids).  Usage:
+  SV_LIB_OVERRIDE=supervillain_amd/variants/libsvhip_wgtime.so python scripts/perf/wg_timeline.py [single|tile] ..."""
+import ctypes
+import sys
+
+import numpy as np
+
+sys.path.insert(0, '.')
+from supervillain_amd import _native  # noqa: E402
+from supervillain_amd._abi import rng_from_numpy  # noqa: E402
+from supervillain_amd.domain import VillainDomain  # noqa: E402
+
+Lib = _native.lib()
+Lib.sv_debug_wgtime.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+
+
+def read(nwg):
+    buf = np.zeros(nwg * 5, dtype=np.uint64)
+    assert Lib.sv_debug_wgtime(buf.ctypes.data, nwg) == 0
+    return buf.reshape(nwg, 5)
+
+
+def summarize(tag, t, nsx=None):
+    idx = np.nonzero(t[:, 0] > 0)[0]
+    t = t[idx]
+    t0 = t[:, 0].min()
+    e, l0, l1, x = [(t[:, i].astype(np.int64) - int(t0)) * 0.01 for i in range(4)]  # us
+    hw = t[:, 4] & 0xFFFFFFFF
+    xcc = (t[:, 4] >> 32) & 0xF
+    cu = (hw >> 8) & 0xF
+    sh = (hw >> 12) & 1
+    se = (hw >> 13) & 7
+    cuid = ((xcc * 8 + se) * 2 + sh) * 16 + cu
+    ncu = len(np.unique(cuid))
+    per_cu = np.bincount(np.unique(cuid, return_inverse=True)[1])
+    print(f'[{tag}] {len(t)} WGs on {ncu} CUs (WGs per CU: min {per_cu.min()} max {per_cu.max()} mean {per_cu.mean():.2f}); '
+          f'span {x.max():.1f} us; entry skew max {e.max():.1f} us (p50 {np.median(e):.1f}); '
+          f'prologue p50 {np.median(l0 - e):.1f} p90 {np.percentile(l0 - e, 90):.1f} us; loop p50 {np.median(l1 - l0):.1f} '
+          f'p90 {np.percentile(l1 - l0, 90):.1f} max {(l1 - l0).max():.1f} us; epilogue p50 {np.median(x - l1):.1f} us; '
+          f'WG lifetime p50 {np.median(x - e):.1f} max {(x - e).max():.1f} us', flush=True)
+    # occupancy over time: WGs resident (entry..exit) in 2-us bins
+    bins = np.arange(0, x.max() + 2, 2.0)
+    occ = [int(((e <= b) & (x > b)).sum()) for b in bins]
+    print(f'[{tag}] resident WGs every 2 us: {occ}', flush=True)
+    if nsx:
+        # logical strip index of each launch slot (hot_body's XCD-aware mapping), its column strip
+        G = len(idx)
+        per, rem = G // 8, G % 8
+        xcd_, k_ = idx & 7, idx >> 3
+        b = xcd_ * per + np.minimum(xcd_, rem) + k_
+        ix = b % nsx
+        loop = l1 - l0
+        by_ix = [float(np.mean(loop[ix == i])) for i in range(nsx)]
+        print(f'[{tag}] loop us by column strip: ' + ' '.join(f'{v:.0f}' for v in by_ix), flush=True)
+        order = np.argsort(e)
+        thirds = np.array_split(order, 4)
+        print(f'[{tag}] loop us by dispatch quarter: ' + ' '.join(f'{np.mean(loop[q]):.1f}' for q in thirds) +
+              f'; lifetime by quarter: ' + ' '.join(f'{np.mean((x - e)[q]):.1f}' for q in thirds), flush=True)
+
+
+mode = sys.argv[1] if len(sys.argv) > 1 else 'single'
+ctx = _native.context(0)
+if mode == 'single':
+    L = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+    h = ctypes.c_void_p()
+    ctx.check(Lib.sv_villain_create(ctx.handle, L, ctypes.byref(h)), 'create')
+    phi = np.zeros((L, L))
+    n = np.zeros((2, L, L), dtype=np.int64)
+    ctx.check(Lib.sv_villain_upload(h, _native.ptr(phi), _native.ptr(n)), 'upload')
+    r = rng_from_numpy(np.random.default_rng(0))
+    st = _native.stats_array(64)
+    for k in range(4):
+        ctx.check(Lib.sv_villain_run(h, 0.5, 1, float(np.pi), 1, 1, ctypes.byref(r), st, 2), 'run')
+        summarize(f'L={L} sweep {k}', read(65536), nsx=(L + 122) // 123)
+else:
+    Nt, Nx = int(sys.argv[2]), int(sys.argv[3])
+    dom = VillainDomain(Nt, Nx, (1, 1), 0.5, 1)
+    dom.cold()
+    g = np.random.default_rng(0)
+    for k in range(3):
+        dom.run(4, g)  # the last launch of a 4-sweep group decides exactly the tile
+        summarize(f'tile {Nt}x{Nx} group {k}', read(65536), nsx=(Nx + 122) // 123)
+    dom.close()

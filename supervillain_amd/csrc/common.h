@@ -171,6 +171,9 @@ struct sv_villain {
     size_t aux_cap = 0;
     double *d_obs = nullptr;       // inline observables: 4 device sums (coarse-grained hipMalloc)
     double *h_obs = nullptr;       // and their pinned host image
+    int32_t *d_strips = nullptr;   // villain_sweep_hot's strip table (strip_schedule), n_strips entries of 3
+    int32_t n_strips = 0;
+    std::string strips_key;        // the schedule the table holds
 };
 
 namespace sv {

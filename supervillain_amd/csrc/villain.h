@@ -67,7 +67,9 @@ struct FArgs {
     const JumpTables *const *Trep;  // per-replica tables, or nullptr (all use T)
     const Affine *advrep;           // per-replica adv[3], or nullptr (all use adv)
     double *obs;                    // OBS kernels: per replica {sum (d phi - 2 pi n)^2, sum (dn)^2, sum n0, sum n1}
-    const int32_t *strip_map = nullptr;  // TILE: launch index -> strip index (interior / boundary launches)
+    // villain_sweep_hot: per strip (in the XCD-aware logical order) its column strip and rows {ix, t0, t1}, or null
+    // (uniform strips of TH rows); lets the strips of the last rounds of slots be shorter (strip_schedule)
+    const int32_t *strips = nullptr;
     const int32_t *rep_map = nullptr;    // replica batches: launch's replica slot -> replica (a subset launch), or identity
     // TILE: the window of the launch's region whose sites are counted in the statistics, [r0, r1) x [c0, c1) in
     // region coordinates (domain.hip's deep halos run sweeps over a tile extended by a ring it does not own)

@@ -167,7 +167,6 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
         b = xcd * per + (xcd < rem ? xcd : rem) + k;
     }
     // domain tiles: the launch covers a subset of the strips (interior ones while the halos travel)
-    if (TILE && A.strip_map) b = __builtin_amdgcn_readfirstlane(A.strip_map[b]);
     // replica of this workgroup (replica batches; 0 otherwise)
     const int slot = REPS ? __builtin_amdgcn_readfirstlane(b / A.tiles_per_rep) : 0;  // uniform: keep it scalar
     if (REPS) b = __builtin_amdgcn_readfirstlane(b - slot * A.tiles_per_rep);
@@ -661,7 +660,7 @@ void farg_single(FArgs &A, int nsx, int nsy) {
     A.Trep = nullptr;
     A.advrep = nullptr;
     A.obs = nullptr;
-    A.strip_map = nullptr;
+    A.strips = nullptr;
     A.rep_map = nullptr;
 }
 
@@ -880,6 +879,43 @@ void run_generic(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, 
     }
 }
 
+// Strip schedule of villain_sweep_hot on a single lattice.  With uniform strips the last round of the chip's
+// workgroup slots is partly empty while its strips finish (the WG timeline of an L=4096 sweep, r3: slots ~80% busy,
+// a ~45 us tail of 240 us).  The lattice rows are cut into 8 bands, one per XCD (workgroup i runs on XCD i mod 8,
+// and hot_body's logical order gives each XCD a contiguous range), and each band into segments whose heights (a
+// descending list, e.g. "56x5,40x5,32") put the tall strips first and the short ones in the last rounds.  Returns
+// the table {ix, t0, t1} per logical strip, or an empty vector when the spec does not apply (then uniform TH).
+std::vector<int32_t> strip_schedule(int32_t Nt, int nsx, const std::string &spec) {
+    std::vector<int32_t> hs;
+    size_t p = 0;
+    while (p < spec.size()) {
+        size_t q = spec.find(',', p);
+        if (q == std::string::npos) q = spec.size();
+        const std::string tok = spec.substr(p, q - p);
+        const size_t x = tok.find('x');
+        const int h = atoi(tok.substr(0, x).c_str()), m = x == std::string::npos ? 1 : atoi(tok.substr(x + 1).c_str());
+        if (h < 4 || h % 4 || m < 1) return {};
+        for (int i = 0; i < m; i++) hs.push_back(h);
+        p = q + 1;
+    }
+    int32_t band = 0;
+    for (int h : hs) band += h;
+    if (hs.empty() || (int64_t)band * 8 != Nt) return {};
+    std::vector<int32_t> tab;
+    for (int xcd = 0; xcd < 8; xcd++) {
+        int32_t t = xcd * band;
+        for (int h : hs) {
+            for (int ix = 0; ix < nsx; ix++) {
+                tab.push_back(ix);
+                tab.push_back(t);
+                tab.push_back(t + h);
+            }
+            t += h;
+        }
+    }
+    return tab;
+}
+
 // returns false if the fused path cannot represent the state (|n| too large): caller falls back
 bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u128 inc, sv_stats *stats,
                int &done_sweeps) {
@@ -916,6 +952,22 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     int sw = 0;
     const bool dbg = getenv("SV_DEBUG_TIMING") != nullptr;
     const bool use_hot = hot_enabled() && V < (int64_t(1) << 28);  // villain_sweep_hot's 32-bit row offsets
+    // the hot kernel's strip schedule (SV_STRIPS overrides; "" = uniform strips of TH rows)
+    {
+        const char *e = getenv("SV_STRIPS");
+        const std::string spec = e ? e : "";
+        if (spec != st->strips_key || !st->d_strips) {
+            const std::vector<int32_t> tab = hot_nw == 4 ? strip_schedule(N, nsx, spec) : std::vector<int32_t>{};
+            if (st->d_strips) SV_HIP(hipFree(st->d_strips));
+            st->d_strips = nullptr;
+            st->n_strips = (int32_t)(tab.size() / 3);
+            if (!tab.empty()) {
+                SV_HIP(hipMalloc(&st->d_strips, tab.size() * sizeof(int32_t)));
+                SV_HIP(hipMemcpy(st->d_strips, tab.data(), tab.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+            }
+            st->strips_key = spec;
+        }
+    }
     // |n| beyond villain_sweep_hot's int16 image: the failing sweep is replayed, and the rest of the call runs, on
     // villain_sweep_fused's int32 image; only an overflow of that one falls back to the per-colour int64 path
     bool hot_off = false;
@@ -930,7 +982,8 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         auto tp1 = std::chrono::steady_clock::now();
         if (dbg) fprintf(stderr, "[sv] plan %d sweeps: %.1f us\n", count, std::chrono::duration<double, std::micro>(tp1 - tp0).count());
         upload_plan(ctx, blocks, skipvec);
-        const int cur0 = st->cur;
+        // sweep k of the batch reads buffer cur ^ (k & 1); after m sweeps the state is in cur ^ (m & 1)
+        auto set_current = [&](int m) { st->cur ^= m & 1; };
         // Timing (sv_ctx_set_timing) measures villain_sweep_hot only: events around each run of consecutive hot
         // launches (mode 1) or around every hot launch (mode 2); the general kernel's replays are not counted
         hipEvent_t seg = nullptr;
@@ -947,7 +1000,8 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         const int CH = CH_env > 0 ? CH_env : (CH_env == 0 || V < (int64_t(1) << 20) ? count : 4);
         int launched = count;
         *ctx->h_flag = 0;
-        for (int k = 0; k < count; k++) {
+        int next_chunk = CH;
+        for (int k = 0; k < count;) {
             const bool hot_k = use_hot && !hot_off && NWv == 4 && hot_ok(P, &blocks[(size_t)k * nb]);
             if (!hot_k && seg) {
                 ctx->time_end(seg, k - seg_k0, seg_k0);
@@ -960,10 +1014,10 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             FArgs A;
             A.P = P;
             A.G = FGeom{N, N, 0, 0, N, N, N, V, 0};
-            A.phi_in = st->phi[st->cur];
-            A.n_in = st->n[st->cur];
-            A.phi_out = st->phi[st->cur ^ 1];
-            A.n_out = st->n[st->cur ^ 1];
+            A.phi_in = st->phi[st->cur ^ (k & 1)];
+            A.n_in = st->n[st->cur ^ (k & 1)];
+            A.phi_out = st->phi[st->cur ^ (k & 1) ^ 1];
+            A.n_out = st->n[st->cur ^ (k & 1) ^ 1];
             A.nsx = nsx;
             A.TH = TH;
             A.nsy = nsy;
@@ -985,7 +1039,8 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                     A.adv[1] = adv8[1];
                     A.adv[2] = adv8[2];
                 }
-                launch_hot(A, grid, ctx->stream);
+                if (st->d_strips) A.strips = st->d_strips;
+                launch_hot(A, st->d_strips ? st->n_strips : grid, ctx->stream);
                 ctx->sweeps_hot++;
             } else {
                 ctx->sweeps_fused++;
@@ -999,14 +1054,15 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                 ctx->time_end(seg, 1, k);
                 seg = nullptr;
             }
-            st->cur ^= 1;
-            if ((k + 1) % CH == 0 && k + 1 < count) {
-                const int j = (k + 1) / CH - 1;  // chunk j is enqueued
+            k++;
+            if (k >= next_chunk && k < count) {
+                const int j = next_chunk / CH - 1;  // chunk j is enqueued
+                next_chunk += CH;
                 SV_HIP(hipEventRecord(ctx->ev_chunk[j & 1], ctx->stream));
                 if (j >= 1) {
                     SV_HIP(hipEventSynchronize(ctx->ev_chunk[(j - 1) & 1]));
                     if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE)) {
-                        launched = k + 1;  // the rest of the batch is not enqueued
+                        launched = k;  // the rest of the batch is not enqueued
                         break;
                     }
                 }
@@ -1039,6 +1095,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             }
             cur = c;
             sw += count;
+            set_current(count);
             continue;
         }
         // earliest failing (sweep, block); an overflow tag sorts after every rejection of its sweep
@@ -1073,7 +1130,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                 }
                 cur = c2;
             }
-            st->cur = cur0 ^ (bad & 1);
+            set_current(bad);
             if (to_int32) {
                 hot_off = true;
                 sw += bad;
@@ -1104,7 +1161,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             }
             cur = c2;
         }
-        st->cur = cur0 ^ (bad & 1);
+        set_current(bad);
         sw += bad;
     }
     done_sweeps = sweeps;
@@ -1160,6 +1217,7 @@ int sv_villain_destroy(sv_villain *st) {
     if (st->d_aux) (void)hipFree(st->d_aux);
     if (st->h_aux) (void)hipHostFree(st->h_aux);
     if (st->d_obs) (void)hipFree(st->d_obs);
+    if (st->d_strips) (void)hipFree(st->d_strips);
     if (st->h_obs) (void)hipHostFree(st->h_obs);
     st->emitter.release();
     delete st;

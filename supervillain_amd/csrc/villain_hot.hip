@@ -38,7 +38,17 @@
 #define SV_HOT_PH_OCC 4  // the counter-based kernel (29.5 KB of LDS, 81 VGPRs): 4, 5 and 6 waves/SIMD measured flat (r336)
 #endif
 
+#ifndef SV_WGTIME
+#define SV_WGTIME 0  // timing experiments: per-workgroup timestamps (sv_debug_wgtime)
+#endif
+
 namespace sv {
+
+#if SV_WGTIME
+// per launch slot: [wg][0..3] = entry, loop start, loop end, exit (s_memrealtime, 100 MHz), [4] = HW_ID
+__device__ uint64_t g_wgtime[65536 * 5];
+__device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
+#endif
 
 struct HotDraws {
     double u, dphi;
@@ -141,8 +151,16 @@ using HotLDS = HotLDST<false>;
 // replica draws unpaired (the EDGE form).  OBS: the inline observables fused into the row stores.
 // PH: the optional counter-based mode (SURVEY.md 8(b) sv_rng mode 1): every draw is Philox4x32-10 of (global site,
 // sweep, slot) -- no stream positions, row bases, jump tables or replays
+// the launch's logical workgroup index: workgroups are dealt round-robin over the 8 XCDs, so each XCD gets a
+// contiguous range of logical indices (neighbouring strips share an L2)
+__device__ __forceinline__ int logical_block() {
+    const int b = blockIdx.x, G = gridDim.x, per = G / 8, rem = G % 8;
+    const int xcd = b & 7, k = b >> 3;
+    return xcd * per + (xcd < rem ? xcd : rem) + k;
+}
+
 template <bool TILE, bool EDGE, bool FR = false, bool OBS = false, bool PH = false, int NWT = 4>
-__device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, NWT> &Ls) {
+__device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, NWT> &Ls, int bl) {
     static_assert(!(FR && TILE), "full-row replica strips are periodic");
     static_assert(NWT == 4 || (NWT == 8 && !FR && !PH), "8-wave strips: single lattices and tiles");
     constexpr int NW = NWT;
@@ -162,6 +180,9 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     int32_t &s_bad = Ls.bad;
 
     if (*(volatile const int32_t *)A.S.abort) return;
+#if SV_WGTIME
+    const uint64_t wg_t0 = rt_now();
+#endif
 
     const FGeom &Gm = A.G;
     const int32_t Nt = Gm.Nt, Nx = Gm.Nx;
@@ -172,13 +193,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     auto mcol = [&](int32_t c) -> int32_t { return TILE ? c : wrapN(c, Nx); };
     const int32_t par0 = (Gm.T0 + Gm.X0) & 1;
 
-    int b = blockIdx.x;
-    {
-        const int G = gridDim.x, per = G / 8, rem = G % 8;
-        const int xcd = b & 7, k = b >> 3;
-        b = xcd * per + (xcd < rem ? xcd : rem) + k;
-    }
-    if (TILE && A.strip_map) b = __builtin_amdgcn_readfirstlane(A.strip_map[b]);
+    int b = bl;
     const int slot = FR ? __builtin_amdgcn_readfirstlane(b / A.tiles_per_rep) : 0;  // uniform: keep it scalar
     if (FR) b = __builtin_amdgcn_readfirstlane(b - slot * A.tiles_per_rep);
     const int rep = FR && A.rep_map ? __builtin_amdgcn_readfirstlane(A.rep_map[slot]) : slot;
@@ -188,11 +203,19 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     const int64_t *n_in = FR ? A.n_in + 2 * rep * A.rep_field : A.n_in;
     double *phi_out = FR ? A.phi_out + rep * A.rep_field : A.phi_out;
     int64_t *n_out = FR ? A.n_out + 2 * rep * A.rep_field : A.n_out;
-    const int ix = b % A.nsx, iy = b / A.nsx;
+    int ix, t0s, t1s;
+    if (!FR && A.strips) {
+        ix = __builtin_amdgcn_readfirstlane(A.strips[3 * b]);
+        t0s = __builtin_amdgcn_readfirstlane(A.strips[3 * b + 1]);
+        t1s = __builtin_amdgcn_readfirstlane(A.strips[3 * b + 2]);
+    } else {
+        ix = b % A.nsx;
+        t0s = (b / A.nsx) * A.TH;
+        t1s = t0s + A.TH < Gm.Ht ? t0s + A.TH : Gm.Ht;
+    }
     const int32_t x0 = (int32_t)((int64_t)ix * Gm.Wt / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * Gm.Wt / A.nsx);
     const int32_t w = x1 - x0;
-    const int32_t t0 = iy * A.TH;
-    const int32_t t1 = t0 + A.TH < Gm.Ht ? t0 + A.TH : Gm.Ht;
+    const int32_t t0 = t0s, t1 = t1s;
     // the sites this strip counts in the statistics (its own, within the launch's owned window)
     const int32_t q_lo = TILE && A.own_r0 > t0 ? A.own_r0 : t0, q_hi = TILE && A.own_r1 < t1 ? A.own_r1 : t1;
     const int32_t c_lo = TILE && A.own_c0 > x0 ? A.own_c0 : x0, c_hi = TILE && A.own_c1 < x1 ? A.own_c1 : x1;
@@ -460,6 +483,9 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
         commit(ra);
     }
     __syncthreads();
+#if SV_WGTIME
+    const uint64_t wg_t1 = rt_now();
+#endif
 
     const double hk = P.half_kappa;
     for (int32_t t = tfirst; t < t1; t += NW) {
@@ -605,6 +631,9 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
         }
         if (!(SV_ABLATE & 32)) __syncthreads();
     }
+#if SV_WGTIME
+    const uint64_t wg_t2 = rt_now();
+#endif
     {
         int32_t tl = tfirst;
         while (tl + NW < t1) tl += NW;
@@ -612,6 +641,19 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     }
     if (s_bad && threadIdx.x == 0) report(A.S, A.sweep, OVERFLOW_BLOCK, 0, (uint32_t)rep);
     flush_stats(FR ? A.stat + (int64_t)rep * A.rep_stat : A.stat, acc_count, psum);
+#if SV_WGTIME
+    __builtin_amdgcn_s_waitcnt(0);
+    if (threadIdx.x == 0 && blockIdx.x < 65536) {
+        uint64_t *o = g_wgtime + 5 * (size_t)blockIdx.x;
+        o[0] = wg_t0;
+        o[1] = wg_t1;
+        o[2] = wg_t2;
+        o[3] = rt_now();
+        // HW_ID (hwreg 4: wave, SIMD, CU, SH, SE) and XCC_ID (hwreg 20)
+        o[4] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+               ((uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32);
+    }
+#endif
     if constexpr (FR && OBS) {
         // |sum n0|, |sum n1| <= 2 sites x 2^14 x strip rows < 2^31: the packed halves decode exactly
         const uint64_t pk = Ls.ol.npk[threadIdx.x];
@@ -640,13 +682,13 @@ __global__ __launch_bounds__(NWT * 64) __attribute__((amdgpu_waves_per_eu(SV_HOT
         const int xcd = b & 7, k = b >> 3;
         b = xcd * per + (xcd < rem ? xcd : rem) + k;
     }
-    if (TILE && A.strip_map) b = A.strip_map[b];
-    const int ix = b % A.nsx;
+    const int ix = A.strips ? A.strips[3 * b] : b % A.nsx;
+    const int bl = b;
     const int32_t x0 = (int32_t)((int64_t)ix * A.G.Wt / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * A.G.Wt / A.nsx);
     const int32_t gx0 = wrapN(A.G.X0 + x0, A.G.Nx);
     const bool interior = gx0 >= 4 && gx0 + (x1 - x0) + 2 < A.G.Nx;
-    if (__builtin_amdgcn_readfirstlane((int)interior)) hot_body<TILE, false, false, false, false, NWT>(A, Ls);
-    else hot_body<TILE, true, false, false, false, NWT>(A, Ls);
+    if (__builtin_amdgcn_readfirstlane((int)interior)) hot_body<TILE, false, false, false, false, NWT>(A, Ls, bl);
+    else hot_body<TILE, true, false, false, false, NWT>(A, Ls, bl);
 }
 
 template __global__ void villain_sweep_hot<false, 4>(FArgs);
@@ -668,9 +710,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4
     const int slot = b / A.tiles_per_rep;
     const Block *blk = A.blocks + (int64_t)(A.rep_map ? A.rep_map[slot] : slot) * A.rep_blocks;
     if (__builtin_amdgcn_readfirstlane((int)(blk[2].has | blk[4].has | blk[7].has | blk[9].has)))
-        hot_body<false, true, true, OBS>(A, Ls);
+        hot_body<false, true, true, OBS>(A, Ls, b);
     else
-        hot_body<false, false, true, OBS>(A, Ls);
+        hot_body<false, false, true, OBS>(A, Ls, b);
 }
 template __global__ void villain_sweep_hot_fr<false>(FArgs);
 template __global__ void villain_sweep_hot_fr<true>(FArgs);
@@ -678,10 +720,16 @@ template __global__ void villain_sweep_hot_fr<true>(FArgs);
 // the counter-based mode on a periodic single lattice (every strip draws the same way)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_PH_OCC))) void villain_sweep_hot_ph(FArgs A) {
     __shared__ HotLDST<true> Ls;
-    hot_body<false, false, false, false, true>(A, Ls);
+    hot_body<false, false, false, false, true>(A, Ls, logical_block());
 }
 
 }  // namespace sv
+
+#if SV_WGTIME
+extern "C" int sv_debug_wgtime(uint64_t *out, int32_t n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(sv::g_wgtime), (size_t)n * 5 * sizeof(uint64_t)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 namespace svh {
 

@@ -9,7 +9,10 @@ every configuration, thermalization cut, blocked-bootstrap means compared within
   WindingSquared, WrappingSquared (observable/action.py:35-47, energy.py:34-47,84-100, winding.py:40-52,
   wrapping.py:28-59) at N = 8, 16 and kappa = 0.3, 0.5, 1.0.
 * Villain: the counter-based NeighborhoodUpdate (Philox mode) against the reference's comparison
-  suite Link + Site + Exact + Cohomology (villain-algorithm-comparison.py:52-60) on the PCG64 replay; ActionDensity,
+  suite Link + Site + Exact + Cohomology (villain-algorithm-comparison.py:52-60) on the PCG64 replay.  The
+  NeighborhoodUpdate alone decorrelates slowly (the reference's own note, villain-algorithm-comparison.py:23; measured
+  with scripts/perf/villain_tau.py: tau_int of ActionDensity up to ~310 sweeps at N=8 and ~770 at N=16, against <= 17
+  for the suite), so its chain is kept every PHILOX_STRIDE sweeps, as KeepEvery does in the reference; ActionDensity,
   InternalEnergyDensity, InternalEnergyDensitySquared, WindingSquared (observable/action.py:25-31, energy.py:25-30,
   70-80, winding.py:30-37) at N = 8, 16 and kappa = 0.25, 0.5, 1.0.
 
@@ -19,7 +22,7 @@ import numpy as np
 import pytest
 
 import supervillain_amd as sv
-from supervillain_amd.generator import Sequentially
+from supervillain_amd.generator import KeepEvery, Sequentially
 from supervillain_amd.generator import villain as V
 from supervillain_amd.generator import worldline as WL
 from tests.statparity import blocked_bootstrap, delta_v
@@ -73,11 +76,14 @@ def worldline_chain(N, kappa, mode, steps, seed, measure_kappa=None):
                                  measure_kappa or kappa, 1)
 
 
+PHILOX_STRIDE = 20  # sweeps per kept configuration of the NeighborhoodUpdate chain (tau_int / 20 <= ~40 kept)
+
+
 def villain_chain(N, kappa, suite, steps, seed, measure_kappa=None):
     L = sv.Lattice2D(N)
     S = sv.Villain(L, kappa, 1)
     if suite == 'philox':
-        gens = [V.NeighborhoodUpdate(S, philox=0x5EED0000 + seed)]
+        gens = [KeepEvery(PHILOX_STRIDE, V.NeighborhoodUpdate(S, philox=0x5EED0000 + seed))]
     else:
         gens = [V.LinkUpdate(S), V.SiteUpdate(S), V.ExactUpdate(S), V.CohomologyUpdate(S)]
         for i, g in enumerate(gens):
@@ -119,7 +125,7 @@ def test_worldline_checkerboard_vs_reference_order(N, kappa):
     assert_agree(zscores(cb, ref, WORLDLINE_NAMES, steps // 10), f'Worldline N={N} kappa={kappa}')
 
 
-VL_STEPS = {8: 40000, 16: 20000}
+VL_STEPS = {8: 20000, 16: 20000}
 
 
 @pytest.mark.parametrize('kappa', [0.25, 0.5, 1.0])
