@@ -91,6 +91,9 @@ def parse():
                                                               'worms', 'ranks'])
     ap.add_argument('--event-timing', default='batch', choices=['launch', 'batch'],
                     help='hipEvents around each batch of 64 fused launches (default) or around every launch')
+    ap.add_argument('--plaquette', default='checkerboard', choices=['checkerboard', 'reference'],
+                    help='worldline workload: the checkerboard Plaquette chain (one fused launch per step) or the '
+                         'bit-exact reference visit order (plaquette.py:63; level-scheduled)')
     ap.add_argument('--replicas', type=int, default=1024, help='replicas workload: total replica count')
     args = ap.parse_args()
     args.strong = not args.weak
@@ -409,16 +412,40 @@ def run_worldline(args, world, rank, dist):
     r = rng_from_numpy(np.random.default_rng(rank))
     Weff = float(args.W)
 
+    reference = args.plaquette == 'reference'
+    legacy = np.random.RandomState(rank + 1)  # the reference's global-RandomState permutation (plaquette.py:63)
+    host_s = [0.0, 0.0]  # reference order: seconds in the NumPy permutation, and in the ordered-run call
+
     def step(k):
-        st = _native.stats_array(2 * k)  # one call: Sequentially(Plaquette, Coexact) x k on the device
-        ctx.check(Lib.sv_worldline_plaquette_coexact_run(h, args.kappa, Weff, 1, k, ctypes.byref(r), st),
-                  'sv_worldline_plaquette_coexact_run')
-        return sum(st[2 * i].accepted for i in range(k))  # Plaquette acceptances
+        if not reference:
+            st = _native.stats_array(2 * k)  # one call: Sequentially(Plaquette, Coexact) x k on the device
+            ctx.check(Lib.sv_worldline_plaquette_coexact_run(h, args.kappa, Weff, 1, k, ctypes.byref(r), st),
+                      'sv_worldline_plaquette_coexact_run')
+            return sum(st[2 * i].accepted for i in range(k))  # Plaquette acceptances
+        # the bit-exact reference order: the caller draws the visit order as plaquette.py:63 does (a permutation
+        # of the row-major coordinates is the permutation of the linear indices, same draws), then the
+        # level-scheduled ordered sweep and one Coexact sweep, both on the PCG64 stream
+        st = _native.stats_array(1)
+        st2 = _native.stats_array(1)
+        acc = 0
+        for _ in range(k):
+            t0 = time.perf_counter()
+            order = legacy.permutation(L * L).astype(np.int64)
+            t1 = time.perf_counter()
+            ctx.check(Lib.sv_worldline_plaquette_ordered_run(h, args.kappa, Weff, _native.ptr(order), ctypes.byref(r),
+                                                             st), 'sv_worldline_plaquette_ordered_run')
+            ctx.check(Lib.sv_worldline_coexact_run(h, args.kappa, Weff, 1, 1, ctypes.byref(r), st2),
+                      'sv_worldline_coexact_run')
+            host_s[0] += t1 - t0
+            host_s[1] += time.perf_counter() - t1
+            acc += st[0].accepted
+        return acc
 
     warm_up(step, args, dist)
     Lib.sv_ctx_set_timing(ctx.handle, 1)
     if dist:
         dist.barrier()
+    host_s[:] = [0.0, 0.0]
     t0 = time.perf_counter()
     acc = step(args.steps)
     t1 = time.perf_counter()
@@ -428,31 +455,47 @@ def run_worldline(args, world, rank, dist):
     ms = ctypes.c_double()
     launches = ctypes.c_int64()
     Lib.sv_ctx_kernel_time(ctx.handle, ctypes.byref(ms), ctypes.byref(launches))
-    step_kernel_s = ms.value / 1e3 / args.steps  # both sweeps' kernels per step
+    step_kernel_s = ms.value / 1e3 / args.steps  # both sweeps' kernels per step (checkerboard)
 
     def baseline():
         from oracle import oracle as O
         mm, vv = np.zeros((2, L, L), dtype=np.int64), np.zeros((L, L), dtype=np.int64)
         g = np.random.default_rng(0)
-        k = 3
+        k = 3 if not reference else 2
+        lg = np.random.RandomState(1)
         t = time.perf_counter()
         for _ in range(k):
-            O.worldline_plaquette_cb(L, args.kappa, Weff, mm, vv, 1, g)
+            if reference:
+                o = lg.permutation(L * L).astype(np.int64)
+                O.worldline_plaquette_seq(L, args.kappa, Weff, mm, vv, o, g)
+            else:
+                O.worldline_plaquette_cb(L, args.kappa, Weff, mm, vv, 1, g)
             O.worldline_coexact(L, args.kappa, Weff, mm, vv, 1, g)
         dt = time.perf_counter() - t
         return {'value': k * L * L / dt, 'unit': 'plaquette-steps/s', 'cores': 1, 'kind': 'port',
-                'sample': f'{k} steps (checkerboard Plaquette + Coexact sweep) of L={L} Worldline, '
-                          'oracle/sv_oracle.c single-threaded'}
+                'sample': f'{k} steps ({"reference-order" if reference else "checkerboard"} Plaquette + Coexact '
+                          f'sweep) of L={L} Worldline, oracle/sv_oracle.c single-threaded'}
 
     if rank == 0:
-        config = {'workload': f'L={L} Worldline: checkerboard PlaquetteUpdate + CoexactUpdate sweep per step, '
-                              f'W={args.W}, kappa={args.kappa}, bit-exact PCG64 replay (one worldline_step_fused '
-                              'launch per step)',
-                  'L': L, 'path': 'worldline', 'parallelism': 'single GPU'}
+        if reference:
+            config = {'workload': f'L={L} Worldline: reference-order PlaquetteUpdate (the NumPy RandomState visit '
+                                  'permutation, plaquette.py:35-104, bit-exact) + CoexactUpdate sweep per step, '
+                                  f'W={args.W}, kappa={args.kappa}, PCG64 replay; level-scheduled launches',
+                      'L': L, 'path': 'worldline-reference-order', 'parallelism': 'single GPU',
+                      'host_permutation_ms_per_step': host_s[0] / args.steps * 1e3,
+                      'ordered_run_plus_coexact_ms_per_step': host_s[1] / args.steps * 1e3}
+            # no single dominant kernel: the roofline line prices the whole device step (both sweeps, 168 B)
+            step_kernel_s = host_s[1] / args.steps
+        else:
+            config = {'workload': f'L={L} Worldline: checkerboard PlaquetteUpdate + CoexactUpdate sweep per step, '
+                                  f'W={args.W}, kappa={args.kappa}, bit-exact PCG64 replay (one worldline_step_fused '
+                                  'launch per step)',
+                      'L': L, 'path': 'worldline', 'parallelism': 'single GPU'}
         report(args, world, world * L * L, L * L, elapsed, acc / (args.steps * L * L), step_kernel_s, config, L,
                metric=f'plaquette-steps/sec (Plaquette + Coexact sweep), L={L} Worldline, W={args.W}',
-               unit='plaquette-steps/s', kernel='worldline_step_fused', alg_bytes=WORLDLINE_BYTES,
-               min_bytes=WORLDLINE_BYTES, baseline=baseline, ctx=ctx, scaling='strong')
+               unit='plaquette-steps/s',
+               kernel='plaquette_level+coexact (whole call)' if reference else 'worldline_step_fused',
+               alg_bytes=WORLDLINE_BYTES, min_bytes=WORLDLINE_BYTES, baseline=baseline, ctx=ctx, scaling='strong')
     Lib.sv_worldline_destroy(h)
 
 

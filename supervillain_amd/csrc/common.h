@@ -194,7 +194,9 @@ struct sv_worldline {
     double *f = nullptr;         // sequential plaquette: f = m - delta(v)/W kept incrementally
     int32_t *order = nullptr;    // sequential plaquette: plaquettes grouped by dependency level
     int32_t *pos = nullptr;      // sequential plaquette: visit position of each plaquette
-    int32_t *done = nullptr;     // (unused)
+    int32_t *lev = nullptr;      // sequential plaquette: dependency level of each plaquette
+    int64_t *ord64 = nullptr;    // sequential plaquette: the caller's visit order, on the device
+    int32_t *lcnt = nullptr;     // sequential plaquette: per-level counts / slots, then LFLAGS flags
     void *stripes = nullptr;     // striped per-sweep statistics (worldline.hip StatStripe[64][16])
     sv::Emitter emitter;
     int32_t *sites = nullptr;

@@ -399,6 +399,87 @@ __global__ __launch_bounds__(256) void plaquette_level(WParams P, int64_t *m, vo
     wflush(stat, acc_count, psum);
 }
 
+// ------------------------------------------------------------------------------------------------
+// The dependency levels of a reference-order sweep, on the device (the visit order of a 1024^2 lattice is 1M
+// plaquettes; the O(V) host pass with its random accesses cost ~20 ms a sweep).  Level l(p) = 1 + max l(q) over the
+// earlier-visited plaquettes q sharing a link with p (its four nearest neighbours); plaquettes of one level share no
+// link and may run in any order.  A random permutation has ~15 levels at L = 1024 (any permutation is accepted:
+// row-major order has 2N - 1).  Flags: [0] not a permutation, [1] max level, [2 + j] iteration j changed a level.
+__global__ void order_positions(const int64_t *order, int64_t V, int32_t *pos, int32_t *flags) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t x = order[i];
+        if (x < 0 || x >= V) {
+            flags[0] = 1;
+            continue;
+        }
+        if (atomicExch(&pos[x], (int32_t)i) != -1) flags[0] = 1;  // pos starts at -1: a repeated plaquette
+    }
+}
+
+// one relaxation of l(p) = 1 + max over earlier neighbours, in place (values only rise toward the unique fixed point,
+// so reading partly updated neighbours is safe); flags[2 + j] = 1 if any level changed
+__global__ void order_levels(int64_t N, const int32_t *pos, int32_t *lev, int32_t *flags, int j) {
+    const int64_t V = N * N;
+    bool changed = false;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < V; x += (int64_t)gridDim.x * blockDim.x) {
+        int64_t t, xx;
+        divmod_site(x, N, t, xx);
+        const int64_t nb[4] = {(t + 1 == N ? 0 : t + 1) * N + xx, (t == 0 ? N - 1 : t - 1) * N + xx,
+                               t * N + (xx + 1 == N ? 0 : xx + 1), t * N + (xx == 0 ? N - 1 : xx - 1)};
+        const int32_t px = pos[x];
+        int32_t l = 0;
+        for (int k = 0; k < 4; k++) {
+            const int32_t ln = lev[nb[k]];
+            if (pos[nb[k]] < px && ln > l) l = ln;
+        }
+        if (l + 1 != lev[x]) {
+            lev[x] = l + 1;
+            changed = true;
+        }
+    }
+    if (__builtin_amdgcn_ballot_w64(changed) && (threadIdx.x & 63) == 0) flags[2 + j] = 1;
+}
+
+// per-level counts (levels below LB aggregated in LDS) and the maximum level
+constexpr int LB = 256;
+constexpr int LFLAGS = 2 + 8;  // flags of order_positions / order_levels: 8 relaxations per host check
+__global__ __launch_bounds__(256) void order_level_counts(const int32_t *lev, int64_t V, int32_t *cnt, int32_t *flags) {
+    __shared__ int32_t h[LB];
+    for (int i = threadIdx.x; i < LB; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    int32_t mx = 0;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < V; x += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t l = lev[x];
+        mx = l > mx ? l : mx;
+        if (l < LB) atomicAdd(&h[l], 1);
+        else atomicAdd(&cnt[l], 1);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < LB; i += blockDim.x)
+        if (h[i]) atomicAdd(&cnt[i], h[i]);
+    atomicMax(&flags[1], mx);
+}
+
+// the plaquettes grouped by level: fill[l] starts at the level's offset and hands out slots (within a level any order)
+__global__ __launch_bounds__(256) void order_level_lists(const int32_t *lev, int64_t V, int32_t *fill, int32_t *list) {
+    __shared__ int32_t h[LB], base[LB];
+    for (int64_t x0 = blockIdx.x * (int64_t)blockDim.x; x0 < V; x0 += (int64_t)gridDim.x * blockDim.x) {
+        for (int i = threadIdx.x; i < LB; i += blockDim.x) h[i] = 0;
+        __syncthreads();
+        const int64_t x = x0 + threadIdx.x;
+        const int32_t l = x < V ? lev[x] : -1;
+        int32_t slot = -1;
+        if (l >= 0 && l < LB) slot = atomicAdd(&h[l], 1);
+        __syncthreads();
+        for (int i = threadIdx.x; i < LB; i += blockDim.x)
+            if (h[i]) base[i] = atomicAdd(&fill[i], h[i]);
+        __syncthreads();
+        if (l >= LB) list[atomicAdd(&fill[l], 1)] = (int32_t)x;
+        else if (l >= 0) list[base[l] + slot] = (int32_t)x;
+        __syncthreads();
+    }
+}
+
 }  // namespace sv
 
 using namespace sv;
@@ -703,7 +784,9 @@ int sv_worldline_destroy(sv_worldline *st) {
     if (st->d_aux) (void)hipFree(st->d_aux);
     if (st->order) (void)hipFree(st->order);
     if (st->pos) (void)hipFree(st->pos);
-    if (st->done) (void)hipFree(st->done);
+    if (st->lev) (void)hipFree(st->lev);
+    if (st->ord64) (void)hipFree(st->ord64);
+    if (st->lcnt) (void)hipFree(st->lcnt);
     st->emitter.release();
     delete st;
     return 0;
@@ -875,39 +958,40 @@ int sv_worldline_plaquette_ordered_run(sv_worldline *st, double kappa, double W_
             SV_HIP(hipMalloc(&st->f, 2 * V * sizeof(double)));
             SV_HIP(hipMalloc(&st->order, V * sizeof(int32_t)));
             SV_HIP(hipMalloc(&st->pos, V * sizeof(int32_t)));
-            SV_HIP(hipMalloc(&st->done, (V + 1) * sizeof(int32_t)));
+            SV_HIP(hipMalloc(&st->lev, V * sizeof(int32_t)));
+            SV_HIP(hipMalloc(&st->ord64, V * sizeof(int64_t)));
+            SV_HIP(hipMalloc(&st->lcnt, (V + 2 + LFLAGS) * sizeof(int32_t)));
         }
-        // Dependency levels of the visit order (host, O(V)): level(p) = 1 + max level of the
-        // earlier-visited plaquettes sharing a link with p (its four nearest neighbours).
-        std::vector<int32_t> pos(V, -1), level(V, 0);
-        for (int64_t i = 0; i < V; i++) {
-            const int64_t x = order[i];
-            if (x < 0 || x >= V || pos[x] >= 0) throw std::invalid_argument("order is not a permutation");
-            pos[x] = (int32_t)i;
+        // Dependency levels of the visit order, on the device (order_positions .. order_level_lists)
+        int32_t *flags = st->lcnt + V + 2;
+        const int lgrid = (int)std::min<int64_t>((V + 255) / 256, 4096);
+        SV_HIP(hipMemcpyAsync(st->ord64, order, V * sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
+        SV_HIP(hipMemsetAsync(st->pos, 0xFF, V * sizeof(int32_t), ctx->stream));
+        SV_HIP(hipMemsetAsync(st->lev, 0, V * sizeof(int32_t), ctx->stream));
+        SV_HIP(hipMemsetAsync(st->lcnt, 0, (V + 2 + LFLAGS) * sizeof(int32_t), ctx->stream));
+        order_positions<<<lgrid, 256, 0, ctx->stream>>>(st->ord64, V, st->pos, flags);
+        int32_t hf[LFLAGS];
+        for (int it = 0;; it += LFLAGS - 2) {
+            // relaxations in batches; a batch whose last relaxation changed nothing has converged
+            if (it > 0) SV_HIP(hipMemsetAsync(flags + 2, 0, (LFLAGS - 2) * sizeof(int32_t), ctx->stream));
+            for (int j = 0; j < LFLAGS - 2; j++) order_levels<<<lgrid, 256, 0, ctx->stream>>>(N, st->pos, st->lev, flags, j);
+            SV_HIP(hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, ctx->stream));
+            SV_HIP(hipStreamSynchronize(ctx->stream));
+            if (hf[0]) throw std::invalid_argument("order is not a permutation");
+            if (!hf[LFLAGS - 1]) break;
+            if (it > 2 * V) throw std::logic_error("order levels did not converge");
         }
+        order_level_counts<<<lgrid, 256, 0, ctx->stream>>>(st->lev, V, st->lcnt, flags);
         int32_t nlev = 0;
-        for (int64_t i = 0; i < V; i++) {
-            const int64_t x = order[i], t = x / N, xx = x - t * N;
-            const int64_t nb[4] = {((t + 1) % N) * N + xx, ((t + N - 1) % N) * N + xx, t * N + (xx + 1) % N,
-                                   t * N + (xx + N - 1) % N};
-            int32_t l = 0;
-            for (int k = 0; k < 4; k++)
-                if (pos[nb[k]] < i && level[nb[k]] > l) l = level[nb[k]];
-            level[x] = l + 1;
-            if (l + 1 > nlev) nlev = l + 1;
-        }
-        std::vector<int32_t> start(nlev + 2, 0), list(V);
-        for (int64_t x = 0; x < V; x++) start[level[x] + 1]++;
-        for (int l = 1; l <= nlev + 1; l++) start[l] += start[l - 1];
-        {
-            std::vector<int32_t> fill(start.begin(), start.end());
-            for (int64_t i = 0; i < V; i++) {  // visit order inside a level (any order is equivalent)
-                const int64_t x = order[i];
-                list[fill[level[x]]++] = (int32_t)x;
-            }
-        }
-        SV_HIP(hipMemcpyAsync(st->order, list.data(), V * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
-        SV_HIP(hipMemcpyAsync(st->pos, pos.data(), V * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+        SV_HIP(hipMemcpyAsync(&nlev, flags + 1, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+        std::vector<int32_t> start(nlev + 2, 0);
+        SV_HIP(hipMemcpyAsync(start.data() + 1, st->lcnt, (nlev + 1) * sizeof(int32_t), hipMemcpyDeviceToHost,
+                              ctx->stream));
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+        for (int l = 1; l <= nlev + 1; l++) start[l] += start[l - 1];  // start[l] = first slot of level l
+        SV_HIP(hipMemcpyAsync(st->lcnt, start.data(), (nlev + 1) * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+        order_level_lists<<<lgrid, 256, 0, ctx->stream>>>(st->lev, V, st->lcnt, st->order);
         std::vector<BlockSpec> specs = {{BOUNDED, (uint32_t)V}, {BOUNDED, (uint32_t)V}, {UNIFORM, (uint32_t)V}};
         SkipMap skips;
         std::vector<Block> blocks;
