@@ -191,6 +191,8 @@ def report(args, world, sites_per_step, sites_per_launch, elapsed, acc, avg_laun
            unit='lattice-site updates/s', kernel='villain_sweep_hot', alg_bytes=SURVEY_BYTES_PER_SITE,
            min_bytes=FUSED_MIN_BYTES_PER_SITE, baseline=None, ctx=None, scaling=None):
     achieved = alg_bytes * sites_per_launch / avg_launch_s / 1e9
+    if 'L=4096 Villain' in metric and args.L != 4096:
+        metric = metric.replace('L=4096', f'L={args.L}')  # a non-headline size names itself
     ceiling = copy_ceiling(ctx) if ctx is not None and not getattr(args, 'no_copy_ceiling', False) else None
     out = {
         'metric': metric,

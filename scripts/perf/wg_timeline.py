@@ -16,9 +16,9 @@ Lib.sv_debug_wgtime.argtypes = [ctypes.c_void_p, ctypes.c_int32]
 
 
 def read(nwg):
-    buf = np.zeros(nwg * 5, dtype=np.uint64)
+    buf = np.zeros(nwg * 6, dtype=np.uint64)
     assert Lib.sv_debug_wgtime(buf.ctypes.data, nwg) == 0
-    return buf.reshape(nwg, 5)
+    return buf.reshape(nwg, 6)
 
 
 def summarize(tag, t, nsx=None):
@@ -39,6 +39,26 @@ def summarize(tag, t, nsx=None):
           f'prologue p50 {np.median(l0 - e):.1f} p90 {np.percentile(l0 - e, 90):.1f} us; loop p50 {np.median(l1 - l0):.1f} '
           f'p90 {np.percentile(l1 - l0, 90):.1f} max {(l1 - l0).max():.1f} us; epilogue p50 {np.median(x - l1):.1f} us; '
           f'WG lifetime p50 {np.median(x - e):.1f} max {(x - e).max():.1f} us', flush=True)
+    loop = l1 - l0
+    life = x - e
+    tb = (t[:, 5].astype(np.int64) - int(t0)) * 0.01
+    print(f'[{tag}] prologue split p50: entry -> row bases {np.median(tb - e):.2f} us, row bases -> loop '
+          f'{np.median(l0 - tb):.2f} us', flush=True)
+    print(f'[{tag}] loop p50 by XCD: ' + ' '.join(f'{np.median(loop[xcc == k]):.1f}' for k in range(8)) +
+          '; exit max by XCD: ' + ' '.join(f'{x[xcc == k].max():.1f}' for k in range(8)), flush=True)
+    inv = np.unique(cuid, return_inverse=True)[1]
+    wgs_on_cu = per_cu[inv]
+    print(f'[{tag}] by WGs on the CU: ' + '; '.join(
+        f'{c}: n={int((wgs_on_cu == c).sum())} loop p50 {np.median(loop[wgs_on_cu == c]):.1f} lifetime p50 '
+        f'{np.median(life[wgs_on_cu == c]):.1f} last exit {x[wgs_on_cu == c].max():.1f}'
+        for c in np.unique(wgs_on_cu)), flush=True)
+    for c in np.unique(wgs_on_cu):
+        cus = np.unique(inv[wgs_on_cu == c])
+        ranks = np.array([np.sort(life[inv == u]) for u in cus])
+        ends = np.array([x[inv == u].max() for u in cus])
+        print(f'[{tag}] CUs with {c} WGs: lifetime by rank within the CU ' +
+              ' '.join(f'{v:.1f}' for v in ranks.mean(axis=0)) +
+              f'; CU finish p10 {np.percentile(ends, 10):.1f} p50 {np.median(ends):.1f} max {ends.max():.1f}', flush=True)
     # occupancy over time: WGs resident (entry..exit) in 2-us bins
     bins = np.arange(0, x.max() + 2, 2.0)
     occ = [int(((e <= b) & (x > b)).sum()) for b in bins]

@@ -45,8 +45,10 @@
 namespace sv {
 
 #if SV_WGTIME
-// per launch slot: [wg][0..3] = entry, loop start, loop end, exit (s_memrealtime, 100 MHz), [4] = HW_ID
-__device__ uint64_t g_wgtime[65536 * 5];
+// per launch slot: [wg][0..3] = entry, loop start, loop end, exit (s_memrealtime, 100 MHz), [4] = HW_ID,
+// [5] = row bases ready (prologue split)
+constexpr int WGT = 6;
+__device__ uint64_t g_wgtime[65536 * WGT];
 __device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 #endif
 
@@ -349,6 +351,9 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
         __builtin_amdgcn_s_waitcnt(0);
         if (base_lane) s_base[wave][lane] = bases;
     }
+#if SV_WGTIME
+    const uint64_t wg_tb = rt_now();
+#endif
 
     // paired-draw lane constants per colour (interior strips; valid for every row of this wave)
     uint32_t pk0 = 0, pk1 = 0;
@@ -644,11 +649,12 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
 #if SV_WGTIME
     __builtin_amdgcn_s_waitcnt(0);
     if (threadIdx.x == 0 && blockIdx.x < 65536) {
-        uint64_t *o = g_wgtime + 5 * (size_t)blockIdx.x;
+        uint64_t *o = g_wgtime + WGT * (size_t)blockIdx.x;
         o[0] = wg_t0;
         o[1] = wg_t1;
         o[2] = wg_t2;
         o[3] = rt_now();
+        o[5] = wg_tb;
         // HW_ID (hwreg 4: wave, SIMD, CU, SH, SE) and XCC_ID (hwreg 20)
         o[4] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
                ((uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32);
@@ -727,7 +733,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_PH_O
 
 #if SV_WGTIME
 extern "C" int sv_debug_wgtime(uint64_t *out, int32_t n) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(sv::g_wgtime), (size_t)n * 5 * sizeof(uint64_t)) == hipSuccess ? 0 : -2;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(sv::g_wgtime), (size_t)n * sv::WGT * sizeof(uint64_t)) == hipSuccess ? 0 : -2;
 }
 #endif
 
