@@ -10,3 +10,5 @@ for r in 1 2; do
 done
 step def timeout -k 10 300 python -u bench.py --no-cpu-baseline > $O/default.json 2> $O/default.err
 python -c "import json; d=json.loads(open('$O/default.json').readline()); print('default', round(d['value']/1e9,2), round(d['ms_per_step']*1e3,2), round(d['roofline']['avg_launch_us'],2), d['config']['lemire_rejections_in_timed_steps'])"
+step ovh env SV_DEBUG_TIMING=1 timeout -k 10 200 python -u scripts/perf/call_overhead.py 4096 20 8 > $O/ovh.log 2>&1
+grep "^call" $O/ovh.log

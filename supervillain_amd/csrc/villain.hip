@@ -788,10 +788,13 @@ int absorb_reports(const AbortInfo &a, int first, SkipMap &skips) {
     for (const Report &r : a.reports)
         if (std::make_pair(r.sweep, r.block) < best) best = {r.sweep, r.block};
     auto &lst = skips[{first + (int)best.first, (int)best.second}];
+    const size_t before = lst.size();
     for (const Report &r : a.reports)
         if (r.sweep == best.first && r.block == best.second) lst.push_back(r.pos);
     std::sort(lst.begin(), lst.end());
     lst.erase(std::unique(lst.begin(), lst.end()), lst.end());
+    // a replay that meets only positions it already skips would repeat forever: a kernel drew a skipped word
+    if (lst.size() == before) throw std::logic_error("rejection replay made no progress (a skipped word was drawn)");
     return (int)best.first;
 }
 
