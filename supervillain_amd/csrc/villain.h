@@ -74,7 +74,7 @@ struct FArgs {
     // TILE: the window of the launch's region whose sites are counted in the statistics, [r0, r1) x [c0, c1) in
     // region coordinates (domain.hip's deep halos run sweeps over a tile extended by a ring it does not own)
     int32_t own_r0 = -(1 << 30), own_r1 = 1 << 30, own_c0 = -(1 << 30), own_c1 = 1 << 30;
-    // villain_sweep_hot: waves (rows per step) of a workgroup, 4 or 8 (adv must then advance 8 rows; TH % 8 == 0)
+    // villain_sweep_hot: waves (rows per step) of a workgroup, 4 or 8 (adv must then advance 8 rows)
     int32_t hot_nw = 4;
 };
 

@@ -930,10 +930,16 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     const int nb = (int)specs.size();
     const int nsx = (N + FW_MAX - 1) / FW_MAX;
     const int NWv = fused_nw();
-    // small lattices (strips cut to the 4-row minimum to fill the chip): 8-wave workgroups over 8-row strips instead,
-    // fewer halo rows per row (L=256: 15.75 -> 14.9-15.1 us per sweep, r369)
+    // small lattices (strips cut to the 4-row minimum to fill the chip): 8-wave workgroups instead, over 5-row strips:
+    // the kernel's row pipeline (colour 0 on rows t+2+w, colour 1 on t+1+w) then covers a strip in ONE row step, its
+    // prologue rows included (8-row strips took two; L=256: 15.75 us per sweep at 4 rows / 4 waves, r369; 15.2 at
+    // 8 rows / 8 waves; 13.5 at 5 rows, r3 -- 4 / 3 / 13 rows: 14.4 / 15.8 / 16.4)
     const bool small8 = !getenv("SV_FUSED_TH") && fused_th(N, nsx) <= 4 && NWv == 4;
-    const int TH = small8 ? 8 : fused_th(N, nsx);
+    static const int small_th = [] {  // SV_SMALL_TH: the 8-wave strip height on small lattices (experiments)
+        const char *e = getenv("SV_SMALL_TH");
+        return e && atoi(e) >= 1 ? atoi(e) : 5;
+    }();
+    const int TH = small8 ? small_th : fused_th(N, nsx);
     const int nsy = (N + TH - 1) / TH;
     const int grid = nsx * nsy;
     static const int BATCH = [] {  // sweeps per host round trip (SV_BATCH overrides; 64 measured best)
