@@ -552,13 +552,19 @@ int domain_th(const sv_domain *d, int nsx, int *nw8 = nullptr) {
     auto wgs = [&](int th) { return (int64_t)nsx * ((d->Ht + th - 1) / th); };
     const int64_t rounds = (wgs(52) + slots - 1) / slots;
     const char *nwe = getenv("SV_HOT_NW");
-    if (nw8 && !(nwe && atoi(nwe) == 4) && hot_enabled() && rounds == 1 && wgs(40) <= slots / 2) {
+    // (heights 8k - 3 / 4k + 1: a strip of TH rows takes ceil((TH + 3) / NW) row steps, fused_th; 37 rows of 8 waves
+    // take the 5 steps 35 would, 40 took 6)
+    static const int th8 = [] {  // SV_DOMAIN_TH8: the 8-wave strip height (A/B measurements)
+        const char *e = getenv("SV_DOMAIN_TH8");
+        return e && atoi(e) >= 8 ? atoi(e) : 37;
+    }();
+    if (nw8 && !(nwe && atoi(nwe) == 4) && hot_enabled() && rounds == 1 && wgs(th8) <= slots / 2) {
         *nw8 = 1;
-        return 40;
+        return th8;
     }
     if (rounds > 2) return fused_th(d->Ht, nsx);
-    int th = 52;
-    while (th > 20 && wgs(th - 4) <= rounds * slots) th -= 4;
+    int th = 53;
+    while (th > 21 && wgs(th - 4) <= rounds * slots) th -= 4;
     return th;
 }
 

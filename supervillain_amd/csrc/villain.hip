@@ -809,19 +809,22 @@ int fused_nw() {
 // recomputed) until the grid has `fill` = 512 workgroups, so that every CU has work (SURVEY.md 8(d)
 // config 2; r203 sweep, us per sweep kernel: L=256 at 52 / 16 / 8 / 4 rows: 88.1 / 35.5 / 24.2 / 19.8;
 // L=1024 at 52 / 32 / 24 / 16 / 12 / 8 rows: 90.8 / 67.3 / 54.6 / 47.9 / 55.7 / 59.5).
+// Heights are 4k + 1: villain_sweep_hot covers a strip of TH rows in ceil((TH + 3) / NW) row steps of NW = 4 rows (the
+// colour-1 pass runs one row and the colour-0 pass two rows ahead of the stores, the first step starting 3 rows
+// above the strip), so 53 rows take the 14 steps 52 did (r3: L=1024 16 -> 17 rows, L=4096 52 -> 53).
 int fused_th(int32_t N, int nsx) {
     const char *e = getenv("SV_FUSED_TH");
     if (e) {
         const int v = atoi(e);
-        if (v >= 4 && v % 4 == 0) return v;
+        if (v >= 4) return v;
     }
     static const int fill = [] {
         const char *f = getenv("SV_FUSED_FILL");
         const int v = f ? atoi(f) : 512;
         return v > 0 ? v : 512;
     }();
-    int th = 52;
-    while (th > 4 && (int64_t)nsx * ((N + th - 1) / th) < fill) th -= 4;
+    int th = 53;
+    while (th > 5 && (int64_t)nsx * ((N + th - 1) / th) < fill) th -= 4;
     return th;
 }
 
@@ -897,7 +900,7 @@ std::vector<int32_t> strip_schedule(int32_t Nt, int nsx, const std::string &spec
         const std::string tok = spec.substr(p, q - p);
         const size_t x = tok.find('x');
         const int h = atoi(tok.substr(0, x).c_str()), m = x == std::string::npos ? 1 : atoi(tok.substr(x + 1).c_str());
-        if (h < 4 || h % 4 || m < 1) return {};
+        if (h < 4 || m < 1) return {};
         for (int i = 0; i < m; i++) hs.push_back(h);
         p = q + 1;
     }
@@ -934,7 +937,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     // the kernel's row pipeline (colour 0 on rows t+2+w, colour 1 on t+1+w) then covers a strip in ONE row step, its
     // prologue rows included (8-row strips took two; L=256: 15.75 us per sweep at 4 rows / 4 waves, r369; 15.2 at
     // 8 rows / 8 waves; 13.5 at 5 rows, r3 -- 4 / 3 / 13 rows: 14.4 / 15.8 / 16.4)
-    const bool small8 = !getenv("SV_FUSED_TH") && fused_th(N, nsx) <= 4 && NWv == 4;
+    const bool small8 = !getenv("SV_FUSED_TH") && fused_th(N, nsx) <= 5 && NWv == 4;
     static const int small_th = [] {  // SV_SMALL_TH: the 8-wave strip height on small lattices (experiments)
         const char *e = getenv("SV_SMALL_TH");
         return e && atoi(e) >= 1 ? atoi(e) : 5;
@@ -969,9 +972,10 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         const char *e = getenv("SV_STRIPS");
         std::string spec = e ? (std::string(e) == "uniform" ? "" : e) : "";
         if (!e && N >= 4096 && N % 32 == 0) {
-            const int band = N / 8, n56 = (int)(0.55 * band / 56), n40 = (band - 56 * n56) / 40;
-            const int rest = band - 56 * n56 - 40 * n40;
-            spec = "56x" + std::to_string(n56) + ",40x" + std::to_string(n40) + (rest ? "," + std::to_string(rest) : "");
+            // (heights 4k + 1, fused_th: L=4096 "57x5,41x5,22")
+            const int band = N / 8, n57 = (int)(0.55 * band / 57 + 0.5), n41 = (band - 57 * n57) / 41;
+            const int rest = band - 57 * n57 - 41 * n41;
+            spec = "57x" + std::to_string(n57) + ",41x" + std::to_string(n41) + (rest ? "," + std::to_string(rest) : "");
         }
         if (spec != st->strips_key || !st->d_strips) {
             const std::vector<int32_t> tab = hot_nw == 4 ? strip_schedule(N, nsx, spec) : std::vector<int32_t>{};
