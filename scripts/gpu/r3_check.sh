@@ -12,3 +12,5 @@ step def timeout -k 10 300 python -u bench.py --no-cpu-baseline > $O/default.jso
 python -c "import json; d=json.loads(open('$O/default.json').readline()); print('default', round(d['value']/1e9,2), round(d['ms_per_step']*1e3,2), round(d['roofline']['avg_launch_us'],2), d['config']['lemire_rejections_in_timed_steps'])"
 step ovh env SV_DEBUG_TIMING=1 timeout -k 10 200 python -u scripts/perf/call_overhead.py 4096 20 8 > $O/ovh.log 2>&1
 grep "^call" $O/ovh.log
+step tr timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/tr -o run --output-format csv -- python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-copy-ceiling > $O/tr.json 2> $O/tr.err
+python -c "import json; d=json.loads(open('$O/tr.json').readline()); print('traced', round(d['value']/1e9,2), round(d['ms_per_step']*1e3,2), round(d['roofline']['avg_launch_us'],2), d['config']['lemire_rejections_in_timed_steps'])"

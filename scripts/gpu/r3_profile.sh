@@ -16,11 +16,20 @@ pmc() {  # NAME KERNEL UNITS ALG MIN -- bench args
   python scripts/summarize_pmc.py $O/$name $TAG $name $kern $units $alg $mn
 }
 B="--steps 4 --warmup 1 --warmup-s 0 --no-cpu-baseline --no-copy-ceiling"
-pmc worldline worldline_step_fused 1048576 168 168 -- --workload worldline $B
-pmc replicas villain_sweep_hot_fr 16777216 88 48 -- --workload replicas $B
+#pmc worldline worldline_step_fused 1048576 168 168 -- --workload worldline $B
+#pmc replicas villain_sweep_hot_fr 16777216 88 48 -- --workload replicas $B
 pmc l256 villain_sweep_hot 65536 88 48 -- --L 256 $B
 step tr_wlref timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_wlref -o run --output-format csv -- python bench.py --workload worldline --plaquette reference --steps 10 --warmup 2 --no-cpu-baseline > $O/trace_wlref.log 2>&1
 cp $O/trace_wlref/run_kernel_stats.csv profiles/${TAG}_kernel_stats_worldline_reference.csv
 step tr_l256 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_l256 -o run --output-format csv -- python bench.py --L 256 --steps 2000 --warmup 100 --no-cpu-baseline --no-copy-ceiling > $O/trace_l256.log 2>&1
 cp $O/trace_l256/run_kernel_stats.csv profiles/${TAG}_kernel_stats_l256.csv
 ls profiles/ | grep $TAG
+# the config-4 per-GPU tile (2048 x 1024, one periodic 1x1 domain: the kernel the 8-GPU run uses per rank)
+cat > /tmp/tile_run.py <<'PY'
+import sys, numpy as np
+sys.path.insert(0, '.')
+from supervillain_amd.domain import VillainDomain
+d = VillainDomain(2048, 1024, (1, 1), kappa=0.5, W=1); d.cold(); g = np.random.default_rng(0); d.run(64, g); d.run(256, g); d.close()
+PY
+step tr_tile timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_tile -o run --output-format csv -- python /tmp/tile_run.py > $O/trace_tile.log 2>&1
+cp $O/trace_tile/run_kernel_stats.csv profiles/${TAG}_kernel_stats_tile2048x1024.csv

@@ -445,9 +445,11 @@ int sv_ctx_create(int device, sv_ctx **out) {
         SV_HIP(hipMalloc(&ctx->d_reports, sv::MAX_REPORTS * sizeof(sv::Report)));
         SV_HIP(hipMemset(ctx->d_abort, 0, sizeof(int32_t)));
         SV_HIP(hipMemset(ctx->d_nreport, 0, sizeof(uint32_t)));
-        SV_HIP(hipHostMalloc((void **)&ctx->h_flag, sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent));
+        SV_HIP(hipHostMalloc((void **)&ctx->h_flag, 2 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent));
         SV_HIP(hipHostGetDevicePointer((void **)&ctx->d_flag, ctx->h_flag, 0));
-        *ctx->h_flag = 0;
+        ctx->h_prog = ctx->h_flag + 1;
+        ctx->d_prog = ctx->d_flag + 1;
+        ctx->h_flag[0] = ctx->h_flag[1] = 0;
         for (auto &e : ctx->ev_chunk) SV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         ctx->ensure_blocks(64);
         ctx->ensure_skips(64);

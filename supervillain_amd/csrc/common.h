@@ -105,6 +105,7 @@ struct sv_ctx {
     // host-mapped abort flag (fine-grained pinned memory: h_flag for the host, d_flag for kernels), written by a
     // kernel's rejection report so that the host can stop enqueueing a batch that has failed (run_fused)
     int32_t *h_flag = nullptr, *d_flag = nullptr;
+    int32_t *h_prog = nullptr, *d_prog = nullptr;  // the next word: batch launches started (FArgs::progress)
     hipEvent_t ev_chunk[2] = {nullptr, nullptr};
     // pinned batch tail (abort flag, report count, statistics) of the single-lattice Villain run: one sync
     char *h_tail = nullptr;

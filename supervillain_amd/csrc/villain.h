@@ -76,7 +76,16 @@ struct FArgs {
     int32_t own_r0 = -(1 << 30), own_r1 = 1 << 30, own_c0 = -(1 << 30), own_c1 = 1 << 30;
     // villain_sweep_hot: waves (rows per step) of a workgroup, 4 or 8 (adv must then advance 8 rows)
     int32_t hot_nw = 4;
+    // single-lattice batches: workgroup 0 of the launch of batch sweep k stores k + 1 here (host-mapped) as it starts,
+    // i.e. once every earlier launch of the stream has finished; the host bounds its queue by it (run_fused)
+    int32_t *progress = nullptr;
 };
+
+// (FArgs::progress) the launch has started: every earlier launch of its stream has finished
+__device__ __forceinline__ void note_progress(const FArgs &A) {
+    if (A.progress && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(A.progress, (int32_t)A.sweep + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 }  // namespace sv
 

@@ -20,6 +20,7 @@
 //   dS_link:                ((kappa/2) * cr) * ((2*r) + cr)            (neighborhood.py:111)
 //   face_sum:               (((0 + f0[x]) + f0[x-e0]) + f1[x]) + f1[x-e1]  (reference.py:48-64)
 //   r update:               (r + d(cphi)) - (2pi)*cn                  (neighborhood.py:129)
+#include <thread>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -141,6 +142,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     __shared__ double s_obs[4];  // OBS: workgroup sums of the inline observables
     __shared__ Block s_blk[11];  // this sweep's descriptors (LDS: no vector-memory waits in the loop)
 
+    note_progress(A);
     if (*(volatile const int32_t *)A.S.abort) return;
 
     const FGeom &Gm = A.G;
@@ -1021,6 +1023,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         const int CH = CH_env > 0 ? CH_env : (CH_env == 0 || V < (int64_t(1) << 20) ? count : 4);
         int launched = count;
         *ctx->h_flag = 0;
+        __atomic_store_n(ctx->h_prog, 0, __ATOMIC_RELEASE);  // (the previous batch's launches have all finished)
         int next_chunk = CH;
         for (int k = 0; k < count;) {
             const bool hot_k = use_hot && !hot_off && NWv == 4 && hot_ok(P, &blocks[(size_t)k * nb]);
@@ -1051,6 +1054,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             A.stat = ctx->d_stats + k;
             A.S = scratch(ctx);
             A.S.hflag = ctx->d_flag;
+            A.progress = ctx->d_prog;
             A.sweep = (uint32_t)k;
             farg_single(A, nsx, nsy);
             if (hot_k) {
@@ -1079,9 +1083,16 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             if (k >= next_chunk && k < count) {
                 const int j = next_chunk / CH - 1;  // chunk j is enqueued
                 next_chunk += CH;
-                SV_HIP(hipEventRecord(ctx->ev_chunk[j & 1], ctx->stream));
                 if (j >= 1) {
-                    SV_HIP(hipEventSynchronize(ctx->ev_chunk[(j - 1) & 1]));
+                    // chunk j - 1 has finished once the first launch of chunk j has started (FArgs::progress).  A
+                    // stream event between the chunks did the same at ~6.5 us of idle GPU per event (its
+                    // end-of-pipe release), 0.7% of a sweep; the host-mapped word costs the kernels one store.
+                    const int32_t target = j * CH + 1;
+                    for (int spin = 0; __atomic_load_n(ctx->h_prog, __ATOMIC_ACQUIRE) < target; spin++) {
+                        if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE)) break;
+                        if ((spin & 255) == 255 && hipStreamQuery(ctx->stream) == hipSuccess) break;  // (drained)
+                        std::this_thread::yield();
+                    }
                     if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE)) {
                         launched = k;  // the rest of the batch is not enqueued
                         break;
