@@ -126,6 +126,8 @@ void launch_fused_batch(const FArgs &A, int grid, bool obs, hipStream_t stream);
 // villain_hot.hip: whether the fast-draw kernel covers the sweep whose 11 descriptors start at `blocks`,
 // and its launch (periodic single lattice or a domain tile, from the geometry)
 bool hot_ok(const VParams &P, const Block *blocks);
+// villain_sweep_hot's default descending strip table for H rows and nsx column strips ({ix, t0, t1} per strip)
+std::vector<int32_t> band_strips(int32_t H, int nsx);
 void launch_hot(const FArgs &A, int grid, hipStream_t stream);
 // full-row replica batches (config 5) on the fast-draw kernel: whether N qualifies, and the launch (the sweep must
 // pass hot_ok for every replica: no skips, no buffered half-word, choice values in range)

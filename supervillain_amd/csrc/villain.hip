@@ -924,6 +924,33 @@ std::vector<int32_t> strip_schedule(int32_t Nt, int nsx, const std::string &spec
     return tab;
 }
 
+// The default descending schedule for H rows (any H >= 64): 8 bands of H / 8 rows (one per XCD), each ~55% in
+// 57-row strips, then 41-row strips, then the rest (heights 4k + 1, fused_th); a remainder under 5 rows joins the
+// band's last strip.  L=4096: "57x5,41x5,22" per band.
+std::vector<int32_t> band_strips(int32_t H, int nsx) {
+    std::vector<int32_t> tab;
+    for (int b = 0; b < 8; b++) {
+        const int32_t r0 = (int32_t)((int64_t)b * H / 8), r1 = (int32_t)((int64_t)(b + 1) * H / 8), h = r1 - r0;
+        std::vector<int32_t> hs;
+        const int n57 = (int)(0.55 * h / 57 + 0.5), n41 = (h - 57 * n57) / 41;
+        for (int i = 0; i < n57; i++) hs.push_back(57);
+        for (int i = 0; i < n41; i++) hs.push_back(41);
+        const int rest = h - 57 * n57 - 41 * n41;
+        if (rest >= 5 || hs.empty()) hs.push_back(rest);
+        else hs.back() += rest;
+        int32_t t = r0;
+        for (int hh : hs) {
+            for (int ix = 0; ix < nsx; ix++) {
+                tab.push_back(ix);
+                tab.push_back(t);
+                tab.push_back(t + hh);
+            }
+            t += hh;
+        }
+    }
+    return tab;
+}
+
 // returns false if the fused path cannot represent the state (|n| too large): caller falls back
 bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u128 inc, sv_stats *stats,
                int &done_sweeps) {
@@ -972,15 +999,11 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     // of 300 sweeps: 230.6 -> 225.5 us per sweep; "52x7,40x3,28" 225.0)
     {
         const char *e = getenv("SV_STRIPS");
-        std::string spec = e ? (std::string(e) == "uniform" ? "" : e) : "";
-        if (!e && N >= 4096 && N % 32 == 0) {
-            // (heights 4k + 1, fused_th: L=4096 "57x5,41x5,22")
-            const int band = N / 8, n57 = (int)(0.55 * band / 57 + 0.5), n41 = (band - 57 * n57) / 41;
-            const int rest = band - 57 * n57 - 41 * n41;
-            spec = "57x" + std::to_string(n57) + ",41x" + std::to_string(n41) + (rest ? "," + std::to_string(rest) : "");
-        }
+        const bool dflt = !e && N >= 4096;
+        const std::string spec = dflt ? "band_strips" : (e ? (std::string(e) == "uniform" ? "" : e) : "");
         if (spec != st->strips_key || !st->d_strips) {
-            const std::vector<int32_t> tab = hot_nw == 4 ? strip_schedule(N, nsx, spec) : std::vector<int32_t>{};
+            const std::vector<int32_t> tab = hot_nw != 4 ? std::vector<int32_t>{}
+                                             : (dflt ? band_strips(N, nsx) : strip_schedule(N, nsx, spec));
             if (st->d_strips) SV_HIP(hipFree(st->d_strips));
             st->d_strips = nullptr;
             st->n_strips = (int32_t)(tab.size() / 3);

@@ -287,6 +287,22 @@ def test_natural_rejections_bench_size(batch, monkeypatch):
     assert sum(s.accepted for s in st) == G.accepted
 
 
+@pytest.mark.parametrize('tiles', [(1, 2), (2, 1)])
+def test_two_rank_layouts_at_scale(tiles):
+    """The N = 2 layouts of L=4096 (tiles of 4096 x 2048 / 2048 x 4096, 37-row strips over ~1.8 rounds of the chip's
+    workgroup slots) in tile emulation: the chain equals the single lattice's (which runs its descending strip
+    table), through a NumPy rejection (seed 2024, sweep 3)."""
+    N = 4096
+    phi0, n0 = np.zeros((N, N)), np.zeros((2, N, N), dtype=np.int64)
+    gen = np.random.default_rng(2024)
+    phi, n, st = run_domain(N, N, tiles, 0.5, 1, phi0, n0, 12, gen)
+    p, m, G = single_lattice(N, 0.5, 1, phi0, n0, 12, np.random.default_rng(2024))
+    assert sum(s.rejections for s in st) >= 1
+    assert (phi == p).all() and (n == m).all()
+    assert gen.bit_generator.state == G.rng.bit_generator.state
+    assert sum(s.accepted for s in st) == G.accepted
+
+
 @pytest.mark.parametrize('predict', ['0', '1'])
 @pytest.mark.parametrize('N,sweeps', [(64, 5), (1024, 3), (256, 40)])
 def test_rccl_loopback(N, sweeps, predict, oracle_lib, monkeypatch):
