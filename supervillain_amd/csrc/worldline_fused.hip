@@ -454,6 +454,8 @@ template __global__ void worldline_step_fused<false, 4>(WFArgs);
 template __global__ void worldline_step_fused<true, 4>(WFArgs);
 template __global__ void worldline_step_fused<false, 8>(WFArgs);
 template __global__ void worldline_step_fused<true, 8>(WFArgs);
+template __global__ void worldline_step_fused<false, 16>(WFArgs);
+template __global__ void worldline_step_fused<true, 16>(WFArgs);
 
 }  // namespace sv
 
@@ -466,9 +468,14 @@ static int wf_th(int32_t N, int nsx, int nw);
 // need for more rows each, at one workgroup per CU (r386 at L=1024: 46.0 -> 43.4 us per step, 8 x 40-row strips; with
 // two 8-wave workgroups per CU at <= 128 VGPRs 44.1 us over 24-row strips, 51 us over 16 or 32); used when one round
 // of them covers at least 3/4 of the CUs, else 4 waves
+// 16-wave workgroups (r3): 41-row strips take ceil((41 + 7) / 16) = 3 row steps at 4 waves per SIMD, one workgroup
+// per CU, where 8 waves took 6 steps over 40 rows at 2 (L=1024: 43.8 -> 40.1 us per step; 16 waves over 25 / 33 / 57
+// rows: 57.0 / 68.0 / 47.8 us, two rounds or fewer CUs); used when one round of them covers at least 3/4 of the CUs
 static int wf_nw(int32_t Ht, int nsx) {
     const char *e = getenv("SV_WF_NW");
-    if (e) return atoi(e) == 8 ? 8 : 4;
+    if (e) return atoi(e) == 16 ? 16 : (atoi(e) == 8 ? 8 : 4);
+    const int64_t g16 = (int64_t)nsx * ((Ht + 40) / 41);
+    if (g16 >= 192 && g16 <= 256) return 16;
     const int th = wf_th(Ht, nsx, 8);
     return (int64_t)nsx * ((Ht + th - 1) / th) >= 192 ? 8 : 4;
 }
@@ -481,8 +488,9 @@ static int wf_th(int32_t N, int nsx, int nw) {
     const char *e = getenv("SV_WF_TH");
     if (e) {
         const int v = atoi(e);
-        if (v >= 4 && v % 4 == 0) return v;
+        if (v >= 4) return v;
     }
+    if (nw == 16) return 41;  // (16 k - 7 rows fill the last row step: the passes reach 7 rows past the strip)
     if (nw == 8) {
         const int slots = 256 * (SV_WF_OCC8 >= 4 ? 2 : 1);
         int th = 8;
@@ -533,7 +541,7 @@ void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
     A.v_out = v_out;
     A.blocks = blocks;
     A.T = T;
-    for (int i = 0; i < 3; i++) A.adv[i] = adv[(nw == 8 ? 3 : 0) + i];
+    for (int i = 0; i < 3; i++) A.adv[i] = nw == 16 ? compose(adv[3 + i], adv[3 + i]) : adv[(nw == 8 ? 3 : 0) + i];
     A.pstat = (StatStripe *)pstat;
     A.cstat = (StatStripe *)cstat;
     A.S = S;
@@ -551,7 +559,10 @@ void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
     A.kt = (uint32_t)(2 * it);
     A.thrt = (uint32_t)((0u - A.kt) % A.kt);
     const bool tile = !(G.T0 == 0 && G.X0 == 0 && G.Ht == G.Nt && G.Wt == G.Nx && G.pitch == G.Nx && G.org == 0);
-    if (nw == 8) {
+    if (nw == 16) {
+        if (tile) worldline_step_fused<true, 16><<<A.nsx * A.nsy, 16 * 64, 0, stream>>>(A);
+        else worldline_step_fused<false, 16><<<A.nsx * A.nsy, 16 * 64, 0, stream>>>(A);
+    } else if (nw == 8) {
         if (tile) worldline_step_fused<true, 8><<<A.nsx * A.nsy, 8 * 64, 0, stream>>>(A);
         else worldline_step_fused<false, 8><<<A.nsx * A.nsy, 8 * 64, 0, stream>>>(A);
     } else {
