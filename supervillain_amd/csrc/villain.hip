@@ -1110,10 +1110,15 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                     // chunk j - 1 has finished once the first launch of chunk j has started (FArgs::progress).  A
                     // stream event between the chunks did the same at ~6.5 us of idle GPU per event (its
                     // end-of-pipe release), 0.7% of a sweep; the host-mapped word costs the kernels one store.
+                    // (no stream query while the chunk runs: a query between submissions left a ~6.5 us gap before
+                    // the next chunk's first launch; only after ~20 ms, as a guard, is the stream asked)
                     const int32_t target = j * CH + 1;
+                    const auto tw = std::chrono::steady_clock::now();
                     for (int spin = 0; __atomic_load_n(ctx->h_prog, __ATOMIC_ACQUIRE) < target; spin++) {
                         if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE)) break;
-                        if ((spin & 255) == 255 && hipStreamQuery(ctx->stream) == hipSuccess) break;  // (drained)
+                        if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - tw > std::chrono::milliseconds(20) &&
+                            hipStreamQuery(ctx->stream) == hipSuccess)
+                            break;  // (drained: a launch that never stored its progress)
                         std::this_thread::yield();
                     }
                     if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE)) {
