@@ -599,7 +599,7 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
     const int nb = (int)specs.size();
     if (stat_of.empty()) stat_of.assign(nb, 0);
     const int64_t V = (int64_t)st->N * st->N;
-    const int BATCH = 64;
+    const int BATCH = 64;  // (the striped statistics hold 64 sweeps)
     SkipMap skips;
     std::vector<Block> blocks;
     std::vector<uint32_t> skipvec;

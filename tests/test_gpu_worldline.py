@@ -343,3 +343,66 @@ def test_plaquette_coexact_forced_rejection(N, oracle_lib):
         assert rej >= 1
         assert (m == mm).all() and (v == vv).all()
         assert gen.bit_generator.state == g.bit_generator.state
+
+
+def _ordered_run(N, kappa, m0, order, seed):
+    """sv_worldline_plaquette_ordered_run through the C-ABI on (m0, v = 0); returns (rc, error, m, v, rng state)."""
+    import ctypes
+    from supervillain_amd import _native
+    from supervillain_amd._abi import rng_from_numpy, rng_to_numpy
+    Lib = _native.lib()
+    ctx = _native.context(_native.default_device())
+    h = ctypes.c_void_p()
+    ctx.check(Lib.sv_worldline_create(ctx.handle, N, 0, ctypes.byref(h)), 'create')
+    try:
+        m = np.ascontiguousarray(m0, dtype=np.int64).copy()
+        v = np.zeros((N, N), dtype=np.int64)
+        ctx.check(Lib.sv_worldline_upload(h, _native.ptr(m), _native.ptr(v)), 'upload')
+        g = np.random.default_rng(seed)
+        r = rng_from_numpy(g)
+        st = _native.stats_array(1)
+        o = np.ascontiguousarray(order, dtype=np.int64)
+        rc = Lib.sv_worldline_plaquette_ordered_run(h, kappa, 1.0, _native.ptr(o), ctypes.byref(r), st)
+        err = Lib.sv_last_error(ctx.handle).decode() if rc else ''
+        if rc == 0:
+            rng_to_numpy(r, g)
+        ctx.check(Lib.sv_worldline_download(h, _native.ptr(m), _native.ptr(v)), 'download')
+        return rc, err, m, v, g.bit_generator.state, st[0].accepted
+    finally:
+        Lib.sv_worldline_destroy(h)
+
+
+@pytest.mark.parametrize('kind', ['row-major', 'column-major', 'reversed'])
+def test_ordered_plaquette_deep_level_plans(kind, oracle_lib):
+    """Visit orders far from random: row-major order chains every plaquette to its left and upper neighbours (2N - 1
+    dependency levels, the device plan's relaxation runs 8 batches at N = 32), column-major likewise, reversed
+    row-major too.  Bit-exact against the sequential oracle (plaquette.py:63-101 given the order)."""
+    N, kappa = 32, 0.5
+    lin = np.arange(N * N, dtype=np.int64)
+    order = {'row-major': lin, 'column-major': (lin % N) * N + lin // N, 'reversed': lin[::-1].copy()}[kind]
+    m0 = np.zeros((2, N, N), dtype=np.int64)
+    rc, err, m, v, state, acc = _ordered_run(N, kappa, m0, order, 5)
+    assert rc == 0, err
+    mm, vv = m0.copy(), np.zeros((N, N), dtype=np.int64)
+    g = np.random.default_rng(5)
+    s = oracle_lib.worldline_plaquette_seq(N, kappa, 1.0, mm, vv, order, g)
+    assert (m == mm).all() and (v == vv).all()
+    assert state == g.bit_generator.state and acc == s.accepted
+
+
+@pytest.mark.parametrize('bad', ['duplicate', 'out of range', 'negative'])
+def test_ordered_plaquette_rejects_non_permutations(bad):
+    """The reference draws its order as a permutation; anything else is refused (the device plan checks it) and the
+    fields are left as they were."""
+    N = 16
+    order = np.arange(N * N, dtype=np.int64)
+    if bad == 'duplicate':
+        order[7] = order[3]
+    elif bad == 'out of range':
+        order[5] = N * N
+    else:
+        order[0] = -1
+    m0 = np.random.default_rng(1).integers(-2, 3, (2, N, N))
+    rc, err, m, v, _, _ = _ordered_run(N, 0.5, m0, order, 1)
+    assert rc != 0 and 'permutation' in err
+    assert (m == m0).all() and (v == 0).all()
