@@ -607,6 +607,7 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
     int sw = 0;
     while (sw < sweeps) {
         const int count = std::min(BATCH, sweeps - sw);
+        bool stats_landed = false;
         if (may_reject) snapshot(st, false);  // no bounded draw that can reject: nothing to replay
         for (int attempt = 0;; attempt++) {
             if (attempt > 256) throw std::runtime_error("rejection replay did not converge");
@@ -629,9 +630,14 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
                 cur = c;
                 break;
             }
+            // the batch's statistics travel with the abort check (one synchronization per batch, not two); an
+            // aborted batch's copy is simply overwritten by its replay's
+            SV_HIP(hipMemcpyAsync(stats + (size_t)sw * nstat, ctx->d_stats, (size_t)count * nstat * sizeof(sv_stats),
+                                  hipMemcpyDeviceToHost, ctx->stream));
             if (!wcheck(ctx, reps)) {
                 ctx->time_collect();
                 cur = c;
+                stats_landed = true;
                 break;
             }
             ctx->time_discard();
@@ -644,7 +650,7 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
         }
         const bool deferred = !may_reject && ctx->defer_stats(stats + (size_t)sw * nstat, (int64_t)count * nstat);
         if (!may_reject && !deferred) svh::loc::queue_abort_copy(ctx);
-        if (!deferred) {
+        if (!deferred && !stats_landed) {
             SV_HIP(hipMemcpyAsync(stats + (size_t)sw * nstat, ctx->d_stats, (size_t)count * nstat * sizeof(sv_stats),
                                   hipMemcpyDeviceToHost, ctx->stream));
             SV_HIP(hipStreamSynchronize(ctx->stream));
