@@ -1,12 +1,13 @@
-"""Gaps between consecutive villain_sweep_hot launches in a rocprofv3 kernel trace: count, mean, p90, and the
-spacing (in launches) of the gaps above 3 us.  Usage: gap_stats.py run_kernel_trace.csv"""
+"""Gaps between consecutive launches of one kernel in a rocprofv3 kernel trace: count, mean, p90, and the spacing
+(in launches) of the gaps above 3 us.  Usage: gap_stats.py run_kernel_trace.csv [kernel substring]"""
 import collections
 import csv
 import statistics
 import sys
 
+KERNEL = sys.argv[2] if len(sys.argv) > 2 else 'villain_sweep_hot'
 tr = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r['Start_Timestamp']))
-hot = [i for i, r in enumerate(tr) if 'villain_sweep_hot' in r['Kernel_Name']]
+hot = [i for i, r in enumerate(tr) if KERNEL in r['Kernel_Name']]
 gaps, big = [], []
 for j, i in enumerate(hot[:-1]):
     if hot[j + 1] == i + 1:
