@@ -28,6 +28,27 @@ void sv_ctx::ensure_blocks(size_t n) {
     SV_HIP(hipMalloc(&d_blocks, blocks_cap * sizeof(sv::Block)));
 }
 
+void sv_ctx::upload_plan(const sv::Block *blocks, size_t nblocks, const uint32_t *skips, size_t nskips) {
+    ensure_blocks(nblocks);
+    ensure_skips(nskips + 1);
+    const size_t bb = nblocks * sizeof(sv::Block), sb = nskips * sizeof(uint32_t);
+    const int i = h_plan_i;
+    h_plan_i ^= 1;
+    if (!ev_plan[i]) SV_HIP(hipEventCreateWithFlags(&ev_plan[i], hipEventDisableTiming));
+    else SV_HIP(hipEventSynchronize(ev_plan[i]));  // (its last copies have long run, unless runs are deferred)
+    if (bb + sb > h_plan_cap[i]) {
+        SV_HIP(hipStreamSynchronize(stream));  // (the buffer may still feed an earlier copy)
+        if (h_plan[i]) SV_HIP(hipHostFree(h_plan[i]));
+        h_plan_cap[i] = std::max<size_t>(2 * (bb + sb), 64 * 1024);
+        SV_HIP(hipHostMalloc((void **)&h_plan[i], h_plan_cap[i], hipHostMallocDefault));
+    }
+    std::memcpy(h_plan[i], blocks, bb);
+    if (sb) std::memcpy(h_plan[i] + bb, skips, sb);
+    SV_HIP(hipMemcpyAsync(d_blocks, h_plan[i], bb, hipMemcpyHostToDevice, stream));
+    if (sb) SV_HIP(hipMemcpyAsync(d_skips, h_plan[i] + bb, sb, hipMemcpyHostToDevice, stream));
+    SV_HIP(hipEventRecord(ev_plan[i], stream));
+}
+
 void sv_ctx::ensure_skips(size_t n) {
     if (n <= skips_cap) return;
     SV_HIP(hipStreamSynchronize(stream));
@@ -477,6 +498,10 @@ int sv_ctx_destroy(sv_ctx *ctx) {
     (void)hipFree(ctx->d_abort);
     if (ctx->h_abort) (void)hipHostFree(ctx->h_abort);
     if (ctx->h_flag) (void)hipHostFree(ctx->h_flag);
+    for (char *h : ctx->h_plan)
+        if (h) (void)hipHostFree(h);
+    for (hipEvent_t e : ctx->ev_plan)
+        if (e) (void)hipEventDestroy(e);
     for (auto &e : ctx->ev_chunk)
         if (e) (void)hipEventDestroy(e);
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);

@@ -150,6 +150,14 @@ struct sv_ctx {
     void ensure_blocks(size_t n);
     void ensure_skips(size_t n);
     void ensure_stats(size_t n);
+    // a batch plan (descriptors, skip positions) to d_blocks / d_skips through pinned staging: two pinned buffers
+    // used in turn (an upload reuses the one of two uploads before, across the batch's synchronization), so the
+    // copies are plain asynchronous DMA instead of pageable staging (~20 us of host time each)
+    void upload_plan(const sv::Block *blocks, size_t nblocks, const uint32_t *skips, size_t nskips);
+    char *h_plan[2] = {nullptr, nullptr};
+    size_t h_plan_cap[2] = {0, 0};
+    hipEvent_t ev_plan[2] = {nullptr, nullptr};  // recorded after each buffer's copies (deferred runs do not sync)
+    int h_plan_i = 0;
 };
 
 struct sv_villain {

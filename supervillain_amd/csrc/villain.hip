@@ -684,13 +684,7 @@ void plan_sweeps(sv_ctx *ctx, Cursor &cur, u128 inc, const std::vector<BlockSpec
 }
 
 void upload_plan(sv_ctx *ctx, const std::vector<Block> &blocks, const std::vector<uint32_t> &skipvec) {
-    ctx->ensure_blocks(blocks.size());
-    ctx->ensure_skips(skipvec.size() + 1);
-    SV_HIP(hipMemcpyAsync(ctx->d_blocks, blocks.data(), blocks.size() * sizeof(Block), hipMemcpyHostToDevice,
-                          ctx->stream));
-    if (!skipvec.empty())
-        SV_HIP(hipMemcpyAsync(ctx->d_skips, skipvec.data(), skipvec.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                              ctx->stream));
+    ctx->upload_plan(blocks.data(), blocks.size(), skipvec.data(), skipvec.size());
 }
 
 VParams make_params(int32_t N, double kappa, int64_t W, double interval_phi, int64_t interval_n) {

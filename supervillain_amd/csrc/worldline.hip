@@ -506,13 +506,7 @@ void wplan(Cursor &cur, u128 inc, const std::vector<BlockSpec> &specs, int first
 }
 
 void wupload(sv_ctx *ctx, const std::vector<Block> &blocks, const std::vector<uint32_t> &skipvec) {
-    ctx->ensure_blocks(blocks.size());
-    ctx->ensure_skips(skipvec.size() + 1);
-    SV_HIP(hipMemcpyAsync(ctx->d_blocks, blocks.data(), blocks.size() * sizeof(Block), hipMemcpyHostToDevice,
-                          ctx->stream));
-    if (!skipvec.empty())
-        SV_HIP(hipMemcpyAsync(ctx->d_skips, skipvec.data(), skipvec.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                              ctx->stream));
+    ctx->upload_plan(blocks.data(), blocks.size(), skipvec.data(), skipvec.size());
 }
 
 bool wcheck(sv_ctx *ctx, std::vector<Report> &reps) {
@@ -569,15 +563,34 @@ WParams wparams(int32_t N, double kappa, double Weff, int64_t it, u128 inc) {
 
 DevScratch wscratch(sv_ctx *ctx) { return DevScratch{ctx->d_abort, ctx->d_nreport, ctx->d_reports}; }
 
+// (m, v) copied in one launch: two hipMemcpyAsync device-to-device calls cost ~35 us of host time each at a batch
+// boundary, the launch ~5 (16-B lanes; both sizes are multiples of 16 B)
+__global__ void copy_pair(uint4 *__restrict__ d0, const uint4 *__restrict__ s0, int64_t n0, uint4 *__restrict__ d1,
+                          const uint4 *__restrict__ s1, int64_t n1) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n0 + n1; i += stride) {
+        if (i < n0) d0[i] = s0[i];
+        else d1[i - n0] = s1[i - n0];
+    }
+}
+
 void snapshot(sv_worldline *st, bool restore) {
     sv_ctx *ctx = st->ctx;
     const size_t V = (size_t)st->N * st->N;
     const size_t vb = V * (st->v_is_float ? sizeof(double) : sizeof(int64_t));
+    const int64_t n0 = (int64_t)(2 * V * sizeof(int64_t) / 16), n1 = (int64_t)(vb / 16);
+    const int grid = (int)std::min<int64_t>((n0 + n1 + 255) / 256, 4096);
     if (!restore) {
         st->m_at_snap = st->m;
         st->v_at_snap = st->v;
-        SV_HIP(hipMemcpyAsync(st->snap_m, st->m, 2 * V * sizeof(int64_t), hipMemcpyDeviceToDevice, ctx->stream));
-        SV_HIP(hipMemcpyAsync(st->snap_v, st->v, vb, hipMemcpyDeviceToDevice, ctx->stream));
+        if ((2 * V * sizeof(int64_t)) % 16 == 0 && vb % 16 == 0) {
+            copy_pair<<<grid, 256, 0, ctx->stream>>>((uint4 *)st->snap_m, (const uint4 *)st->m, n0, (uint4 *)st->snap_v,
+                                                     (const uint4 *)st->v, n1);
+            SV_HIP(hipGetLastError());
+        } else {
+            SV_HIP(hipMemcpyAsync(st->snap_m, st->m, 2 * V * sizeof(int64_t), hipMemcpyDeviceToDevice, ctx->stream));
+            SV_HIP(hipMemcpyAsync(st->snap_v, st->v, vb, hipMemcpyDeviceToDevice, ctx->stream));
+        }
     } else {
         if (st->m_at_snap && st->m != st->m_at_snap) {  // fused steps swapped the buffer pairs since the snapshot
             std::swap(st->m, st->m_alt);
@@ -604,6 +617,12 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
     std::vector<Block> blocks;
     std::vector<uint32_t> skipvec;
     std::vector<Report> reps;
+    // The next batch is planned on the host while this one runs on the device (the plan is most of a batch
+    // boundary: ~160 us per 64 L=1024 steps); a replay in this batch (new skips) discards it
+    std::vector<Block> blocks_next;
+    std::vector<uint32_t> skipvec_next;
+    Cursor c_next{};
+    int sw_next = -1;
     int sw = 0;
     while (sw < sweeps) {
         const int count = std::min(BATCH, sweeps - sw);
@@ -612,7 +631,14 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
         for (int attempt = 0;; attempt++) {
             if (attempt > 256) throw std::runtime_error("rejection replay did not converge");
             Cursor c = cur;
-            wplan(c, inc, specs, sw, count, skips, blocks, skipvec);
+            if (sw_next == sw && attempt == 0) {
+                blocks.swap(blocks_next);
+                skipvec.swap(skipvec_next);
+                c = c_next;
+            } else {
+                wplan(c, inc, specs, sw, count, skips, blocks, skipvec);
+            }
+            sw_next = -1;
             wupload(ctx, blocks, skipvec);
             ctx->ensure_stats((size_t)count * nstat);
             StatStripe *ss = (StatStripe *)st->stripes;
@@ -626,6 +652,12 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
             ctx->time_end(ev, count);
             fold_stripes<<<(count * nstat + 63) / 64, 64, 0, ctx->stream>>>(ss, ctx->d_stats, count * nstat);
             SV_HIP(hipGetLastError());
+            if (sw + count < sweeps) {  // (the device runs this batch meanwhile)
+                c_next = c;
+                wplan(c_next, inc, specs, sw + count, std::min(BATCH, sweeps - sw - count), skips, blocks_next,
+                      skipvec_next);
+                sw_next = sw + count;
+            }
             if (!may_reject) {  // threshold 0: no rejection can occur, so the stats copy is the one sync
                 cur = c;
                 break;
@@ -641,6 +673,7 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
                 break;
             }
             ctx->time_discard();
+            sw_next = -1;  // (the replay changes the skips: the next batch is planned again)
             if (std::any_of(reps.begin(), reps.end(), [](const Report &r) { return r.block == OVERFLOW_BLOCK; })) {
                 st->wf_off = true;  // the fused kernel's int32 image cannot hold the state: replay on the pass kernels
             } else {
