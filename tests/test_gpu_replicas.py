@@ -73,6 +73,37 @@ def test_rejection_in_one_replica(oracle_lib):
         assert stats['rejections'][2].sum() >= 1
 
 
+@pytest.mark.parametrize('inline', [False, True])
+def test_rejections_in_later_batches(oracle_lib, inline):
+    """Several 64-sweep batches (two in flight: the next one is enqueued before the current one has finished):
+    forced Lemire rejections in the second batch's 7th sweep, the first sweep of the third batch and the last
+    sweep of the call; every replica equals its own chain, with its statistics and inline observables."""
+    R, N, sweeps, kappa = 4, 16, 150, 0.4
+    V = N * N
+    phi0, n0 = hot(R, N, 1, 21)
+    crafted = {1: (70 * 4 * V + V + V // 2 + 9, 0), 2: (128 * 4 * V + 3 * V + 7, 1), 3: (149 * 4 * V + 3 * V + 1, 0)}
+
+    def gens_():
+        return [crafted_generator(30 + r, *crafted[r]) if r in crafted else np.random.default_rng(r) for r in range(R)]
+    gens = gens_()
+    phi, n, stats, obs = run_batch(R, N, kappa, 1, phi0, n0, sweeps, gens, inline=inline)
+    ref = gens_()
+    for r in range(R):
+        p, m = phi0[r].copy(), n0[r].copy()
+        st = oracle_lib.villain_neighborhood(N, kappa, 1, p, m, sweeps, ref[r])
+        assert (phi[r] == p).all() and (n[r] == m).all(), r
+        assert gens[r].bit_generator.state == ref[r].bit_generator.state
+        assert list(stats['accepted'][r]) == [s.accepted for s in st]
+        assert list(stats['rejections'][r]) == [s.rejections for s in st]
+        if inline:
+            act, w2, s0, s1 = offline(p, m)
+            np.testing.assert_allclose(obs['ActionDensity'][r, -1], kappa / 2 * act / V, rtol=1e-12)
+            assert obs['WindingSquared'][r, -1] == w2 / V
+            assert list(obs['TorusWrapping'][r, -1]) == [s0, s1]
+    for r in crafted:
+        assert stats['rejections'][r].sum() >= 1, r
+
+
 def test_inline_observables_match_offline(oracle_lib):
     R, N, sweeps, kappa = 3, 32, 4, 0.5
     phi0, n0 = hot(R, N, 2, 4)
