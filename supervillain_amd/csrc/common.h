@@ -61,6 +61,10 @@ struct DevScratch {
     uint32_t *nreport;  // count of reports
     Report *reports;
     int32_t *hflag = nullptr;  // optional host-mapped copy of the abort flag (the host polls it between chunks)
+    // optional (replica batches): the first sweep with a report (atomic min; INT32_MAX when none).  With a gate,
+    // launches exit only behind a sweep that reported, so the failing sweep itself completes for every replica
+    // and only the replicas that reported in it are replayed
+    int32_t *gate = nullptr;
 };
 
 // Asynchronous emission of a resident state: the state is snapshotted on the compute

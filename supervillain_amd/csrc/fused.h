@@ -20,10 +20,18 @@ __device__ __forceinline__ void report(const DevScratch &S, uint32_t sweep, uint
     uint32_t i = atomicAdd(S.nreport, 1u);
     if (i < (uint32_t)MAX_REPORTS) S.reports[i] = Report{sweep, block, pos, rep};
     __hip_atomic_store(S.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (S.gate) __hip_atomic_fetch_min(S.gate, (int32_t)sweep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (S.hflag) __hip_atomic_store(S.hflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     // drain here, on the rare path: a result still pending at the join would make the compiler wait
     // for every outstanding load and store (the row prefetch, the finished-row stores) on the common path
     __builtin_amdgcn_s_waitcnt(0);
+}
+
+// a launch of sweep `sweep` has nothing to do: a report came from an earlier sweep (with a gate, DevScratch), or
+// from any launch since the batch's reset (without)
+__device__ __forceinline__ bool sweep_cancelled(const DevScratch &S, uint32_t sweep) {
+    if (S.gate) return *(volatile const int32_t *)S.gate < (int32_t)sweep;
+    return *(volatile const int32_t *)S.abort != 0;
 }
 
 // stream position of bounded draw d, accounting for known rejected positions (sorted)

@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <array>
 #include <cstring>
+#include <thread>
 
 #include "villain.h"
 
@@ -103,6 +104,7 @@ struct sv_replicas {
     char *h_tail = nullptr;
     size_t tail_cap = 0;
     int32_t *d_map = nullptr;  // replica maps of the split launches of a batch (R * REP_BATCH slots)
+    int32_t *d_gate = nullptr;  // the batch's first sweep with a report (DevScratch::gate)
 };
 
 namespace {
@@ -284,6 +286,19 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         if (!B.hmap.empty())
             SV_HIP(hipMemcpyAsync(b->d_map, B.hmap.data(), B.hmap.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                                   ctx->stream));
+        // The batch goes out in chunks of CH sweeps: after chunk j is enqueued the host waits for chunk j - 1 (the
+        // progress word the first launch of chunk j stores) and reads the host-mapped abort flag, so that a NumPy
+        // Lemire rejection leaves at most ~2 CH launches queued behind it (each an early exit over every workgroup)
+        // instead of the rest of the batch (r3: 220 early-exit launches, 1.1 ms, in a 200-sweep config-5 window)
+        static const int CH_env = [] {  // SV_REP_CHUNK overrides the chunk (0: the whole batch)
+            const char *e = getenv("SV_REP_CHUNK");
+            return e ? atoi(e) : 8;
+        }();
+        const int CH = CH_env > 0 ? CH_env : count;
+        *ctx->h_flag = 0;
+        __atomic_store_n(ctx->h_prog, 0, __ATOMIC_RELEASE);  // (the previous batch has finished)
+        int launched = count;
+        SV_HIP(hipMemsetAsync(b->d_gate, 0x7f, sizeof(int32_t), ctx->stream));  // no report yet (0x7f7f7f7f)
         hipEvent_t ev;
         ctx->time_begin(&ev);
         for (int k = 0; k < count; k++) {
@@ -301,7 +316,8 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
             A.skips = ctx->d_skips;
             A.T = nullptr;
             A.stat = b->d_stats + k;
-            A.S = DevScratch{ctx->d_abort, ctx->d_nreport, ctx->d_reports};
+            A.S = DevScratch{ctx->d_abort, ctx->d_nreport, ctx->d_reports, ctx->d_flag, b->d_gate};
+            A.progress = ctx->d_prog;
             A.sweep = (uint32_t)k;
             A.tiles_per_rep = tiles;
             A.rep_blocks = count * NB;
@@ -332,8 +348,25 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
                 ctx->sweeps_fused++;
             }
             b->cur ^= 1;
+            if ((k + 1) % CH == 0 && k + 1 < count && k + 1 >= 2 * CH) {
+                // chunk j = (k + 1) / CH - 1 is enqueued: wait until chunk j - 1 has finished (the first launch of
+                // chunk j has started), or a rejection was reported, or (guard) the stream has drained
+                const int32_t target = (int32_t)(k + 1 - CH) + 1;
+                const auto tw = clk::now();
+                for (int spin = 0; __atomic_load_n(ctx->h_prog, __ATOMIC_ACQUIRE) < target; spin++) {
+                    if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE)) break;
+                    if ((spin & 1023) == 1023 && clk::now() - tw > std::chrono::milliseconds(20) &&
+                        hipStreamQuery(ctx->stream) == hipSuccess)
+                        break;  // (drained: e.g. a sweep with no launch that stores its progress)
+                    std::this_thread::yield();
+                }
+                if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE)) {
+                    launched = k + 1;  // the rest of the batch is not enqueued
+                    break;
+                }
+            }
         }
-        ctx->time_end(ev, count);
+        ctx->time_end(ev, launched);
         SV_HIP(hipGetLastError());
         // outcome: abort flag, report count, statistics and observables land in the pinned slot
         char *tail = b->h_tail + slot * slot_bytes;
@@ -345,7 +378,8 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
                                   hipMemcpyDeviceToHost, ctx->stream));
     };
     // --- keep sweeps [B.sw, B.sw + good) of a finished batch: statistics and observables into the caller's arrays
-    auto keep = [&](const RepBatch &B, int good) {
+    // (fail: after an abort at sweep `good`, the replicas that did not report in it keep that sweep too)
+    auto keep = [&](const RepBatch &B, int good, const std::vector<char> *fail = nullptr) {
         const char *tail = b->h_tail + B.slot * slot_bytes;
         const sv_stats *h_st = (const sv_stats *)(tail + 64);
         const double *h_ob = (const double *)(tail + 64 + (size_t)R * B.count * sizeof(sv_stats));
@@ -353,14 +387,108 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
             const bool none = skips[r].empty();
             sv_stats *dst = stats + (size_t)r * sweeps + B.sw;
             const sv_stats *src = h_st + (size_t)r * B.count;
-            for (int k = 0; k < good; k++) {
+            const int upto = good + (fail && !(*fail)[r] && good < B.count ? 1 : 0);
+            for (int k = 0; k < upto; k++) {
                 dst[k] = src[k];
                 dst[k].proposed = V;
                 dst[k].rejections = none ? 0 : rejections_in(skips[r], B.sw + k, NB);
             }
             if (obs)
                 std::memcpy(obs + ((size_t)r * sweeps + B.sw) * 4, h_ob + (size_t)r * B.count * 4,
-                            (size_t)good * 4 * sizeof(double));
+                            (size_t)upto * 4 * sizeof(double));
+        }
+    };
+
+    // Sweep k of batch B again for the replicas F that reported in it (their cursors in `cur` are at sweep k), on the
+    // general kernel with the absorbed skip lists, until it completes without a new report; their statistics and
+    // observables of that sweep go straight to the caller's arrays and their cursors move past it
+    auto replay_failed = [&](const RepBatch &B, int k, const std::vector<int32_t> &F) {
+        if (F.empty()) return;
+        const int count = B.count;
+        for (int attempt = 0;; attempt++) {
+            if (attempt > 64) throw std::runtime_error("rejection replay did not converge");
+            std::vector<Cursor> cf(F.size());
+            std::vector<Block> fb((size_t)F.size() * NB);
+            std::vector<uint32_t> allsk;
+            for (size_t i = 0; i < F.size(); i++) {
+                const int r = F[i];
+                Cursor c = cur[r];
+                std::vector<Block> blk;
+                plan_sweeps(ctx, c, inc[r], specs, B.sw + k, 1, skips[r], blk, sk);
+                for (int j = 0; j < NB; j++) {
+                    fb[i * NB + j] = blk[j];
+                    fb[i * NB + j].skip0 += (int32_t)allsk.size();
+                }
+                allsk.insert(allsk.end(), sk.begin(), sk.end());
+                cf[i] = c;
+            }
+            ctx->ensure_skips(allsk.size() + 1);
+            for (size_t i = 0; i < F.size(); i++) {
+                const size_t e = (size_t)F[i] * count + k;
+                SV_HIP(hipMemcpyAsync(b->d_blocks + e * NB, &fb[i * NB], NB * sizeof(Block), hipMemcpyHostToDevice,
+                                      ctx->stream));
+                SV_HIP(hipMemsetAsync(b->d_stats + e, 0, sizeof(sv_stats), ctx->stream));
+                if (obs) SV_HIP(hipMemsetAsync(b->d_obs + 4 * e, 0, 4 * sizeof(double), ctx->stream));
+            }
+            if (!allsk.empty())
+                SV_HIP(hipMemcpyAsync(ctx->d_skips, allsk.data(), allsk.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                      ctx->stream));
+            SV_HIP(hipMemcpyAsync(b->d_map, F.data(), F.size() * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+            clear_abort(ctx);
+            SV_HIP(hipMemsetAsync(b->d_gate, 0x7f, sizeof(int32_t), ctx->stream));
+            FArgs A;
+            A.P = P;
+            A.G = FGeom{b->N, b->N, 0, 0, b->N, b->N, b->N, V, 0};
+            A.phi_in = b->phi[B.cur0 ^ (k & 1)];
+            A.n_in = b->n[B.cur0 ^ (k & 1)];
+            A.phi_out = b->phi[B.cur0 ^ (k & 1) ^ 1];
+            A.n_out = b->n[B.cur0 ^ (k & 1) ^ 1];
+            A.nsx = nsx;
+            A.TH = 8;  // short strips: the few replaying replicas fill more of the chip
+            A.nsy = (b->N + 7) / 8;
+            A.blocks = b->d_blocks + (size_t)k * NB;
+            A.skips = ctx->d_skips;
+            A.T = nullptr;
+            A.stat = b->d_stats + k;
+            A.S = DevScratch{ctx->d_abort, ctx->d_nreport, ctx->d_reports, nullptr, b->d_gate};
+            A.sweep = (uint32_t)k;
+            A.tiles_per_rep = nsx * A.nsy;
+            A.rep_blocks = count * NB;
+            A.rep_field = V;
+            A.rep_stat = count;
+            A.rep_obs = 4 * count;
+            A.Trep = b->d_Trep;
+            A.advrep = b->d_adv;
+            A.obs = obs ? b->d_obs + 4 * k : nullptr;
+            A.rep_map = b->d_map;
+            launch_fused_batch(A, (int)F.size() * A.tiles_per_rep, obs != nullptr, ctx->stream);
+            ctx->sweeps_fused++;
+            SV_HIP(hipGetLastError());
+            AbortInfo a = read_abort(ctx);  // (synchronizes)
+            if (!a.abort) {
+                for (size_t i = 0; i < F.size(); i++) {
+                    const int r = F[i];
+                    const size_t e = (size_t)r * count + k;
+                    sv_stats *dst = stats + (size_t)r * sweeps + B.sw + k;
+                    SV_HIP(hipMemcpy(dst, b->d_stats + e, sizeof(sv_stats), hipMemcpyDeviceToHost));
+                    dst->proposed = V;
+                    dst->rejections = rejections_in(skips[r], B.sw + k, NB);
+                    if (obs)
+                        SV_HIP(hipMemcpy(obs + ((size_t)r * sweeps + B.sw + k) * 4, b->d_obs + 4 * e, 4 * sizeof(double),
+                                         hipMemcpyDeviceToHost));
+                    cur[r] = cf[i];
+                }
+                return;
+            }
+            for (const Report &x : a.reports)
+                if (x.block == OVERFLOW_BLOCK)
+                    throw std::runtime_error("|n| exceeds the general fused kernel's int32 LDS image (|n| < 2^30 required)");
+            for (int r : F) {
+                AbortInfo ar{1, {}};
+                for (const Report &x : a.reports)
+                    if ((int)x.pad == r) ar.reports.push_back(x);
+                if (!ar.reports.empty()) absorb_reports(ar, B.sw, skips[r]);
+            }
         }
     };
 
@@ -398,6 +526,11 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
                 if (!a.reports.empty()) absorb_reports(a, B.sw, skips[r]);
             }
             const int good = (int)bad;
+            // the gate (DevScratch::gate) let the failing sweep complete: only the replicas that reported in it
+            // replay it; every other replica keeps its result
+            std::vector<char> fail(R, 0);
+            for (const Report &x : reps)
+                if (x.sweep == bad) fail[x.pad] = 1;
             const Affine unit = good > 0 ? host_power(u128{1, 0}, (uint64_t)good * 4 * V) : Affine{};
             for (int r = 0; r < R; r++) {
                 if (has_skips(skips[r], B.sw, good)) {
@@ -409,16 +542,32 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
                     advance_closed(cur[r], inc[r], unit);
                 }
             }
-            b->cur = B.cur0 ^ (good & 1);
-            sw = B.sw + good;
+            const Affine unit1 = host_power(u128{1, 0}, (uint64_t)4 * V);
+            std::vector<int32_t> F;
+            for (int r = 0; r < R; r++) {
+                if (fail[r]) {
+                    F.push_back(r);
+                } else if (has_skips(skips[r], B.sw + good, 1)) {
+                    Cursor c = cur[r];
+                    std::vector<Block> blk;
+                    plan_sweeps(ctx, c, inc[r], specs, B.sw + good, 1, skips[r], blk, sk);
+                    cur[r] = c;
+                } else {
+                    advance_closed(cur[r], inc[r], unit1);
+                }
+            }
             const auto t_c = clk::now();
-            // the replay goes out first (into the other slot), the kept sweeps are copied out while it runs
-            if (sw < sweeps) enqueue(batch[cb ^ 1], sw, std::min(REP_BATCH, sweeps - sw), B.slot ^ 1);
+            replay_failed(B, good, F);
+            b->cur = B.cur0 ^ ((good + 1) & 1);
+            sw = B.sw + good + 1;
             const auto t_d = clk::now();
-            keep(B, good);
+            // the next batch goes out first (into the other slot), the kept sweeps are copied out while it runs
+            if (sw < sweeps) enqueue(batch[cb ^ 1], sw, std::min(REP_BATCH, sweeps - sw), B.slot ^ 1);
+            keep(B, good, &fail);
             if (dbg)
-                fprintf(stderr, "[sv replicas] wait %.1f us, abort at %d/%d, replan %.1f us, enqueue %.1f us, keep %.1f us\n",
-                        us(t_a, t_b), good, B.count, us(t_b, t_c), us(t_c, t_d), us(t_d, clk::now()));
+                fprintf(stderr, "[sv replicas] wait %.1f us, abort at %d/%d (%zu replicas replay it), replan %.1f us, "
+                        "replay %.1f us, enqueue + keep %.1f us\n", us(t_a, t_b), good, B.count, F.size(),
+                        us(t_b, t_c), us(t_c, t_d), us(t_d, clk::now()));
             cb ^= 1;
             continue;
         }
@@ -479,6 +628,7 @@ int sv_replicas_create(sv_ctx *ctx, int32_t R, int32_t N, sv_replicas **out) {
         SV_HIP(hipMalloc(&b->d_blocks, (size_t)R * REP_BATCH * NB * sizeof(Block)));
         SV_HIP(hipMalloc(&b->d_stats, (size_t)R * REP_BATCH * sizeof(sv_stats)));
         SV_HIP(hipMalloc(&b->d_obs, (size_t)R * REP_BATCH * 4 * sizeof(double)));
+        SV_HIP(hipMalloc(&b->d_gate, sizeof(int32_t)));
         *out = b;
         return 0;
     } catch (const std::exception &e) {
@@ -502,6 +652,7 @@ int sv_replicas_destroy(sv_replicas *b) {
     (void)hipFree(b->d_Trep);
     (void)hipFree(b->d_adv);
     (void)hipFree(b->d_plan);
+    (void)hipFree(b->d_gate);
     (void)hipFree(b->d_blocks);
     (void)hipFree(b->d_stats);
     (void)hipFree(b->d_obs);

@@ -143,7 +143,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     __shared__ Block s_blk[11];  // this sweep's descriptors (LDS: no vector-memory waits in the loop)
 
     note_progress(A);
-    if (*(volatile const int32_t *)A.S.abort) return;
+    if (sweep_cancelled(A.S, A.sweep)) return;
 
     const FGeom &Gm = A.G;
     const int32_t Nt = Gm.Nt, Nx = Gm.Nx;

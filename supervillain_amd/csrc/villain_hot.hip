@@ -181,8 +181,8 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     auto &s_base = Ls.base;
     int32_t &s_bad = Ls.bad;
 
-    if constexpr (!FR && !PH) note_progress(A);  // (single lattices and tiles only)
-    if (*(volatile const int32_t *)A.S.abort) return;
+    if constexpr (!PH) note_progress(A);  // (FArgs::progress: the chunked enqueues of single lattices and replica batches)
+    if (sweep_cancelled(A.S, A.sweep)) return;
 #if SV_WGTIME
     const uint64_t wg_t0 = rt_now();
 #endif
