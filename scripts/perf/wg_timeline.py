@@ -1,6 +1,7 @@
 """Per-workgroup timeline of villain_sweep_hot (variant built with -DSV_WGTIME=1: entry / loop start / loop end / exit
 timestamps from s_memrealtime, 100 MHz, and the hardware ids).  Usage:
-  SV_LIB_OVERRIDE=supervillain_amd/variants/libsvhip_wgtime.so python scripts/perf/wg_timeline.py [single|tile] ..."""
+  SV_LIB_OVERRIDE=supervillain_amd/variants/libsvhip_wgtime.so python scripts/perf/wg_timeline.py [single|tile] ...
+  (worldline: a variant built with -DSV_WFTIME=1, python scripts/perf/wg_timeline.py worldline [L])"""
 import ctypes
 import sys
 
@@ -12,7 +13,8 @@ from supervillain_amd._abi import rng_from_numpy  # noqa: E402
 from supervillain_amd.domain import VillainDomain  # noqa: E402
 
 Lib = _native.lib()
-Lib.sv_debug_wgtime.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+if hasattr(Lib, 'sv_debug_wgtime'):  # (variants built with -DSV_WGTIME=1; SV_WFTIME=1 builds have sv_debug_wftime)
+    Lib.sv_debug_wgtime.argtypes = [ctypes.c_void_p, ctypes.c_int32]
 
 
 def read(nwg):
@@ -81,6 +83,22 @@ def summarize(tag, t, nsx=None):
 
 mode = sys.argv[1] if len(sys.argv) > 1 else 'single'
 ctx = _native.context(0)
+if mode == 'worldline':
+    # config 3's worldline_step_fused (variant built with -DSV_WFTIME=1): the last launch of each call of 50 steps
+    Lib.sv_debug_wftime.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    L = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+    h = ctypes.c_void_p()
+    ctx.check(Lib.sv_worldline_create(ctx.handle, L, 0, ctypes.byref(h)), 'create')
+    m, v = np.zeros((2, L, L), dtype=np.int64), np.zeros((L, L), dtype=np.int64)
+    ctx.check(Lib.sv_worldline_upload(h, _native.ptr(m), _native.ptr(v)), 'upload')
+    r = rng_from_numpy(np.random.default_rng(0))
+    st = _native.stats_array(2 * 50)
+    for k in range(4):
+        ctx.check(Lib.sv_worldline_plaquette_coexact_run(h, 0.5, 1.0, 1, 50, ctypes.byref(r), st), 'run')
+        buf = np.zeros(65536 * 6, dtype=np.uint64)
+        assert Lib.sv_debug_wftime(buf.ctypes.data, 65536) == 0
+        summarize(f'worldline L={L} call {k}', buf.reshape(65536, 6))
+    sys.exit(0)
 if mode == 'single':
     L = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
     h = ctypes.c_void_p()

@@ -1,5 +1,6 @@
 // plan.hip -- host side of the stream replay: PCG64 jumps, block planning, jump tables, colourings.
 #include <algorithm>
+#include <unordered_map>
 
 #include "common.h"
 
@@ -15,9 +16,28 @@ static Affine power(Affine f, uint64_t k) {
     return r;
 }
 
-u128 host_jump(u128 s, u128 inc, uint64_t steps) { return apply(power(step_map(inc), steps), s); }
+// The planner jumps by the same few distances over and over (a block's draws, its words, one step): the maps
+// are cached per thread by (increment, distance), so a planned block costs three 128-bit affine applications
+// instead of three binary powers (L=4096: 64 sweeps 66 -> ~10 us)
+static const Affine &cached_power(u128 inc, uint64_t steps) {
+    struct Key {
+        uint64_t lo, hi, k;
+        bool operator==(const Key &o) const { return lo == o.lo && hi == o.hi && k == o.k; }
+    };
+    struct Hash {
+        size_t operator()(const Key &x) const { return (size_t)(x.lo * 0x9E3779B97F4A7C15ULL ^ x.hi ^ (x.k * 0xC2B2AE3D27D4EB4FULL)); }
+    };
+    thread_local std::unordered_map<Key, Affine, Hash> cache;
+    const Key key{inc.lo, inc.hi, steps};
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    if (cache.size() >= 4096) cache.clear();  // (bounded: many increments or distances)
+    return cache.emplace(key, power(step_map(inc), steps)).first->second;
+}
 
-Affine host_power(u128 inc, uint64_t steps) { return power(step_map(inc), steps); }
+u128 host_jump(u128 s, u128 inc, uint64_t steps) { return apply(cached_power(inc, steps), s); }
+
+Affine host_power(u128 inc, uint64_t steps) { return cached_power(inc, steps); }
 
 uint64_t host_output_at(u128 s, u128 inc, uint64_t pos) { return xsl_rr(host_jump(s, inc, pos + 1)); }
 

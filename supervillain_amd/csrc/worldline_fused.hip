@@ -19,7 +19,16 @@
 // change_v pair; the host keeps the four pass kernels for the rest (worldline.hip).
 #include "fused.h"
 
+#ifndef SV_WFTIME
+#define SV_WFTIME 0  // timing experiments: per-workgroup timestamps of worldline_step_fused (sv_debug_wftime)
+#endif
 namespace sv {
+
+#if SV_WFTIME
+// per launch slot: [wg][0..3] = entry, loop start, loop end, exit (s_memrealtime, 100 MHz), [4] = HW_ID | XCC_ID << 32,
+// [5] = row bases ready (the layout of villain_hot.hip's g_wgtime)
+__device__ uint64_t g_wftime[65536 * 6];
+#endif
 
 static constexpr int WF_W = 119;          // output columns per strip: region = WF_W + 9 <= RW
 // NW waves = NW rows per step.  Ring rows: during step t the passes read rows t-1..t+NW+3 (C1 reads v[t-1], P0
@@ -92,6 +101,9 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     auto &s_v = Ls.v;
     auto &s_small = Ls.small;
     if (*(volatile const int32_t *)A.S.abort) return;
+#if SV_WFTIME
+    const uint64_t wf_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
 
     const FGeom &Gm = A.G;
     const int32_t N = Gm.Nx, Nt = Gm.Nt;  // global row length (stream layout) and row count
@@ -218,6 +230,9 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     if (base_lane) bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)wf_base_pos(bbnd, grow(brow), N, bx, bhas));
     __builtin_amdgcn_s_waitcnt(0);
     if (base_lane) Ls.base[wave][lane] = bases;
+#if SV_WFTIME
+    const uint64_t wf_tb = __builtin_amdgcn_s_memrealtime();
+#endif
 
     // the first column of pass p's colour on row q: pass p covers rows [t0 - 4 + p, t1 + 3 - p) and columns
     // [x0 - 4 + p, x1 + 3 - p): the links a strip stores are also changed by the plaquettes one row above and
@@ -397,6 +412,9 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
         commit(ra);
     }
     __syncthreads();
+#if SV_WFTIME
+    const uint64_t wf_t1 = __builtin_amdgcn_s_memrealtime();
+#endif
 
     for (int32_t t = tfirst; t < t1; t += NW) {
         prefetch(t + AH);
@@ -420,6 +438,9 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
         }
         __syncthreads();
     }
+#if SV_WFTIME
+    const uint64_t wf_t2 = __builtin_amdgcn_s_memrealtime();
+#endif
     {
         int32_t tl = tfirst;
         while (tl + NW < t1) tl += NW;
@@ -428,6 +449,19 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     if (Ls.bad && threadIdx.x == 0) report(A.S, A.sweep, OVERFLOW_BLOCK, 0, 0);
     wflush(A.pstat, pacc, ppsum);
     wflush(A.cstat, cacc, cpsum);
+#if SV_WFTIME
+    __builtin_amdgcn_s_waitcnt(0);
+    if (threadIdx.x == 0 && blockIdx.x < 65536) {
+        uint64_t *o = g_wftime + 6 * (size_t)blockIdx.x;
+        o[0] = wf_t0;
+        o[1] = wf_t1;
+        o[2] = wf_t2;
+        o[3] = __builtin_amdgcn_s_memrealtime();
+        o[5] = wf_tb;
+        o[4] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+               ((uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32);
+    }
+#endif
 }
 
 #ifndef SV_WF_OCC8
@@ -572,3 +606,9 @@ void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
 }
 
 }  // namespace svh
+
+#if SV_WFTIME
+extern "C" int sv_debug_wftime(uint64_t *out, int32_t n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(sv::g_wftime), (size_t)n * 6 * sizeof(uint64_t)) == hipSuccess ? 0 : -2;
+}
+#endif
