@@ -19,6 +19,9 @@
 // change_v pair; the host keeps the four pass kernels for the rest (worldline.hip).
 #include "fused.h"
 
+#ifndef SV_WF_PF0
+#define SV_WF_PF0 1  // the first prefetch of region rows issued before the prologue's row-base jumps
+#endif
 #ifndef SV_WFTIME
 #define SV_WFTIME 0  // timing experiments: per-workgroup timestamps of worldline_step_fused (sv_debug_wftime)
 #endif
@@ -227,6 +230,9 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     const int32_t tfirst = t0 - 7;
     int32_t brow = tfirst + 3 - bp + wave;
     u128 bases{0, 0};
+#if SV_WF_PF0
+    prefetch(t0 - 5);  // the first region rows in flight while the row bases are jumped to
+#endif
     if (base_lane) bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)wf_base_pos(bbnd, grow(brow), N, bx, bhas));
     __builtin_amdgcn_s_waitcnt(0);
     if (base_lane) Ls.base[wave][lane] = bases;
@@ -408,7 +414,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     };
 
     for (int32_t ra = t0 - 5; ra < tfirst + AH; ra += NW) {
-        prefetch(ra);
+        if (!SV_WF_PF0 || ra != t0 - 5) prefetch(ra);
         commit(ra);
     }
     __syncthreads();
