@@ -1260,6 +1260,7 @@ int sv_villain_create(sv_ctx *ctx, int32_t N, sv_villain **out) {
 int sv_villain_destroy(sv_villain *st) {
     if (!st) return 0;
     (void)hipSetDevice(st->ctx->device);
+    (void)hipStreamSynchronize(st->ctx->stream);  // (no queued work may still use the buffers)
     for (int i = 0; i < 2; i++) {
         (void)hipFree(st->phi[i]);
         (void)hipFree(st->n[i]);

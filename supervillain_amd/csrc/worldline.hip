@@ -814,6 +814,7 @@ int sv_worldline_create(sv_ctx *ctx, int32_t N, int32_t v_is_float, sv_worldline
 int sv_worldline_destroy(sv_worldline *st) {
     if (!st) return 0;
     (void)hipSetDevice(st->ctx->device);
+    (void)hipStreamSynchronize(st->ctx->stream);  // (as the other destroys: no queued work may still use the buffers)
     (void)hipFree(st->m);
     (void)hipFree(st->v);
     (void)hipFree(st->snap_m);
