@@ -3,6 +3,7 @@
 There is no CPU fallback: if the library or a HIP device is missing, every generator step raises.
 """
 import ctypes
+import logging
 import os
 import threading
 
@@ -154,12 +155,22 @@ class Context:
     def end_deferred(self):
         """One synchronization lands every deferred statistic; then the folds run in call order."""
         folds, self.folds = self.folds, None
+        err = None
         try:
             self.check(lib().sv_ctx_set_deferred(self.handle, 0), 'sv_ctx_set_deferred')
-        finally:
-            # the statistics landed even when a member aborted: fold them, so that the counters match the device
+        except NativeError as e:
+            err = e
+        # the statistics landed even when a member aborted: fold them, so that the counters match the device.  The
+        # deferred-run error stays the one raised; a fold that fails after it is chained to it, not raised instead.
+        try:
             for f in folds or ():
                 f()
+        except Exception as fold_error:
+            if err is not None:
+                raise err from fold_error
+            raise
+        if err is not None:
+            raise err
 
     def fold_later(self, fold):
         """Run a counter fold that reads sv_stats now, or at end_deferred inside a deferred step."""
@@ -185,6 +196,22 @@ class Context:
                 _LIB.sv_ctx_destroy(self.handle)
         except Exception:
             pass
+
+
+def destroy(fn, handle, what, ctx=None, in_del=False):
+    """Run an sv_*_destroy.  A destroy first drains the work queued on the context stream; when that work failed
+    the library records which object's destroy saw it (sv_last_error) and returns -2 after freeing everything.  An
+    explicit close raises it as NativeError; a destroy from __del__ (garbage collection) logs it, since it cannot
+    raise -- so a fault is named at the object whose queued work failed, not at the next unrelated call."""
+    rc = fn(handle)
+    if rc == 0:
+        return
+    msg = lib().sv_last_error(ctx.handle) if ctx is not None and ctx.handle else None
+    text = f'{what} failed: {msg.decode() if msg else rc}'
+    if in_del:
+        logging.getLogger('supervillain_amd').error(text)
+    else:
+        raise NativeError(text)
 
 
 def context(device=None):

@@ -3,19 +3,58 @@
 
 #include "common.h"
 
+static bool alloc_log() {
+    static const bool on = getenv("SV_ALLOC_LOG") != nullptr;
+    return on;
+}
+
+hipError_t sv_log_malloc(void **p, size_t bytes, const char *site) {
+    const hipError_t e = (hipMalloc)(p, bytes);
+    if (alloc_log()) fprintf(stderr, "[sv alloc] malloc %p +%zu %s rc=%d\n", *p, bytes, site, (int)e);
+    return e;
+}
+
+hipError_t sv_log_free(void *p, const char *site) {
+    if (alloc_log() && p) fprintf(stderr, "[sv alloc] free %p %s\n", p, site);
+    return (hipFree)(p);
+}
+
+hipError_t sv_log_host_malloc(void **p, size_t bytes, unsigned flags, const char *site) {
+    const hipError_t e = (hipHostMalloc)(p, bytes, flags);
+    if (alloc_log()) fprintf(stderr, "[sv alloc] hostmalloc %p +%zu %s rc=%d\n", *p, bytes, site, (int)e);
+    return e;
+}
+
+hipError_t sv_log_host_free(void *p, const char *site) {
+    if (alloc_log() && p) fprintf(stderr, "[sv alloc] hostfree %p %s\n", p, site);
+    return (hipHostFree)(p);
+}
+
 const sv::JumpTables *sv_ctx::jump_tables(uint64_t inc_hi, uint64_t inc_lo) {
     auto key = std::make_pair(inc_hi, inc_lo);
     auto it = tables.find(key);
     if (it != tables.end()) return it->second;
+    if (tables.size() >= MAX_TABLES) {
+        // a long-lived context seeing many generators drops its cache.  Launches already enqueued on ANY stream of
+        // the device (the context stream, deferred pipeline members, a domain's scan stream, emission copies) may
+        // hold one of these tables, so the whole device drains first -- explicitly, not through hipFree's own
+        // implicit synchronization -- and a failure there is reported, not swallowed.  No caller keeps a table
+        // pointer across calls: every entry point fetches its table on entry.
+        SV_HIP(hipDeviceSynchronize());
+        for (auto &kv : tables) SV_HIP(hipFree(kv.second));
+        tables.clear();
+        table_purges++;
+    }
     sv::JumpTables *h = new sv::JumpTables(sv::make_tables(sv::u128{inc_lo, inc_hi}));
     sv::JumpTables *d = nullptr;
-    SV_HIP(hipMalloc(&d, sizeof(sv::JumpTables)));
-    SV_HIP(hipMemcpy(d, h, sizeof(sv::JumpTables), hipMemcpyHostToDevice));
-    delete h;
-    if (tables.size() > 64) {  // a long-lived context seeing many generators: drop the cache
-        for (auto &kv : tables) (void)hipFree(kv.second);
-        tables.clear();
+    try {
+        SV_HIP(hipMalloc(&d, sizeof(sv::JumpTables)));
+        SV_HIP(hipMemcpy(d, h, sizeof(sv::JumpTables), hipMemcpyHostToDevice));
+    } catch (...) {
+        delete h;
+        throw;
     }
+    delete h;
     tables[key] = d;
     return d;
 }
@@ -149,10 +188,10 @@ void sv::Emitter::wait() {
     busy[0] = busy[1] = false;
 }
 
-void sv::Emitter::release() {
-    if (!copy) return;
+hipError_t sv::Emitter::release() {
+    if (!copy) return hipSuccess;
     (void)hipSetDevice(device);
-    (void)hipStreamSynchronize(copy);
+    const hipError_t e = hipStreamSynchronize(copy);
     for (int i = 0; i < 2; i++) {
         for (int f = 0; f < 2; f++)
             if (buf[i][f]) (void)hipFree(buf[i][f]);
@@ -161,6 +200,7 @@ void sv::Emitter::release() {
     }
     (void)hipStreamDestroy(copy);
     *this = Emitter();
+    return e;
 }
 
 static hipEvent_t take_event(std::vector<hipEvent_t> &pool) {
@@ -471,7 +511,6 @@ int sv_ctx_create(int device, sv_ctx **out) {
         ctx->h_prog = ctx->h_flag + 1;
         ctx->d_prog = ctx->d_flag + 1;
         ctx->h_flag[0] = ctx->h_flag[1] = 0;
-        for (auto &e : ctx->ev_chunk) SV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         ctx->ensure_blocks(64);
         ctx->ensure_skips(64);
         ctx->ensure_stats(64);
@@ -488,7 +527,7 @@ int sv_ctx_create(int device, sv_ctx **out) {
 int sv_ctx_destroy(sv_ctx *ctx) {
     if (!ctx) return 0;
     (void)hipSetDevice(ctx->device);
-    (void)hipStreamSynchronize(ctx->stream);
+    const hipError_t e = hipDeviceSynchronize();  // every stream: no queued launch may still hold a table or scratch
     for (auto &kv : ctx->tables) (void)hipFree(kv.second);
     for (auto &p : ctx->ev_pending) {
         (void)hipEventDestroy(p.first);
@@ -502,8 +541,6 @@ int sv_ctx_destroy(sv_ctx *ctx) {
         if (h) (void)hipHostFree(h);
     for (hipEvent_t e : ctx->ev_plan)
         if (e) (void)hipEventDestroy(e);
-    for (auto &e : ctx->ev_chunk)
-        if (e) (void)hipEventDestroy(e);
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
     if (ctx->h_tail) (void)hipHostFree(ctx->h_tail);
     if (ctx->h_stage_abort) (void)hipHostFree(ctx->h_stage_abort);
@@ -514,7 +551,7 @@ int sv_ctx_destroy(sv_ctx *ctx) {
     sv::worm_release(ctx);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
-    return 0;
+    return e == hipSuccess ? 0 : -2;  // (the context is gone: the caller learns only that its last work failed)
 }
 
 const char *sv_last_error(sv_ctx *ctx) { return ctx ? ctx->err.c_str() : "no context"; }

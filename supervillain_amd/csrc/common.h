@@ -12,6 +12,22 @@
 #include "pcg64.h"
 #include "supervillain_amd.h"
 
+// Allocation log (diagnostics): with SV_ALLOC_LOG set, every device / pinned allocation and free the library makes
+// is written to stderr with its address range and call site, so that the faulting virtual address a GPU memory fault
+// reports (AMD_LOG_LEVEL=1) can be matched to the buffer -- live or already freed -- it belongs to.  Off: one
+// cached flag test per call.
+#define SV_HIDDEN __attribute__((visibility("hidden")))
+SV_HIDDEN hipError_t sv_log_malloc(void **p, size_t bytes, const char *site);
+SV_HIDDEN hipError_t sv_log_free(void *p, const char *site);
+SV_HIDDEN hipError_t sv_log_host_malloc(void **p, size_t bytes, unsigned flags, const char *site);
+SV_HIDDEN hipError_t sv_log_host_free(void *p, const char *site);
+#define SV_STR2(x) #x
+#define SV_STR(x) SV_STR2(x)
+#define hipMalloc(p, n) sv_log_malloc((void **)(p), (n), __FILE__ ":" SV_STR(__LINE__))
+#define hipFree(p) sv_log_free((void *)(p), __FILE__ ":" SV_STR(__LINE__))
+#define hipHostMalloc(p, n, f) sv_log_host_malloc((void **)(p), (n), (f), __FILE__ ":" SV_STR(__LINE__))
+#define hipHostFree(p) sv_log_host_free((void *)(p), __FILE__ ":" SV_STR(__LINE__))
+
 namespace sv {
 
 // ----------------------------------------------------------------------------------------------
@@ -82,7 +98,7 @@ struct Emitter {
     // copy fields (a: bytes0, b: bytes1, either may be null) of the state to the host arrays ha, hb
     void emit(hipStream_t compute, const void *a, size_t bytes0, const void *b, size_t bytes1, void *ha, void *hb);
     void wait();     // every emission has reached the host
-    void release();  // frees the buffers (after wait)
+    hipError_t release();  // drains the copy stream, frees the buffers; the drain's result
 };
 
 }  // namespace sv
@@ -93,7 +109,9 @@ struct sv_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
-    std::map<std::pair<uint64_t, uint64_t>, sv::JumpTables *> tables;  // per PCG64 increment (device)
+    std::map<std::pair<uint64_t, uint64_t>, sv::JumpTables *> tables;  // per PCG64 increment (device, 40 KB each)
+    static constexpr size_t MAX_TABLES = 1024;                         // 40 MB of HBM before the cache is dropped
+    int64_t table_purges = 0;
     // scratch
     int32_t *d_abort = nullptr;
     uint32_t *d_nreport = nullptr;
@@ -110,7 +128,6 @@ struct sv_ctx {
     // kernel's rejection report so that the host can stop enqueueing a batch that has failed (run_fused)
     int32_t *h_flag = nullptr, *d_flag = nullptr;
     int32_t *h_prog = nullptr, *d_prog = nullptr;  // the next word: batch launches started (FArgs::progress)
-    hipEvent_t ev_chunk[2] = {nullptr, nullptr};
     // pinned batch tail (abort flag, report count, statistics) of the single-lattice Villain run: one sync
     char *h_tail = nullptr;
     size_t tail_cap = 0;
@@ -232,6 +249,23 @@ struct sv_worldline {
         if (e_ != hipSuccess)                                                                          \
             throw std::runtime_error(std::string(#call) + " failed: " + hipGetErrorString(e_));       \
     } while (0)
+
+// The drain at the start of every sv_*_destroy: the work queued on the context stream (and on `side`, an object's
+// own stream) ends before anything is freed.  A failure there is the failure of work queued earlier -- by this
+// object or by a call before it -- so it is recorded in the context's error (sv_last_error) with the object's name
+// instead of being discarded, and the destroy still frees everything and returns -2 (the Python wrappers warn).
+inline int sv_destroy_drain(sv_ctx *ctx, const char *what, hipStream_t side = nullptr) {
+    if (!ctx) return 0;
+    (void)hipSetDevice(ctx->device);
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (side) {
+        const hipError_t e2 = hipStreamSynchronize(side);
+        if (e == hipSuccess) e = e2;
+    }
+    if (e == hipSuccess) return 0;
+    ctx->err = std::string(what) + ": work queued before it was destroyed failed: " + hipGetErrorString(e);
+    return -2;
+}
 
 namespace sv {
 // colour lists for D=2 (compact.py:191-239); returns ncol, fills site lists in row-major order

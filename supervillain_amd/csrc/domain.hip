@@ -1095,10 +1095,9 @@ int sv_domain_create_worldline(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tile
 
 int sv_domain_destroy(sv_domain *d) {
     if (!d) return 0;
-    if (d->ctx) {
-        (void)hipSetDevice(d->ctx->device);
-        (void)hipStreamSynchronize(d->ctx->stream);
-    }
+    // both streams drain BEFORE anything is freed: a rejection scan running behind the last batch on scan_stream
+    // writes its tile's Summary (T.sum) and reads d_scan
+    const int rc = sv_destroy_drain(d->ctx, "sv_domain_destroy", d->scan_stream);
     for (auto &T : d->tiles) {
         for (auto p : T.phi) (void)hipFree(p);
         for (auto p : T.n) (void)hipFree(p);
@@ -1110,14 +1109,11 @@ int sv_domain_destroy(sv_domain *d) {
     if (d->comm) (void)ncclCommDestroy(d->comm);
     (void)hipFree(d->gathered);
     (void)hipFree(d->d_scan);
-    if (d->scan_stream) {
-        (void)hipStreamSynchronize(d->scan_stream);
-        (void)hipStreamDestroy(d->scan_stream);
-    }
+    if (d->scan_stream) (void)hipStreamDestroy(d->scan_stream);
     if (d->ev_sum) (void)hipEventDestroy(d->ev_sum);
     if (d->ev_scan) (void)hipEventDestroy(d->ev_scan);
     delete d;
-    return 0;
+    return rc;
 }
 
 int sv_domain_upload(sv_domain *d, const double *phi, const int64_t *n) {

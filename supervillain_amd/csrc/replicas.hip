@@ -297,7 +297,7 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         const int CH = CH_env > 0 ? CH_env : count;
         *ctx->h_flag = 0;
         __atomic_store_n(ctx->h_prog, 0, __ATOMIC_RELEASE);  // (the previous batch has finished)
-        int launched = count;
+        int64_t launches = 0;  // kernel launches enqueued (a split sweep makes two): the timing's per-launch average
         SV_HIP(hipMemsetAsync(b->d_gate, 0x7f, sizeof(int32_t), ctx->stream));  // no report yet (0x7f7f7f7f)
         hipEvent_t ev;
         ctx->time_begin(&ev);
@@ -330,6 +330,7 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
             if (hot_k[k]) {
                 launch_hot_fr(A, R * tiles, obs != nullptr, ctx->stream);
                 ctx->sweeps_hot++;
+                launches++;
             } else if (split[k][3] > 0) {
                 FArgs Ah = A, Ag = A;
                 Ah.rep_map = b->d_map + split[k][0];
@@ -343,9 +344,11 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
                 launch_fused_batch(Ag, (int)split[k][3] * Ag.tiles_per_rep, obs != nullptr, ctx->stream);
                 ctx->sweeps_hot += split[k][1] > 0;
                 ctx->sweeps_fused++;
+                launches += 1 + (split[k][1] > 0);
             } else {
                 launch_fused_batch(A, R * tiles, obs != nullptr, ctx->stream);
                 ctx->sweeps_fused++;
+                launches++;
             }
             b->cur ^= 1;
             if ((k + 1) % CH == 0 && k + 1 < count && k + 1 >= 2 * CH) {
@@ -360,13 +363,10 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
                         break;  // (drained: e.g. a sweep with no launch that stores its progress)
                     std::this_thread::yield();
                 }
-                if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE)) {
-                    launched = k + 1;  // the rest of the batch is not enqueued
-                    break;
-                }
+                if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE)) break;  // the rest of the batch is not enqueued
             }
         }
-        ctx->time_end(ev, launched);
+        ctx->time_end(ev, launches);
         SV_HIP(hipGetLastError());
         // outcome: abort flag, report count, statistics and observables land in the pinned slot
         char *tail = b->h_tail + slot * slot_bytes;
@@ -640,10 +640,7 @@ int sv_replicas_create(sv_ctx *ctx, int32_t R, int32_t N, sv_replicas **out) {
 
 int sv_replicas_destroy(sv_replicas *b) {
     if (!b) return 0;
-    if (b->ctx) {
-        (void)hipSetDevice(b->ctx->device);
-        (void)hipStreamSynchronize(b->ctx->stream);
-    }
+    const int rc = sv_destroy_drain(b->ctx, "sv_replicas_destroy");
     for (int i = 0; i < 2; i++) {
         (void)hipFree(b->phi[i]);
         (void)hipFree(b->n[i]);
@@ -659,7 +656,7 @@ int sv_replicas_destroy(sv_replicas *b) {
     if (b->h_tail) (void)hipHostFree(b->h_tail);
     if (b->d_map) (void)hipFree(b->d_map);
     delete b;
-    return 0;
+    return rc;
 }
 
 int sv_replicas_upload(sv_replicas *b, const double *phi, const int64_t *n) {

@@ -885,7 +885,8 @@ void run_generic(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, 
 // workgroup slots is partly empty while its strips finish (the WG timeline of an L=4096 sweep, r3: slots ~80% busy,
 // a ~45 us tail of 240 us).  The lattice rows are cut into 8 bands, one per XCD (workgroup i runs on XCD i mod 8,
 // and hot_body's logical order gives each XCD a contiguous range), and each band into segments whose heights (a
-// descending list, e.g. "56x5,40x5,32") put the tall strips first and the short ones in the last rounds.  Returns
+// descending list, e.g. "57x5,41x5,22": heights of 4k+1 rows) put the tall strips first and the short ones in the
+// last rounds (band_strips builds the default; SV_STRIPS passes a list here).  Returns
 // the table {ix, t0, t1} per logical strip, or an empty vector when the spec does not apply (then uniform TH).
 std::vector<int32_t> strip_schedule(int32_t Nt, int nsx, const std::string &spec) {
     std::vector<int32_t> hs;
@@ -988,9 +989,9 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     const bool dbg = getenv("SV_DEBUG_TIMING") != nullptr;
     const bool use_hot = hot_enabled() && V < (int64_t(1) << 28);  // villain_sweep_hot's 32-bit row offsets
     // the hot kernel's strip schedule (SV_STRIPS overrides: "uniform" or "" = strips of TH rows).  Default on
-    // lattices of >= 4096 rows: per XCD band, ~55% of the rows in 56-row strips, then 40-row strips, then the rest
-    // (L=4096: "56x5,40x5,32"), so the last rounds of slots run shorter strips (r3 A/B, 6 interleaved repetitions
-    // of 300 sweeps: 230.6 -> 225.5 us per sweep; "52x7,40x3,28" 225.0)
+    // lattices of >= 4096 rows: band_strips -- per XCD band, 57-row strips, then 41-row strips, then the rest (L=4096:
+    // "57x5,41x5,22", heights 4k+1 so the last row step of a strip is full), so the last rounds of slots run shorter
+    // strips (r3 A/B, 6 interleaved repetitions of 300 sweeps: uniform 230.6 -> 225.5 us per sweep)
     {
         const char *e = getenv("SV_STRIPS");
         const bool dflt = !e && N >= 4096;
@@ -1259,8 +1260,7 @@ int sv_villain_create(sv_ctx *ctx, int32_t N, sv_villain **out) {
 
 int sv_villain_destroy(sv_villain *st) {
     if (!st) return 0;
-    (void)hipSetDevice(st->ctx->device);
-    (void)hipStreamSynchronize(st->ctx->stream);  // (no queued work may still use the buffers)
+    int rc = sv_destroy_drain(st->ctx, "sv_villain_destroy");  // (no queued work may still use the buffers)
     for (int i = 0; i < 2; i++) {
         (void)hipFree(st->phi[i]);
         (void)hipFree(st->n[i]);
@@ -1274,9 +1274,13 @@ int sv_villain_destroy(sv_villain *st) {
     if (st->d_obs) (void)hipFree(st->d_obs);
     if (st->d_strips) (void)hipFree(st->d_strips);
     if (st->h_obs) (void)hipHostFree(st->h_obs);
-    st->emitter.release();
+    const hipError_t ee = st->emitter.release();
+    if (ee != hipSuccess && !rc) {
+        st->ctx->err = std::string("sv_villain_destroy: an emission copy failed: ") + hipGetErrorString(ee);
+        rc = -2;
+    }
     delete st;
-    return 0;
+    return rc;
 }
 
 int sv_villain_upload(sv_villain *st, const double *phi, const int64_t *n) {

@@ -813,8 +813,7 @@ int sv_worldline_create(sv_ctx *ctx, int32_t N, int32_t v_is_float, sv_worldline
 
 int sv_worldline_destroy(sv_worldline *st) {
     if (!st) return 0;
-    (void)hipSetDevice(st->ctx->device);
-    (void)hipStreamSynchronize(st->ctx->stream);  // (as the other destroys: no queued work may still use the buffers)
+    int rc = sv_destroy_drain(st->ctx, "sv_worldline_destroy");  // (no queued work may still use the buffers)
     (void)hipFree(st->m);
     (void)hipFree(st->v);
     (void)hipFree(st->snap_m);
@@ -830,9 +829,13 @@ int sv_worldline_destroy(sv_worldline *st) {
     if (st->lev) (void)hipFree(st->lev);
     if (st->ord64) (void)hipFree(st->ord64);
     if (st->lcnt) (void)hipFree(st->lcnt);
-    st->emitter.release();
+    const hipError_t ee = st->emitter.release();
+    if (ee != hipSuccess && !rc) {
+        st->ctx->err = std::string("sv_worldline_destroy: an emission copy failed: ") + hipGetErrorString(ee);
+        rc = -2;
+    }
     delete st;
-    return 0;
+    return rc;
 }
 
 int sv_worldline_upload(sv_worldline *st, const int64_t *m, const void *v) {

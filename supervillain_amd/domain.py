@@ -115,12 +115,14 @@ class VillainDomain:
         dist.broadcast_object_list(box, src=0, group=group)
         return cls(Nt, Nx, tiles, nranks=world, rank=rank, unique_id=box[0], **kw)
 
-    def close(self):
+    def close(self, _in_del=False):
         if getattr(self, 'handle', None) is not None and _native._LIB is not None:
-            _native._LIB.sv_domain_destroy(self.handle)
-            self.handle = None
+            h, self.handle = self.handle, None
+            _native.destroy(_native._LIB.sv_domain_destroy, h, 'sv_domain_destroy (' + type(self).__name__ + ')',
+                            self.ctx, _in_del)
 
-    __del__ = close
+    def __del__(self):
+        self.close(_in_del=True)
 
     def cold(self):
         self.ctx.check(_native.lib().sv_domain_upload(self.handle, None, None), 'sv_domain_upload')

@@ -79,10 +79,9 @@ class NeighborhoodUpdate(DeviceState, Generator):
     def __del__(self):
         dev = self.__dict__.get('_dev')
         if dev is not None and _native._LIB is not None:
-            try:
-                _native._LIB.sv_villain_destroy(dev[2])
-            except Exception:
-                pass
+            self._dev = None
+            _native.destroy(_native._LIB.sv_villain_destroy, dev[2], 'sv_villain_destroy (' + type(self).__name__ + ')',
+                            dev[0], in_del=True)
 
     DEVICE_KIND = 'villain'
 
@@ -230,10 +229,9 @@ class _VillainLocal(DeviceState, Generator):
     def __del__(self):
         dev = self.__dict__.get('_dev')
         if dev is not None and _native._LIB is not None:
-            try:
-                _native._LIB.sv_villain_destroy(dev[2])
-            except Exception:
-                pass
+            self._dev = None
+            _native.destroy(_native._LIB.sv_villain_destroy, dev[2], 'sv_villain_destroy (' + type(self).__name__ + ')',
+                            dev[0], in_del=True)
 
     def _proposals(self):
         return self.Lattice.sites

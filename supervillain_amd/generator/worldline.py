@@ -39,10 +39,8 @@ class _WorldlineDevice(DeviceState):
     def __del__(self):
         dev = self.__dict__.get('_dev')
         if dev is not None and _native._LIB is not None:
-            try:
-                _native._LIB.sv_worldline_destroy(dev[2])
-            except Exception:
-                pass
+            self._dev = None
+            _native.destroy(_native._LIB.sv_worldline_destroy, dev[2], 'sv_worldline_destroy (' + type(self).__name__ + ')', dev[0], in_del=True)
 
     def _fields(self, cfg):
         N = self.Action.Lattice.N

@@ -91,12 +91,14 @@ class DeviceChain:
             self.names = ('m', 'v')
         self.handle = h
 
-    def close(self):
+    def close(self, _in_del=False):
         if getattr(self, 'handle', None) is not None and _native._LIB is not None:
-            (_native._LIB.sv_villain_destroy if self.kind == 'villain' else _native._LIB.sv_worldline_destroy)(self.handle)
-            self.handle = None
+            h, self.handle = self.handle, None
+            fn = _native._LIB.sv_villain_destroy if self.kind == 'villain' else _native._LIB.sv_worldline_destroy
+            _native.destroy(fn, h, f'{fn.__name__} (DeviceChain)', self.ctx, _in_del)
 
-    __del__ = close
+    def __del__(self):
+        self.close(_in_del=True)
 
     def upload(self, cfg):
         x, y = self.names

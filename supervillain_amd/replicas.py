@@ -35,12 +35,13 @@ class VillainReplicas:
                        'sv_replicas_create')
         self.handle = h
 
-    def close(self):
+    def close(self, _in_del=False):
         if getattr(self, 'handle', None) is not None and _native._LIB is not None:
-            _native._LIB.sv_replicas_destroy(self.handle)
-            self.handle = None
+            h, self.handle = self.handle, None
+            _native.destroy(_native._LIB.sv_replicas_destroy, h, 'sv_replicas_destroy', self.ctx, _in_del)
 
-    __del__ = close
+    def __del__(self):
+        self.close(_in_del=True)
 
     def cold(self):
         self.ctx.check(_native.lib().sv_replicas_upload(self.handle, None, None), 'sv_replicas_upload')
