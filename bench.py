@@ -415,8 +415,12 @@ def run_worldline(args, world, rank, dist):
     Weff = float(args.W)
 
     reference = args.plaquette == 'reference'
-    legacy = np.random.RandomState(rank + 1)  # the reference's global-RandomState permutation (plaquette.py:63)
-    host_s = [0.0, 0.0]  # reference order: seconds in the NumPy permutation, and in the ordered-run call
+    # the reference's global-RandomState permutation (plaquette.py:63): a legacy MT19937 state, drawn natively
+    from supervillain_amd._abi import SvMT19937
+    legacy_key = np.random.RandomState(rank + 1).get_state()
+    mt = SvMT19937()
+    ctypes.memmove(mt.key, np.ascontiguousarray(legacy_key[1], dtype=np.uint32).ctypes.data, 624 * 4)
+    mt.pos = int(legacy_key[2])
 
     def step(k):
         if not reference:
@@ -424,30 +428,19 @@ def run_worldline(args, world, rank, dist):
             ctx.check(Lib.sv_worldline_plaquette_coexact_run(h, args.kappa, Weff, 1, k, ctypes.byref(r), st),
                       'sv_worldline_plaquette_coexact_run')
             return sum(st[2 * i].accepted for i in range(k))  # Plaquette acceptances
-        # the bit-exact reference order: the caller draws the visit order as plaquette.py:63 does (a permutation
-        # of the row-major coordinates is the permutation of the linear indices, same draws), then the
-        # level-scheduled ordered sweep and one Coexact sweep, both on the PCG64 stream
-        st = _native.stats_array(1)
-        st2 = _native.stats_array(1)
-        acc = 0
-        for _ in range(k):
-            t0 = time.perf_counter()
-            order = legacy.permutation(L * L).astype(np.int64)
-            t1 = time.perf_counter()
-            ctx.check(Lib.sv_worldline_plaquette_ordered_run(h, args.kappa, Weff, _native.ptr(order), ctypes.byref(r),
-                                                             st), 'sv_worldline_plaquette_ordered_run')
-            ctx.check(Lib.sv_worldline_coexact_run(h, args.kappa, Weff, 1, 1, ctypes.byref(r), st2),
-                      'sv_worldline_coexact_run')
-            host_s[0] += t1 - t0
-            host_s[1] += time.perf_counter() - t1
-            acc += st[0].accepted
-        return acc
+        # the bit-exact reference order: Sequentially(PlaquetteUpdate in the visit order plaquette.py:63 draws from
+        # the legacy global RandomState, CoexactUpdate) x k in one call; the library draws each step's permutation
+        # natively from the MT19937 state (sv_mt19937_permutation), pipelined with the device's sweeps
+        st = _native.stats_array(2 * k)
+        ctx.check(Lib.sv_worldline_plaquette_reference_coexact_run(h, args.kappa, Weff, 1, k, ctypes.byref(mt),
+                                                                   ctypes.byref(r), st),
+                  'sv_worldline_plaquette_reference_coexact_run')
+        return sum(st[2 * i].accepted for i in range(k))
 
     warm_up(step, args, dist)
     Lib.sv_ctx_set_timing(ctx.handle, 1)
     if dist:
         dist.barrier()
-    host_s[:] = [0.0, 0.0]
     t0 = time.perf_counter()
     acc = step(args.steps)
     t1 = time.perf_counter()
@@ -484,10 +477,10 @@ def run_worldline(args, world, rank, dist):
                                   'permutation, plaquette.py:35-104, bit-exact) + CoexactUpdate sweep per step, '
                                   f'W={args.W}, kappa={args.kappa}, PCG64 replay; level-scheduled launches',
                       'L': L, 'path': 'worldline-reference-order', 'parallelism': 'single GPU',
-                      'host_permutation_ms_per_step': host_s[0] / args.steps * 1e3,
-                      'ordered_run_plus_coexact_ms_per_step': host_s[1] / args.steps * 1e3}
-            # no single dominant kernel: the roofline line prices the whole device step (both sweeps, 168 B)
-            step_kernel_s = host_s[1] / args.steps
+                      'visit_order': 'native MT19937 permutation (sv_mt19937_permutation), drawn on host threads while '
+                                     'the device runs the previous steps'}
+            # no single dominant kernel: the roofline line prices the whole step (both sweeps, 168 B) by its wall time
+            step_kernel_s = elapsed / args.steps
         else:
             config = {'workload': f'L={L} Worldline: checkerboard PlaquetteUpdate + CoexactUpdate sweep per step, '
                                   f'W={args.W}, kappa={args.kappa}, bit-exact PCG64 replay (one worldline_step_fused '

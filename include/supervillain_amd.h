@@ -176,6 +176,26 @@ int sv_worldline_coexact(sv_ctx *ctx, int32_t N, double kappa, double W_eff, int
  * permutation the reference draws from NumPy's global RandomState (plaquette.py:63).  One sweep. */
 int sv_worldline_plaquette_ordered_run(sv_worldline *st, double kappa, double W_eff, const int64_t *order,
                                        sv_rng *rng, sv_stats *stats);
+/* NumPy's legacy global RandomState (MT19937) as np.random.get_state() reports it: the 624-word key and the
+ * position of the next word (0..624).  has_gauss / gauss are untouched by permutations (the caller keeps them). */
+typedef struct {
+    uint32_t key[624];
+    int32_t pos;
+} sv_mt19937;
+/* np.random.permutation(n) of that state (numpy/random/mtrand.pyx permutation -> shuffle -> _shuffle_raw with
+ * distributions.c random_interval), advancing *mt exactly as NumPy does; the image of plaquette.py:63's
+ * np.random.permutation(L.coordinates) in row-major site indices.  Host only (no device work). */
+int sv_mt19937_permutation(sv_mt19937 *mt, int64_t n, int64_t *out);
+/* `sweeps` reference-order PlaquetteUpdate sweeps (plaquette.py:35-104), each in the visit order NumPy's legacy
+ * global RandomState draws (plaquette.py:63), drawn natively from *mt (advanced as NumPy would) -- the next sweep's
+ * permutation on a host thread while the device runs the current one; stats has `sweeps` entries. */
+int sv_worldline_plaquette_reference_run(sv_worldline *st, double kappa, double W_eff, int32_t sweeps, sv_mt19937 *mt,
+                                         sv_rng *rng, sv_stats *stats);
+/* Sequentially(PlaquetteUpdate [reference order], CoexactUpdate) (combining.py:38-40) for `steps` steps, both
+ * generators on one Generator (G1.rng is G2.rng), the visit orders from *mt as above; stats[2 s] the Plaquette sweep
+ * of step s, stats[2 s + 1] its Coexact sweep (interval_t: coexact.py:32). */
+int sv_worldline_plaquette_reference_coexact_run(sv_worldline *st, double kappa, double W_eff, int64_t interval_t,
+                                                 int32_t steps, sv_mt19937 *mt, sv_rng *rng, sv_stats *stats);
 /* Checkerboard variant (a different, equally valid chain): colour passes instead of the
  * random sequential order.  `sweeps` consecutive sweeps. */
 int sv_worldline_plaquette_checkerboard_run(sv_worldline *st, double kappa, double W_eff, int32_t sweeps, sv_rng *rng,

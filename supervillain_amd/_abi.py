@@ -7,6 +7,8 @@ NumPy's bounded-integer sampler keeps in the bit generator (``has_uint32``/``uin
 """
 import ctypes
 
+import numpy as np
+
 _M64 = (1 << 64) - 1
 
 
@@ -33,6 +35,29 @@ class SvStats(ctypes.Structure):
         ('acceptance_sum', ctypes.c_double),
         ('rejections', ctypes.c_int64),
     ]
+
+
+class SvMT19937(ctypes.Structure):
+    """sv_mt19937: NumPy's legacy global RandomState (MT19937) key and position (include/supervillain_amd.h)."""
+    _fields_ = [('key', ctypes.c_uint32 * 624), ('pos', ctypes.c_int32)]
+
+
+def legacy_state_get():
+    """The legacy global RandomState (np.random.seed / np.random.permutation) as an SvMT19937, plus the parts of
+    np.random.get_state() a permutation does not touch (has_gauss, cached_gaussian)."""
+    name, key, pos, has_gauss, gauss = np.random.get_state(legacy=True)
+    if name != 'MT19937':
+        raise ValueError(f'unexpected legacy bit generator {name}')
+    mt = SvMT19937()
+    ctypes.memmove(mt.key, np.ascontiguousarray(key, dtype=np.uint32).ctypes.data, 624 * 4)
+    mt.pos = int(pos)
+    return mt, (has_gauss, gauss)
+
+
+def legacy_state_set(mt, rest):
+    """Write an SvMT19937 back into NumPy's legacy global RandomState."""
+    key = np.frombuffer(bytes(mt.key), dtype=np.uint32).copy()
+    np.random.set_state(('MT19937', key, int(mt.pos), rest[0], rest[1]))
 
 
 class _PCG64State(ctypes.Structure):

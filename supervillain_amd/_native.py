@@ -7,7 +7,7 @@ import logging
 import os
 import threading
 
-from supervillain_amd._abi import SvPhilox, SvRng, SvStats
+from supervillain_amd._abi import SvMT19937, SvPhilox, SvRng, SvStats
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('SV_LIB_OVERRIDE') or os.path.join(_HERE, 'libsvhip.so')  # override: timing experiments
@@ -73,6 +73,10 @@ def lib():
         L.sv_worldline_coexact_run.argtypes = [vp, f64, f64, i64, i32, P(SvRng), P(SvStats)]
         L.sv_worldline_coexact.argtypes = [vp, i32, f64, f64, i64, vp, vp, i32, i32, P(SvRng), P(SvStats)]
         L.sv_worldline_plaquette_ordered_run.argtypes = [vp, f64, f64, vp, P(SvRng), P(SvStats)]
+        L.sv_mt19937_permutation.argtypes = [P(SvMT19937), i64, vp]
+        L.sv_worldline_plaquette_reference_run.argtypes = [vp, f64, f64, i32, P(SvMT19937), P(SvRng), P(SvStats)]
+        L.sv_worldline_plaquette_reference_coexact_run.argtypes = [vp, f64, f64, i64, i32, P(SvMT19937), P(SvRng),
+                                                                   P(SvStats)]
         L.sv_worldline_plaquette_checkerboard_run.argtypes = [vp, f64, f64, i32, P(SvRng), P(SvStats)]
         L.sv_worldline_plaquette.argtypes = [vp, i32, f64, f64, vp, vp, i32, vp, P(SvRng), P(SvStats)]
         L.sv_worldline_plaquette_coexact_run.argtypes = [vp, f64, f64, i64, i32, P(SvRng), P(SvStats)]
@@ -114,7 +118,8 @@ EXPORTED = ('sv_ctx_create', 'sv_ctx_destroy', 'sv_last_error', 'sv_device_count
             'sv_ctx_set_deferred', 'sv_ctx_sync',
             'sv_villain_site_run', 'sv_villain_link_run', 'sv_villain_exact_run', 'sv_villain_cohomology_run', 'sv_worldline_create',
             'sv_worldline_destroy', 'sv_worldline_upload', 'sv_worldline_download', 'sv_worldline_coexact_run',
-            'sv_worldline_coexact', 'sv_worldline_plaquette_ordered_run',
+            'sv_worldline_coexact', 'sv_worldline_plaquette_ordered_run', 'sv_mt19937_permutation',
+            'sv_worldline_plaquette_reference_run', 'sv_worldline_plaquette_reference_coexact_run',
             'sv_worldline_plaquette_checkerboard_run', 'sv_worldline_plaquette', 'sv_worldline_plaquette_coexact_run',
             'sv_worldline_vortex_run', 'sv_worldline_wrapping_run',
             'sv_domain_unique_id', 'sv_domain_create', 'sv_domain_destroy', 'sv_domain_upload', 'sv_domain_download',

@@ -227,6 +227,7 @@ struct sv_worldline {
     int32_t *lev = nullptr;      // sequential plaquette: dependency level of each plaquette
     int64_t *ord64 = nullptr;    // sequential plaquette: the caller's visit order, on the device
     int32_t *lcnt = nullptr;     // sequential plaquette: per-level counts / slots, then LFLAGS flags
+    uint32_t *h_perm[2] = {nullptr, nullptr};  // reference-order runs: pinned visit orders (the native permutations)
     void *stripes = nullptr;     // striped per-sweep statistics (worldline.hip StatStripe[64][16])
     sv::Emitter emitter;
     int32_t *sites = nullptr;
@@ -268,6 +269,10 @@ inline int sv_destroy_drain(sv_ctx *ctx, const char *what, hipStream_t side = nu
 }
 
 namespace sv {
+// mt19937.hip: np.random.permutation(n) of NumPy's legacy global RandomState as 32-bit indices, advancing (key, pos)
+void legacy_permutation32(uint32_t *key, int32_t &pos, int64_t n, uint32_t *out);
+void legacy_intervals(uint32_t *key, int32_t &pos, int64_t n, uint32_t *j);  // its two stages: the draws (serial)
+void shuffle_from_intervals(const uint32_t *j, int64_t n, uint32_t *out);    // and the swaps
 // colour lists for D=2 (compact.py:191-239); returns ncol, fills site lists in row-major order
 int build_colors(int32_t N, std::vector<int32_t> &sites, int64_t count[4], int64_t offset[4]);
 }  // namespace sv

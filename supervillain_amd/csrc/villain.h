@@ -126,6 +126,9 @@ void launch_fused_batch(const FArgs &A, int grid, bool obs, hipStream_t stream);
 // villain_hot.hip: whether the fast-draw kernel covers the sweep whose 11 descriptors start at `blocks`,
 // and its launch (periodic single lattice or a domain tile, from the geometry)
 bool hot_ok(const VParams &P, const Block *blocks);
+// the skip form (villain_sweep_hot_skip, 4 waves): sweeps with <= 4 known rejected positions per choice block
+bool hot_skip_ok(const VParams &P, const Block *blocks);
+void launch_hot_skip(const FArgs &A, int grid, hipStream_t stream);
 // villain_sweep_hot's default descending strip table for H rows and nsx column strips ({ix, t0, t1} per strip)
 std::vector<int32_t> band_strips(int32_t H, int nsx);
 void launch_hot(const FArgs &A, int grid, hipStream_t stream);

@@ -1030,21 +1030,25 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         hipEvent_t seg = nullptr;
         int seg_k0 = 0;
         const bool per_launch = ctx->timing_mode == 2;
-        // Large lattices enqueue a batch in chunks of CH sweeps and, after enqueueing chunk j, wait for chunk j-1 and
-        // read the host-mapped abort flag: a sweep that meets a NumPy Lemire rejection then leaves at most ~2 CH
-        // launches queued behind it (each an early exit over every workgroup, ~5 us at L=4096) instead of the rest of
-        // a 64-sweep batch.  The GPU always has a chunk queued (CH sweeps >> the host's enqueue time).
-        static const int CH_env = [] {  // SV_CHUNK overrides the chunk (0: the whole batch)
+        // A batch is enqueued whole: no host thread paces the GPU (round 3 enqueued large lattices in chunks of 4
+        // sweeps behind a host-mapped progress word, so that a NumPy Lemire rejection left at most ~8 early-exit
+        // launches queued; measured r4 on one box, driver form: 69.3-70.0 G either way, a window with a rejection
+        // +0.58 ms chunked vs +0.63 ms whole -- the ~5 us early exits of the queued launches -- and a host that is
+        // descheduled while pacing leaves the GPU idle).  SV_CHUNK = k > 0 restores chunks of k.
+        static const int CH_env = [] {
             const char *e = getenv("SV_CHUNK");
-            return e ? atoi(e) : -1;
+            return e ? atoi(e) : 0;
         }();
-        const int CH = CH_env > 0 ? CH_env : (CH_env == 0 || V < (int64_t(1) << 20) ? count : 4);
+        const int CH = CH_env > 0 ? CH_env : count;
         int launched = count;
         *ctx->h_flag = 0;
         __atomic_store_n(ctx->h_prog, 0, __ATOMIC_RELEASE);  // (the previous batch's launches have all finished)
         int next_chunk = CH;
         for (int k = 0; k < count;) {
             const bool hot_k = use_hot && !hot_off && NWv == 4 && hot_ok(P, &blocks[(size_t)k * nb]);
+            // a sweep with known rejections (a replay) or unequal buffered-half pairs: the hot kernel's skip form
+            const bool skip_k = !hot_k && use_hot && !hot_off && NWv == 4 && hot_nw == 4 &&
+                                hot_skip_ok(P, &blocks[(size_t)k * nb]);
             if (!hot_k && seg) {
                 ctx->time_end(seg, k - seg_k0, seg_k0);
                 seg = nullptr;
@@ -1084,6 +1088,10 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                 }
                 if (st->d_strips) A.strips = st->d_strips;
                 launch_hot(A, st->d_strips ? st->n_strips : grid, ctx->stream);
+                ctx->sweeps_hot++;
+            } else if (skip_k) {
+                if (st->d_strips) A.strips = st->d_strips;
+                launch_hot_skip(A, st->d_strips ? st->n_strips : grid, ctx->stream);
                 ctx->sweeps_hot++;
             } else {
                 ctx->sweeps_fused++;

@@ -79,9 +79,17 @@ __device__ __forceinline__ HotDraws hot_draws_paired(const FArgs &A, int32_t lan
 
 // Edge strips: columns that wrap around the row draw from the second base set (at global column xw); every
 // offset is < SMALL_LDS by construction; words unpaired (the wrap breaks the lane pairing).
+// has4 / buf: each choice block's buffered-half flag and word.  SKIP (a sweep that replays known NumPy Lemire
+// rejections): block j's draw d sits at stream position d + (the skips at or before it) -- skip_pos of the general
+// kernel, with at most HOT_MAXSK positions per block read from LDS -- so its word is a half-word further on, still a
+// small offset ahead of the row base (which sits at the unshifted position); spos returns the positions (reports).
+static constexpr int HOT_MAXSK = 4;
+template <bool SKIP = false>
 __device__ __forceinline__ HotDraws hot_draws_edge(const FArgs &A, int64_t gq, int32_t gx, int32_t xb, int32_t xw,
                                                    const u128 *bA, const u128 *bB, const SmallTab &sm,
-                                                   const uint32_t *has, const uint32_t *buf) {
+                                                   const uint32_t *has4, const uint32_t *buf,
+                                                   const uint32_t (*sk)[HOT_MAXSK] = nullptr, const int32_t *nsk = nullptr,
+                                                   uint32_t *spos = nullptr) {
     const int64_t N = A.G.Nx;
     const bool wr = !(gx >= xb && gx < xb + SMALL_LDS);
     const int32_t xr = wr ? xw : xb;
@@ -92,18 +100,37 @@ __device__ __forceinline__ HotDraws hot_draws_edge(const FArgs &A, int64_t gq, i
     HotDraws D;
     D.u = u53(xsl_rr(hot_apply(sm, (uint32_t)(gx - xr), bs[0])));
     D.dphi = A.P.lo_phi + A.P.range_phi * u53(xsl_rr(hot_apply(sm, (uint32_t)(rank - rb), bs[1])));
+    if constexpr (!SKIP) {
+        // equal flags within each fwd/bwd pair: one word offset per direction
 #pragma unroll
-    for (int mu = 0; mu < 2; mu++) {
-        const int64_t qq = rank - (int64_t)has[mu];
-        const int64_t w0 = (rb - (int64_t)has[mu]) < 0 ? 0 : ((rb - (int64_t)has[mu]) >> 1);
-        const uint32_t off = (uint32_t)((qq < 0 ? 0 : (qq >> 1)) - w0);
+        for (int mu = 0; mu < 2; mu++) {
+            const int64_t qq = rank - (int64_t)has4[2 * mu];
+            const int64_t w0 = (rb - (int64_t)has4[2 * mu]) < 0 ? 0 : ((rb - (int64_t)has4[2 * mu]) >> 1);
+            const uint32_t off = (uint32_t)((qq < 0 ? 0 : (qq >> 1)) - w0);
 #pragma unroll
-        for (int fb = 0; fb < 2; fb++) {
-            const uint64_t X = xsl_rr(hot_apply(sm, off, bs[2 + 2 * mu + fb]));
-            uint32_t word = (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
-            if (qq < 0) word = buf[2 * mu + fb];  // has && rank == 0: the block's buffered half-word
-            D.w[2 * mu + fb] = word;
+            for (int fb = 0; fb < 2; fb++) {
+                const uint64_t X = xsl_rr(hot_apply(sm, off, bs[2 + 2 * mu + fb]));
+                uint32_t word = (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
+                if (qq < 0) word = buf[2 * mu + fb];  // has && rank == 0: the block's buffered half-word
+                D.w[2 * mu + fb] = word;
+            }
         }
+        return D;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        int64_t q = rank;
+#pragma unroll
+        for (int i = 0; i < HOT_MAXSK; i++)
+            if (i < nsk[j] && (int64_t)sk[j][i] <= q) q++;
+        spos[j] = (uint32_t)q;
+        const int64_t qq = q - (int64_t)has4[j];
+        const int64_t w0 = (rb - (int64_t)has4[j]) < 0 ? 0 : ((rb - (int64_t)has4[j]) >> 1);
+        const uint32_t off = (uint32_t)((qq < 0 ? 0 : (qq >> 1)) - w0);
+        const uint64_t X = xsl_rr(hot_apply(sm, off, bs[2 + j]));
+        uint32_t word = (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
+        if (qq < 0) word = buf[j];  // has && position 0: the block's buffered half-word
+        D.w[j] = word;
     }
     return D;
 }
@@ -138,6 +165,9 @@ struct HotLDST {
     // per wave: [8c + ty] block ty's base for the colour-c row at xb; [16 + ..] at xw (edge strips of rows > SMALL_LDS)
     std::conditional_t<PH, HotEmpty, std::conditional_t<OBSL, u128[NWL][16], u128[NWL][32]>> base;
     int32_t bad;
+    // SKIP: per colour and choice block, its known rejected stream positions (not in the replica-observables layout,
+    // which needs every byte for its fourth workgroup per CU)
+    std::conditional_t<OBSL, HotEmpty, uint32_t[2][4][HOT_MAXSK]> sk;
     double obs[4];     // OBS: the workgroup's sums of the inline observables
     std::conditional_t<OBSL, ObsLane, HotEmpty> ol;
 };
@@ -161,9 +191,10 @@ __device__ __forceinline__ int logical_block() {
     return xcd * per + (xcd < rem ? xcd : rem) + k;
 }
 
-template <bool TILE, bool EDGE, bool FR = false, bool OBS = false, bool PH = false, int NWT = 4>
+template <bool TILE, bool EDGE, bool FR = false, bool OBS = false, bool PH = false, int NWT = 4, bool SKIP = false>
 __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, NWT> &Ls, int bl) {
     static_assert(!(FR && TILE), "full-row replica strips are periodic");
+    static_assert(!SKIP || (EDGE && !FR && !PH), "skip lists: the unpaired (edge) draws of single lattices and tiles");
     static_assert(NWT == 4 || (NWT == 8 && !FR && !PH), "8-wave strips: single lattices and tiles");
     constexpr int NW = NWT;
     constexpr int R = HotLDST<PH, FR && OBS, NWT>::R, RR = HotLDST<PH, FR && OBS, NWT>::RR;
@@ -255,16 +286,35 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     }
 
     // per colour: the buffered-half flags and words of the choice blocks (equal within each fwd/bwd pair on
-    // this kernel), uniform
-    uint32_t has_c[2][2], buf_c[2][4];
+    // this kernel unless SKIP), uniform
+    // (non-SKIP edge draws read has4[c][2 mu], the pair's common flag)
+    uint32_t has_c[2][2], buf_c[2][4], has4[2][4];
+    int32_t nsk[2][4];
 #pragma unroll
     for (int c = 0; c < 2; c++) {
 #pragma unroll
         for (int mu = 0; mu < 2; mu++)
             has_c[c][mu] = PH ? 0u : (uint32_t)__builtin_amdgcn_readfirstlane(blocks[2 + 5 * c + 2 * mu].has);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if constexpr (SKIP) {
+                has4[c][j] = (uint32_t)__builtin_amdgcn_readfirstlane(blocks[2 + 5 * c + j].has);
+                nsk[c][j] = __builtin_amdgcn_readfirstlane(blocks[2 + 5 * c + j].nskip);
+            } else {
+                has4[c][j] = has_c[c][j >> 1];
+                nsk[c][j] = 0;
+            }
+        }
         if (edge) {
 #pragma unroll
             for (int j = 0; j < 4; j++) buf_c[c][j] = (uint32_t)__builtin_amdgcn_readfirstlane(blocks[2 + 5 * c + j].buf);
+        }
+    }
+    if constexpr (SKIP) {  // the skip lists into LDS (the host bounds them by HOT_MAXSK per block)
+        if (threadIdx.x < 2 * 4 * HOT_MAXSK) {
+            const int c = threadIdx.x / (4 * HOT_MAXSK), j = (threadIdx.x / HOT_MAXSK) & 3, i = threadIdx.x % HOT_MAXSK;
+            const Block &B = blocks[2 + 5 * c + j];
+            if constexpr (!(FR && OBS)) Ls.sk[c][j][i] = i < B.nskip ? A.skips[B.skip0 + i] : 0xFFFFFFFFu;
         }
     }
     const VParams P = A.P;
@@ -440,6 +490,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     // draws of colour c for global row gq, local column x; the 4 choice values; a rejected word is reported
     auto draw = [&](int c, int32_t q, int32_t x, bool active, HotDraws &D, int32_t cn[4]) {
         const int32_t gq = grow(q);
+        uint32_t spos[4] = {0, 0, 0, 0};  // SKIP: the choice draws' stream positions
         if constexpr (PH) {
             // site s of sweep `ph_sweep`: call (s, sweep, 0) -> u, dphi; call (s, sweep, 1) -> the four choice words; a
             // word Lemire rejects is replaced in place by word 0 of call (s, sweep, 2 + j + 4 t) (sv_oracle.c, philox)
@@ -465,8 +516,11 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
             for (int k = 0; k < 6; k++) bs[k] = s_base[wave][8 * c + k];
             D = hot_draws_paired(A, lane, c == 0 ? pk0 : pk1, bs, s_small);
         } else {
-            D = hot_draws_edge(A, gq, wrapN(X0s + x, Nx), xb, two_sets ? xw : xb, &s_base[wave][8 * c],
-                               &s_base[wave][(two_sets ? 16 : 0) + 8 * c], s_small, has_c[c], buf_c[c]);
+            const uint32_t(*skl)[HOT_MAXSK] = nullptr;
+            if constexpr (SKIP) skl = Ls.sk[c];
+            D = hot_draws_edge<SKIP>(A, gq, wrapN(X0s + x, Nx), xb, two_sets ? xw : xb, &s_base[wave][8 * c],
+                                     &s_base[wave][(two_sets ? 16 : 0) + 8 * c], s_small, has4[c], buf_c[c], skl,
+                                     nsk[c], spos);
         }
         bool rej = false;
 #pragma unroll
@@ -480,7 +534,8 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
             const uint32_t rank = (uint32_t)(((int64_t)gq * Nx + wrapN(X0s + x, Nx)) >> 1);
 #pragma unroll
             for (int j = 0; j < 4; j++)
-                if ((uint32_t)((uint64_t)D.w[j] * kc) < thr) report(A.S, A.sweep, (uint32_t)(1 + 5 * c + 1 + j), rank, (uint32_t)rep);
+                if ((uint32_t)((uint64_t)D.w[j] * kc) < thr)
+                    report(A.S, A.sweep, (uint32_t)(1 + 5 * c + 1 + j), SKIP ? spos[j] : rank, (uint32_t)rep);
         }
     };
 
@@ -698,6 +753,18 @@ __global__ __launch_bounds__(NWT * 64) __attribute__((amdgpu_waves_per_eu(SV_HOT
     else hot_body<TILE, true, false, false, false, NWT>(A, Ls, bl);
 }
 
+// A sweep with known NumPy Lemire rejections in its choice blocks (at most HOT_MAXSK per block; the replay of a
+// rejected sweep) or unequal buffered-half flags within a fwd/bwd pair (the sweep that holds the rejection): every
+// strip draws unpaired, with the skip-adjusted positions (hot_draws_edge<true>) -- the general villain_sweep_fused
+// form of these sweeps ran at ~1.9x the hot kernel's time
+template <bool TILE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4 ? 4 : 3))) void villain_sweep_hot_skip(FArgs A) {
+    __shared__ HotLDST<false, false, 4> Ls;
+    hot_body<TILE, true, false, false, false, 4, true>(A, Ls, logical_block());
+}
+template __global__ void villain_sweep_hot_skip<false>(FArgs);
+template __global__ void villain_sweep_hot_skip<true>(FArgs);
+
 template __global__ void villain_sweep_hot<false, 4>(FArgs);
 template __global__ void villain_sweep_hot<true, 4>(FArgs);
 template __global__ void villain_sweep_hot<false, 8>(FArgs);
@@ -760,6 +827,23 @@ bool hot_ok(const VParams &P, const Block *blocks) {
         if (B[0].has != B[1].has || B[2].has != B[3].has) return false;
     }
     return true;
+}
+
+// The skip form covers any sweep of the hot kernel's parameters whose choice blocks hold at most HOT_MAXSK known
+// rejected positions each (buffered-half flags may differ)
+bool hot_skip_ok(const VParams &P, const Block *blocks) {
+    if (!hot_params_ok(P)) return false;
+    for (int c = 0; c < 2; c++)
+        for (int j = 0; j < 4; j++)
+            if (blocks[2 + 5 * c + j].nskip > HOT_MAXSK) return false;
+    return true;
+}
+
+void launch_hot_skip(const FArgs &A, int grid, hipStream_t stream) {
+    const bool periodic =
+        A.G.org == 0 && A.G.pitch == A.G.Nx && A.G.T0 == 0 && A.G.X0 == 0 && A.G.Ht == A.G.Nt && A.G.Wt == A.G.Nx;
+    if (periodic) villain_sweep_hot_skip<false><<<grid, 4 * 64, 0, stream>>>(A);
+    else villain_sweep_hot_skip<true><<<grid, 4 * 64, 0, stream>>>(A);
 }
 
 // replica batch of full-row lattices: N <= 128 columns (one strip), N % 4 == 0 (row ranks start on whole words)

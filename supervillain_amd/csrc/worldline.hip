@@ -13,6 +13,8 @@
 //    evaluated fresh.  Oracle: oracle/sv_oracle.c sv_o_worldline_plaquette_cb.
 #include <algorithm>
 #include <cmath>
+#include <exception>
+#include <thread>
 
 #include "local.h"
 #include "fused.h"
@@ -405,9 +407,10 @@ __global__ __launch_bounds__(256) void plaquette_level(WParams P, int64_t *m, vo
 // earlier-visited plaquettes q sharing a link with p (its four nearest neighbours); plaquettes of one level share no
 // link and may run in any order.  A random permutation has ~15 levels at L = 1024 (any permutation is accepted:
 // row-major order has 2N - 1).  Flags: [0] not a permutation, [1] max level, [2 + j] iteration j changed a level.
-__global__ void order_positions(const int64_t *order, int64_t V, int32_t *pos, int32_t *flags) {
+template <typename O>
+__global__ void order_positions(const O *order, int64_t V, int32_t *pos, int32_t *flags) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t x = order[i];
+        const int64_t x = (int64_t)order[i];
         if (x < 0 || x >= V) {
             flags[0] = 1;
             continue;
@@ -829,6 +832,8 @@ int sv_worldline_destroy(sv_worldline *st) {
     if (st->lev) (void)hipFree(st->lev);
     if (st->ord64) (void)hipFree(st->ord64);
     if (st->lcnt) (void)hipFree(st->lcnt);
+    for (uint32_t *h : st->h_perm)
+        if (h) (void)hipHostFree(h);
     const hipError_t ee = st->emitter.release();
     if (ee != hipSuccess && !rc) {
         st->ctx->err = std::string("sv_worldline_destroy: an emission copy failed: ") + hipGetErrorString(ee);
@@ -989,33 +994,39 @@ int sv_worldline_plaquette_coexact_run(sv_worldline *st, double kappa, double W_
     }
 }
 
-int sv_worldline_plaquette_ordered_run(sv_worldline *st, double kappa, double W_eff, const int64_t *order,
-                                       sv_rng *rng, sv_stats *stats) {
-    if (!st || !rng || !stats || !order) return -1;
+namespace {
+
+void ordered_alloc(sv_worldline *st) {
+    const int64_t V = (int64_t)st->N * st->N;
+    if (!st->f) {
+        SV_HIP(hipMalloc(&st->f, 2 * V * sizeof(double)));
+        SV_HIP(hipMalloc(&st->order, V * sizeof(int32_t)));
+        SV_HIP(hipMalloc(&st->pos, V * sizeof(int32_t)));
+        SV_HIP(hipMalloc(&st->lev, V * sizeof(int32_t)));
+        SV_HIP(hipMalloc(&st->ord64, V * sizeof(int64_t)));
+        SV_HIP(hipMalloc(&st->lcnt, (V + 2 + LFLAGS) * sizeof(int32_t)));
+    }
+}
+
+// One reference-order Plaquette sweep in the visit order already at st->ord64 on the stream (int64 plaquette
+// indices, or 32-bit ones when o32): dependency levels on the device, then one launch per level; rejection replays
+// as the pass kernels.  Synchronizes the stream before returning.
+void ordered_sweep(sv_worldline *st, double kappa, double W_eff, bool o32, u128 inc, Cursor &cur, sv_stats *stats) {
     sv_ctx *ctx = st->ctx;
-    try {
-        SV_HIP(hipSetDevice(ctx->device));
+    {
         const int64_t N = st->N, V = N * N;
-        WParams P = wparams(st->N, kappa, W_eff, 1, u128{rng->inc_lo, rng->inc_hi});
-        u128 inc{rng->inc_lo, rng->inc_hi};
-        Cursor cur{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
+        WParams P = wparams(st->N, kappa, W_eff, 1, inc);
         const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
-        if (!st->f) {
-            SV_HIP(hipMalloc(&st->f, 2 * V * sizeof(double)));
-            SV_HIP(hipMalloc(&st->order, V * sizeof(int32_t)));
-            SV_HIP(hipMalloc(&st->pos, V * sizeof(int32_t)));
-            SV_HIP(hipMalloc(&st->lev, V * sizeof(int32_t)));
-            SV_HIP(hipMalloc(&st->ord64, V * sizeof(int64_t)));
-            SV_HIP(hipMalloc(&st->lcnt, (V + 2 + LFLAGS) * sizeof(int32_t)));
-        }
         // Dependency levels of the visit order, on the device (order_positions .. order_level_lists)
         int32_t *flags = st->lcnt + V + 2;
         const int lgrid = (int)std::min<int64_t>((V + 255) / 256, 4096);
-        SV_HIP(hipMemcpyAsync(st->ord64, order, V * sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
         SV_HIP(hipMemsetAsync(st->pos, 0xFF, V * sizeof(int32_t), ctx->stream));
         SV_HIP(hipMemsetAsync(st->lev, 0, V * sizeof(int32_t), ctx->stream));
         SV_HIP(hipMemsetAsync(st->lcnt, 0, (V + 2 + LFLAGS) * sizeof(int32_t), ctx->stream));
-        order_positions<<<lgrid, 256, 0, ctx->stream>>>(st->ord64, V, st->pos, flags);
+        if (o32)
+            order_positions<uint32_t><<<lgrid, 256, 0, ctx->stream>>>((const uint32_t *)st->ord64, V, st->pos, flags);
+        else
+            order_positions<int64_t><<<lgrid, 256, 0, ctx->stream>>>(st->ord64, V, st->pos, flags);
         int32_t hf[LFLAGS];
         for (int it = 0;; it += LFLAGS - 2) {
             // relaxations in batches; a batch whose last relaxation changed nothing has converged
@@ -1085,15 +1096,122 @@ int sv_worldline_plaquette_ordered_run(sv_worldline *st, double kappa, double W_
         int64_t rj = 0;
         for (auto &kv : skips) rj += (int64_t)kv.second.size();
         stats->rejections = rj;
-        rng->state_hi = cur.s.hi;
-        rng->state_lo = cur.s.lo;
-        rng->has_uint32 = (int32_t)cur.has;
-        rng->uinteger = cur.buf;
+    }
+}
+
+void store_cursor_w(const Cursor &cur, sv_rng *rng) {
+    rng->state_hi = cur.s.hi;
+    rng->state_lo = cur.s.lo;
+    rng->has_uint32 = (int32_t)cur.has;
+    rng->uinteger = cur.buf;
+}
+
+}  // namespace
+
+int sv_worldline_plaquette_ordered_run(sv_worldline *st, double kappa, double W_eff, const int64_t *order,
+                                       sv_rng *rng, sv_stats *stats) {
+    if (!st || !rng || !stats || !order) return -1;
+    sv_ctx *ctx = st->ctx;
+    try {
+        SV_HIP(hipSetDevice(ctx->device));
+        const int64_t V = (int64_t)st->N * st->N;
+        u128 inc{rng->inc_lo, rng->inc_hi};
+        Cursor cur{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
+        ordered_alloc(st);
+        SV_HIP(hipMemcpyAsync(st->ord64, order, V * sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
+        ordered_sweep(st, kappa, W_eff, false, inc, cur, stats);
+        store_cursor_w(cur, rng);
         return 0;
     } catch (const std::exception &e) {
         ctx->err = e.what();
         return -2;
     }
+}
+
+namespace {
+
+// `sweeps` reference-order Plaquette sweeps, each followed by one CoexactUpdate sweep when interval_t > 0 (stats then
+// [2 s], [2 s + 1]), all on the one PCG64 stream; the visit orders from the legacy MT19937 state *mt
+int reference_steps(sv_worldline *st, double kappa, double W_eff, int64_t interval_t, int32_t sweeps, sv_mt19937 *mt,
+                    sv_rng *rng, sv_stats *stats) {
+    if (!st || !rng || !mt || (sweeps > 0 && !stats)) return -1;
+    sv_ctx *ctx = st->ctx;
+    const int nstat = interval_t > 0 ? 2 : 1;
+    try {
+        if (sweeps < 0) throw std::invalid_argument("sweeps must be >= 0");
+        if (sweeps == 0) return 0;
+        SV_HIP(hipSetDevice(ctx->device));
+        const int64_t V = (int64_t)st->N * st->N;
+        u128 inc{rng->inc_lo, rng->inc_hi};
+        Cursor cur{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
+        ordered_alloc(st);
+        for (int i = 0; i < 2; i++)
+            if (!st->h_perm[i]) SV_HIP(hipHostMalloc((void **)&st->h_perm[i], V * sizeof(uint32_t), hipHostMallocDefault));
+        // Three-stage pipeline over the sweeps: while the device runs sweep s (visit order h_perm[s & 1]), one host
+        // thread draws sweep s + 2's intervals from the legacy MT19937 stream (serial) and another applies sweep
+        // s + 1's swaps.  The legacy state advances in the drawing thread only; the caller's copy on success.
+        sv_mt19937 m = *mt;
+        std::vector<uint32_t> jb[3];
+        for (auto &j : jb) j.resize((size_t)V);
+        sv::legacy_intervals(m.key, m.pos, V, jb[0].data());
+        sv::shuffle_from_intervals(jb[0].data(), V, st->h_perm[0]);
+        if (sweeps > 1) sv::legacy_intervals(m.key, m.pos, V, jb[1].data());
+        for (int s = 0; s < sweeps; s++) {
+            std::exception_ptr e_draw, e_swap;
+            std::thread t_draw, t_swap;
+            struct Join {
+                std::thread &a, &b;
+                ~Join() {
+                    if (a.joinable()) a.join();
+                    if (b.joinable()) b.join();
+                }
+            } join{t_draw, t_swap};
+            if (s + 2 < sweeps)
+                t_draw = std::thread([&, s] {
+                    try {
+                        sv::legacy_intervals(m.key, m.pos, V, jb[(s + 2) % 3].data());
+                    } catch (...) {
+                        e_draw = std::current_exception();
+                    }
+                });
+            // (h_perm[(s + 1) & 1] last fed sweep s - 1's copy, which completed inside that synchronized sweep)
+            if (s + 1 < sweeps)
+                t_swap = std::thread([&, s] { sv::shuffle_from_intervals(jb[(s + 1) % 3].data(), V, st->h_perm[(s + 1) & 1]); });
+            SV_HIP(hipMemcpyAsync(st->ord64, st->h_perm[s & 1], V * sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream));
+            ordered_sweep(st, kappa, W_eff, true, inc, cur, stats + (size_t)s * nstat);
+            if (interval_t > 0) {  // Sequentially(PlaquetteUpdate, CoexactUpdate), combining.py:38-40
+                sv_rng r{cur.s.hi, cur.s.lo, inc.hi, inc.lo, (int32_t)cur.has, cur.buf};
+                if (sv_worldline_coexact_run(st, kappa, W_eff, interval_t, 1, &r, stats + (size_t)s * nstat + 1))
+                    throw std::runtime_error(ctx->err);
+                cur = Cursor{u128{r.state_lo, r.state_hi}, (uint32_t)r.has_uint32, r.uinteger};
+            }
+            if (t_draw.joinable()) t_draw.join();
+            if (t_swap.joinable()) t_swap.join();
+            if (e_draw) std::rethrow_exception(e_draw);
+        }
+        *mt = m;
+        store_cursor_w(cur, rng);
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
+}  // namespace
+
+int sv_worldline_plaquette_reference_run(sv_worldline *st, double kappa, double W_eff, int32_t sweeps, sv_mt19937 *mt,
+                                         sv_rng *rng, sv_stats *stats) {
+    return reference_steps(st, kappa, W_eff, 0, sweeps, mt, rng, stats);
+}
+
+int sv_worldline_plaquette_reference_coexact_run(sv_worldline *st, double kappa, double W_eff, int64_t interval_t,
+                                                 int32_t steps, sv_mt19937 *mt, sv_rng *rng, sv_stats *stats) {
+    if (interval_t < 1) {
+        if (st) st->ctx->err = "interval_t must be >= 1";
+        return -2;
+    }
+    return reference_steps(st, kappa, W_eff, interval_t, steps, mt, rng, stats);
 }
 
 int sv_worldline_plaquette(sv_ctx *ctx, int32_t N, double kappa, double W_eff, int64_t *m, void *v,

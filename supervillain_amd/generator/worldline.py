@@ -11,6 +11,7 @@ import ctypes
 import numpy as np
 
 from supervillain_amd import _native
+from supervillain_amd._abi import legacy_state_get, legacy_state_set
 from supervillain_amd.generator._common import DeviceState, rng_from_numpy, rng_to_numpy, wrap_like
 from supervillain_amd.generator.generator import Generator
 from supervillain_amd.replicas import WORM_MAX_MOVES
@@ -150,14 +151,15 @@ class PlaquetteUpdate(_WorldlineDevice, Generator):
         r = rng_from_numpy(self.rng)
         kappa, W = float(self.Action.kappa), float(self.Action._W)
         if self.mode == 'reference':
-            sts = []
-            for _ in range(sweeps):
-                order = np.random.permutation(L.coordinates)  # plaquette.py:63, global RandomState
-                lin = np.ascontiguousarray((order[:, 0] % L.N) * L.N + (order[:, 1] % L.N), dtype=np.int64)
-                sts.append(_native.stats_array(1))
-                ctx.check(Lib.sv_worldline_plaquette_ordered_run(h, kappa, W, _native.ptr(lin), ctypes.byref(r),
-                                                                 sts[-1]), 'sv_worldline_plaquette_ordered_run')
-            stats = lambda: [(int(s[0].accepted), s[0].acceptance_sum) for s in sts]  # noqa: E731
+            # plaquette.py:63's np.random.permutation(L.coordinates) -- NumPy's legacy global RandomState, whose
+            # row-major coordinates make the visit order the shuffled index array itself -- drawn natively from the
+            # same MT19937 state (sv_mt19937_permutation), which advances exactly as NumPy's would
+            mt, rest = legacy_state_get()
+            st = _native.stats_array(sweeps)
+            ctx.check(Lib.sv_worldline_plaquette_reference_run(h, kappa, W, sweeps, ctypes.byref(mt), ctypes.byref(r), st),
+                      'sv_worldline_plaquette_reference_run')
+            legacy_state_set(mt, rest)
+            stats = lambda: [(int(st[k].accepted), st[k].acceptance_sum) for k in range(sweeps)]  # noqa: E731
         else:
             st = _native.stats_array(sweeps)
             ctx.check(Lib.sv_worldline_plaquette_checkerboard_run(h, kappa, W, sweeps, ctypes.byref(r), st),

@@ -406,3 +406,80 @@ def test_ordered_plaquette_rejects_non_permutations(bad):
     rc, err, m, v, _, _ = _ordered_run(N, 0.5, m0, order, 1)
     assert rc != 0 and 'permutation' in err
     assert (m == m0).all() and (v == 0).all()
+
+
+@pytest.mark.parametrize('N,sweeps', [(16, 1), (48, 2), (64, 7)])
+def test_reference_run_pipelined_sweeps(N, sweeps, oracle_lib):
+    """Several reference-order sweeps in one call (sv_worldline_plaquette_reference_run, via PlaquetteUpdate._steps):
+    the visit orders are drawn natively from the legacy global RandomState on host threads, pipelined with the device
+    (sweep s + 2's draws and s + 1's swaps while s runs), and equal np.random.permutation's, sweep after sweep; the
+    global state afterwards is NumPy's.  Against the sequential oracle fed NumPy's own permutations."""
+    L = sv.Lattice2D(N)
+    S = sv.Worldline(L, 0.45, 1)
+    C = sv.generator.worldline.CoexactUpdate(S)
+    C.rng = np.random.default_rng(12)
+    cfg = S.configurations(1)[0]
+    cfg = cfg | C.step(cfg)  # m != 0
+    m = np.asarray(cfg['m']).copy()
+    v = np.zeros((N, N), dtype=np.int64)
+    G = sv.generator.worldline.PlaquetteUpdate(S)
+    G.rng = np.random.default_rng(13)
+    saved = np.random.get_state()
+    try:
+        np.random.seed(31)
+        cfg = cfg | G._steps(cfg, sweeps)
+        after = np.random.get_state()
+        np.random.seed(31)
+        g = np.random.default_rng(13)
+        acc = 0
+        for _ in range(sweeps):
+            o = np.random.permutation(L.coordinates)
+            acc += oracle_lib.worldline_plaquette_seq(N, 0.45, 1.0, m, v, (o[:, 0] % N) * N + (o[:, 1] % N), g).accepted
+        ref_after = np.random.get_state()
+    finally:
+        np.random.set_state(saved)
+    assert (np.asarray(cfg['m']) == m).all() and (np.asarray(cfg['v'])[0] == v).all()
+    assert G.accepted == acc and G.rng.bit_generator.state == g.bit_generator.state
+    assert (after[1] == ref_after[1]).all() and after[2] == ref_after[2]
+
+
+def test_reference_coexact_steps(oracle_lib):
+    """Sequentially(PlaquetteUpdate [reference order], CoexactUpdate) on one Generator for 5 steps in one call
+    (sv_worldline_plaquette_reference_coexact_run, what bench.py --plaquette reference times) against the oracle."""
+    import ctypes
+    from supervillain_amd import _native
+    from supervillain_amd._abi import SvMT19937, rng_from_numpy, rng_to_numpy
+    N, kappa, steps = 40, 0.5, 5
+    Lib = _native.lib()
+    ctx = _native.context(_native.default_device())
+    h = ctypes.c_void_p()
+    ctx.check(Lib.sv_worldline_create(ctx.handle, N, 0, ctypes.byref(h)), 'create')
+    m = np.zeros((2, N, N), dtype=np.int64)
+    v = np.zeros((N, N), dtype=np.int64)
+    legacy = np.random.RandomState(8)
+    mt = SvMT19937()
+    key = legacy.get_state()
+    ctypes.memmove(mt.key, np.ascontiguousarray(key[1], dtype=np.uint32).ctypes.data, 624 * 4)
+    mt.pos = int(key[2])
+    gen = np.random.default_rng(21)
+    try:
+        ctx.check(Lib.sv_worldline_upload(h, _native.ptr(m), _native.ptr(v)), 'upload')
+        r = rng_from_numpy(gen)
+        st = _native.stats_array(2 * steps)
+        ctx.check(Lib.sv_worldline_plaquette_reference_coexact_run(h, kappa, 1.0, 1, steps, ctypes.byref(mt),
+                                                                   ctypes.byref(r), st), 'reference_coexact')
+        rng_to_numpy(r, gen)
+        ctx.check(Lib.sv_worldline_download(h, _native.ptr(m), _native.ptr(v)), 'download')
+    finally:
+        Lib.sv_worldline_destroy(h)
+    mm, vv = np.zeros((2, N, N), dtype=np.int64), np.zeros((N, N), dtype=np.int64)
+    g = np.random.default_rng(21)
+    lg = np.random.RandomState(8)
+    for s in range(steps):
+        o = lg.permutation(N * N).astype(np.int64)
+        sp = oracle_lib.worldline_plaquette_seq(N, kappa, 1.0, mm, vv, o, g)
+        sc = oracle_lib.worldline_coexact(N, kappa, 1.0, mm, vv, 1, g)[0]
+        assert st[2 * s].accepted == sp.accepted and st[2 * s + 1].accepted == sc.accepted, s
+    assert (m == mm).all() and (v == vv).all()
+    assert gen.bit_generator.state == g.bit_generator.state
+    assert (np.frombuffer(bytes(mt.key), dtype=np.uint32) == lg.get_state()[1]).all() and mt.pos == lg.get_state()[2]
