@@ -34,7 +34,13 @@ const sv::JumpTables *sv_ctx::jump_tables(uint64_t inc_hi, uint64_t inc_lo) {
     auto key = std::make_pair(inc_hi, inc_lo);
     auto it = tables.find(key);
     if (it != tables.end()) return it->second;
-    if (tables.size() >= MAX_TABLES) {
+    static const size_t max_tables = [] {  // SV_MAX_TABLES: a smaller cache (diagnostics: round 3 dropped it at 64)
+        const char *e = getenv("SV_MAX_TABLES");
+        return e && atoi(e) > 0 ? (size_t)atoi(e) : MAX_TABLES;
+    }();
+    if (tables.size() >= max_tables) {
+        if (alloc_log()) fprintf(stderr, "[sv alloc] jump-table cache purge #%lld (%zu tables)\n", (long long)table_purges + 1,
+                                 tables.size());
         // a long-lived context seeing many generators drops its cache.  Launches already enqueued on ANY stream of
         // the device (the context stream, deferred pipeline members, a domain's scan stream, emission copies) may
         // hold one of these tables, so the whole device drains first -- explicitly, not through hipFree's own

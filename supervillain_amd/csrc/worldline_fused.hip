@@ -273,9 +273,10 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
 
     // uniform draw and bounded word at stream offsets of row q's base (set A or, for wrapped columns, set B)
     auto draw_u = [&](const u128 &base, uint32_t off) { return u53(xsl_rr(hot_apply(s_small, off & (SMALL_LDS - 1), base))); };
-    auto word_at = [&](const u128 &base, int64_t rank, uint32_t has, uint32_t buf, int64_t rb) {
-        const int64_t qq = rank - (int64_t)has;
-        const int64_t w0 = (rb - (int64_t)has) < 0 ? 0 : ((rb - (int64_t)has) >> 1);
+    // (32-bit positions: launch_wf keeps V < 2^31, so ranks and word indices fit int32)
+    auto word_at = [&](const u128 &base, int32_t rank, uint32_t has, uint32_t buf, int32_t rb) {
+        const int32_t qq = rank - (int32_t)has;
+        const int32_t w0 = (rb - (int32_t)has) < 0 ? 0 : ((rb - (int32_t)has) >> 1);
         const uint64_t X = xsl_rr(hot_apply(s_small, (uint32_t)((qq < 0 ? 0 : (qq >> 1)) - w0) & (SMALL_LDS - 1), base));
         uint32_t word = (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
         return qq < 0 ? buf : word;
@@ -291,7 +292,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
         const u128 *bs = &Ls.base[wave][8 * p];
         double u;
         uint32_t wm, wv;
-        uint32_t qm = (uint32_t)(((int64_t)gq * N + gx) >> 1), qv = qm;  // stream positions (skip-adjusted)
+        uint32_t qm = ((uint32_t)gq * (uint32_t)N + (uint32_t)gx) >> 1, qv = qm;  // stream positions (skip-adjusted)
         (void)qm;
         if constexpr (!EDGE) {
             u = draw_u(bs[0], pk[p]);
@@ -306,7 +307,8 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
             const bool wr = two_sets && !(gx >= xb && gx < xb + SMALL_LDS);
             const int32_t xr = wr ? xw : xb;
             const u128 *bb = wr ? &Ls.base[wave][32 + 8 * p] : bs;
-            const int64_t rank = ((int64_t)gq * N + gx) >> 1, rb = ((int64_t)gq * N + xr) >> 1;
+            const int32_t rank = (int32_t)(((uint32_t)gq * (uint32_t)N + (uint32_t)gx) >> 1);
+            const int32_t rb = (int32_t)(((uint32_t)gq * (uint32_t)N + (uint32_t)xr) >> 1);
             u = draw_u(bb[0], (uint32_t)(gx - xr));
             if constexpr (MODE == 2) {
                 qm = skip_pos(A.blocks[1 + 2 * c], A.skips, (uint32_t)rank);
@@ -366,7 +368,8 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
         const bool wr = two_sets && !(gx >= xb && gx < xb + SMALL_LDS);
         const int32_t xr = wr ? xw : xb;
         const u128 *bb = wr ? &Ls.base[wave][32 + 8 * p] : &Ls.base[wave][8 * p];
-        const int64_t rank = ((int64_t)gq * N + gx) >> 1, rb = ((int64_t)gq * N + xr) >> 1;
+        const int32_t rank = (int32_t)(((uint32_t)gq * (uint32_t)N + (uint32_t)gx) >> 1);
+        const int32_t rb = (int32_t)(((uint32_t)gq * (uint32_t)N + (uint32_t)xr) >> 1);
         const double u = draw_u(bb[0], (uint32_t)(gx - xr));
         uint32_t qt = (uint32_t)rank, wt;
         if constexpr (MODE == 2) {
@@ -567,6 +570,8 @@ void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
                int64_t *m_out, int64_t *v_out, const Block *blocks, const uint32_t *skips, bool general,
                const JumpTables *T, const Affine adv[6], void *pstat, void *cstat, DevScratch S, uint32_t sweep,
                hipStream_t stream) {
+    if ((int64_t)G.Nt * G.Nx >= (int64_t(1) << 31))
+        throw std::invalid_argument("worldline_step_fused addresses stream positions with 31 bits (V < 2^31)");
     WFArgs A{};
     A.skips = skips;
     A.general = general ? 1 : 0;

@@ -1,0 +1,117 @@
+"""Two real ranks on one GPU: the multi-rank RCCL code (per-peer ncclSend / ncclRecv pairs between two processes,
+the batch-summary ncclAllGather over two ranks, rank-ordered group calls) against the single-process tile emulation,
+bit for bit, for a Villain and a Worldline 1 x 2 decomposition (config 4 and config 3 as two GPUs would run them),
+with NumPy Lemire rejections forced into the chain (the abort / replay protocol across ranks).
+
+This file sorts FIRST among the -m gpu tests on purpose: the two ranks are started (spawn: fresh interpreters) before
+the test process itself has touched the GPU -- a process that has initialised the GPU must not start new programs.
+If RCCL refuses two ranks on one device, the ranks record its exact error and the test is marked xfail with it."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, model, out):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), SV_DEVICE='0', SV_DOMAIN_BATCH='4')
+    import torch.distributed as dist
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from supervillain_amd.domain import VillainDomain, WorldlineDomain
+        from tests.golden import crafted_generator
+        if model == 'villain':
+            Nt, Nx, steps = 64, 128, 9
+            V = Nt * Nx
+            pos = 4 * V + 3 * V + V // 3  # sweep 1's colour-1 choice words: a rejection there
+            gen = lambda: crafted_generator(pos, pos, 1)  # noqa: E731
+            phi0 = np.random.default_rng(4).uniform(-np.pi, np.pi, (Nt, Nx))
+            n0 = np.random.default_rng(5).integers(-2, 3, (2, Nt, Nx)).astype(np.int64)
+            make = lambda **kw: VillainDomain(Nt, Nx, (1, 2), kappa=0.5, W=1, **kw)  # noqa: E731
+            dist_make = lambda: VillainDomain.distributed(Nt, Nx, (1, 2), kappa=0.5, W=1)  # noqa: E731
+        else:
+            Nt, Nx, steps = 64, 128, 6
+            V = Nt * Nx
+            pos = (2 * V + V + V // 2) + V + 3 * V // 4 + 5  # step 1's colour-1 change_v block
+            gen = lambda: crafted_generator(pos, pos, 1)  # noqa: E731
+            phi0 = np.random.default_rng(6).integers(-3, 4, (Nt, Nx)).astype(np.int64)
+            n0 = np.zeros((2, Nt, Nx), dtype=np.int64)
+            make = lambda **kw: WorldlineDomain(Nt, Nx, (1, 2), kappa=0.5, W=1, **kw)  # noqa: E731
+            dist_make = lambda: WorldlineDomain.distributed(Nt, Nx, (1, 2), kappa=0.5, W=1)  # noqa: E731
+        try:
+            dom = dist_make()
+        except Exception as e:  # RCCL refusing two ranks on one device lands here (ncclCommInitRank)
+            with open(f'{out}.refused', 'w') as f:
+                f.write(f'rank {rank}: {e}')
+            return
+        try:
+            if model == 'villain':
+                dom.upload(phi0, n0)
+            else:
+                dom.upload(n0, phi0)
+            g = gen()
+            st = dom.run(steps, g)
+            a, b = dom.download()
+        finally:
+            dom.close()
+        res = [None, None]
+        dist.all_gather_object(res, (a, b, [(s.accepted, s.rejections) for s in st], g.bit_generator.state))
+        if rank == 0:
+            a = res[0][0].copy()
+            b = res[0][1].copy()
+            half = Nx // 2
+            if model == 'villain':  # phi (Nt, Nx), n (2, Nt, Nx): rank 1 owns columns [half, Nx)
+                a[:, half:] = res[1][0][:, half:]
+                b[:, :, half:] = res[1][1][:, :, half:]
+            else:  # m (2, Nt, Nx), v (Nt, Nx)
+                a[:, :, half:] = res[1][0][:, :, half:]
+                b[:, half:] = res[1][1][:, half:]
+            ref = make()
+            try:
+                if model == 'villain':
+                    ref.upload(phi0, n0)
+                else:
+                    ref.upload(n0, phi0)
+                g2 = gen()
+                st2 = ref.run(steps, g2)
+                a2, b2 = ref.download()
+            finally:
+                ref.close()
+            ok = ((a == a2).all() and (b == b2).all() and res[0][2] == [(s.accepted, s.rejections) for s in st2]
+                  and res[1][2] == res[0][2] and res[0][3] == g2.bit_generator.state == res[1][3]
+                  and sum(r for _, r in res[0][2]) >= 1)
+            with open(f'{out}.result', 'w') as f:
+                f.write('ok' if ok else f'mismatch: stats {res[0][2]} vs {[(s.accepted, s.rejections) for s in st2]}')
+    except Exception as e:
+        with open(f'{out}.error', 'a') as f:
+            f.write(f'rank {rank}: {e!r}\n')
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('model', ['villain', 'worldline'])
+def test_two_ranks_one_gpu(model, tmp_path):
+    import time
+
+    import torch.multiprocessing as mp
+    out = str(tmp_path / model)
+    ctx = mp.start_processes(_worker, args=(2, _free_port(), model, out), nprocs=2, join=False, start_method='spawn')
+    deadline = time.time() + 240  # a rendezvous that never completes must not hang the suite
+    while not ctx.join(timeout=5):
+        if time.time() > deadline:
+            for p in ctx.processes:
+                p.kill()
+            pytest.fail('two-rank run did not finish in 240 s')
+    if os.path.exists(f'{out}.refused'):
+        pytest.xfail('RCCL refused two ranks on one device: ' + open(f'{out}.refused').read())
+    assert not os.path.exists(f'{out}.error'), open(f'{out}.error').read()
+    assert open(f'{out}.result').read() == 'ok'
