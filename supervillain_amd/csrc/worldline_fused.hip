@@ -167,6 +167,11 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     for (int k = 0; k < PF; k++) pf_gx[k] = mcol(x0 - 5 + lane + 64 * k);
     auto prefetch = [&](int32_t ra) {
         const int32_t q = ra + wave;
+        if (SV_ABLATE & 16) {  // timing experiments only (fused.h SV_ABLATE): no HBM loads
+#pragma unroll
+            for (int k = 0; k < PF; k++) pf_m0[k] = pf_m1[k] = pf_v[k] = 0;
+            return;
+        }
         if (q >= t0 - 5 && q < t1 + 4) {
             const int64_t g0 = mrow(q);
 #pragma unroll
@@ -202,6 +207,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     };
     auto store_rows = [&](int32_t ra) {
         const int32_t q = ra + wave;
+        if (SV_ABLATE & 8) return;  // timing experiments only: no HBM stores
         if (q >= t0 && q < t1) {
             const int slot = (q - rbase) % R;
             const int64_t g0 = mrow(q) + x0;  // own sites never wrap
