@@ -67,6 +67,9 @@ int sv_ctx_kernel_time(sv_ctx *ctx, double *ms_total, int64_t *launches);
  * replays); generic: the per-colour int64 path.  A domain counts one launch per tile, a replica batch one per
  * launch.  Lets tests prove which kernel ran (e.g. the int32 fallback after |n| >= 2^14). */
 int sv_ctx_sweep_counts(sv_ctx *ctx, int64_t *hot, int64_t *fused, int64_t *generic);
+/* Diagnostic: of the hot sweeps since the last call (then reset), those run K at a time by the multi-sweep band
+ * launches of small periodic lattices (villain_sweep_hot_band, SV_BAND_K), and the number of such launches. */
+int sv_ctx_band_counts(sv_ctx *ctx, int64_t *sweeps, int64_t *launches);
 /* Host-only: copy R NumPy PCG64 bit-generator states into (gather) or out of (scatter) sv_rng records, given
  * each generator's `bit_generator.ctypes.state_address` (NumPy's pcg64_state, numpy/random/src/pcg64/pcg64.h,
  * native 128-bit layout; the Python wrapper verifies it against the public state dict first).  Lets a

@@ -4,6 +4,8 @@ source scripts/gpu/guard.sh
 export TMPDIR=/tmp AMD_LOG_LEVEL=1
 O=gpurun_out/${OUT:-r4_ref}
 mkdir -p $O
+step tworank timeout -k 10 600 python -u -m pytest tests/test_gpu_00_two_ranks.py -v -rxs --timeout 300 --timeout-method thread -m gpu > $O/two_ranks.log 2>&1
+grep -E "^=+ .*(passed|failed|xfail)|XFAIL|refused" $O/two_ranks.log | head -5
 step tests timeout -k 10 600 python -u -m pytest tests/test_gpu_worldline.py tests/test_gpu_villain.py tests/test_gpu_boundary.py tests/test_gpu_overflow.py -x -v -s --timeout 300 --timeout-method thread -m gpu > $O/tests.log 2>&1
 grep -E "^=+ .*(passed|failed)" $O/tests.log
 grep -q -E "^=+ .*[0-9]+ passed" $O/tests.log && ! grep -q -E "^=+ .*failed" $O/tests.log || exit 1

@@ -328,6 +328,14 @@ int sv_ctx_sweep_counts(sv_ctx *ctx, int64_t *hot, int64_t *fused, int64_t *gene
     return 0;
 }
 
+int sv_ctx_band_counts(sv_ctx *ctx, int64_t *sweeps, int64_t *launches) {
+    if (!ctx) return -1;
+    if (sweeps) *sweeps = ctx->sweeps_band;
+    if (launches) *launches = ctx->launches_band;
+    ctx->sweeps_band = ctx->launches_band = 0;
+    return 0;
+}
+
 int sv_ctx_kernel_time(sv_ctx *ctx, double *ms_total, int64_t *launches) {
     if (!ctx) return -1;
     try {

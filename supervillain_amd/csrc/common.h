@@ -143,6 +143,8 @@ struct sv_ctx {
     // Villain NeighborhoodUpdate sweeps by kernel (sv_ctx_sweep_counts): villain_sweep_hot (+ _fr), the general
     // fused kernel (villain_sweep_fused: int32 n image, skip lists), the per-colour int64 path (villain_pass_generic)
     int64_t sweeps_hot = 0, sweeps_fused = 0, sweeps_generic = 0;
+    // of the hot sweeps: those run by multi-sweep band launches, and the launches (sv_ctx_band_counts)
+    int64_t sweeps_band = 0, launches_band = 0;
     void time_begin(hipEvent_t *a);
     void time_end(hipEvent_t a, int64_t launches = 1, int64_t first = 0);
     void time_collect();  // after a stream sync
@@ -204,6 +206,11 @@ struct sv_villain {
     int32_t *d_strips = nullptr;   // villain_sweep_hot's strip table (strip_schedule), n_strips entries of 3
     int32_t n_strips = 0;
     std::string strips_key;        // the schedule the table holds
+    // multi-sweep band launches (villain_sweep_hot_band): the launch's scratch buffers (sweep outputs 1..K-1) and
+    // the per-XCD ticket / barrier counters followed by the batch's gate word
+    std::vector<double *> band_phi;
+    std::vector<int64_t *> band_n;
+    uint32_t *band_ctrl = nullptr;
 };
 
 namespace sv {

@@ -15,6 +15,9 @@ struct VParams {
 };
 
 static constexpr uint32_t OVERFLOW_BLOCK = 0xFFFFu;  // report tag: state not representable on this path
+// report tag: a multi-sweep band launch (villain_sweep_hot_band) could not run as planned (its workgroups were not
+// spread over the XCDs as expected, or a band barrier timed out); the launch's first sweep is replayed without it
+static constexpr uint32_t BAND_FAIL_BLOCK = 0xFFFEu;
 
 // (t, x) = (s / N, s mod N) for a site index s of a lattice of fewer than 2^32 sites (every device path addresses
 // stream positions with 32 bits): one 32-bit unsigned division instead of the 64-bit one (a long emulated
@@ -81,6 +84,27 @@ struct FArgs {
     int32_t *progress = nullptr;
 };
 
+// Multi-sweep launches of small periodic lattices (villain_sweep_hot_band): the lattice rows are cut
+// into one band per XCD; the band's workgroups (all on that XCD, found by its XCC_ID) run K consecutive sweeps, sweep j
+// deciding the band extended by 2(K-1-j) rows above and 3(K-1-j) below (the deep-halo rule of domain.hip: every
+// draw is addressed by its global stream position, so a recomputed halo row equals its owner's), with an XCD-local
+// barrier (atomics and data in that XCD's L2) between sweeps.  Sweep j reads buffer j and writes buffer j + 1:
+// [0] is the launch's input, [K] its output, the rest scratch, so bands never wait on each other.
+static constexpr int BAND_MAXK = 15;
+static constexpr int BAND_CTRL = 64;  // uint32 words per XCD in BandArgs::ctrl: [0] tickets, [32] barrier arrivals
+struct BandArgs {
+    int32_t K;       // sweeps per launch (odd: the output lands in the other buffer of the ping-pong pair)
+    int32_t P;       // workgroups per band
+    int32_t own;     // rows owned by a band (Nt / nbands)
+    int32_t TH;      // strip rows
+    int32_t gen;     // band launches before this one in the batch (ticket and barrier targets)
+    int32_t nb;      // descriptors per sweep
+    int32_t nbands;  // bands = XCDs
+    uint32_t *ctrl;  // nbands * BAND_CTRL counters, zeroed per batch
+    double *phi[BAND_MAXK + 1];
+    int64_t *n[BAND_MAXK + 1];
+};
+
 // (FArgs::progress) the launch has started: every earlier launch of its stream has finished
 __device__ __forceinline__ void note_progress(const FArgs &A) {
     if (A.progress && blockIdx.x == 0 && threadIdx.x == 0)
@@ -113,7 +137,8 @@ AbortInfo read_abort(sv_ctx *ctx);  // synchronizes the stream
 void clear_abort(sv_ctx *ctx);
 // Before a batch, in ONE launch: the abort flag and report count, and up to two arrays (multiples of 8 bytes) zeroed
 // -- each small hipMemsetAsync is a blit of its own on the queue (~4.5 us of GPU time apiece in the Hammer traces)
-void reset_batch(sv_ctx *ctx, void *a, size_t a_bytes, void *b = nullptr, size_t b_bytes = 0);
+// (and, given one, a gate word set to INT32_MAX: no sweep has reported)
+void reset_batch(sv_ctx *ctx, void *a, size_t a_bytes, void *b = nullptr, size_t b_bytes = 0, int32_t *gate = nullptr);
 int64_t rejections_in(const SkipMap &skips, int sweep, int nblocks);
 int fused_th(int32_t N, int nsx);  // rows per strip (SV_FUSED_TH overrides)
 // launch one tile-mode sweep with `grid` workgroups: villain_sweep_hot when `hot` (the sweep passes hot_ok),
@@ -132,6 +157,9 @@ void launch_hot_skip(const FArgs &A, int grid, hipStream_t stream);
 // villain_sweep_hot's default descending strip table for H rows and nsx column strips ({ix, t0, t1} per strip)
 std::vector<int32_t> band_strips(int32_t H, int nsx);
 void launch_hot(const FArgs &A, int grid, hipStream_t stream);
+// the band launch (8-wave strips of B.TH rows); band_residency: how many of its workgroups one CU holds at once
+void launch_hot_band(const FArgs &A, const BandArgs &B, hipStream_t stream);
+int band_residency();
 // full-row replica batches (config 5) on the fast-draw kernel: whether N qualifies, and the launch (the sweep must
 // pass hot_ok for every replica: no skips, no buffered half-word, choice values in range)
 bool hot_fr_ok(int32_t N);

@@ -20,6 +20,7 @@
 //   dS_link:                ((kappa/2) * cr) * ((2*r) + cr)            (neighborhood.py:111)
 //   face_sum:               (((0 + f0[x]) + f0[x-e0]) + f1[x]) + f1[x-e1]  (reference.py:48-64)
 //   r update:               (r + d(cphi)) - (2pi)*cn                  (neighborhood.py:129)
+#include <atomic>
 #include <thread>
 #include <chrono>
 #include <cstdio>
@@ -754,21 +755,23 @@ AbortInfo read_abort_stats(sv_ctx *ctx, int count, sv_stats *stats) {
 }
 
 __global__ __launch_bounds__(256) void reset_batch_kernel(int32_t *abort, uint32_t *nreport, uint64_t *a, int64_t na,
-                                                         uint64_t *b, int64_t nb) {
+                                                         uint64_t *b, int64_t nb, int32_t *gate) {
     const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
     if (t == 0) {
         *abort = 0;
         *nreport = 0;
+        if (gate) *gate = INT32_MAX;
     }
     for (int64_t i = t; i < na; i += stride) a[i] = 0;
     for (int64_t i = t; i < nb; i += stride) b[i] = 0;
 }
 
-void reset_batch(sv_ctx *ctx, void *a, size_t a_bytes, void *b, size_t b_bytes) {
+void reset_batch(sv_ctx *ctx, void *a, size_t a_bytes, void *b, size_t b_bytes, int32_t *gate) {
     if (a_bytes % 8 || b_bytes % 8) throw std::logic_error("reset_batch: sizes must be multiples of 8 bytes");
     const int64_t na = (int64_t)(a_bytes / 8), nb = (int64_t)(b_bytes / 8), n = std::max(na, nb);
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 256));
-    reset_batch_kernel<<<grid, 256, 0, ctx->stream>>>(ctx->d_abort, ctx->d_nreport, (uint64_t *)a, na, (uint64_t *)b, nb);
+    reset_batch_kernel<<<grid, 256, 0, ctx->stream>>>(ctx->d_abort, ctx->d_nreport, (uint64_t *)a, na, (uint64_t *)b, nb,
+                                                      gate);
 }
 
 void clear_abort(sv_ctx *ctx) {
@@ -947,6 +950,9 @@ std::vector<int32_t> band_strips(int32_t H, int nsx) {
 }
 
 // returns false if the fused path cannot represent the state (|n| too large): caller falls back
+// set once a band launch has failed (BAND_FAIL_BLOCK): the process's small lattices then run one sweep per launch
+static std::atomic<bool> band_broken{false};
+
 bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u128 inc, sv_stats *stats,
                int &done_sweeps) {
     sv_ctx *ctx = st->ctx;
@@ -1009,6 +1015,48 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             st->strips_key = spec;
         }
     }
+    // Small lattices: K sweeps per launch, one band of rows per XCD (villain_sweep_hot_band, BandArgs in villain.h).
+    // SV_BAND_K sets K (odd, at most BAND_MAXK; 0 disables); the band's workgroups must all be resident on its XCD.
+    const int nbands = 8;
+    int bandK = 0, bandP = 0;
+    {
+        static const int band_env = [] {
+            const char *e = getenv("SV_BAND_K");
+            return e ? atoi(e) : -1;
+        }();
+        static const int cus = [] {
+            int dev = 0, v = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+                v = 0;
+            return v;
+        }();
+        if (use_hot && small8 && hot_nw == 8 && band_env != 0 && !band_broken.load() && N % nbands == 0 && N <= 512) {
+            const int own = N / nbands, per_xcd = band_residency() * (cus / nbands);
+            int K = std::min(band_env > 0 ? band_env : 7, BAND_MAXK);
+            if (K % 2 == 0) K--;
+            for (; K >= 3; K -= 2) {
+                const int P = nsx * ((own + 5 * (K - 1) + TH - 1) / TH);
+                if (P <= per_xcd && own + 5 * (K - 1) <= N) {
+                    bandK = K;
+                    bandP = P;
+                    break;
+                }
+            }
+        }
+        if (bandK) {
+            while ((int)st->band_phi.size() < bandK - 1) {
+                double *p = nullptr;
+                int64_t *q = nullptr;
+                SV_HIP(hipMalloc(&p, V * sizeof(double)));
+                st->band_phi.push_back(p);
+                SV_HIP(hipMalloc(&q, 2 * V * sizeof(int64_t)));
+                st->band_n.push_back(q);
+            }
+            if (!st->band_ctrl) SV_HIP(hipMalloc(&st->band_ctrl, (nbands * BAND_CTRL + 64) * sizeof(uint32_t)));
+        }
+    }
+    int32_t *band_gate = bandK ? (int32_t *)(st->band_ctrl + nbands * BAND_CTRL) : nullptr;  // (null: no gate)
     // |n| beyond villain_sweep_hot's int16 image: the failing sweep is replayed, and the rest of the call runs, on
     // villain_sweep_fused's int32 image; only an overflow of that one falls back to the per-colour int64 path
     bool hot_off = false;
@@ -1017,7 +1065,12 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         Cursor c = cur;
         // the batch reset first: the device clears the flags and statistics while the host plans
         ctx->ensure_stats(count);
-        reset_batch(ctx, ctx->d_stats, count * sizeof(sv_stats));
+        if (bandK)
+            reset_batch(ctx, ctx->d_stats, count * sizeof(sv_stats), st->band_ctrl, nbands * BAND_CTRL * sizeof(uint32_t),
+                        band_gate);
+        else
+            reset_batch(ctx, ctx->d_stats, count * sizeof(sv_stats));
+        std::vector<int> band_starts;  // first sweeps of this batch's band launches
         auto tp0 = std::chrono::steady_clock::now();
         plan_sweeps(ctx, c, inc, specs, sw, count, skips, blocks, skipvec);
         auto tp1 = std::chrono::steady_clock::now();
@@ -1045,7 +1098,11 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         __atomic_store_n(ctx->h_prog, 0, __ATOMIC_RELEASE);  // (the previous batch's launches have all finished)
         int next_chunk = CH;
         for (int k = 0; k < count;) {
-            const bool hot_k = use_hot && !hot_off && NWv == 4 && hot_ok(P, &blocks[(size_t)k * nb]);
+            // a band launch: the next K sweeps all pass hot_ok
+            bool band_k = bandK && !hot_off && k + bandK <= count;
+            for (int j = 0; band_k && j < bandK; j++) band_k = hot_ok(P, &blocks[(size_t)(k + j) * nb]);
+            const int step = band_k ? bandK : 1;
+            const bool hot_k = band_k || (use_hot && !hot_off && NWv == 4 && hot_ok(P, &blocks[(size_t)k * nb]));
             // a sweep with known rejections (a replay) or unequal buffered-half pairs: the hot kernel's skip form
             const bool skip_k = !hot_k && use_hot && !hot_off && NWv == 4 && hot_nw == 4 &&
                                 hot_skip_ok(P, &blocks[(size_t)k * nb]);
@@ -1078,8 +1135,36 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             A.S.hflag = ctx->d_flag;
             A.progress = ctx->d_prog;
             A.sweep = (uint32_t)k;
+            A.S.gate = band_gate;  // (band batches: a report gates the later launches by sweep)
             farg_single(A, nsx, nsy);
-            if (hot_k) {
+            if (band_k) {
+                A.hot_nw = 8;
+                A.adv[0] = adv8[0];
+                A.adv[1] = adv8[1];
+                A.adv[2] = adv8[2];
+                BandArgs B;
+                B.K = bandK;
+                B.P = bandP;
+                B.own = N / nbands;
+                B.TH = TH;
+                B.gen = (int32_t)band_starts.size();
+                B.nb = nb;
+                B.nbands = nbands;
+                B.ctrl = st->band_ctrl;
+                B.phi[0] = st->phi[st->cur ^ (k & 1)];
+                B.n[0] = st->n[st->cur ^ (k & 1)];
+                for (int j = 1; j < bandK; j++) {
+                    B.phi[j] = st->band_phi[j - 1];
+                    B.n[j] = st->band_n[j - 1];
+                }
+                B.phi[bandK] = st->phi[st->cur ^ (k & 1) ^ 1];  // (K odd: the buffer k + K reads)
+                B.n[bandK] = st->n[st->cur ^ (k & 1) ^ 1];
+                launch_hot_band(A, B, ctx->stream);
+                band_starts.push_back(k);
+                ctx->sweeps_hot += bandK;
+                ctx->sweeps_band += bandK;
+                ctx->launches_band++;
+            } else if (hot_k) {
                 if (hot_nw == 8) {
                     A.hot_nw = 8;
                     A.adv[0] = adv8[0];
@@ -1102,10 +1187,10 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                 else villain_sweep_fused<4, false, false, false><<<grid, 4 * 64, 0, ctx->stream>>>(A);
             }
             if (per_launch && seg) {
-                ctx->time_end(seg, 1, k);
+                ctx->time_end(seg, step, k);
                 seg = nullptr;
             }
-            k++;
+            k += step;
             if (k >= next_chunk && k < count) {
                 const int j = next_chunk / CH - 1;  // chunk j is enqueued
                 next_chunk += CH;
@@ -1161,15 +1246,56 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             set_current(count);
             continue;
         }
+        // A failing sweep inside a band launch: the state before it is that launch's scratch output, not one of the
+        // ping-pong pair -- copied to the buffer the replay reads (after set_current)
+        auto restore_band = [&](int bad) {
+            for (int k0 : band_starts) {
+                if (bad > k0 && bad < k0 + bandK) {
+                    const int j = bad - k0;
+                    SV_HIP(hipMemcpyAsync(st->phi[st->cur], st->band_phi[j - 1], V * sizeof(double),
+                                          hipMemcpyDeviceToDevice, ctx->stream));
+                    SV_HIP(hipMemcpyAsync(st->n[st->cur], st->band_n[j - 1], 2 * V * sizeof(int64_t),
+                                          hipMemcpyDeviceToDevice, ctx->stream));
+                }
+            }
+        };
         // earliest failing (sweep, block); an overflow tag sorts after every rejection of its sweep
         uint32_t first_bad = ~0u;
-        bool overflow = false;
+        bool overflow = false, band_fail = false;
         {
             std::pair<uint32_t, uint32_t> best{~0u, ~0u};
             for (const Report &r : a.reports)
                 if (std::make_pair(r.sweep, r.block) < best) best = {r.sweep, r.block};
             first_bad = best.first;
             overflow = best.second == OVERFLOW_BLOCK;
+            band_fail = best.second == BAND_FAIL_BLOCK;
+        }
+        if (band_fail) {
+            // a band launch could not run as planned (tagged with its first sweep, whose input is intact): the
+            // sweeps before it stand, and band launches are off for the rest of the process
+            if (!band_broken.exchange(true))
+                fprintf(stderr, "[sv] multi-sweep band launch failed (workgroups not spread over %d XCDs as planned, "
+                                "or a band barrier timed out); single-sweep launches from here on\n", nbands);
+            const int bad = (int)first_bad;
+            if (bad > 0) {
+                Cursor c2 = cur;
+                std::vector<Block> b2;
+                std::vector<uint32_t> s2;
+                plan_sweeps(ctx, c2, inc, specs, sw, bad, skips, b2, s2);
+                SV_HIP(hipMemcpyAsync(stats + sw, ctx->d_stats, bad * sizeof(sv_stats), hipMemcpyDeviceToHost,
+                                      ctx->stream));
+                SV_HIP(hipStreamSynchronize(ctx->stream));
+                for (int k = 0; k < bad; k++) {
+                    stats[sw + k].proposed = V;
+                    stats[sw + k].rejections = rejections_in(skips, sw + k, nb);
+                }
+                cur = c2;
+            }
+            set_current(bad);
+            sw += bad;
+            bandK = 0;
+            band_gate = nullptr;
+            continue;
         }
         if (overflow) {
             const int bad = (int)first_bad;
@@ -1194,6 +1320,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                 cur = c2;
             }
             set_current(bad);
+            restore_band(bad);
             if (to_int32) {
                 hot_off = true;
                 sw += bad;
@@ -1225,6 +1352,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             cur = c2;
         }
         set_current(bad);
+        restore_band(bad);
         sw += bad;
     }
     done_sweeps = sweeps;
@@ -1281,6 +1409,9 @@ int sv_villain_destroy(sv_villain *st) {
     if (st->h_aux) (void)hipHostFree(st->h_aux);
     if (st->d_obs) (void)hipFree(st->d_obs);
     if (st->d_strips) (void)hipFree(st->d_strips);
+    for (double *p : st->band_phi) (void)hipFree(p);
+    for (int64_t *p : st->band_n) (void)hipFree(p);
+    if (st->band_ctrl) (void)hipFree(st->band_ctrl);
     if (st->h_obs) (void)hipHostFree(st->h_obs);
     const hipError_t ee = st->emitter.release();
     if (ee != hipSuccess && !rc) {

@@ -49,6 +49,9 @@ namespace sv {
 // [5] = row bases ready (prologue split)
 constexpr int WGT = 6;
 __device__ uint64_t g_wgtime[65536 * WGT];
+// band launches: per (band slot, sweep) entry, row bases, loop start, loop end, exit, barrier passed, HW_ID, XCC_ID
+constexpr int BT = 8, BT_SW = 16;
+__device__ uint64_t g_bandtime[8 * 128 * BT_SW * BT];
 __device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 #endif
 
@@ -170,6 +173,12 @@ struct HotLDST {
     std::conditional_t<OBSL, HotEmpty, uint32_t[2][4][HOT_MAXSK]> sk;
     double obs[4];     // OBS: the workgroup's sums of the inline observables
     std::conditional_t<OBSL, ObsLane, HotEmpty> ol;
+    // band launches (8-wave workgroups): the workgroup's statistics per sweep of the launch, flushed once at its end
+    struct BandStats {
+        unsigned long long acc[16];
+        double ps[16];
+    };
+    std::conditional_t<NWL == 8, BandStats, HotEmpty> bst;
 };
 using HotLDS = HotLDST<false>;
 
@@ -191,11 +200,36 @@ __device__ __forceinline__ int logical_block() {
     return xcd * per + (xcd < rem ? xcd : rem) + k;
 }
 
-template <bool TILE, bool EDGE, bool FR = false, bool OBS = false, bool PH = false, int NWT = 4, bool SKIP = false>
-__device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, NWT> &Ls, int bl) {
+// BAND (villain_sweep_hot_band): one sweep of a multi-sweep launch -- the strip and the counted rows come from the
+// caller, the LDS tables are filled only by the launch's first sweep, and no progress / cancellation checks
+struct HotBand {
+    int32_t ix, t0, t1;   // column strip and rows (lattice rows, may lie outside [0, Nt): they wrap)
+    int32_t q_lo, q_hi;   // rows counted in the statistics (the band's own)
+    bool first;           // the launch's first sweep: fill the LDS tables
+    // the sweep's own descriptors, buffers, statistics slot and number (FArgs holds the launch's first sweep)
+    const Block *blocks;
+    const double *phi_in;
+    const int64_t *n_in;
+    double *phi_out;
+    int64_t *n_out;
+    sv_stats *stat;
+    uint32_t sweep;
+    int32_t j;            // the sweep's index within the launch (its statistics slot in LDS)
+    int32_t tslot;        // SV_WGTIME: the (slot, sweep) record of g_bandtime
+    // the workgroup's strip in the launch's next sweep (next_t0 < next_t1), or none: its row bases are jumped to at the
+    // end of this sweep, so that the jumps' latency overlaps the last stores and the barrier
+    int32_t next_t0, next_t1;
+    const Block *next_blocks;
+};
+
+template <bool TILE, bool EDGE, bool FR = false, bool OBS = false, bool PH = false, int NWT = 4, bool SKIP = false,
+          bool BAND = false>
+__device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, NWT> &Ls, int bl,
+                                         const HotBand *hb = nullptr) {
     static_assert(!(FR && TILE), "full-row replica strips are periodic");
     static_assert(!SKIP || (EDGE && !FR && !PH), "skip lists: the unpaired (edge) draws of single lattices and tiles");
     static_assert(NWT == 4 || (NWT == 8 && !FR && !PH), "8-wave strips: single lattices and tiles");
+    static_assert(!BAND || (!TILE && !FR && !PH && !SKIP), "band sweeps: periodic single lattices");
     constexpr int NW = NWT;
     constexpr int R = HotLDST<PH, FR && OBS, NWT>::R, RR = HotLDST<PH, FR && OBS, NWT>::RR;
     // rows move by 32-bit byte offsets from the uniform bases: the hosts keep every offset below 2^32 on this kernel
@@ -212,8 +246,8 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     auto &s_base = Ls.base;
     int32_t &s_bad = Ls.bad;
 
-    if constexpr (!PH) note_progress(A);  // (FArgs::progress: the chunked enqueues of single lattices and replica batches)
-    if (sweep_cancelled(A.S, A.sweep)) return;
+    if constexpr (!PH && !BAND) note_progress(A);  // (FArgs::progress: the chunked enqueues of single lattices and replica batches)
+    if (!BAND && sweep_cancelled(A.S, A.sweep)) return;
 #if SV_WGTIME
     const uint64_t wg_t0 = rt_now();
 #endif
@@ -231,14 +265,19 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     const int slot = FR ? __builtin_amdgcn_readfirstlane(b / A.tiles_per_rep) : 0;  // uniform: keep it scalar
     if (FR) b = __builtin_amdgcn_readfirstlane(b - slot * A.tiles_per_rep);
     const int rep = FR && A.rep_map ? __builtin_amdgcn_readfirstlane(A.rep_map[slot]) : slot;
-    const Block *blocks = FR ? A.blocks + (int64_t)rep * A.rep_blocks : A.blocks;
+    const Block *blocks = BAND ? hb->blocks : (FR ? A.blocks + (int64_t)rep * A.rep_blocks : A.blocks);
     const JumpTables *Tb = FR ? A.Trep[rep] : A.T;
-    const double *phi_in = FR ? A.phi_in + rep * A.rep_field : A.phi_in;
-    const int64_t *n_in = FR ? A.n_in + 2 * rep * A.rep_field : A.n_in;
-    double *phi_out = FR ? A.phi_out + rep * A.rep_field : A.phi_out;
-    int64_t *n_out = FR ? A.n_out + 2 * rep * A.rep_field : A.n_out;
+    const double *phi_in = BAND ? hb->phi_in : (FR ? A.phi_in + rep * A.rep_field : A.phi_in);
+    const int64_t *n_in = BAND ? hb->n_in : (FR ? A.n_in + 2 * rep * A.rep_field : A.n_in);
+    double *phi_out = BAND ? hb->phi_out : (FR ? A.phi_out + rep * A.rep_field : A.phi_out);
+    int64_t *n_out = BAND ? hb->n_out : (FR ? A.n_out + 2 * rep * A.rep_field : A.n_out);
+    const uint32_t sweep_id = BAND ? hb->sweep : A.sweep;
     int ix, t0s, t1s;
-    if (!FR && A.strips) {
+    if (BAND) {
+        ix = hb->ix;
+        t0s = hb->t0;
+        t1s = hb->t1;
+    } else if (!FR && A.strips) {
         ix = __builtin_amdgcn_readfirstlane(A.strips[3 * b]);
         t0s = __builtin_amdgcn_readfirstlane(A.strips[3 * b + 1]);
         t1s = __builtin_amdgcn_readfirstlane(A.strips[3 * b + 2]);
@@ -251,7 +290,8 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     const int32_t w = x1 - x0;
     const int32_t t0 = t0s, t1 = t1s;
     // the sites this strip counts in the statistics (its own, within the launch's owned window)
-    const int32_t q_lo = TILE && A.own_r0 > t0 ? A.own_r0 : t0, q_hi = TILE && A.own_r1 < t1 ? A.own_r1 : t1;
+    const int32_t q_lo = BAND ? (hb->q_lo > t0 ? hb->q_lo : t0) : (TILE && A.own_r0 > t0 ? A.own_r0 : t0);
+    const int32_t q_hi = BAND ? (hb->q_hi < t1 ? hb->q_hi : t1) : (TILE && A.own_r1 < t1 ? A.own_r1 : t1);
     const int32_t c_lo = TILE && A.own_c0 > x0 ? A.own_c0 : x0, c_hi = TILE && A.own_c1 < x1 ? A.own_c1 : x1;
     // global column origin of this strip: its first column wrapped onto the torus, so that X0s + x stays within
     // [-2, Nx + 126) on the strip wherever the launch's region starts (deep-halo regions start anywhere)
@@ -271,11 +311,13 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     const int32_t xw = gx0 - 2 < 0 ? Nx - 2 : 0;
 
     if constexpr (!PH) {
-        for (int e = threadIdx.x; e < SMALL_LDS; e += NW * 64) {
-            s_small.A[e] = Tb->small[e].A;
-            s_small.C[e] = Tb->small[e].C;
+        if (!BAND || hb->first) {
+            for (int e = threadIdx.x; e < SMALL_LDS; e += NW * 64) {
+                s_small.A[e] = Tb->small[e].A;
+                s_small.C[e] = Tb->small[e].C;
+            }
+            if (threadIdx.x < 3) s_adv[threadIdx.x] = FR ? A.advrep[3 * rep + threadIdx.x] : A.adv[threadIdx.x];
         }
-        if (threadIdx.x < 3) s_adv[threadIdx.x] = FR ? A.advrep[3 * rep + threadIdx.x] : A.adv[threadIdx.x];
     }
     if (threadIdx.x == 0) s_bad = 0;
     if (OBS && threadIdx.x < 4) Ls.obs[threadIdx.x] = 0.0;
@@ -397,10 +439,12 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     int32_t brow = tfirst + 2 - bc + wave;  // colour 0 row t+2+wave, colour 1 row t+1+wave
     int32_t brow1 = tfirst + 1 + wave;      // the colour-1 row, wave-uniform
     if constexpr (!PH) {  // (the running bases live in LDS only: the advance reads them back)
-        u128 bases{0, 0};
-        if (base_lane) bases = full_jump(Tb, &blocks[bblk], (uint32_t)base_pos(bty, grow(brow), Nx, bx, bhas));
-        __builtin_amdgcn_s_waitcnt(0);
-        if (base_lane) s_base[wave][lane] = bases;
+        if (!BAND || hb->first) {  // (a band sweep after the first: its predecessor jumped to them)
+            u128 bases{0, 0};
+            if (base_lane) bases = full_jump(Tb, &blocks[bblk], (uint32_t)base_pos(bty, grow(brow), Nx, bx, bhas));
+            __builtin_amdgcn_s_waitcnt(0);
+            if (base_lane) s_base[wave][lane] = bases;
+        }
     }
 #if SV_WGTIME
     const uint64_t wg_tb = rt_now();
@@ -535,7 +579,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
 #pragma unroll
             for (int j = 0; j < 4; j++)
                 if ((uint32_t)((uint64_t)D.w[j] * kc) < thr)
-                    report(A.S, A.sweep, (uint32_t)(1 + 5 * c + 1 + j), SKIP ? spos[j] : rank, (uint32_t)rep);
+                    report(A.S, sweep_id, (uint32_t)(1 + 5 * c + 1 + j), SKIP ? spos[j] : rank, (uint32_t)rep);
         }
     };
 
@@ -700,11 +744,42 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
         while (tl + NW < t1) tl += NW;
         store_rows(tl);
     }
-    if (s_bad && threadIdx.x == 0) report(A.S, A.sweep, OVERFLOW_BLOCK, 0, (uint32_t)rep);
-    flush_stats(FR ? A.stat + (int64_t)rep * A.rep_stat : A.stat, acc_count, psum);
+    if constexpr (BAND) {
+        // the next sweep's row bases (this wave's own LDS entries, free once its last row step is done)
+        if (hb->next_t0 < hb->next_t1) {
+            const int32_t nbrow = hb->next_t0 - 3 + 2 - bc + wave;
+            const uint32_t nhas = (base_lane && bty >= 2) ? hb->next_blocks[bblk].has : 0u;
+            u128 bases{0, 0};
+            if (base_lane)
+                bases = full_jump(Tb, &hb->next_blocks[bblk], (uint32_t)base_pos(bty, grow(nbrow), Nx, bx, nhas));
+            if (base_lane) s_base[wave][lane] = bases;
+        }
+    }
+    if (s_bad && threadIdx.x == 0) report(A.S, sweep_id, OVERFLOW_BLOCK, 0, (uint32_t)rep);
+    if constexpr (BAND) {
+        // into the workgroup's per-sweep slots (LDS); band_sweeps adds them to the sweeps' statistics at the end
+        unsigned long long a = (unsigned long long)acc_count;
+        for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+        const double ps = wave_sum(psum);
+        if (lane == 0) {
+            atomicAdd(&Ls.bst.acc[hb->j], a);
+            atomicAdd(&Ls.bst.ps[hb->j], ps);
+        }
+    } else {
+        flush_stats(FR ? A.stat + (int64_t)rep * A.rep_stat : A.stat, acc_count, psum);
+    }
 #if SV_WGTIME
     __builtin_amdgcn_s_waitcnt(0);
-    if (threadIdx.x == 0 && blockIdx.x < 65536) {
+    if (BAND && threadIdx.x == 0 && hb->tslot >= 0 && hb->tslot < 8 * 128 * BT_SW) {
+        uint64_t *o = g_bandtime + BT * (size_t)hb->tslot;
+        o[0] = wg_t0;
+        o[1] = wg_tb;
+        o[2] = wg_t1;
+        o[3] = wg_t2;
+        o[4] = rt_now();
+        o[6] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+        o[7] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11));
+    } else if (!BAND && threadIdx.x == 0 && blockIdx.x < 65536) {
         uint64_t *o = g_wgtime + WGT * (size_t)blockIdx.x;
         o[0] = wg_t0;
         o[1] = wg_t1;
@@ -765,6 +840,118 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4
 template __global__ void villain_sweep_hot_skip<false>(FArgs);
 template __global__ void villain_sweep_hot_skip<true>(FArgs);
 
+// ---- multi-sweep band launches of small periodic lattices (BandArgs, villain.h)
+// The XCD-local barrier between two sweeps of a band: every wave's stores acknowledged by the L2, one arrival per
+// workgroup, then a spin (compare-exchange: a read-modify-write, so it executes in the L2 and never sees a stale L1
+// line) until the band's P workgroups have arrived, and this CU's L1 invalidated so that the next sweep's rows come
+// from the L2.  Workgroup-scope atomics stay in the XCD's own L2, which every member of the band shares; nothing here
+// crosses XCDs (the cross-XCD barrier of round 2 paid an L2 write-back per workgroup and cost more than the launch it
+// saved).  A barrier that has waited 20 ms (the band's workgroups not all resident) gives up.
+__device__ __forceinline__ bool band_barrier(uint32_t *cnt, uint32_t target) {
+    __shared__ int32_t s_ok;
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        int ok = 1;
+        for (;;) {
+            uint32_t v = 0xFFFFFFFFu;
+            __hip_atomic_compare_exchange_strong(cnt, &v, 0xFFFFFFFFu, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (v >= target) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000u) {  // 20 ms at 100 MHz
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        asm volatile("buffer_inv sc0" ::: "memory");
+        s_ok = ok;
+    }
+    __syncthreads();
+    return s_ok != 0;
+}
+
+// workgroup i of a band: column strip i % nsx, row strip i / nsx of each sweep's region (the band's rows extended by
+// 2e above and 3e below, e = K-1-j, cut into ceil(rows / TH) strips of at most TH rows; a row strip the shrinking
+// region no longer has leaves the workgroup idle at the barriers)
+template <bool EDGE, int NWT>
+__device__ __forceinline__ void band_sweeps(const FArgs &A, const BandArgs &B, HotLDST<false, false, NWT> &Ls, int band,
+                                            int i) {
+    const int ix = i % A.nsx, r = i / A.nsx;
+    uint32_t *bar = B.ctrl + BAND_CTRL * band + 32;
+    // this workgroup's row strip of sweep j (empty when the shrinking region has no row strip r)
+    auto strip = [&](int j, int32_t &t0, int32_t &t1) {
+        const int32_t e = B.K - 1 - j, R0 = band * B.own - 2 * e, H = B.own + 5 * e, nr = (H + B.TH - 1) / B.TH;
+        t0 = r < nr ? R0 + r * H / nr : 0;
+        t1 = r < nr ? R0 + (r + 1) * H / nr : 0;
+    };
+    if (threadIdx.x < 16) {
+        Ls.bst.acc[threadIdx.x] = 0;
+        Ls.bst.ps[threadIdx.x] = 0.0;
+    }
+    for (int j = 0; j < B.K; j++) {
+        int32_t t0, t1, n0 = 0, n1 = 0;
+        strip(j, t0, t1);
+        if (j + 1 < B.K) strip(j + 1, n0, n1);
+        if (t0 < t1) {
+            const HotBand hb{ix, t0, t1, band * B.own, (band + 1) * B.own, j == 0,
+                             A.blocks + (int64_t)j * B.nb, B.phi[j], B.n[j], B.phi[j + 1], B.n[j + 1], A.stat + j,
+                             A.sweep + (uint32_t)j, j, (band * B.P + i) * 16 + j, n0, n1, A.blocks + (int64_t)(j + 1) * B.nb};
+            hot_body<false, EDGE, false, false, false, NWT, false, true>(A, Ls, 0, &hb);
+        }
+        if (j + 1 < B.K && !band_barrier(bar, (uint32_t)((B.gen * (B.K - 1) + j + 1) * B.P))) {
+            if (threadIdx.x == 0) report(A.S, A.sweep, BAND_FAIL_BLOCK, 0);
+            return;
+        }
+#if SV_WGTIME
+        if (threadIdx.x == 0 && (band * B.P + i) < 8 * 128) g_bandtime[BT * (size_t)((band * B.P + i) * BT_SW + j) + 5] = rt_now();
+#endif
+    }
+    // the launch's statistics: one lane per sweep (each sweep's sum over workgroups is order-free for the count;
+    // the acceptance sums add in any order, as flush_stats' atomics do)
+    __syncthreads();
+    if (threadIdx.x < B.K && (Ls.bst.acc[threadIdx.x] || Ls.bst.ps[threadIdx.x] != 0.0)) {
+        atomicAdd((unsigned long long *)&A.stat[threadIdx.x].accepted, Ls.bst.acc[threadIdx.x]);
+        unsafeAtomicAdd(&A.stat[threadIdx.x].acceptance_sum, Ls.bst.ps[threadIdx.x]);
+    }
+}
+
+template <int NWT>
+__global__ __launch_bounds__(NWT * 64) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4 ? 4 : 3))) void villain_sweep_hot_band(
+    FArgs A, BandArgs B) {
+    __shared__ HotLDST<false, false, NWT> Ls;
+    __shared__ int32_t s_slot;
+    note_progress(A);
+    // run_fused gives band batches a gate: a launch skips only behind a sweep that reported, which this launch's own
+    // reports (sweeps >= A.sweep) never are -- so every workgroup of the launch decides alike
+    if (sweep_cancelled(A.S, A.sweep)) return;
+    if (threadIdx.x == 0) {
+        // the band is this workgroup's XCD; its place in the band, a ticket from that XCD's counter
+        const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11)) & 0xFu;  // HW_REG_XCC_ID
+        int32_t slot = -1;
+        if ((int32_t)xcc < B.nbands) {
+            const int32_t t = (int32_t)__hip_atomic_fetch_add(B.ctrl + BAND_CTRL * xcc, 1u, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_WORKGROUP) - B.gen * B.P;
+            if (t >= 0 && t < B.P) slot = (int32_t)xcc * B.P + t;
+        }
+        s_slot = slot;
+    }
+    __syncthreads();
+    const int slot = s_slot;
+    if (slot < 0) {  // more workgroups on this XCD than the plan has places: some band stays short
+        if (threadIdx.x == 0) report(A.S, A.sweep, BAND_FAIL_BLOCK, 0);
+        return;
+    }
+    const int band = slot / B.P, i = slot % B.P, ix = i % A.nsx;
+    const int32_t x0 = (int32_t)((int64_t)ix * A.G.Wt / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * A.G.Wt / A.nsx);
+    const bool interior = x0 >= 4 && x1 + 2 < A.G.Nx;
+    if (__builtin_amdgcn_readfirstlane((int)interior)) band_sweeps<false, NWT>(A, B, Ls, band, i);
+    else band_sweeps<true, NWT>(A, B, Ls, band, i);
+}
+template __global__ void villain_sweep_hot_band<8>(FArgs, BandArgs);
+
 template __global__ void villain_sweep_hot<false, 4>(FArgs);
 template __global__ void villain_sweep_hot<true, 4>(FArgs);
 template __global__ void villain_sweep_hot<false, 8>(FArgs);
@@ -802,6 +989,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_PH_O
 #if SV_WGTIME
 extern "C" int sv_debug_wgtime(uint64_t *out, int32_t n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(sv::g_wgtime), (size_t)n * sv::WGT * sizeof(uint64_t)) == hipSuccess ? 0 : -2;
+}
+// g_bandtime: [slot][sweep < 16][8] (slot = band * P + i)
+extern "C" int sv_debug_bandtime(uint64_t *out, int32_t slots) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(sv::g_bandtime), (size_t)slots * sv::BT_SW * sv::BT * sizeof(uint64_t)) == hipSuccess ? 0 : -2;
 }
 #endif
 
@@ -855,6 +1046,19 @@ void launch_hot_fr(const FArgs &A, int grid, bool obs, hipStream_t stream) {
 }
 
 void launch_hot_ph(const FArgs &A, int grid, hipStream_t stream) { villain_sweep_hot_ph<<<grid, 4 * 64, 0, stream>>>(A); }
+
+void launch_hot_band(const FArgs &A, const BandArgs &B, hipStream_t stream) {
+    villain_sweep_hot_band<8><<<B.nbands * B.P, 8 * 64, 0, stream>>>(A, B);
+}
+
+int band_residency() {
+    static const int n = [] {
+        int v = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, villain_sweep_hot_band<8>, 8 * 64, 0) != hipSuccess) v = 0;
+        return v;
+    }();
+    return n;
+}
 
 void launch_hot(const FArgs &A, int grid, hipStream_t stream) {
     const bool periodic =
