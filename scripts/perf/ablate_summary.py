@@ -21,20 +21,22 @@ for d in sorted(glob.glob(os.path.join(out, '*_*'))):
     per = {}
     for r in csv.DictReader(open(files[0])):
         did = r.get('Dispatch_Id')
-        per.setdefault(did, {'dur': None})
+        per.setdefault(did, {'dur': None, 'kernel': r.get('Kernel_Name')})
         per[did][r['Counter_Name']] = per[did].get(r['Counter_Name'], 0.0) + float(r['Counter_Value'])
         if r.get('Start_Timestamp') and r.get('End_Timestamp'):
             per[did]['dur'] = int(r['End_Timestamp']) - int(r['Start_Timestamp'])
-    # full dispatches only (early-exit drains are a few us)
-    durs = [p['dur'] for p in per.values() if p['dur']]
-    cut = 0.5 * max(durs) if durs else 0
-    full = [p for p in per.values() if p['dur'] and p['dur'] > cut]
+    # the most dispatched kernel (not a replay form), full dispatches only: early exits after an abort run a few us
+    # and a few hundred thousand instructions
+    kern = statistics.mode(p['kernel'] for p in per.values())
+    mine = [p for p in per.values() if p['kernel'] == kern and p['dur']]
+    top = max(p.get('SQ_INSTS_VALU', 0.0) for p in mine) if mine else 0.0
+    full = [p for p in mine if p.get('SQ_INSTS_VALU', 0.0) > 0.5 * top]
     if not full:
         continue
     med = lambda k: statistics.median(p.get(k, 0.0) for p in full)  # noqa: E731
     unit = UNITS[key.split('_')[0]]
     gui = med('GRBM_GUI_ACTIVE')
-    res[key] = {'dispatches': len(full), 'dur_us': statistics.median(p['dur'] for p in full) / 1e3,
+    res[key] = {'kernel': kern, 'dispatches': len(full), 'dur_us': statistics.median(p['dur'] for p in full) / 1e3,
                 'valu_per_unit': med('SQ_INSTS_VALU') * 64 / unit, 'salu_per_unit': med('SQ_INSTS_SALU') * 64 / unit,
                 'lds_per_unit': med('SQ_INSTS_LDS') * 64 / unit,
                 'valu_busy': med('SQ_ACTIVE_INST_VALU') * 4 / (gui / 8) / 1024 if gui else None,

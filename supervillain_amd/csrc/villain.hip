@@ -1033,7 +1033,8 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         }();
         if (use_hot && small8 && hot_nw == 8 && band_env != 0 && !band_broken.load() && N % nbands == 0 && N <= 512) {
             const int own = N / nbands, per_xcd = band_residency() * (cus / nbands);
-            int K = std::min(band_env > 0 ? band_env : 7, BAND_MAXK);
+            // (K = 3 measured best at L=256, r4: 11.8 / 12.7 / 13.7 us per sweep at K = 3 / 5 / 7, 13.7 one per launch)
+            int K = std::min(band_env > 0 ? band_env : 3, BAND_MAXK);
             if (K % 2 == 0) K--;
             for (; K >= 3; K -= 2) {
                 const int P = nsx * ((own + 5 * (K - 1) + TH - 1) / TH);

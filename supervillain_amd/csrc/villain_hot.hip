@@ -841,6 +841,9 @@ template __global__ void villain_sweep_hot_skip<false>(FArgs);
 template __global__ void villain_sweep_hot_skip<true>(FArgs);
 
 // ---- multi-sweep band launches of small periodic lattices (BandArgs, villain.h)
+#ifndef SV_BAND_CAS
+#define SV_BAND_CAS 0  // poll the band barrier with compare-exchange (r4 A/B) instead of agent-scope loads
+#endif
 // The XCD-local barrier between two sweeps of a band: every wave's stores acknowledged by the L2, one arrival per
 // workgroup, then a spin (compare-exchange: a read-modify-write, so it executes in the L2 and never sees a stale L1
 // line) until the band's P workgroups have arrived, and this CU's L1 invalidated so that the next sweep's rows come
@@ -856,9 +859,16 @@ __device__ __forceinline__ bool band_barrier(uint32_t *cnt, uint32_t target) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         int ok = 1;
         for (;;) {
+#if SV_BAND_CAS
             uint32_t v = 0xFFFFFFFFu;
             __hip_atomic_compare_exchange_strong(cnt, &v, 0xFFFFFFFFu, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+            // an agent-scope load misses the L1 and reads the L2 line the arrivals update; unlike a read-modify-write
+            // it does not queue behind the other pollers in the L2's atomic unit (r4: CAS polling spread the barrier
+            // passes of one band over ~4 us)
+            const uint32_t v = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
             if (v >= target) break;
             if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000u) {  // 20 ms at 100 MHz
                 ok = 0;

@@ -968,7 +968,8 @@ int sv_worldline_plaquette_coexact_run(sv_worldline *st, double kappa, double W_
         run_colour_sweeps(
             st, specs, sweeps, cur, inc, stats,
             [&](const Block *blocks, StatStripe *stat, uint32_t k, const Block *hblocks) {
-                if (use_wf && !st->wf_off && svh::wf_usable(st->N, st->v_is_float, W_eff, interval_t)) {
+                if (use_wf && !st->wf_off && svh::wf_usable(st->N, st->v_is_float, W_eff, interval_t) &&
+                    N * N < (int64_t(1) << 28)) {  // (launch_wf's 32-bit row offsets)
                     // one launch for the whole step (worldline_fused.hip); it writes the other buffer pair
                     const int64_t V = N * N;
                     svh::launch_wf(FGeom{(int32_t)N, (int32_t)N, 0, 0, (int32_t)N, (int32_t)N, N, V, 0}, kappa, W_eff,

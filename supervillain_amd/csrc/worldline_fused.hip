@@ -177,10 +177,12 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
 #pragma unroll
             for (int k = 0; k < PF; k++) {
                 if (lane + 64 * k < cols) {
-                    const int64_t g = g0 + pf_gx[k];
-                    pf_m0[k] = A.m_in[g];
-                    pf_m1[k] = A.m_in[V + g];
-                    pf_v[k] = A.v_in[g];
+                    // 32-bit byte offsets from the uniform bases (global_load's SGPR-base form; launch_wf keeps
+                    // 16 plane < 2^32)
+                    const uint32_t o = ((uint32_t)g0 + (uint32_t)pf_gx[k]) * 8u;
+                    pf_m0[k] = *(const int64_t *)((const char *)A.m_in + o);
+                    pf_m1[k] = *(const int64_t *)((const char *)A.m_in + (o + (uint32_t)V * 8u));
+                    pf_v[k] = *(const int64_t *)((const char *)A.v_in + o);
                 }
             }
         }
@@ -194,9 +196,11 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
             for (int k = 0; k < PF; k++) {
                 const int cx = lane + 64 * k;
                 if (cx < cols) {
-                    // the int32 image must hold the fields exactly, with headroom for one step's changes
-                    bad |= (uint32_t)((uint64_t)((pf_m0[k] >> 30) + 1) > 1) | (uint32_t)((uint64_t)((pf_m1[k] >> 30) + 1) > 1) |
-                           (uint32_t)((uint64_t)((pf_v[k] >> 30) + 1) > 1);
+                    // the int32 image must hold the fields exactly, with headroom for one step's changes: -2^30 <= x
+                    // < 2^30, as one 64-bit add and one unsigned compare
+                    constexpr uint64_t H = uint64_t(1) << 30;
+                    bad |= (uint32_t)((uint64_t)pf_m0[k] + H >= 2 * H) | (uint32_t)((uint64_t)pf_m1[k] + H >= 2 * H) |
+                           (uint32_t)((uint64_t)pf_v[k] + H >= 2 * H);
                     s_m0[slot][cx] = (int32_t)pf_m0[k];
                     s_m1[slot][cx] = (int32_t)pf_m1[k];
                     s_v[slot][cx] = (int32_t)pf_v[k];
@@ -215,10 +219,10 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
             for (int k = 0; k < PF; k++) {
                 const int cc2 = lane + 64 * k;
                 if (cc2 < w) {
-                    const int64_t g = g0 + cc2;
-                    A.m_out[g] = (int64_t)s_m0[slot][cc2 + 5];
-                    A.m_out[V + g] = (int64_t)s_m1[slot][cc2 + 5];
-                    A.v_out[g] = (int64_t)s_v[slot][cc2 + 5];
+                    const uint32_t o = ((uint32_t)g0 + (uint32_t)cc2) * 8u;
+                    *(int64_t *)((char *)A.m_out + o) = (int64_t)s_m0[slot][cc2 + 5];
+                    *(int64_t *)((char *)A.m_out + (o + (uint32_t)V * 8u)) = (int64_t)s_m1[slot][cc2 + 5];
+                    *(int64_t *)((char *)A.v_out + o) = (int64_t)s_v[slot][cc2 + 5];
                 }
             }
         }
@@ -442,7 +446,19 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
         __syncthreads();
         coexact(3, t + wave);
         commit(t + AH);
-        if (base_lane) {
+        // The wave's four rows (t + wave .. t + 3 + wave) move NW rows down.  Unless one of them wraps around the
+        // lattice or sits on global row 0 (where a buffered half-word clamps the word index), every block's position
+        // moves by exactly its stride: one precomputed map per base lane (villain_hot.hip's SV_HOT_ADV), the
+        // position arithmetic kept off the common path by a wave-uniform test.
+        const int32_t glo = grow(t + wave);
+        if (glo >= 1 && glo + NW + 3 < Nt) {
+            if (base_lane) {
+                const Affine &ad = Ls.adv[bbnd ? 2 : 0];
+                bases = mad128c(ad.A, bases, ad.C);
+                brow += NW;
+                Ls.base[wave][lane] = bases;
+            }
+        } else if (base_lane) {
             const int64_t p_old = wf_base_pos(bbnd, grow(brow), N, bx, bhas);
             const int64_t p_new = wf_base_pos(bbnd, grow(brow + NW), N, bx, bhas);
             const int64_t step = bbnd ? (int64_t)NW * N / 4 : (int64_t)NW * N;
@@ -578,6 +594,8 @@ void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
                hipStream_t stream) {
     if ((int64_t)G.Nt * G.Nx >= (int64_t(1) << 31))
         throw std::invalid_argument("worldline_step_fused addresses stream positions with 31 bits (V < 2^31)");
+    if (G.plane >= (int64_t(1) << 28))
+        throw std::invalid_argument("worldline_step_fused moves rows by 32-bit byte offsets (plane < 2^28)");
     WFArgs A{};
     A.skips = skips;
     A.general = general ? 1 : 0;
