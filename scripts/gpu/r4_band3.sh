@@ -1,5 +1,4 @@
-# Round 4: band barrier polled with agent-scope loads -- parity tests, config 2 at K = 3, 5, 7, timeline K = 5, then
-# PC sampling of the two hot kernels (r4_pcs.sh).
+# Round 4: band barrier polled with agent-scope loads -- parity tests, config 2 at K = 3, 5, 7, timeline K = 5
 set -u
 export TMPDIR=/tmp
 O=gpurun_out/${OUT:-r4_band3}
@@ -30,4 +29,3 @@ for rep in 1 2; do
   done
 done
 unset SV_LIB_OVERRIDE
-OUT=r4_pcs bash scripts/gpu/r4_pcs.sh
