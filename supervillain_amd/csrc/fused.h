@@ -532,6 +532,11 @@ __device__ __forceinline__ u128 hot_apply(const SmallTab &sm, uint32_t i, u128 b
 #define SV_HOT_MUL24 0
 #endif
 __device__ __forceinline__ double u53(uint64_t x) {
+    if (SV_HOT_U53 == 2) {
+        // one 64-bit shift gives both halves of m = x >> 11 (h < 2^21, l < 2^32); h 2^-21 + l 2^-53 is exact
+        const uint64_t m = x >> 11;
+        return __builtin_fma((double)(uint32_t)(m >> 32), 0x1p-21, (double)(uint32_t)m * 0x1p-53);
+    }
     if (!SV_HOT_U53) return to_double(x);
     const uint32_t h = (uint32_t)(x >> 43);
     const uint32_t l = __builtin_amdgcn_alignbit((uint32_t)(x >> 32), (uint32_t)x, 11);

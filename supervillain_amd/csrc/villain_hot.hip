@@ -38,6 +38,16 @@
 #define SV_HOT_PH_OCC 4  // the counter-based kernel (29.5 KB of LDS, 81 VGPRs): 4, 5 and 6 waves/SIMD measured flat (r336)
 #endif
 
+#ifndef SV_HOT_PF_EARLY
+#define SV_HOT_PF_EARLY 0  // issue the next row step's row loads right after the commit, before the step's barrier
+#endif
+#ifndef SV_HOT_I16
+#define SV_HOT_I16 0  // n read from LDS with sign-extending loads (the value made opaque after the load)
+#endif
+#ifndef SV_HOT_BSEL
+#define SV_HOT_BSEL 0  // paired words: each lane reads the base set it draws from (per-lane LDS address), no selects
+#endif
+
 #ifndef SV_WGTIME
 #define SV_WGTIME 0  // timing experiments: per-workgroup timestamps (sv_debug_wgtime)
 #endif
@@ -72,6 +82,25 @@ __device__ __forceinline__ HotDraws hot_draws_paired(const FArgs &A, int32_t lan
         const uint32_t half = (pk >> (28 + mu)) & 1u;
         const uint64_t X = xsl_rr(hot_apply(sm, (pk >> (14 + 7 * mu)) & (SMALL_LDS - 1), half ? bs[3 + 2 * mu] : bs[2 + 2 * mu]));
         // lo lanes computed the fwd word (send its high half), hi lanes the bwd word (send its low half)
+        const uint32_t send = half ? (uint32_t)X : (uint32_t)(X >> 32);
+        const uint32_t got = pair_exchange(send, half, lane);
+        D.w[2 * mu] = half ? got : (uint32_t)X;
+        D.w[2 * mu + 1] = half ? (uint32_t)(X >> 32) : got;
+    }
+    return D;
+}
+
+// The same, each lane reading the one word base of each direction it composes with (bw: the wave's colour set in
+// LDS): a per-lane LDS address instead of two broadcast reads and four selects per direction (SV_HOT_BSEL)
+__device__ __forceinline__ HotDraws hot_draws_paired_sel(const FArgs &A, int32_t lane, uint32_t pk, const u128 *bw,
+                                                         const SmallTab &sm) {
+    HotDraws D;
+    D.u = u53(xsl_rr(hot_apply(sm, pk & (SMALL_LDS - 1), bw[0])));
+    D.dphi = A.P.lo_phi + A.P.range_phi * u53(xsl_rr(hot_apply(sm, (pk >> 7) & (SMALL_LDS - 1), bw[1])));
+#pragma unroll
+    for (int mu = 0; mu < 2; mu++) {
+        const uint32_t half = (pk >> (28 + mu)) & 1u;
+        const uint64_t X = xsl_rr(hot_apply(sm, (pk >> (14 + 7 * mu)) & (SMALL_LDS - 1), bw[2 + 2 * mu + half]));
         const uint32_t send = half ? (uint32_t)X : (uint32_t)(X >> 32);
         const uint32_t got = pair_exchange(send, half, lane);
         D.w[2 * mu] = half ? got : (uint32_t)X;
@@ -554,6 +583,8 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
             }
             (void)active;
             return;
+        } else if constexpr (!edge && SV_HOT_BSEL) {
+            D = hot_draws_paired_sel(A, lane, c == 0 ? pk0 : pk1, &s_base[wave][8 * c], s_small);
         } else if constexpr (!edge) {
             u128 bs[6];
 #pragma unroll
@@ -593,8 +624,9 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
 #endif
 
     const double hk = P.half_kappa;
+    if (SV_HOT_PF_EARLY) prefetch(tfirst + 3 + NW);
     for (int32_t t = tfirst; t < t1; t += NW) {
-        prefetch(t + 3 + NW);
+        if (!SV_HOT_PF_EARLY) prefetch(t + 3 + NW);
         store_rows(t - NW);
         // ---------------- colour 0 on row q = t+2+wave
         {
@@ -611,7 +643,10 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
                 const int sm = (lr - 1) % R, s0 = lr % R, sp = (lr + 1) % R;
                 const int cx = x - cofs, cp = cxp(cx), cm = cxm(cx);
                 const double ph = s_phi[s0][cx];
-                const int32_t n_f0 = s_n0[s0][cx], n_b0 = s_n0[sm][cx], n_f1 = s_n1[s0][cx], n_b1 = s_n1[s0][cm];
+                int32_t n_f0 = s_n0[s0][cx], n_b0 = s_n0[sm][cx], n_f1 = s_n1[s0][cx], n_b1 = s_n1[s0][cm];
+                if (SV_HOT_I16) {  // every later use takes the sign-extended value: ds_read_i16, no v_bfe_i32
+                    asm volatile("" : "+v"(n_f0), "+v"(n_b0), "+v"(n_f1), "+v"(n_b1));
+                }
                 // r on the four links f0=(0,q,x), b0=(0,q-1,x), f1=(1,q,x), b1=(1,q,x-1) (neighborhood.py:91)
                 double r0[4];
                 r0[0] = (s_phi[sp][cx] - ph) - TWO_PI * (double)n_f0;
@@ -707,6 +742,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
             }
         }
         commit(t + 3 + NW);
+        if (SV_HOT_PF_EARLY && t + NW < t1) prefetch(t + 3 + 2 * NW);
         // The bases of the wave's two rows (brow1, brow1 + 1) move NW rows down.  Unless a row wraps around the
         // lattice or sits on global row 0 (where a buffered half-word clamps the word index), every block's
         // position moves by exactly its stride, so each base lane applies its precomputed advance map; the

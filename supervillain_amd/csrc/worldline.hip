@@ -23,10 +23,10 @@ namespace svh {
 // worldline_fused.hip
 bool wf_usable(int32_t N, bool v_is_float, double W_eff, int64_t it);
 bool wf_fast(const sv::Block *blocks);
-void launch_wf(const sv::FGeom &G, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in,
+bool launch_wf(const sv::FGeom &G, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in,
                int64_t *m_out, int64_t *v_out, const sv::Block *blocks, const uint32_t *skips, bool general,
                const sv::JumpTables *T, const sv::Affine adv[6], void *pstat, void *cstat, sv::DevScratch S,
-               uint32_t sweep, hipStream_t stream);
+               uint32_t sweep, hipStream_t stream, const sv::WfChain *chain = nullptr);
 }  // namespace svh
 
 namespace sv {
@@ -651,7 +651,7 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
             ctx->time_begin(&ev);
             for (int k = 0; k < count; k++)
                 launch(ctx->d_blocks + (size_t)k * nb, ss + (size_t)k * nstat * NSTRIPE, (uint32_t)k,
-                       blocks.data() + (size_t)k * nb);
+                       blocks.data() + (size_t)k * nb, k + 1 < count ? blocks.data() + (size_t)(k + 1) * nb : nullptr);
             ctx->time_end(ev, count);
             fold_stripes<<<(count * nstat + 63) / 64, 64, 0, ctx->stream>>>(ss, ctx->d_stats, count * nstat);
             SV_HIP(hipGetLastError());
@@ -823,6 +823,8 @@ int sv_worldline_destroy(sv_worldline *st) {
     (void)hipFree(st->snap_v);
     (void)hipFree(st->m_alt);
     (void)hipFree(st->v_alt);
+    for (void *b : st->wf_bases)
+        if (b) (void)hipFree(b);
     (void)hipFree(st->stripes);
     (void)hipFree(st->sites);
     if (st->f) (void)hipFree(st->f);
@@ -886,7 +888,9 @@ int sv_worldline_coexact_run(sv_worldline *st, double kappa, double W_eff, int64
         const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
         run_colour_sweeps(
             st, coexact_specs(st), sweeps, cur, inc, stats,
-            [&](const Block *blocks, StatStripe *stat, uint32_t k, const Block *) { launch_coexact(st, P, blocks, stat, k, T); }, 1, {},
+            [&](const Block *blocks, StatStripe *stat, uint32_t k, const Block *, const Block *) {
+                launch_coexact(st, P, blocks, stat, k, T);
+            }, 1, {},
             P.thr != 0);
         rng->state_hi = cur.s.hi;
         rng->state_lo = cur.s.lo;
@@ -922,7 +926,9 @@ int sv_worldline_plaquette_checkerboard_run(sv_worldline *st, double kappa, doub
         Cursor cur{u128{rng->state_lo, rng->state_hi}, (uint32_t)rng->has_uint32, rng->uinteger};
         const JumpTables *T = ctx->jump_tables(inc.hi, inc.lo);
         run_colour_sweeps(st, plaquette_cb_specs(st), sweeps, cur, inc, stats,
-                          [&](const Block *blocks, StatStripe *stat, uint32_t k, const Block *) { launch_plaquette_cb(st, P, blocks, stat, k, T); });
+                          [&](const Block *blocks, StatStripe *stat, uint32_t k, const Block *, const Block *) {
+                              launch_plaquette_cb(st, P, blocks, stat, k, T);
+                          });
         rng->state_hi = cur.s.hi;
         rng->state_lo = cur.s.lo;
         rng->has_uint32 = (int32_t)cur.has;
@@ -967,20 +973,30 @@ int sv_worldline_plaquette_coexact_run(sv_worldline *st, double kappa, double W_
         }
         run_colour_sweeps(
             st, specs, sweeps, cur, inc, stats,
-            [&](const Block *blocks, StatStripe *stat, uint32_t k, const Block *hblocks) {
+            [&](const Block *blocks, StatStripe *stat, uint32_t k, const Block *hblocks, const Block *hnext) {
                 if (use_wf && !st->wf_off && svh::wf_usable(st->N, st->v_is_float, W_eff, interval_t) &&
                     N * N < (int64_t(1) << 28)) {  // (launch_wf's 32-bit row offsets)
                     // one launch for the whole step (worldline_fused.hip); it writes the other buffer pair
                     const int64_t V = N * N;
-                    svh::launch_wf(FGeom{(int32_t)N, (int32_t)N, 0, 0, (int32_t)N, (int32_t)N, N, V, 0}, kappa, W_eff,
-                                   interval_t, st->m, (const int64_t *)st->v, st->m_alt, (int64_t *)st->v_alt,
-                                   blocks, ctx->d_skips, !svh::wf_fast(hblocks), T, adv, stat, stat + NSTRIPE,
-                                   wscratch(ctx), k, ctx->stream);
+                    // chained row bases: this step reads what the previous launch of the batch prepared, and prepares
+                    // the next step's when that one runs in a fast mode too
+                    WfChain ch;
+                    ch.buf = st->wf_bases;
+                    ch.cap = &st->wf_bases_cap;
+                    ch.parity = (int)(k & 1);
+                    ch.bases_ready = k > 0 && st->wf_bases_next;
+                    ch.next_blocks = hnext && svh::wf_fast(hnext) ? blocks + specs.size() : nullptr;
+                    st->wf_bases_next =
+                        svh::launch_wf(FGeom{(int32_t)N, (int32_t)N, 0, 0, (int32_t)N, (int32_t)N, N, V, 0}, kappa, W_eff,
+                                       interval_t, st->m, (const int64_t *)st->v, st->m_alt, (int64_t *)st->v_alt,
+                                       blocks, ctx->d_skips, !svh::wf_fast(hblocks), T, adv, stat, stat + NSTRIPE,
+                                       wscratch(ctx), k, ctx->stream, &ch);
                     std::swap(st->m, st->m_alt);
                     std::swap(st->v, st->v_alt);
                 } else {
                     launch_plaquette_cb(st, Pp, blocks, stat, k, T);
                     launch_coexact(st, Pc, blocks + np, stat + NSTRIPE, k, T);
+                    st->wf_bases_next = false;
                 }
             },
             2, stat_of);

@@ -64,7 +64,23 @@ struct WFArgs {
     int32_t it;            // coexact: t in -it..-1, 1..it
     uint32_t kt, thrt;     // its choice count 2 it and Lemire threshold
     int32_t general;       // MODE 2 for every strip (wf_body)
+    int32_t xe = 0;        // periodic lattices: the width of the two edge strips (0: every strip Wt / nsx wide)
+    // chained steps (WfChain): this step's row bases (or null: jump to them), and the next step's descriptors and
+    // where its bases go (or null); [(logical workgroup * NW + wave) * 64 + lane]
+    const u128 *bases_in = nullptr;
+    const Block *next_blocks = nullptr;
+    u128 *bases_out = nullptr;
 };
+
+// Column strip boundaries: uniform, or (xe > 0) two narrower edge strips -- the strips at the lattice's column seam
+// draw unpaired words from two base sets (MODE 1, ~11% longer row steps, profiles/r03b_worldline_wg_timeline.log),
+// and with one workgroup per CU the launch lasts as long as its slowest strip
+__device__ __forceinline__ int32_t wf_xb(const WFArgs &A, int ix) {
+    if (A.xe <= 0) return (int32_t)((int64_t)ix * A.G.Wt / A.nsx);
+    if (ix <= 0) return 0;
+    if (ix >= A.nsx) return A.G.Wt;
+    return A.xe + (int32_t)((int64_t)(ix - 1) * (A.G.Wt - 2 * A.xe) / (A.nsx - 2));
+}
 
 template <int NW>
 struct WFLDS {
@@ -119,7 +135,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
         b = xcd * per + (xcd < rem ? xcd : rem) + k;
     }
     const int ix = b % A.nsx, iy = b / A.nsx;
-    const int32_t x0 = (int32_t)((int64_t)ix * Gm.Wt / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * Gm.Wt / A.nsx);
+    const int32_t x0 = wf_xb(A, ix), x1 = wf_xb(A, ix + 1);
     const int32_t w = x1 - x0;
     const int32_t t0 = iy * A.TH;
     const int32_t t1 = t0 + A.TH < Gm.Ht ? t0 + A.TH : Gm.Ht;
@@ -243,7 +259,11 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
 #if SV_WF_PF0
     prefetch(t0 - 5);  // the first region rows in flight while the row bases are jumped to
 #endif
-    if (base_lane) bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)wf_base_pos(bbnd, grow(brow), N, bx, bhas));
+    if (A.bases_in) {  // (chained bases: [(b * NW + wave) * 64 + lane])
+        if (base_lane) bases = A.bases_in[((int64_t)b * NW + wave) * 64 + (threadIdx.x & 63)];
+    } else if (base_lane) {
+        bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)wf_base_pos(bbnd, grow(brow), N, bx, bhas));
+    }
     __builtin_amdgcn_s_waitcnt(0);
     if (base_lane) Ls.base[wave][lane] = bases;
 #if SV_WFTIME
@@ -477,6 +497,12 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
         while (tl + NW < t1) tl += NW;
         store_rows(tl);
     }
+    if (A.bases_out && base_lane) {
+        // the next step's row bases for this strip (the same jump its prologue would make), while the stores drain
+        const uint32_t nhas = bbnd ? A.next_blocks[bblk].has : 0u;
+        A.bases_out[((int64_t)b * NW + wave) * 64 + (threadIdx.x & 63)] =
+            full_jump(A.T, &A.next_blocks[bblk], (uint32_t)wf_base_pos(bbnd, grow(tfirst + 3 - bp + wave), N, bx, nhas));
+    }
     if (Ls.bad && threadIdx.x == 0) report(A.S, A.sweep, OVERFLOW_BLOCK, 0, 0);
     wflush(A.pstat, pacc, ppsum);
     wflush(A.cstat, cacc, cpsum);
@@ -508,7 +534,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 8
         b = xcd * per + (xcd < rem ? xcd : rem) + k;
     }
     const int ix = b % A.nsx;
-    const int32_t x0 = (int32_t)((int64_t)ix * A.G.Wt / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * A.G.Wt / A.nsx);
+    const int32_t x0 = wf_xb(A, ix), x1 = wf_xb(A, ix + 1);
     const int32_t gx0 = A.G.X0 + x0;
     const bool interior = gx0 - 5 >= 0 && gx0 + (x1 - x0) + 4 <= A.G.Nx && A.G.Nx > SMALL_LDS;
     if (A.general) wf_body<TILE, 2, NW>(A, Ls);
@@ -588,10 +614,11 @@ bool wf_fast(const Block *blocks) {
     return true;
 }
 
-void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in,
+// returns whether the launch prepares the next step's row bases (WfChain)
+bool launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in,
                int64_t *m_out, int64_t *v_out, const Block *blocks, const uint32_t *skips, bool general,
                const JumpTables *T, const Affine adv[6], void *pstat, void *cstat, DevScratch S, uint32_t sweep,
-               hipStream_t stream) {
+               hipStream_t stream, const WfChain *chain) {
     if ((int64_t)G.Nt * G.Nx >= (int64_t(1) << 31))
         throw std::invalid_argument("worldline_step_fused addresses stream positions with 31 bits (V < 2^31)");
     if (G.plane >= (int64_t(1) << 28))
@@ -601,6 +628,19 @@ void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
     A.general = general ? 1 : 0;
     A.G = G;
     A.nsx = (G.Wt + WF_W - 1) / WF_W;
+    {
+        // periodic lattices of >= 3 strips: edge strips SV_WF_EDGE percent as wide as the uniform split (default 88,
+        // the interior strips then <= WF_W)
+        static const int pct = [] {
+            const char *e = getenv("SV_WF_EDGE");
+            return e ? atoi(e) : 88;
+        }();
+        const bool periodic = G.T0 == 0 && G.X0 == 0 && G.Ht == G.Nt && G.Wt == G.Nx && G.pitch == G.Nx && G.org == 0;
+        if (periodic && pct > 0 && pct < 100 && A.nsx >= 3) {
+            const int32_t xe = (int32_t)((int64_t)G.Wt * pct / (100 * A.nsx));
+            if (xe >= 8 && (G.Wt - 2 * xe + A.nsx - 3) / (A.nsx - 2) <= WF_W) A.xe = xe;
+        }
+    }
     const int nw = wf_nw(G.Ht, A.nsx);
     A.TH = wf_th(G.Ht, A.nsx, nw);
     A.nsy = (G.Ht + A.TH - 1) / A.TH;
@@ -627,6 +667,31 @@ void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
     A.it = (int32_t)it;
     A.kt = (uint32_t)(2 * it);
     A.thrt = (uint32_t)((0u - A.kt) % A.kt);
+    static const bool chain_on = [] {  // SV_WF_CHAIN=0: every step jumps to its own row bases (A/B)
+        const char *e = getenv("SV_WF_CHAIN");
+        return !(e && atoi(e) == 0);
+    }();
+    bool wrote = false;
+    if (chain_on && chain && chain->buf && !general) {
+        // bases per (workgroup, wave, lane); a general step (skip lists) neither reads nor prepares them
+        const size_t need = (size_t)A.nsx * A.nsy * nw * 64 * sizeof(u128);
+        if (*chain->cap < need) {
+            SV_HIP(hipStreamSynchronize(stream));
+            for (int i = 0; i < 2; i++) {
+                if (chain->buf[i]) SV_HIP(hipFree(chain->buf[i]));
+                chain->buf[i] = nullptr;
+            }
+            for (int i = 0; i < 2; i++) SV_HIP(hipMalloc(&chain->buf[i], need));
+            *chain->cap = need;
+        } else {
+            if (chain->bases_ready) A.bases_in = (const u128 *)chain->buf[chain->parity];
+            if (chain->next_blocks) {
+                A.next_blocks = chain->next_blocks;
+                A.bases_out = (u128 *)chain->buf[1 - chain->parity];
+                wrote = true;
+            }
+        }
+    }
     const bool tile = !(G.T0 == 0 && G.X0 == 0 && G.Ht == G.Nt && G.Wt == G.Nx && G.pitch == G.Nx && G.org == 0);
     if (nw == 16) {
         if (tile) worldline_step_fused<true, 16><<<A.nsx * A.nsy, 16 * 64, 0, stream>>>(A);
@@ -638,6 +703,7 @@ void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
         if (tile) worldline_step_fused<true, 4><<<A.nsx * A.nsy, 4 * 64, 0, stream>>>(A);
         else worldline_step_fused<false, 4><<<A.nsx * A.nsy, 4 * 64, 0, stream>>>(A);
     }
+    return wrote;
 }
 
 }  // namespace svh
