@@ -1061,6 +1061,12 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     // |n| beyond villain_sweep_hot's int16 image: the failing sweep is replayed, and the rest of the call runs, on
     // villain_sweep_fused's int32 image; only an overflow of that one falls back to the per-colour int64 path
     bool hot_off = false;
+    // The next batch is planned on the host while the device runs this one (a batch boundary otherwise leaves the
+    // GPU idle for the plan of 64 sweeps, ~0.3 ms: 5 us per L=4096 sweep in the driver form); an abort discards it
+    std::vector<Block> blocks_next;
+    std::vector<uint32_t> skipvec_next;
+    Cursor c_next{};
+    int sw_next = -1;
     while (sw < sweeps) {
         const int count = std::min(BATCH, sweeps - sw);
         Cursor c = cur;
@@ -1073,7 +1079,14 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             reset_batch(ctx, ctx->d_stats, count * sizeof(sv_stats));
         std::vector<int> band_starts;  // first sweeps of this batch's band launches
         auto tp0 = std::chrono::steady_clock::now();
-        plan_sweeps(ctx, c, inc, specs, sw, count, skips, blocks, skipvec);
+        if (sw_next == sw) {
+            blocks.swap(blocks_next);
+            skipvec.swap(skipvec_next);
+            c = c_next;
+        } else {
+            plan_sweeps(ctx, c, inc, specs, sw, count, skips, blocks, skipvec);
+        }
+        sw_next = -1;
         auto tp1 = std::chrono::steady_clock::now();
         if (dbg) fprintf(stderr, "[sv] plan %d sweeps: %.1f us\n", count, std::chrono::duration<double, std::micro>(tp1 - tp0).count());
         upload_plan(ctx, blocks, skipvec);
@@ -1219,6 +1232,16 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         }
         if (seg) ctx->time_end(seg, launched - seg_k0, seg_k0);
         SV_HIP(hipGetLastError());
+        static const bool preplan = [] {  // SV_PREPLAN=0: plan each batch after the previous one's sync (A/B)
+            const char *e = getenv("SV_PREPLAN");
+            return !(e && atoi(e) == 0);
+        }();
+        if (preplan && launched == count && sw + count < sweeps) {  // (the device runs this batch meanwhile)
+            c_next = c;
+            plan_sweeps(ctx, c_next, inc, specs, sw + count, std::min(BATCH, sweeps - sw - count), skips, blocks_next,
+                        skipvec_next);
+            sw_next = sw + count;
+        }
         auto tp2 = std::chrono::steady_clock::now();
         AbortInfo a = read_abort_stats(ctx, count, stats + sw);
         auto tp3 = std::chrono::steady_clock::now();
@@ -1260,6 +1283,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                 }
             }
         };
+        sw_next = -1;  // (an abort changes the skips, or the kernel: the next batch is planned again)
         // earliest failing (sweep, block); an overflow tag sorts after every rejection of its sweep
         uint32_t first_bad = ~0u;
         bool overflow = false, band_fail = false;
