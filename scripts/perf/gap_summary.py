@@ -7,6 +7,8 @@ import os
 import sys
 
 d = sys.argv[1]
+KEY = sys.argv[2] if len(sys.argv) > 2 else 'villain_sweep'  # the sweep kernels' name fragment
+MINK = int(sys.argv[3]) if len(sys.argv) > 3 else 20       # a timed call has at least this many of them
 ev = []
 for f in glob.glob(os.path.join(d, '**', '*kernel_trace.csv'), recursive=True):
     for r in csv.DictReader(open(f)):
@@ -24,13 +26,13 @@ for e in ev:
     cur.append(e)
 if cur:
     calls.append(cur)
-hot = [c for c in calls if sum('villain_sweep' in x[2] for x in c) >= 20]
+hot = [c for c in calls if sum(KEY in x[2] for x in c) >= MINK]
 c = hot[-1] if hot else calls[-1]
 t0 = c[0][0]
 busy = sum(e[1] - e[0] for e in c)
-sweep = sum(e[1] - e[0] for e in c if 'villain_sweep' in e[2])
+sweep = sum(e[1] - e[0] for e in c if KEY in e[2])
 print(f'call: {len(c)} events, span {(c[-1][1] - t0) / 1e3:.1f} us, busy {busy / 1e3:.1f} us, sweep kernels {sweep / 1e3:.1f} us '
-      f'({sum("villain_sweep" in x[2] for x in c)} launches), idle {(c[-1][1] - t0 - busy) / 1e3:.1f} us')
+      f'({sum(KEY in x[2] for x in c)} launches), idle {(c[-1][1] - t0 - busy) / 1e3:.1f} us')
 prev = t0
 for s, e, n in c:
     if 'villain_sweep' not in n or s - prev > 3000:

@@ -22,6 +22,9 @@
 #ifndef SV_WF_PF0
 #define SV_WF_PF0 1  // the first prefetch of region rows issued before the prologue's row-base jumps
 #endif
+#ifndef SV_WF_PF2
+#define SV_WF_PF2 1  // the prologue's second round of region rows requested with the first
+#endif
 #ifndef SV_WFTIME
 #define SV_WFTIME 0  // timing experiments: per-workgroup timestamps of worldline_step_fused (sv_debug_wftime)
 #endif
@@ -181,7 +184,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     int pf_gx[PF];
 #pragma unroll
     for (int k = 0; k < PF; k++) pf_gx[k] = mcol(x0 - 5 + lane + 64 * k);
-    auto prefetch = [&](int32_t ra) {
+    auto prefetch_to = [&](int32_t ra, int64_t(&pf_m0)[PF], int64_t(&pf_m1)[PF], int64_t(&pf_v)[PF]) {
         const int32_t q = ra + wave;
         if (SV_ABLATE & 16) {  // timing experiments only (fused.h SV_ABLATE): no HBM loads
 #pragma unroll
@@ -203,7 +206,8 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
             }
         }
     };
-    auto commit = [&](int32_t ra) {
+    auto prefetch = [&](int32_t ra) { prefetch_to(ra, pf_m0, pf_m1, pf_v); };
+    auto commit_from = [&](int32_t ra, const int64_t(&pf_m0)[PF], const int64_t(&pf_m1)[PF], const int64_t(&pf_v)[PF]) {
         const int32_t q = ra + wave;
         if (q >= t0 - 5 && q < t1 + 4) {
             const int slot = (q - rbase) % R;
@@ -225,6 +229,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
             if (bad) Ls.bad = 1;
         }
     };
+    auto commit = [&](int32_t ra) { commit_from(ra, pf_m0, pf_m1, pf_v); };
     auto store_rows = [&](int32_t ra) {
         const int32_t q = ra + wave;
         if (SV_ABLATE & 8) return;  // timing experiments only: no HBM stores
@@ -259,6 +264,10 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
 #if SV_WF_PF0
     prefetch(t0 - 5);  // the first region rows in flight while the row bases are jumped to
 #endif
+    // (SV_WF_PF2) the second round of region rows too, into a register set of its own: the prologue's two rounds of
+    // row loads then wait once, not twice (one round of workgroups per launch on config 3: nothing hides them)
+    int64_t q_m0[PF], q_m1[PF], q_v[PF];
+    if (SV_WF_PF0 && SV_WF_PF2) prefetch_to(t0 - 5 + NW, q_m0, q_m1, q_v);
     if (A.bases_in) {  // (chained bases: [(b * NW + wave) * 64 + lane])
         if (base_lane) bases = A.bases_in[((int64_t)b * NW + wave) * 64 + (threadIdx.x & 63)];
     } else if (base_lane) {
@@ -447,6 +456,10 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     };
 
     for (int32_t ra = t0 - 5; ra < tfirst + AH; ra += NW) {
+        if (SV_WF_PF0 && SV_WF_PF2 && ra == t0 - 5 + NW) {
+            commit_from(ra, q_m0, q_m1, q_v);
+            continue;
+        }
         if (!SV_WF_PF0 || ra != t0 - 5) prefetch(ra);
         commit(ra);
     }
