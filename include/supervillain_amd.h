@@ -70,6 +70,10 @@ int sv_ctx_sweep_counts(sv_ctx *ctx, int64_t *hot, int64_t *fused, int64_t *gene
 /* Diagnostic: of the hot sweeps since the last call (then reset), those run K at a time by the multi-sweep band
  * launches of small periodic lattices (villain_sweep_hot_band, SV_BAND_K), and the number of such launches. */
 int sv_ctx_band_counts(sv_ctx *ctx, int64_t *sweeps, int64_t *launches);
+/* Diagnostic (tests): the context's PCG64 jump-table cache holds at most `cap` increments (0: the default, 1024 or
+ * SV_MAX_TABLES); a full cache drains the device and is dropped.  sv_ctx_table_purges reports how often it was. */
+int sv_ctx_set_table_cap(sv_ctx *ctx, int32_t cap);
+int sv_ctx_table_purges(sv_ctx *ctx, int64_t *purges);
 /* Host-only: copy R NumPy PCG64 bit-generator states into (gather) or out of (scatter) sv_rng records, given
  * each generator's `bit_generator.ctypes.state_address` (NumPy's pcg64_state, numpy/random/src/pcg64/pcg64.h,
  * native 128-bit layout; the Python wrapper verifies it against the public state dict first).  Lets a

@@ -38,7 +38,7 @@ const sv::JumpTables *sv_ctx::jump_tables(uint64_t inc_hi, uint64_t inc_lo) {
         const char *e = getenv("SV_MAX_TABLES");
         return e && atoi(e) > 0 ? (size_t)atoi(e) : MAX_TABLES;
     }();
-    if (tables.size() >= max_tables) {
+    if (tables.size() >= (table_cap ? table_cap : max_tables)) {
         if (alloc_log()) fprintf(stderr, "[sv alloc] jump-table cache purge #%lld (%zu tables)\n", (long long)table_purges + 1,
                                  tables.size());
         // a long-lived context seeing many generators drops its cache.  Launches already enqueued on ANY stream of
@@ -325,6 +325,18 @@ int sv_ctx_sweep_counts(sv_ctx *ctx, int64_t *hot, int64_t *fused, int64_t *gene
     if (fused) *fused = ctx->sweeps_fused;
     if (generic) *generic = ctx->sweeps_generic;
     ctx->sweeps_hot = ctx->sweeps_fused = ctx->sweeps_generic = 0;
+    return 0;
+}
+
+int sv_ctx_set_table_cap(sv_ctx *ctx, int32_t cap) {
+    if (!ctx || cap < 0) return -1;
+    ctx->table_cap = (size_t)cap;
+    return 0;
+}
+
+int sv_ctx_table_purges(sv_ctx *ctx, int64_t *purges) {
+    if (!ctx || !purges) return -1;
+    *purges = ctx->table_purges;
     return 0;
 }
 

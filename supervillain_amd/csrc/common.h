@@ -112,6 +112,7 @@ struct sv_ctx {
     std::map<std::pair<uint64_t, uint64_t>, sv::JumpTables *> tables;  // per PCG64 increment (device, 40 KB each)
     static constexpr size_t MAX_TABLES = 1024;                         // 40 MB of HBM before the cache is dropped
     int64_t table_purges = 0;
+    size_t table_cap = 0;  // sv_ctx_set_table_cap (tests): a smaller cache for this context; 0 = the default
     // scratch
     int32_t *d_abort = nullptr;
     uint32_t *d_nreport = nullptr;
