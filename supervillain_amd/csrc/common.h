@@ -250,23 +250,7 @@ struct sv_worldline {
     int64_t *m_at_snap = nullptr;  // the (m, v) pointers a snapshot was taken from (restore puts them back)
     void *v_at_snap = nullptr;
     bool wf_off = false;           // |m| or |v| outgrew the fused kernel's int32 image: four-pass kernels only
-    void *wf_bases[2] = {nullptr, nullptr};  // worldline_step_fused's chained row bases (sv::WfChain), per parity
-    size_t wf_bases_cap = 0;                 // bytes of each
-    bool wf_bases_next = false;              // the last launch of the batch so far wrote the next step's bases
 };
-
-namespace sv {
-// Consecutive worldline_step_fused launches of one batch: step k jumps to step k+1's row bases at its end (its
-// workgroups then wait on their last stores anyway) and step k+1 loads them instead of jumping in its prologue
-// (one round of 225 workgroups on config 3: the prologue is not hidden behind other workgroups)
-struct WfChain {
-    const Block *next_blocks = nullptr;  // step k+1's descriptors (device), or null: no next fused step to prepare
-    bool bases_ready = false;            // the previous launch wrote this step's row bases
-    int parity = 0;                      // this step reads buffer parity, writes 1 - parity
-    void **buf = nullptr;                // the owner's two buffers (grown by launch_wf)
-    size_t *cap = nullptr;
-};
-}  // namespace sv
 
 #define SV_HIP(call)                                                                                   \
     do {                                                                                               \

@@ -35,10 +35,10 @@ namespace svh {
 // worldline_fused.hip
 bool wf_usable(int32_t N, bool v_is_float, double W_eff, int64_t it);
 bool wf_fast(const sv::Block *blocks);
-bool launch_wf(const sv::FGeom &G, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in,
+void launch_wf(const sv::FGeom &G, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in,
                int64_t *m_out, int64_t *v_out, const sv::Block *blocks, const uint32_t *skips, bool general,
                const sv::JumpTables *T, const sv::Affine adv[6], void *pstat, void *cstat, sv::DevScratch S,
-               uint32_t sweep, hipStream_t stream, const sv::WfChain *chain = nullptr);
+               uint32_t sweep, hipStream_t stream);
 }  // namespace svh
 
 namespace sv {

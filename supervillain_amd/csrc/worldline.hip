@@ -23,10 +23,10 @@ namespace svh {
 // worldline_fused.hip
 bool wf_usable(int32_t N, bool v_is_float, double W_eff, int64_t it);
 bool wf_fast(const sv::Block *blocks);
-bool launch_wf(const sv::FGeom &G, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in,
+void launch_wf(const sv::FGeom &G, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in,
                int64_t *m_out, int64_t *v_out, const sv::Block *blocks, const uint32_t *skips, bool general,
                const sv::JumpTables *T, const sv::Affine adv[6], void *pstat, void *cstat, sv::DevScratch S,
-               uint32_t sweep, hipStream_t stream, const sv::WfChain *chain = nullptr);
+               uint32_t sweep, hipStream_t stream);
 }  // namespace svh
 
 namespace sv {
@@ -823,8 +823,6 @@ int sv_worldline_destroy(sv_worldline *st) {
     (void)hipFree(st->snap_v);
     (void)hipFree(st->m_alt);
     (void)hipFree(st->v_alt);
-    for (void *b : st->wf_bases)
-        if (b) (void)hipFree(b);
     (void)hipFree(st->stripes);
     (void)hipFree(st->sites);
     if (st->f) (void)hipFree(st->f);
@@ -973,30 +971,20 @@ int sv_worldline_plaquette_coexact_run(sv_worldline *st, double kappa, double W_
         }
         run_colour_sweeps(
             st, specs, sweeps, cur, inc, stats,
-            [&](const Block *blocks, StatStripe *stat, uint32_t k, const Block *hblocks, const Block *hnext) {
+            [&](const Block *blocks, StatStripe *stat, uint32_t k, const Block *hblocks, const Block *) {
                 if (use_wf && !st->wf_off && svh::wf_usable(st->N, st->v_is_float, W_eff, interval_t) &&
                     N * N < (int64_t(1) << 28)) {  // (launch_wf's 32-bit row offsets)
                     // one launch for the whole step (worldline_fused.hip); it writes the other buffer pair
                     const int64_t V = N * N;
-                    // chained row bases: this step reads what the previous launch of the batch prepared, and prepares
-                    // the next step's when that one runs in a fast mode too
-                    WfChain ch;
-                    ch.buf = st->wf_bases;
-                    ch.cap = &st->wf_bases_cap;
-                    ch.parity = (int)(k & 1);
-                    ch.bases_ready = k > 0 && st->wf_bases_next;
-                    ch.next_blocks = hnext && svh::wf_fast(hnext) ? blocks + specs.size() : nullptr;
-                    st->wf_bases_next =
-                        svh::launch_wf(FGeom{(int32_t)N, (int32_t)N, 0, 0, (int32_t)N, (int32_t)N, N, V, 0}, kappa, W_eff,
-                                       interval_t, st->m, (const int64_t *)st->v, st->m_alt, (int64_t *)st->v_alt,
-                                       blocks, ctx->d_skips, !svh::wf_fast(hblocks), T, adv, stat, stat + NSTRIPE,
-                                       wscratch(ctx), k, ctx->stream, &ch);
+                    svh::launch_wf(FGeom{(int32_t)N, (int32_t)N, 0, 0, (int32_t)N, (int32_t)N, N, V, 0}, kappa, W_eff,
+                                   interval_t, st->m, (const int64_t *)st->v, st->m_alt, (int64_t *)st->v_alt,
+                                   blocks, ctx->d_skips, !svh::wf_fast(hblocks), T, adv, stat, stat + NSTRIPE,
+                                   wscratch(ctx), k, ctx->stream);
                     std::swap(st->m, st->m_alt);
                     std::swap(st->v, st->v_alt);
                 } else {
                     launch_plaquette_cb(st, Pp, blocks, stat, k, T);
                     launch_coexact(st, Pc, blocks + np, stat + NSTRIPE, k, T);
-                    st->wf_bases_next = false;
                 }
             },
             2, stat_of);

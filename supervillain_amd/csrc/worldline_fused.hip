@@ -68,11 +68,6 @@ struct WFArgs {
     uint32_t kt, thrt;     // its choice count 2 it and Lemire threshold
     int32_t general;       // MODE 2 for every strip (wf_body)
     int32_t xe = 0;        // periodic lattices: the width of the two edge strips (0: every strip Wt / nsx wide)
-    // chained steps (WfChain): this step's row bases (or null: jump to them), and the next step's descriptors and
-    // where its bases go (or null); [(logical workgroup * NW + wave) * 64 + lane]
-    const u128 *bases_in = nullptr;
-    const Block *next_blocks = nullptr;
-    u128 *bases_out = nullptr;
 };
 
 // Column strip boundaries: uniform, or (xe > 0) two narrower edge strips -- the strips at the lattice's column seam
@@ -268,11 +263,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     // row loads then wait once, not twice (one round of workgroups per launch on config 3: nothing hides them)
     int64_t q_m0[PF], q_m1[PF], q_v[PF];
     if (SV_WF_PF0 && SV_WF_PF2) prefetch_to(t0 - 5 + NW, q_m0, q_m1, q_v);
-    if (A.bases_in) {  // (chained bases: [(b * NW + wave) * 64 + lane])
-        if (base_lane) bases = A.bases_in[((int64_t)b * NW + wave) * 64 + (threadIdx.x & 63)];
-    } else if (base_lane) {
-        bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)wf_base_pos(bbnd, grow(brow), N, bx, bhas));
-    }
+    if (base_lane) bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)wf_base_pos(bbnd, grow(brow), N, bx, bhas));
     __builtin_amdgcn_s_waitcnt(0);
     if (base_lane) Ls.base[wave][lane] = bases;
 #if SV_WFTIME
@@ -510,12 +501,6 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
         while (tl + NW < t1) tl += NW;
         store_rows(tl);
     }
-    if (A.bases_out && base_lane) {
-        // the next step's row bases for this strip (the same jump its prologue would make), while the stores drain
-        const uint32_t nhas = bbnd ? A.next_blocks[bblk].has : 0u;
-        A.bases_out[((int64_t)b * NW + wave) * 64 + (threadIdx.x & 63)] =
-            full_jump(A.T, &A.next_blocks[bblk], (uint32_t)wf_base_pos(bbnd, grow(tfirst + 3 - bp + wave), N, bx, nhas));
-    }
     if (Ls.bad && threadIdx.x == 0) report(A.S, A.sweep, OVERFLOW_BLOCK, 0, 0);
     wflush(A.pstat, pacc, ppsum);
     wflush(A.cstat, cacc, cpsum);
@@ -627,11 +612,10 @@ bool wf_fast(const Block *blocks) {
     return true;
 }
 
-// returns whether the launch prepares the next step's row bases (WfChain)
-bool launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in,
+void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in,
                int64_t *m_out, int64_t *v_out, const Block *blocks, const uint32_t *skips, bool general,
                const JumpTables *T, const Affine adv[6], void *pstat, void *cstat, DevScratch S, uint32_t sweep,
-               hipStream_t stream, const WfChain *chain) {
+               hipStream_t stream) {
     if ((int64_t)G.Nt * G.Nx >= (int64_t(1) << 31))
         throw std::invalid_argument("worldline_step_fused addresses stream positions with 31 bits (V < 2^31)");
     if (G.plane >= (int64_t(1) << 28))
@@ -642,11 +626,12 @@ bool launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
     A.G = G;
     A.nsx = (G.Wt + WF_W - 1) / WF_W;
     {
-        // periodic lattices of >= 3 strips: edge strips SV_WF_EDGE percent as wide as the uniform split (default 88,
-        // the interior strips then <= WF_W)
+        // periodic lattices of >= 3 strips: edge strips SV_WF_EDGE percent as wide as the uniform split (the interior
+        // strips then <= WF_W).  Off by default: 88 / 94 measured level with uniform strips (39.8 / 39.7 vs 39.8 us
+        // per L=1024 step, r4) -- the seam strips' longer row steps do not set the launch's length
         static const int pct = [] {
             const char *e = getenv("SV_WF_EDGE");
-            return e ? atoi(e) : 88;
+            return e ? atoi(e) : 0;
         }();
         const bool periodic = G.T0 == 0 && G.X0 == 0 && G.Ht == G.Nt && G.Wt == G.Nx && G.pitch == G.Nx && G.org == 0;
         if (periodic && pct > 0 && pct < 100 && A.nsx >= 3) {
@@ -680,31 +665,6 @@ bool launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
     A.it = (int32_t)it;
     A.kt = (uint32_t)(2 * it);
     A.thrt = (uint32_t)((0u - A.kt) % A.kt);
-    static const bool chain_on = [] {  // SV_WF_CHAIN=0: every step jumps to its own row bases (A/B)
-        const char *e = getenv("SV_WF_CHAIN");
-        return !(e && atoi(e) == 0);
-    }();
-    bool wrote = false;
-    if (chain_on && chain && chain->buf && !general) {
-        // bases per (workgroup, wave, lane); a general step (skip lists) neither reads nor prepares them
-        const size_t need = (size_t)A.nsx * A.nsy * nw * 64 * sizeof(u128);
-        if (*chain->cap < need) {
-            SV_HIP(hipStreamSynchronize(stream));
-            for (int i = 0; i < 2; i++) {
-                if (chain->buf[i]) SV_HIP(hipFree(chain->buf[i]));
-                chain->buf[i] = nullptr;
-            }
-            for (int i = 0; i < 2; i++) SV_HIP(hipMalloc(&chain->buf[i], need));
-            *chain->cap = need;
-        } else {
-            if (chain->bases_ready) A.bases_in = (const u128 *)chain->buf[chain->parity];
-            if (chain->next_blocks) {
-                A.next_blocks = chain->next_blocks;
-                A.bases_out = (u128 *)chain->buf[1 - chain->parity];
-                wrote = true;
-            }
-        }
-    }
     const bool tile = !(G.T0 == 0 && G.X0 == 0 && G.Ht == G.Nt && G.Wt == G.Nx && G.pitch == G.Nx && G.org == 0);
     if (nw == 16) {
         if (tile) worldline_step_fused<true, 16><<<A.nsx * A.nsy, 16 * 64, 0, stream>>>(A);
@@ -716,7 +676,6 @@ bool launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
         if (tile) worldline_step_fused<true, 4><<<A.nsx * A.nsy, 4 * 64, 0, stream>>>(A);
         else worldline_step_fused<false, 4><<<A.nsx * A.nsy, 4 * 64, 0, stream>>>(A);
     }
-    return wrote;
 }
 
 }  // namespace svh
