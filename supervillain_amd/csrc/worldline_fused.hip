@@ -22,9 +22,6 @@
 #ifndef SV_WF_PF0
 #define SV_WF_PF0 1  // the first prefetch of region rows issued before the prologue's row-base jumps
 #endif
-#ifndef SV_WF_PF2
-#define SV_WF_PF2 1  // the prologue's second round of region rows requested with the first
-#endif
 #ifndef SV_WFTIME
 #define SV_WFTIME 0  // timing experiments: per-workgroup timestamps of worldline_step_fused (sv_debug_wftime)
 #endif
@@ -259,10 +256,6 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
 #if SV_WF_PF0
     prefetch(t0 - 5);  // the first region rows in flight while the row bases are jumped to
 #endif
-    // (SV_WF_PF2) the second round of region rows too, into a register set of its own: the prologue's two rounds of
-    // row loads then wait once, not twice (one round of workgroups per launch on config 3: nothing hides them)
-    int64_t q_m0[PF], q_m1[PF], q_v[PF];
-    if (SV_WF_PF0 && SV_WF_PF2) prefetch_to(t0 - 5 + NW, q_m0, q_m1, q_v);
     if (base_lane) bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)wf_base_pos(bbnd, grow(brow), N, bx, bhas));
     __builtin_amdgcn_s_waitcnt(0);
     if (base_lane) Ls.base[wave][lane] = bases;
@@ -447,10 +440,6 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     };
 
     for (int32_t ra = t0 - 5; ra < tfirst + AH; ra += NW) {
-        if (SV_WF_PF0 && SV_WF_PF2 && ra == t0 - 5 + NW) {
-            commit_from(ra, q_m0, q_m1, q_v);
-            continue;
-        }
         if (!SV_WF_PF0 || ra != t0 - 5) prefetch(ra);
         commit(ra);
     }
