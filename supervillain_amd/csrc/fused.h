@@ -526,7 +526,7 @@ __device__ __forceinline__ u128 hot_apply(const SmallTab &sm, uint32_t i, u128 b
 // NumPy random(): (x >> 11) * 2^-53, exactly: with m = x >> 11 = h 2^32 + l (h < 2^21),
 // m 2^-53 = h 2^-21 + l 2^-53; l 2^-53 is exact, and the fma's sum is m 2^-53 (53 significant bits)
 #ifndef SV_HOT_U53
-#define SV_HOT_U53 0
+#define SV_HOT_U53 2  // 2: one 64-bit shift and an exact fma (r4, with villain_hot.hip's switches); 1: alignbit form
 #endif
 #ifndef SV_HOT_MUL24
 #define SV_HOT_MUL24 0

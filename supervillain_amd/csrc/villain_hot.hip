@@ -38,14 +38,16 @@
 #define SV_HOT_PH_OCC 4  // the counter-based kernel (29.5 KB of LDS, 81 VGPRs): 4, 5 and 6 waves/SIMD measured flat (r336)
 #endif
 
+// r4 A/B (L=4096, two interleaved repetitions on one box, kernel us per sweep): base 221.8 / 225.3, the four
+// switches below together 218.7 / 221.2 (each alone within the noise); bit-exact (Villain, overflow, worldline suites)
 #ifndef SV_HOT_PF_EARLY
-#define SV_HOT_PF_EARLY 0  // issue the next row step's row loads right after the commit, before the step's barrier
+#define SV_HOT_PF_EARLY 1  // the next row step's row loads issued right after the commit, before the step's barrier
 #endif
 #ifndef SV_HOT_I16
-#define SV_HOT_I16 0  // n read from LDS with sign-extending loads (the value made opaque after the load)
+#define SV_HOT_I16 1  // n read from LDS with sign-extending loads (the value made opaque after the load)
 #endif
 #ifndef SV_HOT_BSEL
-#define SV_HOT_BSEL 0  // paired words: each lane reads the base set it draws from (per-lane LDS address), no selects
+#define SV_HOT_BSEL 1  // paired words: each lane reads the base set it draws from (per-lane LDS address), no selects
 #endif
 
 #ifndef SV_WGTIME
