@@ -248,6 +248,7 @@ struct sv_domain {
     int64_t pitch = 0, plane = 0, org = 0;
     int R = 2, cur = 0;
     int depth = 1;                  // Villain: sweeps per halo exchange (deep halos, see villain_depth)
+    std::map<int32_t, std::pair<int32_t *, int32_t>> tile_strips;  // two_wave_strips per region height (device, count)
     u128 *d_scan = nullptr;         // rejection prediction: per-sweep start states of the scanned batch
     hipStream_t scan_stream = nullptr;  // lowest priority: the scan fills the slots the sweeps leave free
     hipEvent_t ev_sum = nullptr, ev_scan = nullptr;
@@ -756,7 +757,39 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
                     A.own_c0 = left;
                     A.own_c1 = left + d->Wt;
                 }
-                launch_fused_tile(A, A.nsx * A.nsy, ctx->stream, hot[k]);
+                int grid = A.nsx * A.nsy;
+                if (hot[k] && nw8) {
+                    // two waves of strips, taller for the workgroups dispatched first (two_wave_strips; SV_TILE_SCHED=0:
+                    // uniform strips of TH rows)
+                    static const int sched = [] {
+                        const char *e = getenv("SV_TILE_SCHED");
+                        return e ? atoi(e) : 1;
+                    }();
+                    static const int cus = [] {
+                        int dev = 0, v = 0;
+                        if (hipGetDevice(&dev) != hipSuccess ||
+                            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+                            v = 0;
+                        return v;
+                    }();
+                    if (sched && cus > 0) {
+                        auto it = d->tile_strips.find(A.G.Ht);
+                        if (it == d->tile_strips.end()) {
+                            const std::vector<int32_t> tab = two_wave_strips(A.G.Ht, A.nsx, cus, 45, 29);
+                            int32_t *dt = nullptr;
+                            if (!tab.empty()) {
+                                SV_HIP(hipMalloc(&dt, tab.size() * sizeof(int32_t)));
+                                SV_HIP(hipMemcpy(dt, tab.data(), tab.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+                            }
+                            it = d->tile_strips.emplace(A.G.Ht, std::make_pair(dt, (int32_t)(tab.size() / 3))).first;
+                        }
+                        if (it->second.first) {
+                            A.strips = it->second.first;
+                            grid = it->second.second;
+                        }
+                    }
+                }
+                launch_fused_tile(A, grid, ctx->stream, hot[k]);
                 (hot[k] ? ctx->sweeps_hot : ctx->sweeps_fused)++;
             }
             d->cur = out;
@@ -1109,6 +1142,8 @@ int sv_domain_destroy(sv_domain *d) {
     if (d->comm) (void)ncclCommDestroy(d->comm);
     (void)hipFree(d->gathered);
     (void)hipFree(d->d_scan);
+    for (auto &kv : d->tile_strips)
+        if (kv.second.first) (void)hipFree(kv.second.first);
     if (d->scan_stream) (void)hipStreamDestroy(d->scan_stream);
     if (d->ev_sum) (void)hipEventDestroy(d->ev_sum);
     if (d->ev_scan) (void)hipEventDestroy(d->ev_scan);

@@ -156,6 +156,9 @@ bool hot_skip_ok(const VParams &P, const Block *blocks);
 void launch_hot_skip(const FArgs &A, int grid, hipStream_t stream);
 // villain_sweep_hot's default descending strip table for H rows and nsx column strips ({ix, t0, t1} per strip)
 std::vector<int32_t> band_strips(int32_t H, int nsx);
+// two waves of 8-wave strips for a region one round covers: `first` strips of `tall` rows dispatched first, then strips
+// of `shrt` rows ({ix, t0, t1} per logical block), or empty when the region does not fit
+std::vector<int32_t> two_wave_strips(int32_t H, int nsx, int first, int tall, int shrt);
 void launch_hot(const FArgs &A, int grid, hipStream_t stream);
 // the band launch (8-wave strips of B.TH rows); band_residency: how many of its workgroups one CU holds at once
 void launch_hot_band(const FArgs &A, const BandArgs &B, hipStream_t stream);

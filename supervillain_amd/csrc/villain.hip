@@ -20,6 +20,7 @@
 //   dS_link:                ((kappa/2) * cr) * ((2*r) + cr)            (neighborhood.py:111)
 //   face_sum:               (((0 + f0[x]) + f0[x-e0]) + f1[x]) + f1[x-e1]  (reference.py:48-64)
 //   r update:               (r + d(cphi)) - (2pi)*cn                  (neighborhood.py:129)
+#include <array>
 #include <atomic>
 #include <thread>
 #include <chrono>
@@ -949,6 +950,54 @@ std::vector<int32_t> band_strips(int32_t H, int nsx) {
     return tab;
 }
 
+// Two-wave strip table for a region that one round of 8-wave workgroups covers, two per CU (the config-4 tile): the
+// first `first` workgroups to be dispatched (one per CU) get strips of `tall` rows, the second wave strips of `shrt`
+// rows.  Two equal strips on one CU finish at 31 and 41 us (oldest-first issue, r3 WG timeline): the older
+// workgroup is barely slowed, the younger runs on what is left and then alone, so the CU's time is set by the
+// younger one.  6 row steps for the older and 4 for the younger balance that.  Rows of each column
+// strip: its tall strips, then its short ones, the last one shortened to the region.  {ix, t0, t1} per logical block
+// (logical_block's XCD-aware order; dispatch order is blockIdx, dealt round-robin over the 8 XCDs); empty when the
+// region does not fit two waves.
+std::vector<int32_t> two_wave_strips(int32_t H, int nsx, int first, int tall, int shrt) {
+    std::vector<std::array<int32_t, 3>> T, S;
+    for (int c = 0; c < nsx; c++) {
+        const int nt = first / nsx + (c < first % nsx ? 1 : 0);
+        int32_t t = 0;
+        for (int i = 0; i < nt && t < H; i++) {
+            const int32_t h = std::min<int32_t>(tall, H - t);
+            T.push_back({c, t, t + h});
+            t += h;
+        }
+        while (t < H) {
+            const int32_t h = std::min<int32_t>(shrt, H - t);
+            S.push_back({c, t, t + h});
+            t += h;
+        }
+    }
+    const int G = (int)(T.size() + S.size());
+    if ((int)T.size() > first || G > 2 * first) return {};
+    // dispatch rank (blockIdx) of each logical block
+    const int per = G / 8, rem = G % 8;
+    std::vector<std::pair<int, int>> order;  // (blockIdx, logical)
+    for (int x = 0; x < 8; x++) {
+        const int start = x * per + std::min(x, rem), n = per + (x < rem ? 1 : 0);
+        for (int k = 0; k < n; k++) order.push_back({8 * k + x, start + k});
+    }
+    std::sort(order.begin(), order.end());
+    std::vector<int32_t> tab(3 * (size_t)G);
+    // the earliest-dispatched logical blocks take the tall strips; each group in logical (XCD-range) order, so an
+    // XCD's strips are neighbours in their column
+    std::vector<int> first_wave, second_wave;
+    for (int i = 0; i < G; i++) (i < (int)T.size() ? first_wave : second_wave).push_back(order[i].second);
+    std::sort(first_wave.begin(), first_wave.end());
+    std::sort(second_wave.begin(), second_wave.end());
+    for (size_t i = 0; i < T.size(); i++)
+        for (int j = 0; j < 3; j++) tab[3 * (size_t)first_wave[i] + j] = T[i][j];
+    for (size_t i = 0; i < S.size(); i++)
+        for (int j = 0; j < 3; j++) tab[3 * (size_t)second_wave[i] + j] = S[i][j];
+    return tab;
+}
+
 // returns false if the fused path cannot represent the state (|n| too large): caller falls back
 // set once a band launch has failed (BAND_FAIL_BLOCK): the process's small lattices then run one sweep per launch
 static std::atomic<bool> band_broken{false};
@@ -1118,7 +1167,11 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             const int step = band_k ? bandK : 1;
             const bool hot_k = band_k || (use_hot && !hot_off && NWv == 4 && hot_ok(P, &blocks[(size_t)k * nb]));
             // a sweep with known rejections (a replay) or unequal buffered-half pairs: the hot kernel's skip form
-            const bool skip_k = !hot_k && use_hot && !hot_off && NWv == 4 && hot_nw == 4 &&
+            static const bool skip_on = [] {  // SV_HOT_SKIP=0: replays on the general int32 kernel (A/B)
+                const char *e = getenv("SV_HOT_SKIP");
+                return !(e && atoi(e) == 0);
+            }();
+            const bool skip_k = skip_on && !hot_k && use_hot && !hot_off && NWv == 4 && hot_nw == 4 &&
                                 hot_skip_ok(P, &blocks[(size_t)k * nb]);
             if (!hot_k && seg) {
                 ctx->time_end(seg, k - seg_k0, seg_k0);
