@@ -759,11 +759,12 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
                 }
                 int grid = A.nsx * A.nsy;
                 if (hot[k] && nw8) {
-                    // two waves of strips, taller for the workgroups dispatched first (two_wave_strips; SV_TILE_SCHED=0:
-                    // uniform strips of TH rows)
+                    // SV_TILE_SCHED=1: two waves of strips, taller for the workgroups dispatched first (two_wave_strips).
+                    // Off by default: 50.8 / 50.9 vs 49.5 / 49.6 us per 2048 x 1024 tile sweep with uniform strips (r4,
+                    // profiles/r04_tile_ab.txt) -- the second wave does not line up behind the first as assumed
                     static const int sched = [] {
                         const char *e = getenv("SV_TILE_SCHED");
-                        return e ? atoi(e) : 1;
+                        return e ? atoi(e) : 0;
                     }();
                     static const int cus = [] {
                         int dev = 0, v = 0;

@@ -1167,9 +1167,13 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             const int step = band_k ? bandK : 1;
             const bool hot_k = band_k || (use_hot && !hot_off && NWv == 4 && hot_ok(P, &blocks[(size_t)k * nb]));
             // a sweep with known rejections (a replay) or unequal buffered-half pairs: the hot kernel's skip form
-            static const bool skip_on = [] {  // SV_HOT_SKIP=0: replays on the general int32 kernel (A/B)
+            // SV_HOT_SKIP=1: replays on the hot kernel's skip form.  Off: it runs a replayed L=4096 sweep in ~566 us
+            // (unpaired draws on every strip, skip scans, spills), the general int32 kernel in less -- a 20-sweep window
+            // with a rejection costs +0.48 ms on the general kernel against +0.65 ms on the skip form (r4, 150 calls
+            // each, profiles/r04_replay_ab.txt)
+            static const bool skip_on = [] {
                 const char *e = getenv("SV_HOT_SKIP");
-                return !(e && atoi(e) == 0);
+                return e && atoi(e) == 1;
             }();
             const bool skip_k = skip_on && !hot_k && use_hot && !hot_off && NWv == 4 && hot_nw == 4 &&
                                 hot_skip_ok(P, &blocks[(size_t)k * nb]);
