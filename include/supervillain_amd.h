@@ -70,6 +70,13 @@ int sv_ctx_sweep_counts(sv_ctx *ctx, int64_t *hot, int64_t *fused, int64_t *gene
 /* Diagnostic: of the hot sweeps since the last call (then reset), those run K at a time by the multi-sweep band
  * launches of small periodic lattices (villain_sweep_hot_band, SV_BAND_K), and the number of such launches. */
 int sv_ctx_band_counts(sv_ctx *ctx, int64_t *sweeps, int64_t *launches);
+/* Diagnostic: the same for the temporal-blocking launches (villain_sweep_block: K sweeps per launch, each workgroup
+ * on its own block and deep-halo frame in LDS). */
+int sv_ctx_block_counts(sv_ctx *ctx, int64_t *sweeps, int64_t *launches);
+/* Which multi-sweep launches small periodic lattices may use: 0 temporal blocks or else bands (default), 1 blocks
+ * only, 2 bands only, 3 one sweep per launch; K: sweeps per temporal-blocking launch (0: the default; an even K runs
+ * as K - 1, and K shrinks until the launch's frame fits).  Returns -1 for another mode or K outside 0..15. */
+int sv_ctx_set_multisweep(sv_ctx *ctx, int32_t mode, int32_t K);
 /* Diagnostic (tests): the context's PCG64 jump-table cache holds at most `cap` increments (0: the default, 1024 or
  * SV_MAX_TABLES); a full cache drains the device and is dropped.  sv_ctx_table_purges reports how often it was. */
 int sv_ctx_set_table_cap(sv_ctx *ctx, int32_t cap);

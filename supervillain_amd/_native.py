@@ -44,6 +44,8 @@ def lib():
         L.sv_ctx_kernel_time.argtypes = [vp, P(f64), P(i64)]
         L.sv_ctx_sweep_counts.argtypes = [vp, P(i64), P(i64), P(i64)]
         L.sv_ctx_band_counts.argtypes = [vp, P(i64), P(i64)]
+        L.sv_ctx_block_counts.argtypes = [vp, P(i64), P(i64)]
+        L.sv_ctx_set_multisweep.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
         L.sv_ctx_set_table_cap.argtypes = [vp, ctypes.c_int32]
         L.sv_ctx_table_purges.argtypes = [vp, P(i64)]
         L.sv_hbm_copy.argtypes = [vp, i64, i32, i32, P(f64)]
@@ -114,7 +116,7 @@ def lib():
 
 
 EXPORTED = ('sv_ctx_create', 'sv_ctx_destroy', 'sv_last_error', 'sv_device_count', 'sv_build_info',
-            'sv_ctx_set_timing', 'sv_ctx_kernel_time', 'sv_ctx_sweep_counts', 'sv_ctx_band_counts', 'sv_ctx_set_table_cap', 'sv_ctx_table_purges', 'sv_hbm_copy', 'sv_rng_gather', 'sv_rng_scatter',
+            'sv_ctx_set_timing', 'sv_ctx_kernel_time', 'sv_ctx_sweep_counts', 'sv_ctx_band_counts', 'sv_ctx_block_counts', 'sv_ctx_set_multisweep', 'sv_ctx_set_table_cap', 'sv_ctx_table_purges', 'sv_hbm_copy', 'sv_rng_gather', 'sv_rng_scatter',
             'sv_villain_neighborhood', 'sv_villain_create', 'sv_villain_destroy', 'sv_villain_upload',
             'sv_villain_download', 'sv_villain_run', 'sv_villain_observables', 'sv_villain_emit', 'sv_villain_emit_wait', 'sv_villain_run_philox',
             'sv_worldline_emit', 'sv_worldline_emit_wait', 'sv_host_register', 'sv_host_unregister',
@@ -198,6 +200,17 @@ class Context:
         c = [ctypes.c_int64() for _ in range(2)]
         self.check(lib().sv_ctx_band_counts(self.handle, *[ctypes.byref(x) for x in c]), 'sv_ctx_band_counts')
         return dict(zip(('sweeps', 'launches'), (x.value for x in c)))
+
+    def block_counts(self):
+        """Temporal-blocking launches since the last call: {'sweeps', 'launches'} (sv_ctx_block_counts)."""
+        c = [ctypes.c_int64() for _ in range(2)]
+        self.check(lib().sv_ctx_block_counts(self.handle, *[ctypes.byref(x) for x in c]), 'sv_ctx_block_counts')
+        return dict(zip(('sweeps', 'launches'), (x.value for x in c)))
+
+    def set_multisweep(self, mode, K=0):
+        """Multi-sweep launches of small lattices: 0 blocks or bands, 1 blocks, 2 bands, 3 none; K sweeps per
+        temporal-blocking launch (0: the default) (sv_ctx_set_multisweep)."""
+        self.check(lib().sv_ctx_set_multisweep(self.handle, int(mode), int(K)), 'sv_ctx_set_multisweep')
 
     def set_table_cap(self, cap):
         """Bound this context's jump-table cache to `cap` increments (0: the default; tests) (sv_ctx_set_table_cap)."""

@@ -348,6 +348,21 @@ int sv_ctx_band_counts(sv_ctx *ctx, int64_t *sweeps, int64_t *launches) {
     return 0;
 }
 
+int sv_ctx_block_counts(sv_ctx *ctx, int64_t *sweeps, int64_t *launches) {
+    if (!ctx) return -1;
+    if (sweeps) *sweeps = ctx->sweeps_block;
+    if (launches) *launches = ctx->launches_block;
+    ctx->sweeps_block = ctx->launches_block = 0;
+    return 0;
+}
+
+int sv_ctx_set_multisweep(sv_ctx *ctx, int32_t mode, int32_t K) {
+    if (!ctx || mode < 0 || mode > 3 || K < 0 || K > 15) return -1;  // (BAND_MAXK)
+    ctx->multisweep = mode;
+    ctx->block_k = K;
+    return 0;
+}
+
 int sv_ctx_kernel_time(sv_ctx *ctx, double *ms_total, int64_t *launches) {
     if (!ctx) return -1;
     try {

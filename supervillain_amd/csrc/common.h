@@ -146,6 +146,10 @@ struct sv_ctx {
     int64_t sweeps_hot = 0, sweeps_fused = 0, sweeps_generic = 0;
     // of the hot sweeps: those run by multi-sweep band launches, and the launches (sv_ctx_band_counts)
     int64_t sweeps_band = 0, launches_band = 0;
+    // the same for temporal-blocking launches (sv_ctx_block_counts), and the multi-sweep mode (sv_ctx_set_multisweep:
+    // 0 blocks or bands, 1 blocks only, 2 bands only, 3 one sweep per launch)
+    int64_t sweeps_block = 0, launches_block = 0;
+    int32_t multisweep = 0, block_k = 0;  // (block_k: sweeps per temporal-blocking launch, 0 = the default)
     void time_begin(hipEvent_t *a);
     void time_end(hipEvent_t a, int64_t launches = 1, int64_t first = 0);
     void time_collect();  // after a stream sync

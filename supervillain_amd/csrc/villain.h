@@ -105,6 +105,29 @@ struct BandArgs {
     int64_t *n[BAND_MAXK + 1];
 };
 
+// Multi-sweep launches by temporal blocking (villain_sweep_block, villain_block.hip): each workgroup
+// owns a bs x bs block and keeps the block's deep-halo frame for the whole launch in LDS (sweep j decides the block
+// extended by 2(K-1-j) rows / columns above and left and 3(K-1-j) below and right, and reads two more around that), so
+// no workgroup waits for another.  Buffers as BandArgs: sweep j's own blocks go to buffer j + 1.  The launch's later
+// sweeps move their row bases by `step` (the map of one sweep's stream length: the host checks that every descriptor of
+// sweep j + 1 is `step` of sweep j's, with equal buffered-half flags).
+struct BlockArgs {
+    int32_t K;     // sweeps per launch (odd, as BandArgs)
+    int32_t bs;    // block side
+    int32_t nbx;   // blocks per row of blocks (N / bs)
+    int32_t nb;    // descriptors per sweep
+    Affine step;
+    double *phi[BAND_MAXK + 1];
+    int64_t *n[BAND_MAXK + 1];
+};
+// the frame's side (rows = columns) and the launch's dynamic LDS bytes
+__host__ __device__ inline int32_t block_frame(int32_t bs, int32_t K) { return bs + 5 * (K - 1) + 5; }
+__host__ __device__ inline size_t block_lds_bytes(int32_t F) {
+    // small-offset maps, row bases [F][2 sets][2 colours][6], phi / r0 / r1 (f64) and n0 / n1 (int32) per frame
+    // site, per-sweep statistics (16 + 16 words) and the overflow flag
+    return 2 * 16 * (size_t)SMALL_LDS + (size_t)F * 24 * 16 + (size_t)F * F * 32 + 256 + 16;
+}
+
 // (FArgs::progress) the launch has started: every earlier launch of its stream has finished
 __device__ __forceinline__ void note_progress(const FArgs &A) {
     if (A.progress && blockIdx.x == 0 && threadIdx.x == 0)
@@ -163,6 +186,8 @@ void launch_hot(const FArgs &A, int grid, hipStream_t stream);
 // the band launch (8-wave strips of B.TH rows); band_residency: how many of its workgroups one CU holds at once
 void launch_hot_band(const FArgs &A, const BandArgs &B, hipStream_t stream);
 int band_residency();
+// the temporal-blocking launch (nbx * nbx workgroups of 8 waves)
+void launch_block(const FArgs &A, const BlockArgs &B, hipStream_t stream);
 // full-row replica batches (config 5) on the fast-draw kernel: whether N qualifies, and the launch (the sweep must
 // pass hot_ok for every replica: no skips, no buffered half-word, choice values in range)
 bool hot_fr_ok(int32_t N);

@@ -1068,6 +1068,48 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     // SV_BAND_K sets K (odd, at most BAND_MAXK; 0 disables); the band's workgroups must all be resident on its XCD.
     const int nbands = 8;
     int bandK = 0, bandP = 0;
+    // Temporal blocking (villain_sweep_block, BlockArgs in villain.h) is preferred where it applies: bs x bs blocks (bs =
+    // N / 16, at least 4; SV_BLOCK_BS overrides) whose frame of K sweeps fits the lattice and the small-offset maps.
+    // sv_ctx_set_multisweep: 0 either (blocks first), 1 blocks only, 2 bands only, 3 neither.  SV_BLOCK_K sets K.
+    int blockK = 0, blockBS = 0;
+    Affine block_step{};
+    static const int mode_env = [] {  // SV_MULTISWEEP: the mode of contexts that set none (experiments)
+        const char *e = getenv("SV_MULTISWEEP");
+        return e ? atoi(e) : 0;
+    }();
+    const int mode = ctx->multisweep ? ctx->multisweep : mode_env;
+    {
+        static const int bk_env = [] {
+            const char *e = getenv("SV_BLOCK_K");
+            return e ? atoi(e) : -1;
+        }();
+        static const int bs_env = [] {
+            const char *e = getenv("SV_BLOCK_BS");
+            return e ? atoi(e) : 0;
+        }();
+        // one sweep's stream length in u64s (the buffered-half flags repeat from sweep to sweep when the bounded
+        // words of a sweep are even in number; the launch checks every descriptor anyway)
+        uint64_t S = 0, bounded = 0;
+        for (const BlockSpec &b : specs) (b.kind == UNIFORM ? S : bounded) += b.count;
+        if ((mode == 0 || mode == 1) && bk_env != 0 && use_hot && hot_params_ok(P) && N % 2 == 0 && N <= 512 &&
+            bounded % 2 == 0) {
+            int bs = bs_env > 0 ? bs_env : std::max(4, N / 16);
+            while (bs > 2 && N % bs) bs--;
+            int K = std::min(ctx->block_k > 0 ? ctx->block_k : (bk_env > 0 ? bk_env : 3), BAND_MAXK);
+            if (K % 2 == 0) K--;
+            if (N % bs == 0) {
+                for (; K >= 3; K -= 2) {
+                    const int F = block_frame(bs, K);
+                    if (F <= N && F <= SMALL_LDS - 2 && block_lds_bytes(F) <= 160 * 1024) break;
+                }
+                if (K >= 3) {
+                    blockK = K;
+                    blockBS = bs;
+                    block_step = host_power(inc, S + bounded / 2);
+                }
+            }
+        }
+    }
     {
         static const int band_env = [] {
             const char *e = getenv("SV_BAND_K");
@@ -1080,7 +1122,8 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                 v = 0;
             return v;
         }();
-        if (use_hot && small8 && hot_nw == 8 && band_env != 0 && !band_broken.load() && N % nbands == 0 && N <= 512) {
+        if (!blockK && (mode == 0 || mode == 2) && use_hot && small8 && hot_nw == 8 && band_env != 0 &&
+            !band_broken.load() && N % nbands == 0 && N <= 512) {
             const int own = N / nbands, per_xcd = band_residency() * (cus / nbands);
             // (K = 3 measured best at L=256, r4: 11.8 / 12.7 / 13.7 us per sweep at K = 3 / 5 / 7, 13.7 one per launch)
             int K = std::min(band_env > 0 ? band_env : 3, BAND_MAXK);
@@ -1094,6 +1137,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                 }
             }
         }
+        if (blockK) bandK = blockK;  // (the band launches' buffers, gate and replay protocol)
         if (bandK) {
             while ((int)st->band_phi.size() < bandK - 1) {
                 double *p = nullptr;
@@ -1164,6 +1208,13 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             // a band launch: the next K sweeps all pass hot_ok
             bool band_k = bandK && !hot_off && k + bandK <= count;
             for (int j = 0; band_k && j < bandK; j++) band_k = hot_ok(P, &blocks[(size_t)(k + j) * nb]);
+            // a block launch: every descriptor of sweep j + 1 one sweep's stream length after sweep j's
+            for (int j = 0; band_k && blockK && j + 1 < bandK; j++)
+                for (int b = 0; band_k && b < nb; b++) {
+                    const Block &x = blocks[(size_t)(k + j) * nb + b], &y = blocks[(size_t)(k + j + 1) * nb + b];
+                    const u128 nx = apply(block_step, u128{x.base_lo, x.base_hi});
+                    band_k = nx.lo == y.base_lo && nx.hi == y.base_hi && x.has == y.has;
+                }
             const int step = band_k ? bandK : 1;
             const bool hot_k = band_k || (use_hot && !hot_off && NWv == 4 && hot_ok(P, &blocks[(size_t)k * nb]));
             // a sweep with known rejections (a replay) or unequal buffered-half pairs: the hot kernel's skip form
@@ -1208,7 +1259,27 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             A.sweep = (uint32_t)k;
             A.S.gate = band_gate;  // (band batches: a report gates the later launches by sweep)
             farg_single(A, nsx, nsy);
-            if (band_k) {
+            if (band_k && blockK) {
+                BlockArgs B;
+                B.K = blockK;
+                B.bs = blockBS;
+                B.nbx = N / blockBS;
+                B.nb = nb;
+                B.step = block_step;
+                B.phi[0] = st->phi[st->cur ^ (k & 1)];
+                B.n[0] = st->n[st->cur ^ (k & 1)];
+                for (int j = 1; j < blockK; j++) {
+                    B.phi[j] = st->band_phi[j - 1];
+                    B.n[j] = st->band_n[j - 1];
+                }
+                B.phi[blockK] = st->phi[st->cur ^ (k & 1) ^ 1];
+                B.n[blockK] = st->n[st->cur ^ (k & 1) ^ 1];
+                launch_block(A, B, ctx->stream);
+                band_starts.push_back(k);
+                ctx->sweeps_hot += blockK;
+                ctx->sweeps_block += blockK;
+                ctx->launches_block++;
+            } else if (band_k) {
                 A.hot_nw = 8;
                 A.adv[0] = adv8[0];
                 A.adv[1] = adv8[1];

@@ -67,11 +67,6 @@ __device__ uint64_t g_bandtime[8 * 128 * BT_SW * BT];
 __device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 #endif
 
-struct HotDraws {
-    double u, dphi;
-    uint32_t w[4];  // the uint32 each choice block (f0, b0, f1, b1) draws for this site
-};
-
 // Interior strips: the fwd/bwd blocks of a direction read the two halves of one u64 for two adjacent lanes
 // (draws_fastp in fused.h explains the packing of pk)
 __device__ __forceinline__ HotDraws hot_draws_paired(const FArgs &A, int32_t lane, uint32_t pk, const u128 *bs,
@@ -107,64 +102,6 @@ __device__ __forceinline__ HotDraws hot_draws_paired_sel(const FArgs &A, int32_t
         const uint32_t got = pair_exchange(send, half, lane);
         D.w[2 * mu] = half ? got : (uint32_t)X;
         D.w[2 * mu + 1] = half ? (uint32_t)(X >> 32) : got;
-    }
-    return D;
-}
-
-// Edge strips: columns that wrap around the row draw from the second base set (at global column xw); every
-// offset is < SMALL_LDS by construction; words unpaired (the wrap breaks the lane pairing).
-// has4 / buf: each choice block's buffered-half flag and word.  SKIP (a sweep that replays known NumPy Lemire
-// rejections): block j's draw d sits at stream position d + (the skips at or before it) -- skip_pos of the general
-// kernel, with at most HOT_MAXSK positions per block read from LDS -- so its word is a half-word further on, still a
-// small offset ahead of the row base (which sits at the unshifted position); spos returns the positions (reports).
-static constexpr int HOT_MAXSK = 4;
-template <bool SKIP = false>
-__device__ __forceinline__ HotDraws hot_draws_edge(const FArgs &A, int64_t gq, int32_t gx, int32_t xb, int32_t xw,
-                                                   const u128 *bA, const u128 *bB, const SmallTab &sm,
-                                                   const uint32_t *has4, const uint32_t *buf,
-                                                   const uint32_t (*sk)[HOT_MAXSK] = nullptr, const int32_t *nsk = nullptr,
-                                                   uint32_t *spos = nullptr) {
-    const int64_t N = A.G.Nx;
-    const bool wr = !(gx >= xb && gx < xb + SMALL_LDS);
-    const int32_t xr = wr ? xw : xb;
-    const int64_t lin = gq * N + gx, rank = lin >> 1, rb = (gq * N + xr) >> 1;
-    // bA, bB point at the wave's two base sets in LDS: each lane reads the set it draws from (one base in
-    // registers at a time, not both sets)
-    const u128 *bs = wr ? bB : bA;
-    HotDraws D;
-    D.u = u53(xsl_rr(hot_apply(sm, (uint32_t)(gx - xr), bs[0])));
-    D.dphi = A.P.lo_phi + A.P.range_phi * u53(xsl_rr(hot_apply(sm, (uint32_t)(rank - rb), bs[1])));
-    if constexpr (!SKIP) {
-        // equal flags within each fwd/bwd pair: one word offset per direction
-#pragma unroll
-        for (int mu = 0; mu < 2; mu++) {
-            const int64_t qq = rank - (int64_t)has4[2 * mu];
-            const int64_t w0 = (rb - (int64_t)has4[2 * mu]) < 0 ? 0 : ((rb - (int64_t)has4[2 * mu]) >> 1);
-            const uint32_t off = (uint32_t)((qq < 0 ? 0 : (qq >> 1)) - w0);
-#pragma unroll
-            for (int fb = 0; fb < 2; fb++) {
-                const uint64_t X = xsl_rr(hot_apply(sm, off, bs[2 + 2 * mu + fb]));
-                uint32_t word = (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
-                if (qq < 0) word = buf[2 * mu + fb];  // has && rank == 0: the block's buffered half-word
-                D.w[2 * mu + fb] = word;
-            }
-        }
-        return D;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        int64_t q = rank;
-#pragma unroll
-        for (int i = 0; i < HOT_MAXSK; i++)
-            if (i < nsk[j] && (int64_t)sk[j][i] <= q) q++;
-        spos[j] = (uint32_t)q;
-        const int64_t qq = q - (int64_t)has4[j];
-        const int64_t w0 = (rb - (int64_t)has4[j]) < 0 ? 0 : ((rb - (int64_t)has4[j]) >> 1);
-        const uint32_t off = (uint32_t)((qq < 0 ? 0 : (qq >> 1)) - w0);
-        const uint64_t X = xsl_rr(hot_apply(sm, off, bs[2 + j]));
-        uint32_t word = (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
-        if (qq < 0) word = buf[j];  // has && position 0: the block's buffered half-word
-        D.w[j] = word;
     }
     return D;
 }

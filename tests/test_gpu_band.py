@@ -15,6 +15,18 @@ from tests.test_gpu_overflow import single
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def bands_only():
+    """Band launches only (the default prefers temporal blocks where they apply, tests/test_gpu_block.py)."""
+    from supervillain_amd import _native
+    ctx = _native.context()
+    ctx.set_multisweep(2)
+    try:
+        yield
+    finally:
+        ctx.set_multisweep(0)
+
+
 def check(N, kappa, W, phi0, n0, sweeps, make_gen, oracle_lib, band_expected=True):
     from supervillain_amd import _native
     ctx = _native.context()
