@@ -229,6 +229,26 @@ __device__ __forceinline__ u128 full_jump(const JumpTables *T, const Block *blk,
     __builtin_amdgcn_s_waitcnt(0);
     return r;
 }
+// The same with the level tables' entries loaded together (digit 0's entry is the identity map): one memory round
+// trip instead of up to JUMP_LEVELS dependent ones, for the compositions with the identity maps of zero digits and 32
+// more live registers -- for the kernels' prologues (row bases), not their loops
+#ifndef SV_FLAT_JUMP
+#define SV_FLAT_JUMP 1
+#endif
+__device__ __forceinline__ u128 full_jump_flat(const JumpTables *T, const Block *blk, uint32_t pos) {
+#if SV_FLAT_JUMP
+    Affine m[JUMP_LEVELS];
+#pragma unroll
+    for (int l = 0; l < JUMP_LEVELS; l++) m[l] = T->level[l][(pos >> (l * JUMP_DIGIT_BITS)) & (JUMP_DIGITS - 1)];
+    u128 r = block_base(*blk);
+#pragma unroll
+    for (int l = 0; l < JUMP_LEVELS; l++) r = apply(m[l], r);
+    __builtin_amdgcn_s_waitcnt(0);
+    return r;
+#else
+    return full_jump(T, blk, pos);
+#endif
+}
 
 __device__ __forceinline__ u128 from_base(const JumpTables *T, const Block *blk, const SmallTab &sm, u128 base,
                                           int64_t bpos, int64_t pos) {

@@ -409,7 +409,10 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     if constexpr (!PH) {  // (the running bases live in LDS only: the advance reads them back)
         if (!BAND || hb->first) {  // (a band sweep after the first: its predecessor jumped to them)
             u128 bases{0, 0};
-            if (base_lane) bases = full_jump(Tb, &blocks[bblk], (uint32_t)base_pos(bty, grow(brow), Nx, bx, bhas));
+            // (flat table loads: not in the replica kernels, whose registers they would push into scratch)
+            if (base_lane)
+                bases = FR ? full_jump(Tb, &blocks[bblk], (uint32_t)base_pos(bty, grow(brow), Nx, bx, bhas))
+                           : full_jump_flat(Tb, &blocks[bblk], (uint32_t)base_pos(bty, grow(brow), Nx, bx, bhas));
             __builtin_amdgcn_s_waitcnt(0);
             if (base_lane) s_base[wave][lane] = bases;
         }

@@ -256,7 +256,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
 #if SV_WF_PF0
     prefetch(t0 - 5);  // the first region rows in flight while the row bases are jumped to
 #endif
-    if (base_lane) bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)wf_base_pos(bbnd, grow(brow), N, bx, bhas));
+    if (base_lane) bases = full_jump_flat(A.T, &A.blocks[bblk], (uint32_t)wf_base_pos(bbnd, grow(brow), N, bx, bhas));
     __builtin_amdgcn_s_waitcnt(0);
     if (base_lane) Ls.base[wave][lane] = bases;
 #if SV_WFTIME
