@@ -2,7 +2,7 @@
 # (scripts/profile.sh r04), worldline_step_fused PMC (VALU per plaquette-step).
 source scripts/gpu/guard.sh
 export TMPDIR=/tmp
-O=gpurun_out/r4_final
+O=${OUT:-gpurun_out/r4_final}
 mkdir -p $O/bench
 export AMD_LOG_LEVEL=1
 step tests timeout -k 10 1000 python -u -m pytest tests -x -q --timeout 300 --timeout-method thread -m gpu > $O/tests.log 2>&1
@@ -20,6 +20,6 @@ step l256 timeout -k 10 300 python -u bench.py --L 256 > $O/bench/l256.json 2> $
 step rep timeout -k 10 300 python -u bench.py --workload replicas > $O/bench/replicas.json 2> $O/bench/replicas.err
 step t8 timeout -k 10 300 python -u bench.py --tiles 2x4 --steps 40 --warmup 5 --no-cpu-baseline > $O/bench/tiles2x4.json 2> $O/bench/tiles2x4.err
 for f in $O/bench/*.json; do python -c "import json,sys; d=json.loads(open('$f').readline()); print('$f', round(d['value']/1e9,2), round(d['ms_per_step']*1e3,2), round(d['roofline']['avg_launch_us'],2), round(d['roofline']['frac'],3), d['config'].get('lemire_rejections_in_timed_steps'))"; done
-step prof timeout -k 10 900 bash scripts/profile.sh r04
+step prof timeout -k 10 900 bash scripts/profile.sh ${PTAG:-r04}
 step wfpmc timeout -s KILL 120 rocprofv3 --kernel-include-regex worldline_step_fused --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d $O/wf_pmc -o p --output-format csv -- python bench.py --workload worldline --steps 12 --warmup 2 --no-cpu-baseline > $O/wf_pmc.log 2>&1
 mkdir -p $O/ab && cp -r $O/wf_pmc $O/ab/wf_base && python scripts/perf/ablate_summary.py $O/ab
