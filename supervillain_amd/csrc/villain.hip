@@ -1024,11 +1024,14 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     const int TH = small8 ? small_th : fused_th(N, nsx);
     const int nsy = (N + TH - 1) / TH;
     const int grid = nsx * nsy;
-    static const int BATCH = [] {  // sweeps per host round trip (SV_BATCH overrides; 64 measured best)
+    // sweeps per host round trip (SV_BATCH overrides): 64 measured best at L=4096; small lattices amortize the ~80 us
+    // batch boundary (statistics read back, the next batch's reset and plan upload) over 256 (L=256, r4: 8.4-8.6 vs
+    // 9.1-9.7 us per sweep wall, profiles/r04_block_l256_batch.txt)
+    static const int BATCH_env = [] {
         const char *e = getenv("SV_BATCH");
-        const int v = e ? atoi(e) : 64;
-        return v >= 1 ? v : 64;
+        return e && atoi(e) >= 1 ? atoi(e) : 0;
     }();
+    const int BATCH = BATCH_env ? BATCH_env : (V <= (1 << 18) ? 256 : 64);
     // row-base advance maps for NW rows: NW*N metropolis draws, NW*N/2 ranks, NW*N/4 words
     if ((int64_t)NWv * N % 4) throw std::invalid_argument("fused path needs NW*N divisible by 4");
     const Affine adv[3] = {host_power(inc, (uint64_t)NWv * N), host_power(inc, (uint64_t)NWv * N / 2),

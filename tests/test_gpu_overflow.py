@@ -70,19 +70,32 @@ def near_bound(shape, seed):
     return (B14 - 2) * np.where(r.random(shape) < 0.5, 1, -1).astype(np.int64)
 
 
-def test_single_lattice_crosses_the_int16_bound(oracle_lib):
-    N, kappa, sweeps = 64, 1e-9, 6
-    phi0 = np.random.default_rng(1).uniform(-np.pi, np.pi, (N, N))
-    n0 = near_bound((2, N, N), 2)
-    phi, n, st, counts = single(N, kappa, 1, phi0, n0, sweeps, np.random.default_rng(3))
+@pytest.mark.parametrize('mode', [3, 1])
+def test_single_lattice_crosses_the_int16_bound(mode, oracle_lib):
+    """One sweep per launch (mode 3): the int16 kernel until the sweep that meets |n| >= 2^14, the int32 one from
+    there.  Temporal blocks (mode 1, the default at this size): their int32 LDS image takes the crossing in stride."""
+    ctx = _native.context()
+    ctx.set_multisweep(mode)
+    try:
+        N, kappa, sweeps = 64, 1e-9, 6
+        phi0 = np.random.default_rng(1).uniform(-np.pi, np.pi, (N, N))
+        n0 = near_bound((2, N, N), 2)
+        ctx.block_counts()
+        phi, n, st, counts = single(N, kappa, 1, phi0, n0, sweeps, np.random.default_rng(3))
+        blocks = ctx.block_counts()
+    finally:
+        ctx.set_multisweep(0)
     g = np.random.default_rng(3)
     p, m = phi0.copy(), n0.copy()
     ref = oracle_lib.villain_neighborhood(N, kappa, 1, p, m, sweeps, g)
     assert np.abs(m).max() >= B14  # the chain did cross the bound
     assert (phi == p).all() and (n == m).all()
     assert [s.accepted for s in st] == [s.accepted for s in ref]
-    # the first sweep ran on the int16 kernel; from the sweep that met |n| >= 2^14 on, the int32 one
-    assert counts['hot'] >= 1 and counts['fused'] >= 1 and counts['generic'] == 0, counts
+    if mode == 3:
+        # the first sweep ran on the int16 kernel; from the sweep that met |n| >= 2^14 on, the int32 one
+        assert counts['hot'] >= 1 and counts['fused'] >= 1 and counts['generic'] == 0, counts
+    else:
+        assert counts['hot'] == sweeps and blocks['sweeps'] == sweeps, (counts, blocks)
 
 
 @pytest.mark.parametrize('W,interval_n', [(1, 20000), (4096, 3), (3, 2731)])
