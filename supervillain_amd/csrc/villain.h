@@ -116,6 +116,7 @@ struct BlockArgs {
     int32_t bs;    // block side
     int32_t nbx;   // blocks per row of blocks (N / bs)
     int32_t nb;    // descriptors per sweep
+    int32_t xcd;   // 1: blocks dealt to the XCDs in contiguous runs (neighbouring blocks share an L2), 0: round-robin
     Affine step;
     double *phi[BAND_MAXK + 1];
     int64_t *n[BAND_MAXK + 1];

@@ -1269,6 +1269,11 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                 B.nbx = N / blockBS;
                 B.nb = nb;
                 B.step = block_step;
+                static const int xcd_env = [] {
+                    const char *e = getenv("SV_BLOCK_XCD");
+                    return e ? atoi(e) : 0;
+                }();
+                B.xcd = xcd_env;
                 B.phi[0] = st->phi[st->cur ^ (k & 1)];
                 B.n[0] = st->n[st->cur ^ (k & 1)];
                 for (int j = 1; j < blockK; j++) {

@@ -74,7 +74,12 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
     const int32_t N = A.G.Nx;
     const int64_t V = A.G.plane;
     const int K = B.K, E = K - 1, bs = B.bs;
-    const int by = (int)blockIdx.x / B.nbx, bx = (int)blockIdx.x - by * B.nbx;
+    int bl = (int)blockIdx.x;
+    if (B.xcd) {  // workgroup i runs on XCD i mod 8: give each XCD a contiguous run of blocks
+        const int G = (int)gridDim.x, per = G / 8, rem = G % 8, xcd = bl & 7, k = bl >> 3;
+        bl = xcd * per + (xcd < rem ? xcd : rem) + k;
+    }
+    const int by = bl / B.nbx, bx = bl - by * B.nbx;
     const int32_t r0 = by * bs, c0 = bx * bs;
     const int F = block_frame(bs, K);
     const int32_t FR0 = r0 - 2 * E - 2, FC0 = c0 - 2 * E - 2;  // frame origin (lattice coordinates, may be < 0)
