@@ -23,3 +23,4 @@ for f in $O/bench/*.json; do python -c "import json,sys; d=json.loads(open('$f')
 step prof timeout -k 10 900 bash scripts/profile.sh ${PTAG:-r04}
 step wfpmc timeout -s KILL 120 rocprofv3 --kernel-include-regex worldline_step_fused --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d $O/wf_pmc -o p --output-format csv -- python bench.py --workload worldline --steps 12 --warmup 2 --no-cpu-baseline > $O/wf_pmc.log 2>&1
 mkdir -p $O/ab && cp -r $O/wf_pmc $O/ab/wf_base && python scripts/perf/ablate_summary.py $O/ab
+[ "${PTAG:-}" = r04b ] && bash scripts/gpu/r4_l256dbg.sh
