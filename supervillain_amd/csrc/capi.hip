@@ -73,8 +73,9 @@ void sv_ctx::ensure_blocks(size_t n) {
     SV_HIP(hipMalloc(&d_blocks, blocks_cap * sizeof(sv::Block)));
 }
 
-void sv_ctx::upload_plan(const sv::Block *blocks, size_t nblocks, const uint32_t *skips, size_t nskips) {
-    ensure_blocks(nblocks);
+void sv_ctx::upload_plan(const sv::Block *blocks, size_t nblocks, const uint32_t *skips, size_t nskips, size_t offset) {
+    if (offset && offset + nblocks > blocks_cap) throw std::logic_error("upload_plan: a second part beyond the capacity");
+    ensure_blocks(offset + nblocks);
     ensure_skips(nskips + 1);
     const size_t bb = nblocks * sizeof(sv::Block), sb = nskips * sizeof(uint32_t);
     const int i = h_plan_i;
@@ -89,7 +90,7 @@ void sv_ctx::upload_plan(const sv::Block *blocks, size_t nblocks, const uint32_t
     }
     std::memcpy(h_plan[i], blocks, bb);
     if (sb) std::memcpy(h_plan[i] + bb, skips, sb);
-    SV_HIP(hipMemcpyAsync(d_blocks, h_plan[i], bb, hipMemcpyHostToDevice, stream));
+    SV_HIP(hipMemcpyAsync(d_blocks + offset, h_plan[i], bb, hipMemcpyHostToDevice, stream));
     if (sb) SV_HIP(hipMemcpyAsync(d_skips, h_plan[i] + bb, sb, hipMemcpyHostToDevice, stream));
     SV_HIP(hipEventRecord(ev_plan[i], stream));
 }

@@ -181,7 +181,9 @@ struct sv_ctx {
     // a batch plan (descriptors, skip positions) to d_blocks / d_skips through pinned staging: two pinned buffers
     // used in turn (an upload reuses the one of two uploads before, across the batch's synchronization), so the
     // copies are plain asynchronous DMA instead of pageable staging (~20 us of host time each)
-    void upload_plan(const sv::Block *blocks, size_t nblocks, const uint32_t *skips, size_t nskips);
+    // (offset: the descriptors go to d_blocks + offset -- the second part of a two-part plan, whose capacity the first
+    // part ensured, so that d_blocks does not move under launches already enqueued)
+    void upload_plan(const sv::Block *blocks, size_t nblocks, const uint32_t *skips, size_t nskips, size_t offset = 0);
     char *h_plan[2] = {nullptr, nullptr};
     size_t h_plan_cap[2] = {0, 0};
     hipEvent_t ev_plan[2] = {nullptr, nullptr};  // recorded after each buffer's copies (deferred runs do not sync)

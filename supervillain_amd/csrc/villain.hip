@@ -1175,10 +1175,22 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             reset_batch(ctx, ctx->d_stats, count * sizeof(sv_stats));
         std::vector<int> band_starts;  // first sweeps of this batch's band launches
         auto tp0 = std::chrono::steady_clock::now();
+        // A batch that is not pre-planned (a call's first) on a small lattice is planned in two parts: the first few
+        // launches' sweeps, uploaded and launched, then the rest while the device runs them (the plan of a 200-sweep
+        // L=256 batch is ~55 us, ~3% of the call, r4 profiles/r04b_l256_host_phases.log).  Only without known skips.
+        static const int plan2_env = [] {
+            const char *e = getenv("SV_PLAN2");
+            return e ? atoi(e) : 1;
+        }();
+        int part = count;  // sweeps of the batch planned and uploaded
         if (sw_next == sw) {
             blocks.swap(blocks_next);
             skipvec.swap(skipvec_next);
             c = c_next;
+        } else if (plan2_env && skips.empty() && V <= (1 << 18) && count >= 4 * 3 * std::max(bandK, 1)) {
+            part = 3 * std::max(bandK, 1);
+            plan_sweeps(ctx, c, inc, specs, sw, part, skips, blocks, skipvec);
+            ctx->ensure_blocks((size_t)count * nb);  // (the second part must not move d_blocks under the first launches)
         } else {
             plan_sweeps(ctx, c, inc, specs, sw, count, skips, blocks, skipvec);
         }
@@ -1208,6 +1220,14 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         __atomic_store_n(ctx->h_prog, 0, __ATOMIC_RELEASE);  // (the previous batch's launches have all finished)
         int next_chunk = CH;
         for (int k = 0; k < count;) {
+            if (part < count && k + std::max(bandK, 1) > part) {  // the two-part plan's second part
+                std::vector<Block> b2;
+                std::vector<uint32_t> s2;
+                plan_sweeps(ctx, c, inc, specs, sw + part, count - part, skips, b2, s2);
+                ctx->upload_plan(b2.data(), b2.size(), s2.data(), s2.size(), (size_t)part * nb);
+                blocks.insert(blocks.end(), b2.begin(), b2.end());
+                part = count;
+            }
             // a band launch: the next K sweeps all pass hot_ok
             bool band_k = bandK && !hot_off && k + bandK <= count;
             for (int j = 0; band_k && j < bandK; j++) band_k = hot_ok(P, &blocks[(size_t)(k + j) * nb]);
