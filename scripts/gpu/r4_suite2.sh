@@ -1,6 +1,6 @@
 # Full -m gpu suite after the temporal-blocking changes (runtime error log on), smoke, L=256 and headline lines
 source scripts/gpu/guard.sh
-O=gpurun_out/r4_suite2
+O=${OUT:-gpurun_out/r4_suite2}
 mkdir -p $O
 export AMD_LOG_LEVEL=1
 step tests timeout -k 10 1000 python -u -m pytest tests -x -q --timeout 300 --timeout-method thread -m gpu > $O/tests.log 2>&1
