@@ -124,9 +124,9 @@ struct BlockArgs {
 // the frame's side (rows = columns) and the launch's dynamic LDS bytes
 __host__ __device__ inline int32_t block_frame(int32_t bs, int32_t K) { return bs + 5 * (K - 1) + 5; }
 __host__ __device__ inline size_t block_lds_bytes(int32_t F) {
-    // small-offset maps, row bases [2 buffers][F][2 sets][2 colours][6], phi / r0 / r1 (f64) and n0 / n1 (int32) per frame
+    // small-offset maps, row bases [F][2 sets][2 colours][6], phi / r0 / r1 (f64) and n0 / n1 (int32) per frame
     // site, per-sweep statistics (16 + 16 words), the overflow flag and the choice-block descriptors (16 sweeps x 8)
-    return 2 * 16 * (size_t)SMALL_LDS + (size_t)F * 48 * 16 + (size_t)F * F * 32 + 256 + 16 + 16 * 8 * 8;
+    return 2 * 16 * (size_t)SMALL_LDS + (size_t)F * 24 * 16 + (size_t)F * F * 32 + 256 + 16 + 16 * 8 * 8;
 }
 
 // (FArgs::progress) the launch has started: every earlier launch of its stream has finished

@@ -33,9 +33,6 @@ __device__ uint64_t g_blktime[4096 * BLT];
 #ifndef SV_BLK_DRAW1
 #define SV_BLK_DRAW1 1  // the colour-1 draws made in the colour-0 pass (one round of lanes per colour)
 #endif
-#ifndef SV_BLK_DRAW2
-#define SV_BLK_DRAW2 1  // the next sweep's colour-0 draws made in the colour-1 pass (with SV_BLK_DRAW1)
-#endif
 #ifndef SV_BLK_FLATJUMP
 #define SV_BLK_FLATJUMP 1
 #endif
@@ -88,9 +85,8 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
     const int32_t FR0 = r0 - 2 * E - 2, FC0 = c0 - 2 * E - 2;  // frame origin (lattice coordinates, may be < 0)
 
     SmallTab &s_small = *reinterpret_cast<SmallTab *>(blk_lds);
-    // row bases [F][set][colour][6], two buffers: sweep j draws from buffer j & 1 while the next sweep's are made
-    u128 *s_base = reinterpret_cast<u128 *>(blk_lds + sizeof(SmallTab));
-    double *s_phi = reinterpret_cast<double *>(s_base + (size_t)F * 48);
+    u128 *s_base = reinterpret_cast<u128 *>(blk_lds + sizeof(SmallTab));  // [F][set][colour][6]
+    double *s_phi = reinterpret_cast<double *>(s_base + (size_t)F * 24);
     double *s_r0 = s_phi + F * F;  // residual of link (0, q, x) at (q, x)
     double *s_r1 = s_r0 + F * F;   // residual of link (1, q, x) at (q, x)
     int32_t *s_n0 = reinterpret_cast<int32_t *>(s_r1 + F * F);
@@ -183,13 +179,8 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
     const int32_t Wn = (int32_t)P.W, nW = (int32_t)(P.W * P.interval_n);
     const double hk = P.half_kappa;
 
-    // the colour-0 draws of sweep j + 1, made in sweep j's colour-1 pass (one round of lanes per colour)
-    HotDraws Dp;
-    int32_t cnp[4] = {0, 0, 0, 0};
-    bool have_p = false;
     for (int j = 0; j < K; j++) {
         const int e = E - j;
-        u128 *const sb = s_base + (size_t)(j & 1) * F * 24, *const sb_next = s_base + (size_t)((j + 1) & 1) * F * 24;
         const int32_t ra = r0 - 2 * e, rb = r0 + bs + 3 * e, ca = c0 - 2 * e, cb = c0 + bs + 3 * e;
         const uint32_t sweep_id = A.sweep + (uint32_t)j;
         __syncthreads();  // (the frame, the bases and the descriptors; the previous sweep's stores and advance)
@@ -219,25 +210,20 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
             spr[c] = (xhi[c] - xlo[c] + 2) >> 1;
             inv[c] = 1.0f / (float)spr[c];
         }
-        auto site_at = [](int c, int idx, int32_t ql, int32_t qh, int32_t xl, int32_t xh, int32_t &q, int32_t &x) {
-            const int nr = qh - ql + 1, sp = (xh - xl + 2) >> 1;
-            const int row = (int)(((float)idx + 0.5f) * (1.0f / (float)sp)), k = idx - row * sp;
-            q = ql + row;
-            x = xl + ((q + xl + c) & 1) + 2 * k;  // colour c: q + x = c mod 2
-            return row < nr && x <= xh;
-        };
         auto site_of = [&](int c, int idx, int32_t &q, int32_t &x) {
-            return site_at(c, idx, qlo[c], qhi[c], xlo[c], xhi[c], q, x);
+            const int row = (int)(((float)idx + 0.5f) * inv[c]), k = idx - row * spr[c];
+            q = qlo[c] + row;
+            x = xlo[c] + ((q + xlo[c] + c) & 1) + 2 * k;  // colour c: q + x = c mod 2
+            return row < nrows[c] && x <= xhi[c];
         };
-        // the site's draws and the choice values W (index - interval_n) (neighborhood.py:105-107) from the row bases
-        // bb of sweep `sid` (descriptors h4 / b4); a rejected word is reported
-        auto draw_site = [&](auto C, int32_t q, int32_t x, HotDraws &D, int32_t (&cn)[4], const u128 *bb,
-                             const uint32_t (&h4)[2][4], const uint32_t (&b4)[2][4], uint32_t sid) {
+        // the site's draws and the choice values W (index - interval_n) (neighborhood.py:105-107); a rejected word is
+        // reported
+        auto draw_site = [&](auto C, int32_t q, int32_t x, HotDraws &D, int32_t (&cn)[4]) {
             constexpr int c = decltype(C)::value;
             const int lq = q - FR0;
             const int32_t gq = wrapN(q, N), gx = wrapN(x, N);
-            D = blk_draws(P, N, gq, gx, xb, &bb[(lq * 2) * 12 + 6 * c], &bb[(lq * 2 + 1) * 12 + 6 * c], s_small, h4[c],
-                          b4[c]);
+            D = blk_draws(P, N, gq, gx, xb, &s_base[(lq * 2) * 12 + 6 * c], &s_base[(lq * 2 + 1) * 12 + 6 * c], s_small,
+                          has4[c], buf4[c]);
             bool rej = false;
 #pragma unroll
             for (int jj = 0; jj < 4; jj++) {
@@ -249,7 +235,7 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
                 const uint32_t rank = (uint32_t)((gq * N + gx) >> 1);
 #pragma unroll
                 for (int jj = 0; jj < 4; jj++)
-                    if ((uint32_t)((uint64_t)D.w[jj] * kc) < thr) report(A.S, sid, (uint32_t)(1 + 5 * c + 1 + jj), rank);
+                    if ((uint32_t)((uint64_t)D.w[jj] * kc) < thr) report(A.S, sweep_id, (uint32_t)(1 + 5 * c + 1 + jj), rank);
             }
         };
         auto update = [&](auto C, int32_t q, int32_t x, const HotDraws &D, const int32_t (&cn)[4]) {
@@ -330,49 +316,23 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
         };
         const std::integral_constant<int, 0> C0{};
         const std::integral_constant<int, 1> C1{};
-        // the next sweep's row bases (one sweep's stream length further on), into the other buffer
-        auto advance = [&]() {
-            for (int idx = threadIdx.x; idx < (F - 2) * nset * 12; idx += NT) {
-                const int i = 1 + idx / (nset * 12), rem = idx % (nset * 12), o = (i * 2 + rem / 12) * 12 + rem % 12;
-                sb_next[o] = apply(B.step, sb[o]);
-            }
-        };
         // (8-wave workgroups only: the 16-wave form must stay within 128 VGPRs)
         if (SV_BLK_DRAW1 && NWT == 8 && nrows[0] * spr[0] <= NT && nrows[1] * spr[1] <= NT) {
-            // one round of lanes per colour (and so for every later sweep of the launch): the colour-1 draws
-            // (independent of the state) are made in the colour-0 pass, beside its site-updates, with the next sweep's
-            // row bases; the next sweep's colour-0 draws in the colour-1 pass (SV_BLK_DRAW2); each held in registers
-            // across the barrier
+            // one round of lanes per colour: the colour-1 draws (independent of the state) are made in the colour-0
+            // pass, beside its site-update, and held in registers across the barrier
             int32_t q1, x1;
             const bool a1 = site_of(1, threadIdx.x, q1, x1);
             HotDraws D1;
             int32_t cn1[4];
-            if (a1) draw_site(C1, q1, x1, D1, cn1, sb, has4, buf4, sweep_id);
+            if (a1) draw_site(C1, q1, x1, D1, cn1);
             int32_t q0, x0;
             if (site_of(0, threadIdx.x, q0, x0)) {
-                if (!have_p) draw_site(C0, q0, x0, Dp, cnp, sb, has4, buf4, sweep_id);
-                update(C0, q0, x0, Dp, cnp);
+                HotDraws D0;
+                int32_t cn0[4];
+                draw_site(C0, q0, x0, D0, cn0);
+                update(C0, q0, x0, D0, cn0);
             }
-            if (j + 1 < K) advance();
             __syncthreads();
-            have_p = false;
-            if (SV_BLK_DRAW2 && j + 1 < K) {
-                // sweep j + 1's colour-0 site of this lane: its region is 2 rows / columns smaller above and left and 3
-                // below and right
-                uint32_t hn[2][4], bn[2][4];
-#pragma unroll
-                for (int c = 0; c < 2; c++)
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        hn[c][q] = (uint32_t)__builtin_amdgcn_readfirstlane(s_desc[2 * (8 * (j + 1) + 4 * c + q)]);
-                        bn[c][q] = (uint32_t)__builtin_amdgcn_readfirstlane(s_desc[2 * (8 * (j + 1) + 4 * c + q) + 1]);
-                    }
-                int32_t qn, xn;
-                if (site_at(0, threadIdx.x, ra + 2 - 1, rb - 3 + 1, ca + 2 - 1, cb - 3 + 1, qn, xn)) {
-                    draw_site(C0, qn, xn, Dp, cnp, sb_next, hn, bn, sweep_id + 1);
-                    have_p = true;
-                }
-            }
             if (a1) update(C1, q1, x1, D1, cn1);
             __syncthreads();
         } else {
@@ -381,7 +341,7 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
                 if (!site_of(0, base + threadIdx.x, q, x)) continue;
                 HotDraws D;
                 int32_t cn[4];
-                draw_site(C0, q, x, D, cn, sb, has4, buf4, sweep_id);
+                draw_site(C0, q, x, D, cn);
                 update(C0, q, x, D, cn);
             }
             __syncthreads();
@@ -390,10 +350,9 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
                 if (!site_of(1, base + threadIdx.x, q, x)) continue;
                 HotDraws D;
                 int32_t cn[4];
-                draw_site(C1, q, x, D, cn, sb, has4, buf4, sweep_id);
+                draw_site(C1, q, x, D, cn);
                 update(C1, q, x, D, cn);
             }
-            if (j + 1 < K) advance();
             __syncthreads();
         }
 
@@ -424,6 +383,14 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
             }
         }
         BLK_T(3 + j);
+        // the next sweep's row bases: one sweep's stream length further on
+        if (j + 1 < K) {
+            for (int idx = threadIdx.x; idx < (F - 2) * nset * 12; idx += NT) {
+                const int i = 1 + idx / (nset * 12), rem = idx % (nset * 12);
+                u128 &b = s_base[(i * 2 + rem / 12) * 12 + rem % 12];
+                b = apply(B.step, b);
+            }
+        }
     }
     __syncthreads();
     if (*s_bad && threadIdx.x == 0) report(A.S, A.sweep, OVERFLOW_BLOCK, 0);
