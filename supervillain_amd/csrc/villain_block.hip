@@ -33,9 +33,6 @@ __device__ uint64_t g_blktime[4096 * BLT];
 #ifndef SV_BLK_DRAW1
 #define SV_BLK_DRAW1 1  // the colour-1 draws made in the colour-0 pass (one round of lanes per colour)
 #endif
-#ifndef SV_BLK_SPLIT
-#define SV_BLK_SPLIT 1  // frame rows in LDS as even columns, then odd ones (no stride-2 bank conflicts)
-#endif
 #ifndef SV_BLK_FLATJUMP
 #define SV_BLK_FLATJUMP 1
 #endif
@@ -86,10 +83,6 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
     const int32_t r0 = by * bs, c0 = bx * bs;
     const int F = block_frame(bs, K);
     const int32_t FR0 = r0 - 2 * E - 2, FC0 = c0 - 2 * E - 2;  // frame origin (lattice coordinates, may be < 0)
-    // LDS position of frame site (i, k): each frame row holds its even columns, then its odd ones (SV_BLK_SPLIT), so
-    // that a colour pass's lanes -- every other column of a row -- read consecutive words
-    const int FHALF = (F + 1) >> 1;
-    auto at = [&](int i, int k) { return SV_BLK_SPLIT ? i * F + (k & 1) * FHALF + (k >> 1) : i * F + k; };
 
     SmallTab &s_small = *reinterpret_cast<SmallTab *>(blk_lds);
     u128 *s_base = reinterpret_cast<u128 *>(blk_lds + sizeof(SmallTab));  // [F][set][colour][6]
@@ -147,14 +140,13 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
         for (int u = 0; u < FU; u++) {
             const int idx = i0 + u * NT;
             if (idx < F * F) {
-                const int li = at(idx / F, idx % F);
                 // the +0.0 every site receives once per sweep (neighborhood.py:128), applied once: an accepted change
                 // is added to the normalised value, which stays normalised (villain_hot.hip's commit)
-                s_phi[li] = fp[u] + 0.0;
+                s_phi[idx] = fp[u] + 0.0;
                 // the int32 image holds n exactly with room for K sweeps of changes (|W| interval_n <= 2^13)
                 bad |= (uint32_t)((uint64_t)((fa[u] >> 30) + 1) > 1) | (uint32_t)((uint64_t)((fc[u] >> 30) + 1) > 1);
-                s_n0[li] = (int32_t)fa[u];
-                s_n1[li] = (int32_t)fc[u];
+                s_n0[idx] = (int32_t)fa[u];
+                s_n1[idx] = (int32_t)fc[u];
             }
         }
     };
@@ -248,19 +240,18 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
         };
         auto update = [&](auto C, int32_t q, int32_t x, const HotDraws &D, const int32_t (&cn)[4]) {
             constexpr int c = decltype(C)::value;
-            const int lq = q - FR0, lx = x - FC0;
-            const int s0 = at(lq, lx), sl = at(lq, lx - 1), sr = at(lq, lx + 1);  // (sites above / below: s0 -+ F)
+            const int s0 = (q - FR0) * F + (x - FC0);
             const bool own = q >= r0 && q < r0 + bs && x >= c0 && x < c0 + bs;
             const double mdp = 0.0 - D.dphi;  // d(change_phi) on a forward link, neighborhood.py:110
             if constexpr (c == 0) {
                 const double ph = s_phi[s0];
-                const int32_t n_f0 = s_n0[s0], n_b0 = s_n0[s0 - F], n_f1 = s_n1[s0], n_b1 = s_n1[sl];
+                const int32_t n_f0 = s_n0[s0], n_b0 = s_n0[s0 - F], n_f1 = s_n1[s0], n_b1 = s_n1[s0 - 1];
                 // r on the four links f0=(0,q,x), b0=(0,q-1,x), f1=(1,q,x), b1=(1,q,x-1) (neighborhood.py:91)
                 double r[4];
                 r[0] = (s_phi[s0 + F] - ph) - TWO_PI * (double)n_f0;
                 r[1] = (ph - s_phi[s0 - F]) - TWO_PI * (double)n_b0;
-                r[2] = (s_phi[sr] - ph) - TWO_PI * (double)n_f1;
-                r[3] = (ph - s_phi[sl]) - TWO_PI * (double)n_b1;
+                r[2] = (s_phi[s0 + 1] - ph) - TWO_PI * (double)n_f1;
+                r[3] = (ph - s_phi[s0 - 1]) - TWO_PI * (double)n_b1;
                 double tc[4], cr[4];
 #pragma unroll
                 for (int kk = 0; kk < 4; kk++) tc[kk] = TWO_PI * (double)cn[kk];
@@ -284,7 +275,7 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
                     s_n0[s0] = n_f0 + cn[0];
                     s_n0[s0 - F] = n_b0 + cn[1];
                     s_n1[s0] = n_f1 + cn[2];
-                    s_n1[sl] = n_b1 + cn[3];
+                    s_n1[s0 - 1] = n_b1 + cn[3];
                     r[0] = (r[0] + mdp) - tc[0];
                     r[1] = (r[1] + D.dphi) - tc[1];
                     r[2] = (r[2] + mdp) - tc[2];
@@ -293,13 +284,13 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
                 s_r0[s0] = r[0];
                 s_r0[s0 - F] = r[1];
                 s_r1[s0] = r[2];
-                s_r1[sl] = r[3];
+                s_r1[s0 - 1] = r[3];
             } else {
                 double ri[4], cr[4];
                 ri[0] = s_r0[s0];
                 ri[1] = s_r0[s0 - F];
                 ri[2] = s_r1[s0];
-                ri[3] = s_r1[sl];
+                ri[3] = s_r1[s0 - 1];
                 cr[0] = mdp - TWO_PI * (double)cn[0];
                 cr[1] = D.dphi - TWO_PI * (double)cn[1];
                 cr[2] = mdp - TWO_PI * (double)cn[2];
@@ -319,7 +310,7 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
                     s_n0[s0] += cn[0];
                     s_n0[s0 - F] += cn[1];
                     s_n1[s0] += cn[2];
-                    s_n1[sl] += cn[3];
+                    s_n1[s0 - 1] += cn[3];
                 }
             }
         };
@@ -384,7 +375,7 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
             int64_t *n_out = B.n[j + 1];
             for (int idx = threadIdx.x; idx < bs * bs; idx += NT) {
                 const int i = idx / bs, k = idx - i * bs;
-                const int s0 = at(r0 + i - FR0, c0 + k - FC0);
+                const int s0 = (r0 + i - FR0) * F + (c0 + k - FC0);
                 const int64_t g = (int64_t)(r0 + i) * N + (c0 + k);
                 phi_out[g] = s_phi[s0];
                 n_out[g] = (int64_t)s_n0[s0];
