@@ -73,6 +73,10 @@ int sv_ctx_band_counts(sv_ctx *ctx, int64_t *sweeps, int64_t *launches);
 /* Diagnostic: the same for the temporal-blocking launches (villain_sweep_block: K sweeps per launch, each workgroup
  * on its own block and deep-halo frame in LDS). */
 int sv_ctx_block_counts(sv_ctx *ctx, int64_t *sweeps, int64_t *launches);
+/* Diagnostic: single-lattice sweeps replayed since the last call (then reset) on the split replay
+ * (villain_sweep_hot_split): the re-run of a sweep that met NumPy Lemire rejections -- at most one per choice block --
+ * drawing each row from the block segment it lies in (the reference draws again, neighborhood.py:105-107). */
+int sv_ctx_split_counts(sv_ctx *ctx, int64_t *sweeps);
 /* Which multi-sweep launches small periodic lattices may use: 0 temporal blocks or else bands (default), 1 blocks
  * only, 2 bands only, 3 one sweep per launch; K: sweeps per temporal-blocking launch (0: the default; an even K runs
  * as K - 1, and K shrinks until the launch's frame fits).  Returns -1 for another mode or K outside 0..15. */

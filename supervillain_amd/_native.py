@@ -45,6 +45,7 @@ def lib():
         L.sv_ctx_sweep_counts.argtypes = [vp, P(i64), P(i64), P(i64)]
         L.sv_ctx_band_counts.argtypes = [vp, P(i64), P(i64)]
         L.sv_ctx_block_counts.argtypes = [vp, P(i64), P(i64)]
+        L.sv_ctx_split_counts.argtypes = [vp, P(i64)]
         L.sv_ctx_set_multisweep.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
         L.sv_ctx_set_table_cap.argtypes = [vp, ctypes.c_int32]
         L.sv_ctx_table_purges.argtypes = [vp, P(i64)]
@@ -116,7 +117,7 @@ def lib():
 
 
 EXPORTED = ('sv_ctx_create', 'sv_ctx_destroy', 'sv_last_error', 'sv_device_count', 'sv_build_info',
-            'sv_ctx_set_timing', 'sv_ctx_kernel_time', 'sv_ctx_sweep_counts', 'sv_ctx_band_counts', 'sv_ctx_block_counts', 'sv_ctx_set_multisweep', 'sv_ctx_set_table_cap', 'sv_ctx_table_purges', 'sv_hbm_copy', 'sv_rng_gather', 'sv_rng_scatter',
+            'sv_ctx_set_timing', 'sv_ctx_kernel_time', 'sv_ctx_sweep_counts', 'sv_ctx_band_counts', 'sv_ctx_block_counts', 'sv_ctx_split_counts', 'sv_ctx_set_multisweep', 'sv_ctx_set_table_cap', 'sv_ctx_table_purges', 'sv_hbm_copy', 'sv_rng_gather', 'sv_rng_scatter',
             'sv_villain_neighborhood', 'sv_villain_create', 'sv_villain_destroy', 'sv_villain_upload',
             'sv_villain_download', 'sv_villain_run', 'sv_villain_observables', 'sv_villain_emit', 'sv_villain_emit_wait', 'sv_villain_run_philox',
             'sv_worldline_emit', 'sv_worldline_emit_wait', 'sv_host_register', 'sv_host_unregister',
@@ -194,6 +195,12 @@ class Context:
         c = [ctypes.c_int64() for _ in range(3)]
         self.check(lib().sv_ctx_sweep_counts(self.handle, *[ctypes.byref(x) for x in c]), 'sv_ctx_sweep_counts')
         return dict(zip(('hot', 'fused', 'generic'), (x.value for x in c)))
+
+    def split_counts(self):
+        """Sweeps replayed on the split replay kernel since the last call (sv_ctx_split_counts)."""
+        c = ctypes.c_int64()
+        self.check(lib().sv_ctx_split_counts(self.handle, ctypes.byref(c)), 'sv_ctx_split_counts')
+        return c.value
 
     def band_counts(self):
         """Multi-sweep band launches since the last call: {'sweeps', 'launches'} (sv_ctx_band_counts)."""

@@ -329,6 +329,13 @@ int sv_ctx_sweep_counts(sv_ctx *ctx, int64_t *hot, int64_t *fused, int64_t *gene
     return 0;
 }
 
+int sv_ctx_split_counts(sv_ctx *ctx, int64_t *sweeps) {
+    if (!ctx) return -1;
+    if (sweeps) *sweeps = ctx->sweeps_split;
+    ctx->sweeps_split = 0;
+    return 0;
+}
+
 int sv_ctx_set_table_cap(sv_ctx *ctx, int32_t cap) {
     if (!ctx || cap < 0) return -1;
     ctx->table_cap = (size_t)cap;
@@ -542,10 +549,11 @@ int sv_ctx_create(int device, sv_ctx **out) {
         ctx->device = device;
         SV_HIP(hipSetDevice(device));
         SV_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-        // abort flag and report count side by side: a batch tail reads both with one copy
-        SV_HIP(hipMalloc(&ctx->d_abort, 2 * sizeof(int32_t)));
+        // abort flag, report count and the reports in one allocation: a batch tail reads the flag, the count and the
+        // first TAIL_REPORTS reports with one copy
+        SV_HIP(hipMalloc(&ctx->d_abort, 16 + sv::MAX_REPORTS * sizeof(sv::Report)));
         ctx->d_nreport = reinterpret_cast<uint32_t *>(ctx->d_abort + 1);
-        SV_HIP(hipMalloc(&ctx->d_reports, sv::MAX_REPORTS * sizeof(sv::Report)));
+        ctx->d_reports = reinterpret_cast<sv::Report *>(reinterpret_cast<char *>(ctx->d_abort) + 16);
         SV_HIP(hipMemset(ctx->d_abort, 0, sizeof(int32_t)));
         SV_HIP(hipMemset(ctx->d_nreport, 0, sizeof(uint32_t)));
         SV_HIP(hipHostMalloc((void **)&ctx->h_flag, 2 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent));
@@ -586,7 +594,6 @@ int sv_ctx_destroy(sv_ctx *ctx) {
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
     if (ctx->h_tail) (void)hipHostFree(ctx->h_tail);
     if (ctx->h_stage_abort) (void)hipHostFree(ctx->h_stage_abort);
-    (void)hipFree(ctx->d_reports);
     (void)hipFree(ctx->d_blocks);
     (void)hipFree(ctx->d_skips);
     (void)hipFree(ctx->d_stats);

@@ -70,6 +70,8 @@ struct Report {
     uint32_t sweep, block, pos, pad;
 };
 static constexpr int MAX_REPORTS = 1024;
+// reports copied with a batch's tail (sv_ctx: d_abort, d_nreport and d_reports are one allocation, 16 B apart)
+static constexpr int TAIL_REPORTS = 15;
 
 // Device-side per-call scratch: abort flag, reports, stats accumulators.
 struct DevScratch {
@@ -144,6 +146,7 @@ struct sv_ctx {
     // Villain NeighborhoodUpdate sweeps by kernel (sv_ctx_sweep_counts): villain_sweep_hot (+ _fr), the general
     // fused kernel (villain_sweep_fused: int32 n image, skip lists), the per-colour int64 path (villain_pass_generic)
     int64_t sweeps_hot = 0, sweeps_fused = 0, sweeps_generic = 0;
+    int64_t sweeps_split = 0;  // replays of rejected sweeps on villain_sweep_hot_split (sv_ctx_split_counts)
     // of the hot sweeps: those run by multi-sweep band launches, and the launches (sv_ctx_band_counts)
     int64_t sweeps_band = 0, launches_band = 0;
     // the same for temporal-blocking launches (sv_ctx_block_counts), and the multi-sweep mode (sv_ctx_set_multisweep:
@@ -212,6 +215,7 @@ struct sv_villain {
     double *h_obs = nullptr;       // and their pinned host image
     int32_t *d_strips = nullptr;   // villain_sweep_hot's strip table (strip_schedule), n_strips entries of 3
     int32_t n_strips = 0;
+    std::vector<int32_t> h_strips;  // (its host copy: the split replay orders its straddling strips first)
     std::string strips_key;        // the schedule the table holds
     // multi-sweep band launches (villain_sweep_hot_band): the launch's scratch buffers (sweep outputs 1..K-1) and
     // the per-XCD ticket / barrier counters followed by the batch's gate word

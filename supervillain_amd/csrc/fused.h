@@ -29,9 +29,16 @@ __device__ __forceinline__ void report(const DevScratch &S, uint32_t sweep, uint
 
 // a launch of sweep `sweep` has nothing to do: a report came from an earlier sweep (with a gate, DevScratch), or
 // from any launch since the batch's reset (without)
+// The flags are read through the scalar cache (a constant-address-space load: one s_load per wave, cached per CU), not
+// by a vector load that bypasses the caches: a launch queued behind an abort then drains at the speed its workgroups
+// are dispatched.  The scalar cache is invalidated at every kernel's start, so a launch sees every earlier launch's
+// flag; within the reporting launch a stale 0 only means that a workgroup runs on (its results are discarded).
+__device__ __forceinline__ int32_t scalar_read(const int32_t *p) {
+    return *(const __attribute__((address_space(4))) int32_t *)(p);
+}
 __device__ __forceinline__ bool sweep_cancelled(const DevScratch &S, uint32_t sweep) {
-    if (S.gate) return *(volatile const int32_t *)S.gate < (int32_t)sweep;
-    return *(volatile const int32_t *)S.abort != 0;
+    if (S.gate) return scalar_read(S.gate) < (int32_t)sweep;
+    return scalar_read(S.abort) != 0;
 }
 
 // stream position of bounded draw d, accounting for known rejected positions (sorted)
@@ -386,6 +393,37 @@ __device__ __forceinline__ uint32_t fast_pack(const uint32_t *hasw, int32_t lane
     return pk;
 }
 
+// fast_pack for per-block buffered-half flags (h4: f0, b0, f1, b1), the replay of a sweep that met a NumPy Lemire
+// rejection (villain_sweep_hot_split): a rejected word shifts the rest of its block by one half-word, so a direction's
+// fwd and bwd blocks can sit at opposite pairing parities.  Then ("mismatched", bit mu of `mism`) every lane computes
+// the one word in which it holds the LOW half (the fwd word when its fwd draw is a low half, else the bwd word) and
+// passes that word's high half to lane + 1: still one word per lane and direction.  Matched directions pair as in
+// fast_pack (bits 28 + mu: the block the lane computes, 0 fwd / 1 bwd).  Lane 63 (never an active site: strips have
+// <= 63 colour sites per row) computes the word in which lane 0 holds the high half.
+__device__ __forceinline__ uint32_t fast_pack_g(const uint32_t *h4, int32_t lane, uint32_t rowlin, uint32_t xs,
+                                                uint32_t gx, uint32_t xb, uint32_t &mism) {
+    const uint32_t lin = rowlin + gx, rank = lin >> 1;
+    const uint32_t PR = (rowlin + xb) >> 1;
+    uint32_t pk = ((gx - xb) & (SMALL_LDS - 1)) | (((rank - PR) & (SMALL_LDS - 1)) << 7);
+    const uint32_t R0 = (rowlin + xs) >> 1;  // rank of lane 0
+    mism = 0;
+#pragma unroll
+    for (int mu = 0; mu < 2; mu++) {
+        const uint32_t hf = h4[2 * mu], hb = h4[2 * mu + 1];
+        if (hf != hb) mism |= 1u << mu;
+        uint32_t sel = (rank - hf) & 1u, r = rank;
+        if (lane == 63) {
+            if ((R0 - hf) & 1u) sel = 0u, r = R0;       // lane 0's fwd draw is a high half
+            else if ((R0 - hb) & 1u) sel = 1u, r = R0;  // lane 0's bwd draw is a high half
+        }
+        const uint32_t h = sel ? hb : hf;
+        const uint32_t PW = (PR - h) >> 1;  // word index of the row base (PR >= 1 on interior strips)
+        pk |= ((((r - h) >> 1) - PW) & (SMALL_LDS - 1)) << (14 + 7 * mu);
+        pk |= sel << (28 + mu);
+    }
+    return pk;
+}
+
 // The row bases are the same for every lane of a wave (one row per wave): held in SGPRs they feed the
 // 128-bit multiplies as scalar operands instead of occupying VGPRs.
 #ifndef SV_K3
@@ -605,7 +643,9 @@ struct HotDraws {
 // kernel, with at most HOT_MAXSK positions per block read from LDS -- so its word is a half-word further on, still a
 // small offset ahead of the row base (which sits at the unshifted position); spos returns the positions (reports).
 static constexpr int HOT_MAXSK = 4;
-template <bool SKIP = false>
+// PB (the split replay, villain_sweep_hot_split): every choice block has its own buffered-half flag (a fwd/bwd pair
+// may differ), so each block's word offset is computed from its own flag
+template <bool SKIP = false, bool PB = false>
 __device__ __forceinline__ HotDraws hot_draws_edge(const FArgs &A, int64_t gq, int32_t gx, int32_t xb, int32_t xw,
                                                    const u128 *bA, const u128 *bB, const SmallTab &sm,
                                                    const uint32_t *has4, const uint32_t *buf,
@@ -621,7 +661,19 @@ __device__ __forceinline__ HotDraws hot_draws_edge(const FArgs &A, int64_t gq, i
     HotDraws D;
     D.u = u53(xsl_rr(hot_apply(sm, (uint32_t)(gx - xr), bs[0])));
     D.dphi = A.P.lo_phi + A.P.range_phi * u53(xsl_rr(hot_apply(sm, (uint32_t)(rank - rb), bs[1])));
-    if constexpr (!SKIP) {
+    if constexpr (PB) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t qq = rank - (int64_t)has4[j];
+            const int64_t w0 = (rb - (int64_t)has4[j]) < 0 ? 0 : ((rb - (int64_t)has4[j]) >> 1);
+            const uint32_t off = (uint32_t)((qq < 0 ? 0 : (qq >> 1)) - w0);
+            const uint64_t X = xsl_rr(hot_apply(sm, off, bs[2 + j]));
+            uint32_t word = (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
+            if (qq < 0) word = buf[j];
+            D.w[j] = word;
+        }
+        return D;
+    } else if constexpr (!SKIP) {
         // equal flags within each fwd/bwd pair: one word offset per direction
 #pragma unroll
         for (int mu = 0; mu < 2; mu++) {

@@ -121,6 +121,47 @@ struct BlockArgs {
     double *phi[BAND_MAXK + 1];
     int64_t *n[BAND_MAXK + 1];
 };
+// The replay of a sweep that met NumPy Lemire rejections, at most one per choice block (villain_sweep_hot_split,
+// DESIGN.md 5.0): block j of colour c (blocks[2 + 5 c + j]) draws its sites of rank >= s[4 c + j] from the stream one
+// half-word further on -- the rejected word is skipped, neighborhood.py:105-107 drawing again -- which is the block
+// descriptor blocksB[2 + 5 c + j] (s = UINT32_MAX: no switch; blocksB is the sweep's 11 descriptors with those
+// replaced).  Each row draws from the descriptors of its side of every switch: a strip whose rows all lie on one side
+// with one descriptor per block, a strip whose rows contain a switch's row (or wrap around the torus) per row, and the
+// few strips whose columns straddle a switch's site in its row on the skip-list body (~2.5x slower: they are dispatched
+// first on their XCDs, swap[]).
+static constexpr int SPLIT_SWAPS = 32;
+struct SplitArgs {
+    uint32_t s[8];
+    const Block *blocksB;
+    int32_t nswap;
+    int32_t swap[SPLIT_SWAPS][2];  // logical block pairs exchanged (split_order)
+};
+// whether strip [t0, t1) x [x0, x1) of an Nt x Nx periodic lattice draws on both sides of the switch at site rank s
+// within one row (sites of rank >= s: linear index >= 2 s, one site of each colour per pair of sites): the switch's
+// row lies among the rows it draws in (halo and base rows included) and its site among the columns (lane 63's word and
+// the lane pairs included), or the strip's columns wrap around the torus; the switch's row qs, and whether the strip's
+// columns lie after its site
+__host__ __device__ inline bool split_straddles(uint32_t s, int32_t Nt, int32_t Nx, int32_t t0, int32_t t1, int32_t x0,
+                                                int32_t x1, int32_t *qs_out, bool *after) {
+    const uint32_t lin = 2u * s;
+    const int32_t qs = (int32_t)(lin / (uint32_t)Nx), xs = (int32_t)(lin % (uint32_t)Nx);
+    const int32_t ra = t0 - 3, rb = t1 + 3, ca = x0 - 4, cb = x0 + 127;
+    *qs_out = qs;
+    *after = ca >= xs;
+    int32_t d = (qs - ra) % Nt;
+    if (d < 0) d += Nt;
+    if (!(rb - ra + 1 >= Nt || d <= rb - ra)) return false;
+    const bool interior = x0 >= 4 && x1 + 2 < Nx;
+    return !interior || (ca < xs && xs <= cb);
+}
+
+// whether strip [t0, t1)'s rows (halo and base rows included) contain row qs or wrap around the torus: its rows then lie
+// on both sides of a switch in row qs, and the descriptors are chosen per row
+__host__ __device__ inline bool split_rows(int32_t qs, int32_t Nt, int32_t t0, int32_t t1) {
+    const int32_t ra = t0 - 3, rb = t1 + 3;
+    return ra < 0 || rb >= Nt || (ra <= qs && qs <= rb);
+}
+
 // the frame's side (rows = columns) and the launch's dynamic LDS bytes
 __host__ __device__ inline int32_t block_frame(int32_t bs, int32_t K) { return bs + 5 * (K - 1) + 5; }
 __host__ __device__ inline size_t block_lds_bytes(int32_t F) {
@@ -178,6 +219,15 @@ bool hot_ok(const VParams &P, const Block *blocks);
 // the skip form (villain_sweep_hot_skip, 4 waves): sweeps with <= 4 known rejected positions per choice block
 bool hot_skip_ok(const VParams &P, const Block *blocks);
 void launch_hot_skip(const FArgs &A, int grid, hipStream_t stream);
+// the split replay (villain_sweep_hot_split, periodic single lattices, 4 waves): whether it covers the sweep whose
+// descriptors start at `blocks` (<= 1 known rejected position per choice block), filling its SplitArgs; its launch
+// descriptors start at `blocks` (<= 1 known rejected position per choice block), filling S.s and the sweep's 11
+// descriptors after the switches (Bset)
+bool split_plan(const VParams &P, const Block *blocks, const uint32_t *skips, u128 inc, SplitArgs &S, Block *Bset);
+void launch_hot_split(const FArgs &A, const SplitArgs &S, int grid, hipStream_t stream);
+// fill S.nswap / S.swap: the skip-list strips (strip table `tab` of `grid` entries, or uniform strips of TH rows) moved
+// to the start of their XCD's range
+void split_order(SplitArgs &S, int32_t N, int nsx, int grid, const int32_t *tab, int TH);
 // villain_sweep_hot's default descending strip table for H rows and nsx column strips ({ix, t0, t1} per strip)
 std::vector<int32_t> band_strips(int32_t H, int nsx);
 // two waves of 8-wave strips for a region one round covers: `first` strips of `tall` rows dispatched first, then strips

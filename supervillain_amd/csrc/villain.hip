@@ -722,32 +722,39 @@ AbortInfo read_abort(sv_ctx *ctx) {
     return a;
 }
 
-// The batch tail in one synchronization: abort flag, report count and the batch's statistics land in a pinned
-// host block (DMA copies); the stats are kept only when no rejection aborted the batch.
-AbortInfo read_abort_stats(sv_ctx *ctx, int count, sv_stats *stats) {
-    const size_t bytes = 64 + (size_t)count * sizeof(sv_stats);
+// The batch tail in one synchronization: abort flag, report count, the first TAIL_REPORTS reports and the batch's
+// statistics land in a pinned host block (DMA copies); the stats are copied to `stats` only when no rejection aborted
+// the batch -- after an abort, `landed` points at them (the sweeps before the failing one are kept from there), and
+// only a batch with more than TAIL_REPORTS reports needs a second copy
+static constexpr size_t TAIL_HEAD = 16 + TAIL_REPORTS * sizeof(Report);  // 256 B
+AbortInfo read_abort_stats(sv_ctx *ctx, int count, sv_stats *stats, const sv_stats **landed = nullptr) {
+    const size_t bytes = TAIL_HEAD + (size_t)count * sizeof(sv_stats);
     if (bytes > ctx->tail_cap) {
         SV_HIP(hipStreamSynchronize(ctx->stream));
         if (ctx->h_tail) SV_HIP(hipHostFree(ctx->h_tail));
-        ctx->tail_cap = std::max<size_t>(bytes, 64 + 64 * sizeof(sv_stats));
+        ctx->tail_cap = std::max<size_t>(bytes, TAIL_HEAD + 64 * sizeof(sv_stats));
         SV_HIP(hipHostMalloc((void **)&ctx->h_tail, ctx->tail_cap, hipHostMallocDefault));
     }
     int32_t *h_ab = (int32_t *)ctx->h_tail;
     uint32_t *h_nrep = (uint32_t *)(ctx->h_tail + 4);
-    sv_stats *h_st = (sv_stats *)(ctx->h_tail + 64);
-    SV_HIP(hipMemcpyAsync(h_ab, ctx->d_abort, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));  // + d_nreport
+    const Report *h_rep = (const Report *)(ctx->h_tail + 16);
+    sv_stats *h_st = (sv_stats *)(ctx->h_tail + TAIL_HEAD);
+    SV_HIP(hipMemcpyAsync(ctx->h_tail, ctx->d_abort, TAIL_HEAD, hipMemcpyDeviceToHost, ctx->stream));  // + d_nreport, reports
     SV_HIP(hipMemcpyAsync(h_st, ctx->d_stats, count * sizeof(sv_stats), hipMemcpyDeviceToHost, ctx->stream));
     SV_HIP(hipStreamSynchronize(ctx->stream));
     AbortInfo a;
     a.abort = *h_ab;
     uint32_t nrep = *h_nrep;
+    if (landed) *landed = h_st;
     if (!a.abort) {
         std::memcpy(stats, h_st, count * sizeof(sv_stats));
         return a;
     }
     if (nrep > (uint32_t)MAX_REPORTS) nrep = MAX_REPORTS;
     a.reports.resize(nrep);
-    if (nrep) {
+    if (nrep <= (uint32_t)TAIL_REPORTS) {
+        std::memcpy(a.reports.data(), h_rep, nrep * sizeof(Report));
+    } else {
         SV_HIP(hipMemcpyAsync(a.reports.data(), ctx->d_reports, nrep * sizeof(Report), hipMemcpyDeviceToHost,
                               ctx->stream));
         SV_HIP(hipStreamSynchronize(ctx->stream));
@@ -1059,6 +1066,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                                              : (dflt ? band_strips(N, nsx) : strip_schedule(N, nsx, spec));
             if (st->d_strips) SV_HIP(hipFree(st->d_strips));
             st->d_strips = nullptr;
+            st->h_strips = tab;
             st->n_strips = (int32_t)(tab.size() / 3);
             if (!tab.empty()) {
                 SV_HIP(hipMalloc(&st->d_strips, tab.size() * sizeof(int32_t)));
@@ -1197,6 +1205,26 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         sw_next = -1;
         auto tp1 = std::chrono::steady_clock::now();
         if (dbg) fprintf(stderr, "[sv] plan %d sweeps: %.1f us\n", count, std::chrono::duration<double, std::micro>(tp1 - tp0).count());
+        // Sweeps with known rejections, at most one per choice block (the replay of a rejected sweep): the split replay
+        // (villain_sweep_hot_split), ~one hot sweep; the descriptors after each switch go up with the batch's plan.  The
+        // general int32 kernel takes the rest (~1.9 hot sweeps).  (r4 measured a skip-list form of the hot kernel on
+        // every strip: slower than the general kernel)
+        std::vector<std::pair<int, SplitArgs>> splits;
+        std::vector<size_t> split_off;
+        if (!skips.empty() && use_hot && !hot_off && NWv == 4 && hot_nw == 4 && nb == 11) {
+            for (int k = 0; k < part; k++) {
+                const Block *bk = &blocks[(size_t)k * nb];
+                if (hot_ok(P, bk)) continue;
+                SplitArgs SA;
+                Block Bset[11];
+                if (!split_plan(P, bk, skipvec.data(), inc, SA, Bset)) continue;
+                split_order(SA, N, nsx, st->d_strips ? st->n_strips : grid, st->d_strips ? st->h_strips.data() : nullptr,
+                            TH);
+                splits.push_back({k, SA});
+                split_off.push_back(blocks.size());
+                blocks.insert(blocks.end(), Bset, Bset + 11);
+            }
+        }
         upload_plan(ctx, blocks, skipvec);
         // sweep k of the batch reads buffer cur ^ (k & 1); after m sweeps the state is in cur ^ (m & 1)
         auto set_current = [&](int m) { st->cur ^= m & 1; };
@@ -1205,16 +1233,13 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         hipEvent_t seg = nullptr;
         int seg_k0 = 0;
         const bool per_launch = ctx->timing_mode == 2;
-        // A batch is enqueued whole: no host thread paces the GPU (round 3 enqueued large lattices in chunks of 4
-        // sweeps behind a host-mapped progress word, so that a NumPy Lemire rejection left at most ~8 early-exit
-        // launches queued; measured r4 on one box, driver form: 69.3-70.0 G either way, a window with a rejection
-        // +0.58 ms chunked vs +0.63 ms whole -- the ~5 us early exits of the queued launches -- and a host that is
-        // descheduled while pacing leaves the GPU idle).  SV_CHUNK = k > 0 restores chunks of k.
-        static const int CH_env = [] {
-            const char *e = getenv("SV_CHUNK");
-            return e ? atoi(e) : 0;
-        }();
-        const int CH = CH_env > 0 ? CH_env : count;
+        // Large lattices (>= 2^22 sites: a sweep takes >= 50 us) are enqueued two sweeps at a time behind the host-mapped
+        // progress word (FArgs::progress): a NumPy Lemire rejection then leaves at most ~4 early-exit launches queued
+        // (~5 us each) instead of the rest of the batch.  r5, scripts/perf/reject_window.py 4096 20 150, two runs each
+        // (profiles/r05_chunk_ab.txt): extra per call that meets a rejection 0.270 / 0.274 ms whole, 0.225 / 0.228 ms in
+        // chunks of 2, 0.241 / 0.254 in chunks of 4; clean calls level (4.38-4.40 ms).  Small lattices are enqueued whole
+        // (their sweeps are a few us: the host would pace the GPU).
+        const int CH = V >= (int64_t(1) << 22) ? 2 : count;
         int launched = count;
         *ctx->h_flag = 0;
         __atomic_store_n(ctx->h_prog, 0, __ATOMIC_RELEASE);  // (the previous batch's launches have all finished)
@@ -1240,17 +1265,11 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                 }
             const int step = band_k ? bandK : 1;
             const bool hot_k = band_k || (use_hot && !hot_off && NWv == 4 && hot_ok(P, &blocks[(size_t)k * nb]));
-            // a sweep with known rejections (a replay) or unequal buffered-half pairs: the hot kernel's skip form
-            // SV_HOT_SKIP=1: replays on the hot kernel's skip form.  Off: it runs a replayed L=4096 sweep in ~566 us
-            // (unpaired draws on every strip, skip scans, spills), the general int32 kernel in less -- a 20-sweep window
-            // with a rejection costs +0.48 ms on the general kernel against +0.65 ms on the skip form (r4, 150 calls
-            // each, profiles/r04_replay_ab.txt)
-            static const bool skip_on = [] {
-                const char *e = getenv("SV_HOT_SKIP");
-                return e && atoi(e) == 1;
-            }();
-            const bool skip_k = skip_on && !hot_k && use_hot && !hot_off && NWv == 4 && hot_nw == 4 &&
-                                hot_skip_ok(P, &blocks[(size_t)k * nb]);
+            int split_i = -1;  // this sweep's split replay
+            if (!hot_k && !hot_off)
+                for (size_t i = 0; i < splits.size(); i++)
+                    if (splits[i].first == k) split_i = (int)i;
+            const bool split_k = split_i >= 0;
             if (!hot_k && seg) {
                 ctx->time_end(seg, k - seg_k0, seg_k0);
                 seg = nullptr;
@@ -1344,10 +1363,12 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                 if (st->d_strips) A.strips = st->d_strips;
                 launch_hot(A, st->d_strips ? st->n_strips : grid, ctx->stream);
                 ctx->sweeps_hot++;
-            } else if (skip_k) {
+            } else if (split_k) {
                 if (st->d_strips) A.strips = st->d_strips;
-                launch_hot_skip(A, st->d_strips ? st->n_strips : grid, ctx->stream);
-                ctx->sweeps_hot++;
+                SplitArgs &SA = splits[split_i].second;
+                SA.blocksB = ctx->d_blocks + split_off[split_i];
+                launch_hot_split(A, SA, st->d_strips ? st->n_strips : grid, ctx->stream);
+                ctx->sweeps_split++;
             } else {
                 ctx->sweeps_fused++;
                 if (NWv == 6) villain_sweep_fused<6, false, false, false><<<grid, 6 * 64, 0, ctx->stream>>>(A);
@@ -1399,7 +1420,8 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             sw_next = sw + count;
         }
         auto tp2 = std::chrono::steady_clock::now();
-        AbortInfo a = read_abort_stats(ctx, count, stats + sw);
+        const sv_stats *landed = nullptr;
+        AbortInfo a = read_abort_stats(ctx, count, stats + sw, &landed);
         auto tp3 = std::chrono::steady_clock::now();
         if (dbg)
             fprintf(stderr, "[sv] launch %.1f us, wait %.1f us\n", std::chrono::duration<double, std::micro>(tp2 - tp1).count(),
@@ -1463,9 +1485,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                 std::vector<Block> b2;
                 std::vector<uint32_t> s2;
                 plan_sweeps(ctx, c2, inc, specs, sw, bad, skips, b2, s2);
-                SV_HIP(hipMemcpyAsync(stats + sw, ctx->d_stats, bad * sizeof(sv_stats), hipMemcpyDeviceToHost,
-                                      ctx->stream));
-                SV_HIP(hipStreamSynchronize(ctx->stream));
+                std::memcpy(stats + sw, landed, bad * sizeof(sv_stats));  // (landed with the batch's tail)
                 for (int k = 0; k < bad; k++) {
                     stats[sw + k].proposed = V;
                     stats[sw + k].rejections = rejections_in(skips, sw + k, nb);
@@ -1486,9 +1506,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                 std::vector<Block> b2;
                 std::vector<uint32_t> s2;
                 plan_sweeps(ctx, c2, inc, specs, sw, bad, skips, b2, s2);
-                SV_HIP(hipMemcpyAsync(stats + sw, ctx->d_stats, bad * sizeof(sv_stats), hipMemcpyDeviceToHost,
-                                      ctx->stream));
-                SV_HIP(hipStreamSynchronize(ctx->stream));
+                std::memcpy(stats + sw, landed, bad * sizeof(sv_stats));  // (landed with the batch's tail)
                 for (int k = 0; k < bad; k++) {
                     stats[sw + k].proposed = V;
                     int64_t rj = 0;
@@ -1518,9 +1536,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             std::vector<Block> b2;
             std::vector<uint32_t> s2;
             plan_sweeps(ctx, c2, inc, specs, sw, bad, skips, b2, s2);
-            SV_HIP(hipMemcpyAsync(stats + sw, ctx->d_stats, bad * sizeof(sv_stats), hipMemcpyDeviceToHost,
-                                  ctx->stream));
-            SV_HIP(hipStreamSynchronize(ctx->stream));
+            std::memcpy(stats + sw, landed, bad * sizeof(sv_stats));  // (landed with the batch's tail)
             for (int k = 0; k < bad; k++) {
                 stats[sw + k].proposed = V;
                 int64_t rj = 0;

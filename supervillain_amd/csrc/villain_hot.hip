@@ -106,6 +106,51 @@ __device__ __forceinline__ HotDraws hot_draws_paired_sel(const FArgs &A, int32_t
     return D;
 }
 
+// The split replay's paired draws (fast_pack_g): a matched direction as hot_draws_paired_sel; a mismatched one (bit mu
+// of the wave-uniform `mism`) keeps the low half of the word it computed and passes the high half to lane + 1
+__device__ __forceinline__ HotDraws hot_draws_paired_g(const FArgs &A, int32_t lane, uint32_t pk, uint32_t mism,
+                                                       const u128 *bw, const SmallTab &sm) {
+    HotDraws D;
+    D.u = u53(xsl_rr(hot_apply(sm, pk & (SMALL_LDS - 1), bw[0])));
+    D.dphi = A.P.lo_phi + A.P.range_phi * u53(xsl_rr(hot_apply(sm, (pk >> 7) & (SMALL_LDS - 1), bw[1])));
+#pragma unroll
+    for (int mu = 0; mu < 2; mu++) {
+        const uint32_t sel = (pk >> (28 + mu)) & 1u;
+        const uint64_t X = xsl_rr(hot_apply(sm, (pk >> (14 + 7 * mu)) & (SMALL_LDS - 1), bw[2 + 2 * mu + sel]));
+        const uint32_t mm = (mism >> mu) & 1u;
+        const uint32_t oh = mm ? 0u : sel;  // the half of X this lane draws itself: 1 high, 0 low
+        const uint32_t send = oh ? (uint32_t)X : (uint32_t)(X >> 32);
+        const uint32_t got = pair_exchange(send, mm | sel, lane);  // (mm | sel): from lane - 1, else lane + 1
+        const uint32_t own = oh ? (uint32_t)(X >> 32) : (uint32_t)X;
+        D.w[2 * mu] = sel ? got : own;
+        D.w[2 * mu + 1] = sel ? own : got;
+    }
+    return D;
+}
+
+// The split replay's switches as one workgroup sees them (at most two; villain_sweep_hot_split): switch k changes
+// block blk[k] (4 c + j) at global row qs[k] -- rows after it draw from blocksB, rows before from blocks, and row qs[k]
+// itself by `after` (the strip's columns all lie after the switch's site, or all before: strips whose columns straddle
+// it run the skip-list body)
+struct SplitSw {
+    int32_t qs[2];       // INT32_MAX: no switch
+    uint32_t blk[2];     // 4 c + j
+    uint32_t after;      // bit k
+    __device__ __forceinline__ uint32_t mask(int c, int32_t gq) const {
+        uint32_t m = 0;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const bool on = gq > qs[k] || (gq == qs[k] && ((after >> k) & 1u));
+            m |= (on && (blk[k] >> 2) == (uint32_t)c) ? 1u << (blk[k] & 3u) : 0u;
+        }
+        return m;
+    }
+    // a switch row within [g - 1, g + span]
+    __device__ __forceinline__ bool near(int32_t g, int32_t span) const {
+        return (qs[0] >= g - 1 && qs[0] <= g + span) || (qs[1] >= g - 1 && qs[1] <= g + span);
+    }
+};
+
 // The workgroup's LDS (one allocation shared by the two bodies below)
 struct HotEmpty {};
 // PH (counter-based mode) keeps no small-offset maps, row-advance maps or row bases: its LDS is 6 KB smaller, which
@@ -136,6 +181,7 @@ struct HotLDST {
     // per wave: [8c + ty] block ty's base for the colour-c row at xb; [16 + ..] at xw (edge strips of rows > SMALL_LDS)
     std::conditional_t<PH, HotEmpty, std::conditional_t<OBSL, u128[NWL][16], u128[NWL][32]>> base;
     int32_t bad;
+    int32_t stop;  // POLL: a rejection was reported by some workgroup: leave the (discarded) sweep
     // SKIP: per colour and choice block, its known rejected stream positions (not in the replica-observables layout,
     // which needs every byte for its fourth workgroup per CU)
     std::conditional_t<OBSL, HotEmpty, uint32_t[2][4][HOT_MAXSK]> sk;
@@ -190,10 +236,18 @@ struct HotBand {
     const Block *next_blocks;
 };
 
+// SPLIT (villain_sweep_hot_split): the replay of a sweep that met NumPy Lemire rejections (at most one per choice block,
+// two in all): a row of colour c draws choice block j from blocksB[2 + 5 c + j] (the descriptor after the block's
+// switch) when the row lies after the switch (SplitSw::mask), else from blocks; the flags are per block (a fwd/bwd pair
+// may sit at opposite pairing parities: fast_pack_g, hot_draws_edge<false, true>)
+// ROWM (SPLIT): the strip's rows lie on both sides of a switch (the switch's row is among them, or they wrap around the
+// torus): the mask is re-evaluated per row; otherwise it is the strip's constant.
 template <bool TILE, bool EDGE, bool FR = false, bool OBS = false, bool PH = false, int NWT = 4, bool SKIP = false,
-          bool BAND = false>
+          bool BAND = false, bool SPLIT = false, bool ROWM = false>
 __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, NWT> &Ls, int bl,
-                                         const HotBand *hb = nullptr) {
+                                         const HotBand *hb = nullptr, const Block *blocksB = nullptr,
+                                         const SplitSw *sw = nullptr) {
+    static_assert(!SPLIT || (!TILE && !FR && !PH && !SKIP && !BAND && NWT == 4), "split replays: periodic single lattices");
     static_assert(!(FR && TILE), "full-row replica strips are periodic");
     static_assert(!SKIP || (EDGE && !FR && !PH), "skip lists: the unpaired (edge) draws of single lattices and tiles");
     static_assert(NWT == 4 || (NWT == 8 && !FR && !PH), "8-wave strips: single lattices and tiles");
@@ -287,7 +341,17 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
             if (threadIdx.x < 3) s_adv[threadIdx.x] = FR ? A.advrep[3 * rep + threadIdx.x] : A.adv[threadIdx.x];
         }
     }
+    // POLL (single lattices): the abort flag is polled by wave 0 at the start and once per row step (an agent-scope
+    // load: the reporting workgroup may sit on another XCD, whose L2 the plain loads do not see), and a workgroup leaves
+    // the sweep as soon as it is set -- a sweep that met a rejection is discarded and replayed, so its remaining work
+    // is waste.  The poll is issued just before the next rows' prefetch and read after their commit, so it adds no wait.
+    constexpr bool POLL = !TILE && !FR && !BAND && !PH;
+    int32_t pv = 0;
+    if constexpr (POLL) {
+        if (wave == 0) pv = __hip_atomic_load(A.S.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (threadIdx.x == 0) s_bad = 0;
+    if (POLL && threadIdx.x == 0) Ls.stop = 0;
     if (OBS && threadIdx.x < 4) Ls.obs[threadIdx.x] = 0.0;
     if constexpr (FR && OBS) {  // this lane's running sums (only this lane touches its slots)
         Ls.ol.act[threadIdx.x] = 0.0;
@@ -319,6 +383,21 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
 #pragma unroll
             for (int j = 0; j < 4; j++) buf_c[c][j] = (uint32_t)__builtin_amdgcn_readfirstlane(blocks[2 + 5 * c + j].buf);
         }
+    }
+    // SPLIT: each colour's current row mask (bit j: block j draws from blocksB) and those descriptors' flags
+    uint32_t cur_m[2] = {0u, 0u};
+    auto seg_load = [&](int c, uint32_t m) {
+        cur_m[c] = m;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const Block &Bd = ((m >> j) & 1u) ? blocksB[2 + 5 * c + j] : blocks[2 + 5 * c + j];
+            has4[c][j] = (uint32_t)__builtin_amdgcn_readfirstlane(Bd.has);
+            buf_c[c][j] = (uint32_t)__builtin_amdgcn_readfirstlane(Bd.buf);
+        }
+    };
+    if constexpr (SPLIT) {
+        seg_load(0, sw->mask(0, grow(t0s - 3 + 2 + wave)));
+        seg_load(1, sw->mask(1, grow(t0s - 3 + 1 + wave)));
     }
     if constexpr (SKIP) {  // the skip lists into LDS (the host bounds them by HOT_MAXSK per block)
         if (threadIdx.x < 2 * 4 * HOT_MAXSK) {
@@ -403,6 +482,14 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     const int32_t bx = lane >= 16 ? xw : xb;
     const int bblk = bty == 0 ? 0 : 1 + 5 * bc + bty - 1;
     const uint32_t bhas = (!PH && base_lane && bty >= 2) ? blocks[bblk].has : 0u;
+    // SPLIT: this base lane's descriptor (blocks or blocksB) for a row
+    auto bdsc = [&](int32_t row) -> const Block * {
+        if constexpr (SPLIT) {
+            const uint32_t m = ROWM ? (bc ? sw->mask(1, grow(row)) : sw->mask(0, grow(row))) : (bc ? cur_m[1] : cur_m[0]);
+            if (bty >= 2 && ((m >> (bty - 2)) & 1u)) return &blocksB[bblk];
+        }
+        return &blocks[bblk];
+    };
     const int32_t tfirst = t0 - 3;
     int32_t brow = tfirst + 2 - bc + wave;  // colour 0 row t+2+wave, colour 1 row t+1+wave
     int32_t brow1 = tfirst + 1 + wave;      // the colour-1 row, wave-uniform
@@ -410,7 +497,10 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
         if (!BAND || hb->first) {  // (a band sweep after the first: its predecessor jumped to them)
             u128 bases{0, 0};
             // (flat table loads: not in the replica kernels, whose registers they would push into scratch)
-            if (base_lane)
+            if (SPLIT && base_lane) {
+                const Block *d = bdsc(brow);
+                bases = full_jump_flat(Tb, d, (uint32_t)base_pos(bty, grow(brow), Nx, bx, bty >= 2 ? d->has : 0u));
+            } else if (base_lane)
                 bases = FR ? full_jump(Tb, &blocks[bblk], (uint32_t)base_pos(bty, grow(brow), Nx, bx, bhas))
                            : full_jump_flat(Tb, &blocks[bblk], (uint32_t)base_pos(bty, grow(brow), Nx, bx, bhas));
             __builtin_amdgcn_s_waitcnt(0);
@@ -423,7 +513,20 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
 
     // paired-draw lane constants per colour (interior strips; valid for every row of this wave)
     uint32_t pk0 = 0, pk1 = 0;
-    if constexpr (!edge && !PH) {
+    uint32_t mism0 = 0, mism1 = 0;  // SPLIT: mismatched directions (fast_pack_g)
+    // SPLIT: the paired-draw constants of colour c for its row q (the row's flags)
+    auto pack_g = [&](int c, int32_t q) {
+        const int32_t xs = c == 0 ? (x0 - 1) + ((par0 + q + x0 - 1) & 1) : x0 + ((par0 + q + x0 + 1) & 1);
+        uint32_t mm = 0;
+        const uint32_t pk = fast_pack_g(has4[c], lane, (uint32_t)grow(q) * (uint32_t)Nx, (uint32_t)(X0s + xs),
+                                        (uint32_t)(X0s + xs + 2 * lane), (uint32_t)xb, mm);
+        if (c == 0) pk0 = pk, mism0 = mm;
+        else pk1 = pk, mism1 = mm;
+    };
+    if constexpr (SPLIT && !edge) {
+        pack_g(0, tfirst + 2 + wave);
+        pack_g(1, tfirst + 1 + wave);
+    } else if constexpr (!edge && !PH) {
         {
             const int32_t q = tfirst + 2 + wave;
             const int32_t xs = FR ? ((par0 + q) & 1) : (x0 - 1) + ((par0 + q + x0 - 1) & 1);
@@ -525,6 +628,19 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
             }
             (void)active;
             return;
+        } else if constexpr (SPLIT) {
+            if constexpr (ROWM) {
+                const uint32_t m = sw->mask(c, gq);  // (wave-uniform)
+                if (m != cur_m[c]) {                // the row crossed a switch: its descriptors and flags
+                    seg_load(c, m);
+                    if constexpr (!edge) pack_g(c, q);
+                }
+            }
+            if constexpr (!edge)
+                D = hot_draws_paired_g(A, lane, c == 0 ? pk0 : pk1, c == 0 ? mism0 : mism1, &s_base[wave][8 * c], s_small);
+            else
+                D = hot_draws_edge<false, true>(A, gq, wrapN(X0s + x, Nx), xb, two_sets ? xw : xb, &s_base[wave][8 * c],
+                                                &s_base[wave][(two_sets ? 16 : 0) + 8 * c], s_small, has4[c], buf_c[c]);
         } else if constexpr (!edge && SV_HOT_BSEL) {
             D = hot_draws_paired_sel(A, lane, c == 0 ? pk0 : pk1, &s_base[wave][8 * c], s_small);
         } else if constexpr (!edge) {
@@ -552,7 +668,8 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
 #pragma unroll
             for (int j = 0; j < 4; j++)
                 if ((uint32_t)((uint64_t)D.w[j] * kc) < thr)
-                    report(A.S, sweep_id, (uint32_t)(1 + 5 * c + 1 + j), SKIP ? spos[j] : rank, (uint32_t)rep);
+                    report(A.S, sweep_id, (uint32_t)(1 + 5 * c + 1 + j), SKIP ? spos[j] : rank + (SPLIT ? ((cur_m[c] >> j) & 1u) : 0u),
+                           (uint32_t)rep);
         }
     };
 
@@ -560,7 +677,13 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
         prefetch(ra);
         commit(ra);
     }
+    if constexpr (POLL) {
+        if (wave == 0 && lane == 0 && pv) Ls.stop = 1;
+    }
     __syncthreads();
+    if constexpr (POLL) {
+        if (Ls.stop) return;
+    }
 #if SV_WGTIME
     const uint64_t wg_t1 = rt_now();
 #endif
@@ -568,6 +691,9 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     const double hk = P.half_kappa;
     if (SV_HOT_PF_EARLY) prefetch(tfirst + 3 + NW);
     for (int32_t t = tfirst; t < t1; t += NW) {
+        if constexpr (POLL) {
+            if (Ls.stop) return;
+        }
         if (!SV_HOT_PF_EARLY) prefetch(t + 3 + NW);
         store_rows(t - NW);
         // ---------------- colour 0 on row q = t+2+wave
@@ -684,6 +810,10 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
             }
         }
         commit(t + 3 + NW);
+        if constexpr (POLL) {
+            if (wave == 0 && lane == 0 && pv) Ls.stop = 1;
+            if (wave == 0) pv = __hip_atomic_load(A.S.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         if (SV_HOT_PF_EARLY && t + NW < t1) prefetch(t + 3 + 2 * NW);
         // The bases of the wave's two rows (brow1, brow1 + 1) move NW rows down.  Unless a row wraps around the
         // lattice or sits on global row 0 (where a buffered half-word clamps the word index), every block's
@@ -693,20 +823,23 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
         brow1 += NW;
         if constexpr (PH) {
             // no row bases
-        } else if (SV_HOT_ADV && glo >= 1 && glo + NW + 1 < Nt) {
+        } else if (SV_HOT_ADV && glo >= 1 && glo + NW + 1 < Nt && !(ROWM && sw->near(glo, NW + 2))) {
             if (base_lane) {
                 const int ai = bty == 0 ? 0 : (bty == 1 ? 1 : 2);
                 s_base[wave][lane] = mad128c(s_adv[ai].A, s_base[wave][lane], s_adv[ai].C);
             }
             brow += NW;
         } else if (base_lane) {
-            const int64_t p_old = base_pos(bty, grow(brow), Nx, bx, bhas);
-            const int64_t p_new = base_pos(bty, grow(brow + NW), Nx, bx, bhas);
+            // (SPLIT: a row that crosses a switch takes the other descriptor: a full jump)
+            const Block *d_old = bdsc(brow), *d_new = bdsc(brow + NW);
+            const uint32_t h_old = SPLIT ? (bty >= 2 ? d_old->has : 0u) : bhas, h_new = SPLIT ? (bty >= 2 ? d_new->has : 0u) : bhas;
+            const int64_t p_old = base_pos(bty, grow(brow), Nx, bx, h_old);
+            const int64_t p_new = base_pos(bty, grow(brow + NW), Nx, bx, h_new);
             const int ai = bty == 0 ? 0 : (bty == 1 ? 1 : 2);
             const int64_t step = bty == 0 ? (int64_t)NW * Nx : (bty == 1 ? (int64_t)NW * Nx / 2 : (int64_t)NW * Nx / 4);
             u128 bases = s_base[wave][lane];
-            if (p_new - p_old == step) bases = apply(s_adv[ai], bases);
-            else bases = full_jump(Tb, &blocks[bblk], (uint32_t)p_new);
+            if (p_new - p_old == step && d_old == d_new) bases = apply(s_adv[ai], bases);
+            else bases = full_jump(Tb, d_new, (uint32_t)p_new);
             brow += NW;
             s_base[wave][lane] = bases;
         } else {
@@ -817,6 +950,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4
 }
 template __global__ void villain_sweep_hot_skip<false>(FArgs);
 template __global__ void villain_sweep_hot_skip<true>(FArgs);
+
+// The replay of a sweep that met NumPy Lemire rejections, at most one per choice block (periodic single lattices):
+// a strip whose rows all lie on one side of each block's switch runs the hot kernel's draws with one descriptor per
+// block (paired on interior strips, a fwd/bwd pair at opposite pairing parities included); the strips whose rows contain
+// a switch's row or wrap around the torus run the skip-list body, dispatched first.  A replay thus costs about one hot
+// sweep instead of a general-kernel sweep (~1.9x).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4 ? 4 : 3))) void villain_sweep_hot_split(
+    FArgs A, SplitArgs S) {
+    __shared__ HotLDST<false, false, 4> Ls;
+    // the skip-list strips swap places with their XCD's first-dispatched strips (SplitArgs::swap)
+    const int lb = logical_block();
+    int b = lb;
+    for (int i = 0; i < S.nswap; i++) {
+        if (lb == S.swap[i][0]) b = S.swap[i][1];
+        else if (lb == S.swap[i][1]) b = S.swap[i][0];
+    }
+    int ix, t0, t1;
+    if (A.strips) {
+        ix = A.strips[3 * b];
+        t0 = A.strips[3 * b + 1];
+        t1 = A.strips[3 * b + 2];
+    } else {
+        ix = b % A.nsx;
+        t0 = (b / A.nsx) * A.TH;
+        t1 = t0 + A.TH < A.G.Ht ? t0 + A.TH : A.G.Ht;
+    }
+    const int32_t x0 = (int32_t)((int64_t)ix * A.G.Nx / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * A.G.Nx / A.nsx);
+    const bool interior = x0 >= 4 && x1 + 2 < A.G.Nx;
+    bool straddle = false, rows = false;
+    SplitSw sw;
+    sw.qs[0] = sw.qs[1] = INT32_MAX;
+    sw.blk[0] = sw.blk[1] = 0;
+    sw.after = 0;
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        if (S.s[i] == 0xFFFFFFFFu || k >= 2) continue;
+        bool after = false;
+        straddle |= split_straddles(S.s[i], A.G.Nt, A.G.Nx, t0, t1, x0, x1, &sw.qs[k], &after);
+        rows |= split_rows(sw.qs[k], A.G.Nt, t0, t1);
+        sw.blk[k] = (uint32_t)i;
+        sw.after |= (uint32_t)after << k;
+        k++;
+    }
+    if (__builtin_amdgcn_readfirstlane((int)straddle))
+        hot_body<false, true, false, false, false, 4, true>(A, Ls, b);
+    else if (__builtin_amdgcn_readfirstlane((int)rows))
+        hot_body<false, true, false, false, false, 4, false, false, true, true>(A, Ls, b, nullptr, S.blocksB, &sw);
+    else if (__builtin_amdgcn_readfirstlane((int)interior))
+        hot_body<false, false, false, false, false, 4, false, false, true>(A, Ls, b, nullptr, S.blocksB, &sw);
+    else
+        hot_body<false, true, false, false, false, 4, false, false, true>(A, Ls, b, nullptr, S.blocksB, &sw);
+}
 
 // ---- multi-sweep band launches of small periodic lattices (BandArgs, villain.h)
 #ifndef SV_BAND_CAS
@@ -1016,6 +1202,68 @@ bool hot_skip_ok(const VParams &P, const Block *blocks) {
         for (int j = 0; j < 4; j++)
             if (blocks[2 + 5 * c + j].nskip > HOT_MAXSK) return false;
     return true;
+}
+
+// The split replay covers a sweep of the hot kernel's parameters whose choice blocks hold at most one known rejected
+// position each; `S` receives each switch and the descriptor after it: a rejected half-word at stream position p moves
+// every later draw of the block one half-word on, which for a block starting on a buffered half (has = 1) is the same
+// words with has = 0, and otherwise the next word's stream with has = 1 and word 0's high half buffered
+bool split_plan(const VParams &P, const Block *blocks, const uint32_t *skips, u128 inc, SplitArgs &S, Block *Bset) {
+    if (!hot_params_ok(P)) return false;
+    int nsw = 0;
+    for (int i = 0; i < 11; i++) Bset[i] = blocks[i];
+    for (int c = 0; c < 2; c++)
+        for (int j = 0; j < 4; j++) {
+            const Block &b = blocks[2 + 5 * c + j];
+            Block &B = Bset[2 + 5 * c + j];
+            B.nskip = 0;
+            S.s[4 * c + j] = 0xFFFFFFFFu;
+            if (b.nskip > 1) return false;
+            if (b.nskip == 0) continue;
+            if (++nsw > 2) return false;  // (SplitSw: at most two switches)
+            S.s[4 * c + j] = skips[b.skip0];
+            const u128 base{b.base_lo, b.base_hi};
+            if (b.has) {
+                B.has = 0;
+            } else {
+                const u128 nb = host_jump(base, inc, 1);
+                B.base_lo = nb.lo;
+                B.base_hi = nb.hi;
+                B.has = 1;
+                B.buf = (uint32_t)(xsl_rr(base) >> 32);
+            }
+        }
+    return true;
+}
+
+void split_order(SplitArgs &S, int32_t N, int nsx, int grid, const int32_t *tab, int TH) {
+    // logical blocks are dealt to the XCDs in contiguous ranges (logical_block), dispatched from the range's start; a
+    // skip-list strip swaps places with the next not yet swapped strip at the start of its own XCD's range, so that the
+    // XCD's set of strips (its share of the work) is unchanged
+    S.nswap = 0;
+    const int per = grid / 8, rem = grid % 8;
+    int used[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int b = 0; b < grid && S.nswap < SPLIT_SWAPS; b++) {
+        const int ix = tab ? tab[3 * b] : b % nsx;
+        const int32_t t0 = tab ? tab[3 * b + 1] : (b / nsx) * TH;
+        const int32_t t1 = tab ? tab[3 * b + 2] : std::min(t0 + TH, N);
+        const int32_t x0 = (int32_t)((int64_t)ix * N / nsx), x1 = (int32_t)((int64_t)(ix + 1) * N / nsx);
+        bool st = false, after;
+        int32_t qs;
+        for (int i = 0; i < 8 && !st; i++) st = S.s[i] != 0xFFFFFFFFu && split_straddles(S.s[i], N, N, t0, t1, x0, x1, &qs, &after);
+        if (!st) continue;
+        int x = 0;
+        while (x < 7 && b >= (x + 1) * per + std::min(x + 1, rem)) x++;
+        const int a = x * per + std::min(x, rem) + used[x]++;
+        if (a >= b) continue;  // (already among the first)
+        S.swap[S.nswap][0] = a;
+        S.swap[S.nswap][1] = b;
+        S.nswap++;
+    }
+}
+
+void launch_hot_split(const FArgs &A, const SplitArgs &S, int grid, hipStream_t stream) {
+    villain_sweep_hot_split<<<grid, 4 * 64, 0, stream>>>(A, S);
 }
 
 void launch_hot_skip(const FArgs &A, int grid, hipStream_t stream) {

@@ -61,3 +61,21 @@ def crafted_generator(seed, position, half):
     st['uinteger'] = 0
     gen.bit_generator.state = st
     return gen
+
+
+def observable_start(c):
+    """The starting fields of a villain_observables.npz chain (tools/make_golden_observables.hot_start: cold, or phi
+    uniform in [-pi, pi) and n in W * {-2..2} from the chain's hot-start seed)."""
+    N, W = c['N'], c['W']
+    if c['hot_seed'] < 0:
+        return np.zeros((N, N)), np.zeros((2, N, N), dtype=np.int64)
+    r = np.random.default_rng(c['hot_seed'])
+    return r.uniform(-np.pi, np.pi, (1, N, N))[0], (W * r.integers(-2, 3, (2, N, N))).astype(np.int64)
+
+
+def observable_groups():
+    """villain_observables.npz chains by group (one N, kappa, W per group: a replica batch)."""
+    groups = {}
+    for c in cases('villain_observables.npz'):
+        groups.setdefault(c['group'], []).append(c)
+    return groups

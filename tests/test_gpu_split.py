@@ -1,0 +1,93 @@
+"""The split replay (villain_sweep_hot_split) of a sweep that met a NumPy Lemire rejection, against the CPU oracle.
+
+A rejected uint32 (neighborhood.py:105-107: NumPy's bounded sampler draws again) moves every later draw of its choice
+block one half-word on; the replay runs each row with the descriptor of the block segment it lies in, fwd/bwd pairs
+at opposite pairing parities included, and the strips whose rows straddle the switch on the skip-list body.  Forced
+rejections (crafted PCG64 states) in each of the eight choice blocks, at the first rank (row 0: edge strips), the last
+rank, interior ranks (one strip straddles, the rest run the split body) and a strip's first column, with the first
+choice block starting on a whole word or on a buffered half-word: phi, n, the generator state and the counters must
+equal the oracle's, and sv_ctx_split_counts proves the split kernel ran."""
+import numpy as np
+import pytest
+
+import supervillain_amd as sv
+from tests.golden import crafted_generator
+
+pytestmark = pytest.mark.gpu
+
+
+def hot(N, W, seed):
+    r = np.random.default_rng(seed)
+    return r.uniform(-np.pi, np.pi, (N, N)), W * r.integers(-2, 3, (2, N, N)).astype(np.int64)
+
+
+def forced(seed, pos, half, has0):
+    g = crafted_generator(seed, pos, half)
+    if has0:  # the first choice block starts on a buffered half-word (uniform draws leave the buffer alone)
+        st = g.bit_generator.state
+        st['has_uint32'] = 1
+        st['uinteger'] = 0x9E3779B9
+        g.bit_generator.state = st
+    return g
+
+
+def word_of(N, c, j, rank, has0):
+    """(u64 stream position in sweep 0, half) of the draw of rank `rank` in choice block j of colour c."""
+    V = N * N
+    q = rank - has0  # half-word index within the block's words (rank 0 with has0 = 1 is the buffered half)
+    assert q >= 0
+    return V + c * (V // 2 + V) + V // 2 + j * (V // 4) + q // 2, q % 2
+
+
+def run(N, sweeps, gen, phi0, n0):
+    L = sv.Lattice2D(N)
+    S = sv.Villain(L, 0.5, 1)
+    G = sv.generator.villain.NeighborhoodUpdate(S, path=2)
+    G.rng = gen
+    cfg = {'phi': sv.Form(phi0.reshape(1, N, N).copy(), degree=0, lattice=L),
+           'n': sv.Form(n0.copy(), degree=1, lattice=L)}
+    ctx = G._state()[0]
+    ctx.sweep_counts()
+    ctx.split_counts()
+    cfg = G._steps(cfg, sweeps)
+    return G, np.asarray(cfg['phi'])[0], np.asarray(cfg['n']), ctx.split_counts(), ctx.sweep_counts()
+
+
+N = 1024
+# ranks: the first (row 0, column 0: an edge strip), an interior rank (row 517), the first column of an interior strip
+# (strip 3 starts at column 341), a rank in the last row, the last rank
+RANKS = [0, (517 * N + 300) // 2, (600 * N + 341) // 2, (1023 * N + 700) // 2, N * N // 2 - 1]
+
+
+@pytest.mark.parametrize('has0', [0, 1])
+@pytest.mark.parametrize('blk', range(8))
+def test_split_replay_each_block(blk, has0, oracle_lib):
+    c, j = divmod(blk, 4)
+    for i, rank in enumerate(RANKS):
+        if has0 and rank == 0:
+            continue  # (rank 0 draws the buffered half-word, not a fresh word)
+        pos, half = word_of(N, c, j, rank, has0)
+        seed = 1000 + 37 * blk + 5 * i + has0
+        phi0, n0 = hot(N, 1, seed)
+        G, phi, n, nsplit, counts = run(N, 2, forced(seed, pos, half, has0), phi0, n0)
+        g = forced(seed, pos, half, has0)
+        p, m = phi0.copy(), n0.copy()
+        st = oracle_lib.villain_neighborhood(N, 0.5, 1, p, m, 2, g)
+        assert sum(s.rejections for s in st) >= 1
+        assert (phi == p).all() and (n == m).all(), (blk, rank, has0)
+        assert G.rng.bit_generator.state == g.bit_generator.state
+        assert G.accepted == sum(s.accepted for s in st)
+        assert nsplit >= 1 and counts['fused'] == 0, (blk, rank, has0, nsplit, counts)
+
+
+def test_split_replay_natural_rejections_4096(oracle_lib):
+    """The bench-size lattice meets a natural rejection (seed 2024: in sweep 3) and replays it on the split kernel."""
+    N4 = 4096
+    phi0, n0 = np.zeros((N4, N4)), np.zeros((2, N4, N4), dtype=np.int64)
+    G, phi, n, nsplit, counts = run(N4, 5, np.random.default_rng(2024), phi0, n0)
+    g = np.random.default_rng(2024)
+    st = oracle_lib.villain_neighborhood(N4, 0.5, 1, phi0, n0, 5, g)
+    assert sum(s.rejections for s in st) >= 1
+    assert (phi == phi0).all() and (n == n0).all()
+    assert G.rng.bit_generator.state == g.bit_generator.state
+    assert nsplit >= 1

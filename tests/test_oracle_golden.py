@@ -184,3 +184,32 @@ def test_multicore_oracle_matches(oracle_lib):
         O.villain_neighborhood_mt(N, 0.4, W, b[0], b[1], 5, b[2], 3)
         assert (a[0] == b[0]).all() and (a[1] == b[1]).all()
         assert a[2].bit_generator.state == b[2].bit_generator.state
+
+
+def _offline_observables(phi, n, kappa):
+    """(ActionDensity, InternalEnergyDensity, WindingSquared, TorusWrapping) of one Villain configuration, restated
+    from observable/action.py:25-31, energy.py:25-30, winding.py:30-37, wrapping.py:17-25 and action/villain.py:51-66."""
+    N = phi.shape[0]
+    l0 = (0.0 + (np.roll(phi, -1, axis=0) - phi)) - 2 * np.pi * n[0]
+    l1 = (0.0 + (np.roll(phi, -1, axis=1) - phi)) - 2 * np.pi * n[1]
+    S = kappa / 2 * ((l0 ** 2).sum() + (l1 ** 2).sum())
+    dn = (np.roll(n[1], -1, axis=0) - n[1]) - (np.roll(n[0], -1, axis=1) - n[0])
+    return S / N ** 2, S / (N ** 2 * kappa), (dn ** 2).mean(), n.sum(axis=(1, 2))
+
+
+def test_observables_golden(oracle_lib):
+    """The oracle's chain, measured after every sweep, gives the reference's own observable values
+    (tests/golden/villain_observables.npz, tools/make_golden_observables.py): the fixture the GPU's inline
+    observables are compared with is the oracle's chain."""
+    from tests.golden import observable_start
+    for c in cases('villain_observables.npz'):
+        g = generator_from(c['rng0'])
+        phi, n = observable_start(c)
+        for s in range(c['sweeps']):
+            oracle_lib.villain_neighborhood(c['N'], c['kappa'], c['W'], phi, n, 1, g)
+            ad, ie, w2, tw = _offline_observables(phi, n, c['kappa'])
+            np.testing.assert_allclose(ad, c['ActionDensity'][s], rtol=1e-12)
+            np.testing.assert_allclose(ie, c['InternalEnergyDensity'][s], rtol=1e-12)
+            np.testing.assert_allclose(w2, c['WindingSquared'][s], rtol=1e-12)
+            assert (tw == c['TorusWrapping'][s]).all()
+        assert (state_of(g) == c['rng1']).all()
