@@ -8,12 +8,14 @@ with the fields resident in HBM.
 
   N = 1: one L x L lattice on one GPU (the single-lattice fused sweep kernel).
   N > 1: one process per GPU (torch.distributed.run; `python bench.py --gpus N` launches it itself when
-         WORLD_SIZE is unset, before anything touches a GPU).  BASELINE config 4: the ONE L x L lattice
-         is domain-decomposed into ty x tx tiles (1x2, 2x2, 2x4 for N = 2, 4, 8), one tile per GPU, with
-         RCCL halo exchanges (strong scaling; the chain is bit-identical to the 1-GPU chain).  Each rank
-         also times its own tile alone as a periodic lattice (R1 of SURVEY.md 8(d)'s weak-scaling
-         E_N = R_N / (N R1)), reported under config.weak_scaling.  --weak grows the lattice to
-         (ty L) x (tx L) instead (L x L per GPU).
+         WORLD_SIZE is unset, before anything touches a GPU).  Weak scaling (north_star: >= 0.75 weak-scaling
+         efficiency at 8 GPUs): a (ty L) x (tx L) lattice domain-decomposed into ty x tx tiles of L x L (1x2,
+         2x2, 2x4 for N = 2, 4, 8), one tile per GPU, with RCCL halo exchanges -- every GPU sweeps an L = 4096
+         tile, the headline's per-GPU work.  --strong: BASELINE config 4 instead, the ONE L x L lattice cut
+         into the N tiles (strong scaling; the chain is bit-identical to the 1-GPU chain).  Each rank also
+         times its own tile alone as a periodic lattice (R1 of SURVEY.md 8(d)'s E_N = R_N / (N R1)),
+         reported under config.weak_scaling.  --tiles TYxTX on one GPU emulates a decomposition (strong unless
+         --weak).
 Rank 0 prints one JSON line.
 
 Secondary workloads (not the headline line; BASELINE.json configs 5 and 3):
@@ -78,8 +80,10 @@ def parse():
                          'the optional counter-based mode (SURVEY.md 8(b) sv_rng mode 1, a different chain)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-sweeps', type=int, default=5)
-    ap.add_argument('--weak', action='store_true', help='N>1: an L x L tile per GPU (weak scaling) instead of one '
-                                                        'L x L lattice decomposed (strong scaling, the default)')
+    ap.add_argument('--weak', action='store_true', help='an L x L tile per GPU (weak scaling: the default for N > 1; '
+                                                        'with --tiles on one GPU, emulate that layout)')
+    ap.add_argument('--strong', action='store_true', help='N > 1: one L x L lattice decomposed over the N GPUs '
+                                                          '(BASELINE config 4, strong scaling)')
     ap.add_argument('--warmup-s', type=float, default=1.0,
                     help='after the W warmup steps, keep warming (untimed) until this many seconds have passed: '
                          'clocks and page mappings reach steady state before the timed region')
@@ -96,7 +100,11 @@ def parse():
                          'bit-exact reference visit order (plaquette.py:63; level-scheduled)')
     ap.add_argument('--replicas', type=int, default=1024, help='replicas workload: total replica count')
     args = ap.parse_args()
-    args.strong = not args.weak
+    if args.strong and args.weak:
+        ap.error('--strong and --weak exclude each other')
+    # weak scaling for N > 1 unless --strong; a one-GPU --tiles emulation is strong (config 4) unless --weak
+    gpus = args.gpus if args.gpus is not None else int(os.environ.get('WORLD_SIZE', '1'))
+    args.strong = args.strong or (gpus <= 1 and not args.weak)
     if args.workload in ('replicas', 'worms'):
         args.L = 128 if args.L == 4096 else args.L
         args.W = 2 if args.W == 1 else args.W

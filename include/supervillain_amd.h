@@ -79,7 +79,8 @@ int sv_ctx_block_counts(sv_ctx *ctx, int64_t *sweeps, int64_t *launches);
 int sv_ctx_split_counts(sv_ctx *ctx, int64_t *sweeps);
 /* Which multi-sweep launches small periodic lattices may use: 0 temporal blocks or else bands (default), 1 blocks
  * only, 2 bands only, 3 one sweep per launch; K: sweeps per temporal-blocking launch (0: the default; an even K runs
- * as K - 1, and K shrinks until the launch's frame fits).  Returns -1 for another mode or K outside 0..15. */
+ * as K - 1, and K shrinks until the launch's frame fits; one sweep per launch is mode 3).  Returns -1 for another
+ * mode or K outside {0, 3..15}. */
 int sv_ctx_set_multisweep(sv_ctx *ctx, int32_t mode, int32_t K);
 /* Diagnostic (tests): the context's PCG64 jump-table cache holds at most `cap` increments (0: the default, 1024 or
  * SV_MAX_TABLES); a full cache drains the device and is dropped.  sv_ctx_table_purges reports how often it was. */

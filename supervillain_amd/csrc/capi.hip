@@ -34,11 +34,8 @@ const sv::JumpTables *sv_ctx::jump_tables(uint64_t inc_hi, uint64_t inc_lo) {
     auto key = std::make_pair(inc_hi, inc_lo);
     auto it = tables.find(key);
     if (it != tables.end()) return it->second;
-    static const size_t max_tables = [] {  // SV_MAX_TABLES: a smaller cache (diagnostics: round 3 dropped it at 64)
-        const char *e = getenv("SV_MAX_TABLES");
-        return e && atoi(e) > 0 ? (size_t)atoi(e) : MAX_TABLES;
-    }();
-    if (tables.size() >= (table_cap ? table_cap : max_tables)) {
+
+    if (tables.size() >= (table_cap ? table_cap : MAX_TABLES)) {
         if (alloc_log()) fprintf(stderr, "[sv alloc] jump-table cache purge #%lld (%zu tables)\n", (long long)table_purges + 1,
                                  tables.size());
         // a long-lived context seeing many generators drops its cache.  Launches already enqueued on ANY stream of
@@ -46,7 +43,12 @@ const sv::JumpTables *sv_ctx::jump_tables(uint64_t inc_hi, uint64_t inc_lo) {
         // hold one of these tables, so the whole device drains first -- explicitly, not through hipFree's own
         // implicit synchronization -- and a failure there is reported, not swallowed.  No caller keeps a table
         // pointer across calls: every entry point fetches its table on entry.
-        SV_HIP(hipDeviceSynchronize());
+        // (the drain covers every stream of the device: an error it meets may come from work this context did not
+        // enqueue, and is reported as such)
+        const hipError_t de = hipDeviceSynchronize();
+        if (de != hipSuccess)
+            throw std::runtime_error(std::string("jump-table purge: draining the device (every stream, this context's and "
+                                                 "any other's) failed: ") + hipGetErrorString(de));
         for (auto &kv : tables) SV_HIP(hipFree(kv.second));
         tables.clear();
         table_purges++;
@@ -365,7 +367,8 @@ int sv_ctx_block_counts(sv_ctx *ctx, int64_t *sweeps, int64_t *launches) {
 }
 
 int sv_ctx_set_multisweep(sv_ctx *ctx, int32_t mode, int32_t K) {
-    if (!ctx || mode < 0 || mode > 3 || K < 0 || K > 15) return -1;  // (BAND_MAXK)
+    // (K = 1, 2 would leave no odd K >= 3: rejected rather than silently running the default; BAND_MAXK = 15)
+    if (!ctx || mode < 0 || mode > 3 || K < 0 || K == 1 || K == 2 || K > 15) return -1;
     ctx->multisweep = mode;
     ctx->block_k = K;
     return 0;

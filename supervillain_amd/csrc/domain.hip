@@ -248,7 +248,6 @@ struct sv_domain {
     int64_t pitch = 0, plane = 0, org = 0;
     int R = 2, cur = 0;
     int depth = 1;                  // Villain: sweeps per halo exchange (deep halos, see villain_depth)
-    std::map<int32_t, std::pair<int32_t *, int32_t>> tile_strips;  // two_wave_strips per region height (device, count)
     u128 *d_scan = nullptr;         // rejection prediction: per-sweep start states of the scanned batch
     hipStream_t scan_stream = nullptr;  // lowest priority: the scan fills the slots the sweeps leave free
     hipEvent_t ev_sum = nullptr, ev_scan = nullptr;
@@ -559,7 +558,7 @@ int domain_th(const sv_domain *d, int nsx, int *nw8 = nullptr) {
         const char *e = getenv("SV_DOMAIN_TH8");
         return e && atoi(e) >= 8 ? atoi(e) : 37;
     }();
-    if (nw8 && !(nwe && atoi(nwe) == 4) && hot_enabled() && rounds == 1 && wgs(th8) <= slots / 2) {
+    if (nw8 && !(nwe && atoi(nwe) == 4) && rounds == 1 && wgs(th8) <= slots / 2) {
         *nw8 = 1;
         return th8;
     }
@@ -699,7 +698,7 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
         std::vector<char> hot(count);
         // (villain_sweep_hot's 32-bit row offsets: 16 plane < 2^32)
         for (int k = 0; k < count; k++)
-            hot[k] = !no_hot && hot_enabled() && d->plane < (int64_t(1) << 28) && hot_ok(P, &blocks[(size_t)k * nb]);
+            hot[k] = !no_hot && d->plane < (int64_t(1) << 28) && hot_ok(P, &blocks[(size_t)k * nb]);
         for (auto &Tl : d->tiles) SV_HIP(hipMemsetAsync(Tl.sum, 0, sizeof(Summary), ctx->stream));
         if (predict) SV_HIP(hipEventRecord(d->ev_sum, ctx->stream));
         const int cur0 = d->cur;
@@ -758,38 +757,8 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
                     A.own_c1 = left + d->Wt;
                 }
                 int grid = A.nsx * A.nsy;
-                if (hot[k] && nw8) {
-                    // SV_TILE_SCHED=1: two waves of strips, taller for the workgroups dispatched first (two_wave_strips).
-                    // Off by default: 50.8 / 50.9 vs 49.5 / 49.6 us per 2048 x 1024 tile sweep with uniform strips (r4,
-                    // profiles/r04_tile_ab.txt) -- the second wave does not line up behind the first as assumed
-                    static const int sched = [] {
-                        const char *e = getenv("SV_TILE_SCHED");
-                        return e ? atoi(e) : 0;
-                    }();
-                    static const int cus = [] {
-                        int dev = 0, v = 0;
-                        if (hipGetDevice(&dev) != hipSuccess ||
-                            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-                            v = 0;
-                        return v;
-                    }();
-                    if (sched && cus > 0) {
-                        auto it = d->tile_strips.find(A.G.Ht);
-                        if (it == d->tile_strips.end()) {
-                            const std::vector<int32_t> tab = two_wave_strips(A.G.Ht, A.nsx, cus, 45, 29);
-                            int32_t *dt = nullptr;
-                            if (!tab.empty()) {
-                                SV_HIP(hipMalloc(&dt, tab.size() * sizeof(int32_t)));
-                                SV_HIP(hipMemcpy(dt, tab.data(), tab.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-                            }
-                            it = d->tile_strips.emplace(A.G.Ht, std::make_pair(dt, (int32_t)(tab.size() / 3))).first;
-                        }
-                        if (it->second.first) {
-                            A.strips = it->second.first;
-                            grid = it->second.second;
-                        }
-                    }
-                }
+                // (two waves of strips, taller for the workgroups dispatched first, measured slower than uniform strips:
+                // 50.8 / 50.9 vs 49.5 / 49.6 us per 2048 x 1024 tile sweep, r4 profiles/r04_tile_ab.txt)
                 launch_fused_tile(A, grid, ctx->stream, hot[k]);
                 (hot[k] ? ctx->sweeps_hot : ctx->sweeps_fused)++;
             }
@@ -1124,7 +1093,21 @@ int sv_domain_create_worldline(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tile
         if (ctx) ctx->err = "the Worldline decomposition needs even lattice extents";
         return -2;
     }
-    return domain_create(ctx, 1, Nt, Nx, tiles_t, tiles_x, nranks, rank, unique_id, out);
+    // worldline_step_fused (the decomposition's only kernel) addresses stream positions with 31 bits and moves rows by
+    // 32-bit byte offsets: refuse here, before any exchange is enqueued, what its first launch would
+    if ((int64_t)Nt * Nx >= (int64_t(1) << 31)) {
+        if (ctx) ctx->err = "the Worldline decomposition needs Nt * Nx < 2^31 (worldline_step_fused's 31-bit positions)";
+        return -2;
+    }
+    const int rc = domain_create(ctx, 1, Nt, Nx, tiles_t, tiles_x, nranks, rank, unique_id, out);
+    if (rc == 0 && (*out)->plane >= (int64_t(1) << 28)) {
+        (void)sv_domain_destroy(*out);
+        *out = nullptr;
+        ctx->err = "the Worldline decomposition needs tiles of < 2^28 sites with their ghost frames (worldline_step_fused's "
+                   "32-bit row offsets): use more tiles";
+        return -2;
+    }
+    return rc;
 }
 
 int sv_domain_destroy(sv_domain *d) {
@@ -1143,8 +1126,6 @@ int sv_domain_destroy(sv_domain *d) {
     if (d->comm) (void)ncclCommDestroy(d->comm);
     (void)hipFree(d->gathered);
     (void)hipFree(d->d_scan);
-    for (auto &kv : d->tile_strips)
-        if (kv.second.first) (void)hipFree(kv.second.first);
     if (d->scan_stream) (void)hipStreamDestroy(d->scan_stream);
     if (d->ev_sum) (void)hipEventDestroy(d->ev_sum);
     if (d->ev_scan) (void)hipEventDestroy(d->ev_scan);

@@ -29,16 +29,13 @@ __device__ __forceinline__ void report(const DevScratch &S, uint32_t sweep, uint
 
 // a launch of sweep `sweep` has nothing to do: a report came from an earlier sweep (with a gate, DevScratch), or
 // from any launch since the batch's reset (without)
-// The flags are read through the scalar cache (a constant-address-space load: one s_load per wave, cached per CU), not
-// by a vector load that bypasses the caches: a launch queued behind an abort then drains at the speed its workgroups
-// are dispatched.  The scalar cache is invalidated at every kernel's start, so a launch sees every earlier launch's
-// flag; within the reporting launch a stale 0 only means that a workgroup runs on (its results are discarded).
-__device__ __forceinline__ int32_t scalar_read(const int32_t *p) {
-    return *(const __attribute__((address_space(4))) int32_t *)(p);
-}
+// The flag decides correctness, not only speed: the launch of sweep k + 1 writes the buffer sweep k read, so behind a
+// failing sweep it must exit (the replay reads that buffer).  Hence a load that bypasses the caches (volatile: every
+// XCD sees the report's agent-scope store).  (A scalar-cache read was measured no faster for the drains, r5: ~5.1 us
+// per early-exit launch either way, profiles/r05_reject_trace_*.)
 __device__ __forceinline__ bool sweep_cancelled(const DevScratch &S, uint32_t sweep) {
-    if (S.gate) return scalar_read(S.gate) < (int32_t)sweep;
-    return scalar_read(S.abort) != 0;
+    if (S.gate) return *(volatile const int32_t *)S.gate < (int32_t)sweep;
+    return *(volatile const int32_t *)S.abort != 0;
 }
 
 // stream position of bounded draw d, accounting for known rejected positions (sorted)

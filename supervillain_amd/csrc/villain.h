@@ -116,7 +116,6 @@ struct BlockArgs {
     int32_t bs;    // block side
     int32_t nbx;   // blocks per row of blocks (N / bs)
     int32_t nb;    // descriptors per sweep
-    int32_t xcd;   // 1: blocks dealt to the XCDs in contiguous runs (neighbouring blocks share an L2), 0: round-robin
     Affine step;
     double *phi[BAND_MAXK + 1];
     int64_t *n[BAND_MAXK + 1];
@@ -187,6 +186,7 @@ using SkipMap = std::map<std::pair<int, int>, std::vector<uint32_t>>;
 struct AbortInfo {
     int32_t abort;
     std::vector<Report> reports;
+    uint32_t raw = 0;  // the device's report count (reports past MAX_REPORTS were dropped, in arrival order)
 };
 
 // One sweep's block sequence: metropolis uniform(V), then per colour
@@ -209,16 +209,12 @@ int fused_th(int32_t N, int nsx);  // rows per strip (SV_FUSED_TH overrides)
 // launch one tile-mode sweep with `grid` workgroups: villain_sweep_hot when `hot` (the sweep passes hot_ok),
 // villain_sweep_fused<4, true> otherwise
 void launch_fused_tile(const FArgs &A, int grid, hipStream_t stream, bool hot);
-bool hot_enabled();  // false when SV_HOT=0
 int hot_waves(int TH);  // waves per workgroup of villain_sweep_hot for strips of TH rows (4, or 8)
 // launch villain_sweep_fused<4, false, obs> over a replica batch (grid = replicas * tiles_per_rep)
 void launch_fused_batch(const FArgs &A, int grid, bool obs, hipStream_t stream);
 // villain_hot.hip: whether the fast-draw kernel covers the sweep whose 11 descriptors start at `blocks`,
 // and its launch (periodic single lattice or a domain tile, from the geometry)
 bool hot_ok(const VParams &P, const Block *blocks);
-// the skip form (villain_sweep_hot_skip, 4 waves): sweeps with <= 4 known rejected positions per choice block
-bool hot_skip_ok(const VParams &P, const Block *blocks);
-void launch_hot_skip(const FArgs &A, int grid, hipStream_t stream);
 // the split replay (villain_sweep_hot_split, periodic single lattices, 4 waves): whether it covers the sweep whose
 // descriptors start at `blocks` (<= 1 known rejected position per choice block), filling its SplitArgs; its launch
 // descriptors start at `blocks` (<= 1 known rejected position per choice block), filling S.s and the sweep's 11
@@ -230,9 +226,6 @@ void launch_hot_split(const FArgs &A, const SplitArgs &S, int grid, hipStream_t 
 void split_order(SplitArgs &S, int32_t N, int nsx, int grid, const int32_t *tab, int TH);
 // villain_sweep_hot's default descending strip table for H rows and nsx column strips ({ix, t0, t1} per strip)
 std::vector<int32_t> band_strips(int32_t H, int nsx);
-// two waves of 8-wave strips for a region one round covers: `first` strips of `tall` rows dispatched first, then strips
-// of `shrt` rows ({ix, t0, t1} per logical block), or empty when the region does not fit
-std::vector<int32_t> two_wave_strips(int32_t H, int nsx, int first, int tall, int shrt);
 void launch_hot(const FArgs &A, int grid, hipStream_t stream);
 // the band launch (8-wave strips of B.TH rows); band_residency: how many of its workgroups one CU holds at once
 void launch_hot_band(const FArgs &A, const BandArgs &B, hipStream_t stream);

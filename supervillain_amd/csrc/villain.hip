@@ -551,10 +551,6 @@ __global__ __launch_bounds__(4 * 64) __attribute__((amdgpu_waves_per_eu(3))) voi
 }
 
 template __global__ void villain_sweep_fused<4, false, false, false>(FArgs);
-#if SV_K3
-template __global__ void villain_sweep_fused<4, false, false, false, true>(FArgs);
-#endif
-template __global__ void villain_sweep_fused<6, false, false, false>(FArgs);
 template __global__ void villain_sweep_fused<4, true, false, false>(FArgs);
 template __global__ void villain_sweep_fused<4, false, true, false>(FArgs);
 template __global__ void villain_sweep_fused<4, false, true, true>(FArgs);
@@ -639,13 +635,6 @@ int hot_waves(int TH) {
     return nw == 8 && TH % 8 == 0 ? 8 : 4;
 }
 
-bool hot_enabled() {  // SV_HOT=0: every sweep on villain_sweep_fused (A/B measurements)
-    static const bool on = [] {
-        const char *e = getenv("SV_HOT");
-        return !(e && atoi(e) == 0);
-    }();
-    return on;
-}
 
 void launch_fused_batch(const FArgs &A, int grid, bool obs, hipStream_t stream) {
     const bool fr = A.nsx == 1 && A.G.Nx <= RW;  // full-row strips
@@ -745,6 +734,7 @@ AbortInfo read_abort_stats(sv_ctx *ctx, int count, sv_stats *stats, const sv_sta
     AbortInfo a;
     a.abort = *h_ab;
     uint32_t nrep = *h_nrep;
+    a.raw = nrep;
     if (landed) *landed = h_st;
     if (!a.abort) {
         std::memcpy(stats, h_st, count * sizeof(sv_stats));
@@ -805,12 +795,6 @@ int absorb_reports(const AbortInfo &a, int first, SkipMap &skips) {
     return (int)best.first;
 }
 
-// Tunables (overridable for experiments with SV_FUSED_NW in {4,6} and SV_FUSED_TH)
-int fused_nw() {
-    const char *e = getenv("SV_FUSED_NW");
-    int v = e ? atoi(e) : 4;
-    return v == 6 ? 6 : 4;
-}
 // rows per strip.  52 measured best at L=4096 (322 us vs 328 at 64, 324 at 48, 345 at 80; r73 sweep).
 // Small lattices have few strips: there the strips are cut shorter (down to 4 rows, more halo rows
 // recomputed) until the grid has `fill` = 512 workgroups, so that every CU has work (SURVEY.md 8(d)
@@ -957,54 +941,6 @@ std::vector<int32_t> band_strips(int32_t H, int nsx) {
     return tab;
 }
 
-// Two-wave strip table for a region that one round of 8-wave workgroups covers, two per CU (the config-4 tile): the
-// first `first` workgroups to be dispatched (one per CU) get strips of `tall` rows, the second wave strips of `shrt`
-// rows.  Two equal strips on one CU finish at 31 and 41 us (oldest-first issue, r3 WG timeline): the older
-// workgroup is barely slowed, the younger runs on what is left and then alone, so the CU's time is set by the
-// younger one.  6 row steps for the older and 4 for the younger balance that.  Rows of each column
-// strip: its tall strips, then its short ones, the last one shortened to the region.  {ix, t0, t1} per logical block
-// (logical_block's XCD-aware order; dispatch order is blockIdx, dealt round-robin over the 8 XCDs); empty when the
-// region does not fit two waves.
-std::vector<int32_t> two_wave_strips(int32_t H, int nsx, int first, int tall, int shrt) {
-    std::vector<std::array<int32_t, 3>> T, S;
-    for (int c = 0; c < nsx; c++) {
-        const int nt = first / nsx + (c < first % nsx ? 1 : 0);
-        int32_t t = 0;
-        for (int i = 0; i < nt && t < H; i++) {
-            const int32_t h = std::min<int32_t>(tall, H - t);
-            T.push_back({c, t, t + h});
-            t += h;
-        }
-        while (t < H) {
-            const int32_t h = std::min<int32_t>(shrt, H - t);
-            S.push_back({c, t, t + h});
-            t += h;
-        }
-    }
-    const int G = (int)(T.size() + S.size());
-    if ((int)T.size() > first || G > 2 * first) return {};
-    // dispatch rank (blockIdx) of each logical block
-    const int per = G / 8, rem = G % 8;
-    std::vector<std::pair<int, int>> order;  // (blockIdx, logical)
-    for (int x = 0; x < 8; x++) {
-        const int start = x * per + std::min(x, rem), n = per + (x < rem ? 1 : 0);
-        for (int k = 0; k < n; k++) order.push_back({8 * k + x, start + k});
-    }
-    std::sort(order.begin(), order.end());
-    std::vector<int32_t> tab(3 * (size_t)G);
-    // the earliest-dispatched logical blocks take the tall strips; each group in logical (XCD-range) order, so an
-    // XCD's strips are neighbours in their column
-    std::vector<int> first_wave, second_wave;
-    for (int i = 0; i < G; i++) (i < (int)T.size() ? first_wave : second_wave).push_back(order[i].second);
-    std::sort(first_wave.begin(), first_wave.end());
-    std::sort(second_wave.begin(), second_wave.end());
-    for (size_t i = 0; i < T.size(); i++)
-        for (int j = 0; j < 3; j++) tab[3 * (size_t)first_wave[i] + j] = T[i][j];
-    for (size_t i = 0; i < S.size(); i++)
-        for (int j = 0; j < 3; j++) tab[3 * (size_t)second_wave[i] + j] = S[i][j];
-    return tab;
-}
-
 // returns false if the fused path cannot represent the state (|n| too large): caller falls back
 // set once a band launch has failed (BAND_FAIL_BLOCK): the process's small lattices then run one sweep per launch
 static std::atomic<bool> band_broken{false};
@@ -1018,7 +954,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     auto specs = villain_specs(st, P.k > 1);
     const int nb = (int)specs.size();
     const int nsx = (N + FW_MAX - 1) / FW_MAX;
-    const int NWv = fused_nw();
+    constexpr int NWv = 4;  // (6-wave strips measured slower: 557-575 vs 320 us per sweep, round 1)
     // small lattices (strips cut to the 4-row minimum to fill the chip): 8-wave workgroups instead, over 5-row strips:
     // the kernel's row pipeline (colour 0 on rows t+2+w, colour 1 on t+1+w) then covers a strip in ONE row step, its
     // prologue rows included (8-row strips took two; L=256: 15.75 us per sweep at 4 rows / 4 waves, r369; 15.2 at
@@ -1052,7 +988,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     std::vector<uint32_t> skipvec;
     int sw = 0;
     const bool dbg = getenv("SV_DEBUG_TIMING") != nullptr;
-    const bool use_hot = hot_enabled() && V < (int64_t(1) << 28);  // villain_sweep_hot's 32-bit row offsets
+    const bool use_hot = V < (int64_t(1) << 28);  // villain_sweep_hot's 32-bit row offsets
     // the hot kernel's strip schedule (SV_STRIPS overrides: "uniform" or "" = strips of TH rows).  Default on
     // lattices of >= 4096 rows: band_strips -- per XCD band, 57-row strips, then 41-row strips, then the rest (L=4096:
     // "57x5,41x5,22", heights 4k+1 so the last row step of a strip is full), so the last rounds of slots run shorter
@@ -1186,16 +1122,13 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         // A batch that is not pre-planned (a call's first) on a small lattice is planned in two parts: the first few
         // launches' sweeps, uploaded and launched, then the rest while the device runs them (the plan of a 200-sweep
         // L=256 batch is ~55 us, ~3% of the call, r4 profiles/r04b_l256_host_phases.log).  Only without known skips.
-        static const int plan2_env = [] {
-            const char *e = getenv("SV_PLAN2");
-            return e ? atoi(e) : 1;
-        }();
+
         int part = count;  // sweeps of the batch planned and uploaded
         if (sw_next == sw) {
             blocks.swap(blocks_next);
             skipvec.swap(skipvec_next);
             c = c_next;
-        } else if (plan2_env && skips.empty() && V <= (1 << 18) && count >= 4 * 3 * std::max(bandK, 1)) {
+        } else if (skips.empty() && V <= (1 << 18) && count >= 4 * 3 * std::max(bandK, 1)) {
             part = 3 * std::max(bandK, 1);
             plan_sweeps(ctx, c, inc, specs, sw, part, skips, blocks, skipvec);
             ctx->ensure_blocks((size_t)count * nb);  // (the second part must not move d_blocks under the first launches)
@@ -1308,11 +1241,6 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                 B.nbx = N / blockBS;
                 B.nb = nb;
                 B.step = block_step;
-                static const int xcd_env = [] {
-                    const char *e = getenv("SV_BLOCK_XCD");
-                    return e ? atoi(e) : 0;
-                }();
-                B.xcd = xcd_env;
                 B.phi[0] = st->phi[st->cur ^ (k & 1)];
                 B.n[0] = st->n[st->cur ^ (k & 1)];
                 for (int j = 1; j < blockK; j++) {
@@ -1371,11 +1299,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                 ctx->sweeps_split++;
             } else {
                 ctx->sweeps_fused++;
-                if (NWv == 6) villain_sweep_fused<6, false, false, false><<<grid, 6 * 64, 0, ctx->stream>>>(A);
-#if SV_K3
-                else if (P.k == 3) villain_sweep_fused<4, false, false, false, true><<<grid, 4 * 64, 0, ctx->stream>>>(A);
-#endif
-                else villain_sweep_fused<4, false, false, false><<<grid, 4 * 64, 0, ctx->stream>>>(A);
+                villain_sweep_fused<4, false, false, false><<<grid, 4 * 64, 0, ctx->stream>>>(A);
             }
             if (per_launch && seg) {
                 ctx->time_end(seg, step, k);
@@ -1409,11 +1333,8 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         }
         if (seg) ctx->time_end(seg, launched - seg_k0, seg_k0);
         SV_HIP(hipGetLastError());
-        static const bool preplan = [] {  // SV_PREPLAN=0: plan each batch after the previous one's sync (A/B)
-            const char *e = getenv("SV_PREPLAN");
-            return !(e && atoi(e) == 0);
-        }();
-        if (preplan && launched == count && sw + count < sweeps) {  // (the device runs this batch meanwhile)
+
+        if (launched == count && sw + count < sweeps) {  // (the device runs this batch meanwhile)
             c_next = c;
             plan_sweeps(ctx, c_next, inc, specs, sw + count, std::min(BATCH, sweeps - sw - count), skips, blocks_next,
                         skipvec_next);
@@ -1472,6 +1393,41 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             first_bad = best.first;
             overflow = best.second == OVERFLOW_BLOCK;
             band_fail = best.second == BAND_FAIL_BLOCK;
+        }
+        // Multi-sweep launches report a rejected word once per workgroup that recomputes its site, from sweeps that run
+        // concurrently; past MAX_REPORTS the reports are dropped in arrival order, so the earliest failing sweep (the
+        // gate's atomic minimum) may have lost all of its reports.  Then the sweeps before the gate stand and the
+        // rest of the call runs one sweep per launch, whose reports name the rejections anew.
+        if (a.raw > (uint32_t)MAX_REPORTS && band_gate) {
+            int32_t g = INT32_MAX;
+            SV_HIP(hipMemcpy(&g, band_gate, sizeof(int32_t), hipMemcpyDeviceToHost));
+            if (g >= 0 && (uint32_t)g < first_bad) {
+                first_bad = (uint32_t)g;
+                overflow = false;
+                band_fail = true;  // (the band-failure path: keep the sweeps before it, multi-sweep launches off)
+            }
+        }
+        if (band_fail && a.raw > (uint32_t)MAX_REPORTS) {
+            // (truncated reports, above: multi-sweep launches off for the rest of this call only)
+            const int bad = (int)first_bad;
+            if (bad > 0) {
+                Cursor c2 = cur;
+                std::vector<Block> b2;
+                std::vector<uint32_t> s2;
+                plan_sweeps(ctx, c2, inc, specs, sw, bad, skips, b2, s2);
+                std::memcpy(stats + sw, landed, bad * sizeof(sv_stats));  // (landed with the batch's tail)
+                for (int k = 0; k < bad; k++) {
+                    stats[sw + k].proposed = V;
+                    stats[sw + k].rejections = rejections_in(skips, sw + k, nb);
+                }
+                cur = c2;
+            }
+            set_current(bad);
+            restore_band(bad);
+            sw += bad;
+            bandK = 0;
+            band_gate = nullptr;
+            continue;
         }
         if (band_fail) {
             // a band launch could not run as planned (tagged with its first sweep, whose input is intact): the

@@ -74,11 +74,8 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
     const int32_t N = A.G.Nx;
     const int64_t V = A.G.plane;
     const int K = B.K, E = K - 1, bs = B.bs;
-    int bl = (int)blockIdx.x;
-    if (B.xcd) {  // workgroup i runs on XCD i mod 8: give each XCD a contiguous run of blocks
-        const int G = (int)gridDim.x, per = G / 8, rem = G % 8, xcd = bl & 7, k = bl >> 3;
-        bl = xcd * per + (xcd < rem ? xcd : rem) + k;
-    }
+    // (blocks dealt to the XCDs in contiguous runs measured level with round-robin, r4 profiles/r04_block_xcd_ab.txt)
+    const int bl = (int)blockIdx.x;
     const int by = bl / B.nbx, bx = bl - by * B.nbx;
     const int32_t r0 = by * bs, c0 = bx * bs;
     const int F = block_frame(bs, K);
@@ -367,10 +364,7 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
             }
         }
         // the own block into the sweep's output buffer
-#ifndef SV_BLK_NOSCRATCH
-#define SV_BLK_NOSCRATCH 0  // timing experiments: the scratch buffers not written (a rejection's replay then wrong)
-#endif
-        if (!SV_BLK_NOSCRATCH || j + 1 == K) {
+        {
             double *phi_out = B.phi[j + 1];
             int64_t *n_out = B.n[j + 1];
             for (int idx = threadIdx.x; idx < bs * bs; idx += NT) {

@@ -939,17 +939,6 @@ __global__ __launch_bounds__(NWT * 64) __attribute__((amdgpu_waves_per_eu(SV_HOT
     else hot_body<TILE, true, false, false, false, NWT>(A, Ls, bl);
 }
 
-// A sweep with known NumPy Lemire rejections in its choice blocks (at most HOT_MAXSK per block; the replay of a
-// rejected sweep) or unequal buffered-half flags within a fwd/bwd pair (the sweep that holds the rejection): every
-// strip draws unpaired, with the skip-adjusted positions (hot_draws_edge<true>) -- the general villain_sweep_fused
-// form of these sweeps ran at ~1.9x the hot kernel's time
-template <bool TILE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4 ? 4 : 3))) void villain_sweep_hot_skip(FArgs A) {
-    __shared__ HotLDST<false, false, 4> Ls;
-    hot_body<TILE, true, false, false, false, 4, true>(A, Ls, logical_block());
-}
-template __global__ void villain_sweep_hot_skip<false>(FArgs);
-template __global__ void villain_sweep_hot_skip<true>(FArgs);
 
 // The replay of a sweep that met NumPy Lemire rejections, at most one per choice block (periodic single lattices):
 // a strip whose rows all lie on one side of each block's switch runs the hot kernel's draws with one descriptor per
@@ -1194,16 +1183,6 @@ bool hot_ok(const VParams &P, const Block *blocks) {
     return true;
 }
 
-// The skip form covers any sweep of the hot kernel's parameters whose choice blocks hold at most HOT_MAXSK known
-// rejected positions each (buffered-half flags may differ)
-bool hot_skip_ok(const VParams &P, const Block *blocks) {
-    if (!hot_params_ok(P)) return false;
-    for (int c = 0; c < 2; c++)
-        for (int j = 0; j < 4; j++)
-            if (blocks[2 + 5 * c + j].nskip > HOT_MAXSK) return false;
-    return true;
-}
-
 // The split replay covers a sweep of the hot kernel's parameters whose choice blocks hold at most one known rejected
 // position each; `S` receives each switch and the descriptor after it: a rejected half-word at stream position p moves
 // every later draw of the block one half-word on, which for a block starting on a buffered half (has = 1) is the same
@@ -1266,15 +1245,9 @@ void launch_hot_split(const FArgs &A, const SplitArgs &S, int grid, hipStream_t 
     villain_sweep_hot_split<<<grid, 4 * 64, 0, stream>>>(A, S);
 }
 
-void launch_hot_skip(const FArgs &A, int grid, hipStream_t stream) {
-    const bool periodic =
-        A.G.org == 0 && A.G.pitch == A.G.Nx && A.G.T0 == 0 && A.G.X0 == 0 && A.G.Ht == A.G.Nt && A.G.Wt == A.G.Nx;
-    if (periodic) villain_sweep_hot_skip<false><<<grid, 4 * 64, 0, stream>>>(A);
-    else villain_sweep_hot_skip<true><<<grid, 4 * 64, 0, stream>>>(A);
-}
 
 // replica batch of full-row lattices: N <= 128 columns (one strip), N % 4 == 0 (row ranks start on whole words)
-bool hot_fr_ok(int32_t N) { return hot_enabled() && N <= RW && N % 4 == 0 && N >= 8; }
+bool hot_fr_ok(int32_t N) { return N <= RW && N % 4 == 0 && N >= 8; }
 
 void launch_hot_fr(const FArgs &A, int grid, bool obs, hipStream_t stream) {
     if (obs) villain_sweep_hot_fr<true><<<grid, 4 * 64, 0, stream>>>(A);

@@ -959,8 +959,7 @@ int sv_worldline_plaquette_coexact_run(sv_worldline *st, double kappa, double W_
         for (const BlockSpec &b : coexact_specs(st)) specs.push_back(b);
         std::vector<int> stat_of(specs.size(), 0);
         for (size_t b = np; b < specs.size(); b++) stat_of[b] = 1;
-        const char *wf_env = getenv("SV_WF");  // SV_WF=0: the four pass kernels only (A/B measurements)
-        const bool use_wf = !(wf_env && atoi(wf_env) == 0);
+        constexpr bool use_wf = true;  // (worldline_step_fused; the four pass kernels where it does not apply)
         const int64_t N = st->N;
         // row-base advance maps of worldline_step_fused for 4 and 8 waves (rows per step NW: NW N draws, NW N / 4 words)
         const Affine adv[6] = {host_power(inc, 4 * (uint64_t)N), host_power(inc, 2 * (uint64_t)N), host_power(inc, (uint64_t)N),

@@ -64,18 +64,10 @@ struct WFArgs {
     int32_t it;            // coexact: t in -it..-1, 1..it
     uint32_t kt, thrt;     // its choice count 2 it and Lemire threshold
     int32_t general;       // MODE 2 for every strip (wf_body)
-    int32_t xe = 0;        // periodic lattices: the width of the two edge strips (0: every strip Wt / nsx wide)
 };
 
-// Column strip boundaries: uniform, or (xe > 0) two narrower edge strips -- the strips at the lattice's column seam
-// draw unpaired words from two base sets (MODE 1, ~11% longer row steps, profiles/r03b_worldline_wg_timeline.log),
-// and with one workgroup per CU the launch lasts as long as its slowest strip
-__device__ __forceinline__ int32_t wf_xb(const WFArgs &A, int ix) {
-    if (A.xe <= 0) return (int32_t)((int64_t)ix * A.G.Wt / A.nsx);
-    if (ix <= 0) return 0;
-    if (ix >= A.nsx) return A.G.Wt;
-    return A.xe + (int32_t)((int64_t)(ix - 1) * (A.G.Wt - 2 * A.xe) / (A.nsx - 2));
-}
+// Column strip boundaries (uniform: narrower seam strips, whose MODE 1 row steps are ~11% longer, measured level, r4)
+__device__ __forceinline__ int32_t wf_xb(const WFArgs &A, int ix) { return (int32_t)((int64_t)ix * A.G.Wt / A.nsx); }
 
 template <int NW>
 struct WFLDS {
@@ -614,20 +606,6 @@ void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
     A.general = general ? 1 : 0;
     A.G = G;
     A.nsx = (G.Wt + WF_W - 1) / WF_W;
-    {
-        // periodic lattices of >= 3 strips: edge strips SV_WF_EDGE percent as wide as the uniform split (the interior
-        // strips then <= WF_W).  Off by default: 88 / 94 measured level with uniform strips (39.8 / 39.7 vs 39.8 us
-        // per L=1024 step, r4) -- the seam strips' longer row steps do not set the launch's length
-        static const int pct = [] {
-            const char *e = getenv("SV_WF_EDGE");
-            return e ? atoi(e) : 0;
-        }();
-        const bool periodic = G.T0 == 0 && G.X0 == 0 && G.Ht == G.Nt && G.Wt == G.Nx && G.pitch == G.Nx && G.org == 0;
-        if (periodic && pct > 0 && pct < 100 && A.nsx >= 3) {
-            const int32_t xe = (int32_t)((int64_t)G.Wt * pct / (100 * A.nsx));
-            if (xe >= 8 && (G.Wt - 2 * xe + A.nsx - 3) / (A.nsx - 2) <= WF_W) A.xe = xe;
-        }
-    }
     const int nw = wf_nw(G.Ht, A.nsx);
     A.TH = wf_th(G.Ht, A.nsx, nw);
     A.nsy = (G.Ht + A.TH - 1) / A.TH;
