@@ -694,11 +694,26 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
         pred.valid = false;
         Cursor c = cur;
         plan_sweeps(ctx, c, inc, specs, sw, count, skips, blocks, skipvec);
-        upload_plan(ctx, blocks, skipvec);
         std::vector<char> hot(count);
         // (villain_sweep_hot's 32-bit row offsets: 16 plane < 2^32)
         for (int k = 0; k < count; k++)
             hot[k] = !no_hot && d->plane < (int64_t(1) << 28) && hot_ok(P, &blocks[(size_t)k * nb]);
+        // sweeps with known (predicted or reported) rejections, at most one per choice block: the split replay
+        // (villain_sweep_hot_split in tile mode), its descriptors after the switches uploaded with the batch's plan
+        std::vector<int> split_i(count, -1);
+        std::vector<SplitArgs> splits;
+        std::vector<size_t> split_off;
+        for (int k = 0; k < count; k++) {
+            if (hot[k] || no_hot || d->plane >= (int64_t(1) << 28) || nb != 11) continue;
+            SplitArgs SA;
+            Block Bset[11];
+            if (!split_plan(P, &blocks[(size_t)k * nb], skipvec.data(), inc, SA, Bset)) continue;
+            split_i[k] = (int)splits.size();
+            splits.push_back(SA);
+            split_off.push_back(blocks.size());
+            blocks.insert(blocks.end(), Bset, Bset + 11);
+        }
+        upload_plan(ctx, blocks, skipvec);
         for (auto &Tl : d->tiles) SV_HIP(hipMemsetAsync(Tl.sum, 0, sizeof(Summary), ctx->stream));
         if (predict) SV_HIP(hipEventRecord(d->ev_sum, ctx->stream));
         const int cur0 = d->cur;
@@ -759,8 +774,16 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
                 int grid = A.nsx * A.nsy;
                 // (two waves of strips, taller for the workgroups dispatched first, measured slower than uniform strips:
                 // 50.8 / 50.9 vs 49.5 / 49.6 us per 2048 x 1024 tile sweep, r4 profiles/r04_tile_ab.txt)
-                launch_fused_tile(A, grid, ctx->stream, hot[k]);
-                (hot[k] ? ctx->sweeps_hot : ctx->sweeps_fused)++;
+                if (split_i[k] >= 0) {
+                    SplitArgs SA = splits[split_i[k]];
+                    SA.blocksB = ctx->d_blocks + split_off[split_i[k]];
+                    split_order(SA, A.G, A.nsx, A.TH, grid, A.strips);
+                    launch_hot_split(A, SA, grid, ctx->stream);
+                    ctx->sweeps_split++;
+                } else {
+                    launch_fused_tile(A, grid, ctx->stream, hot[k]);
+                    (hot[k] ? ctx->sweeps_hot : ctx->sweeps_fused)++;
+                }
             }
             d->cur = out;
         }

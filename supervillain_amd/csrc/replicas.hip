@@ -108,6 +108,43 @@ struct sv_replicas {
     size_t tail_cap = 0;
     int32_t *d_map = nullptr;  // replica maps of the split launches of a batch (R * REP_BATCH slots)
     int32_t *d_gate = nullptr;  // the batch's first sweep with a report (DevScratch::gate)
+    // Host-to-device uploads of a batch (cursors, host-planned descriptors, skips, replica maps) go through pinned
+    // staging: an asynchronous copy from pageable memory waits for the stream, which would drain the GPU at every
+    // batch boundary behind the batch before
+    struct Stage {
+        char *h[2] = {nullptr, nullptr};
+        size_t cap[2] = {0, 0}, used = 0;
+        int i = 0;
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        void begin() {
+            i ^= 1;
+            used = 0;
+            if (ev[i]) SV_HIP(hipEventSynchronize(ev[i]));  // (the slot's copies of two batches ago)
+        }
+        void put(hipStream_t s, void *dst, const void *src, size_t bytes) {
+            if (!bytes) return;
+            if (used + bytes > cap[i]) {
+                SV_HIP(hipStreamSynchronize(s));  // (this slot's earlier copies have landed)
+                if (h[i]) SV_HIP(hipHostFree(h[i]));
+                cap[i] = std::max<size_t>(std::max<size_t>(2 * cap[i], bytes), 256 * 1024);
+                SV_HIP(hipHostMalloc((void **)&h[i], cap[i], hipHostMallocDefault));
+                used = 0;
+            }
+            std::memcpy(h[i] + used, src, bytes);
+            SV_HIP(hipMemcpyAsync(dst, h[i] + used, bytes, hipMemcpyHostToDevice, s));
+            used += (bytes + 255) & ~size_t(255);
+        }
+        void end(hipStream_t s) {
+            if (!ev[i]) SV_HIP(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+            SV_HIP(hipEventRecord(ev[i], s));
+        }
+        void release() {
+            for (int k = 0; k < 2; k++) {
+                if (h[k]) (void)hipHostFree(h[k]);
+                if (ev[k]) (void)hipEventDestroy(ev[k]);
+            }
+        }
+    } stage;
 };
 
 namespace {
@@ -217,7 +254,8 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         B.slot = slot;
         B.cur0 = b->cur;
         for (int r = 0; r < R; r++) pin[r] = PlanIn{cur[r].s.lo, cur[r].s.hi, cur[r].has, cur[r].buf};
-        SV_HIP(hipMemcpyAsync(b->d_plan, pin.data(), R * sizeof(PlanIn), hipMemcpyHostToDevice, ctx->stream));
+        b->stage.begin();
+        b->stage.put(ctx->stream, b->d_plan, pin.data(), R * sizeof(PlanIn));
         const int64_t nplan = (int64_t)R * count * NB;
         plan_replicas<<<(unsigned)((nplan + 255) / 256), 256, 0, ctx->stream>>>(b->d_plan, b->d_Trep, b->d_blocks, R,
                                                                                   count, (uint64_t)V);
@@ -236,13 +274,10 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
             for (Block &x : blk) x.skip0 += (int32_t)B.hskip.size();
             B.hskip.insert(B.hskip.end(), sk.begin(), sk.end());
             B.end_host[r] = c;
-            SV_HIP(hipMemcpyAsync(b->d_blocks + (size_t)r * count * NB, blk.data(), blk.size() * sizeof(Block),
-                                  hipMemcpyHostToDevice, ctx->stream));
+            b->stage.put(ctx->stream, b->d_blocks + (size_t)r * count * NB, blk.data(), blk.size() * sizeof(Block));
         }
         ctx->ensure_skips(B.hskip.size() + 1);
-        if (!B.hskip.empty())
-            SV_HIP(hipMemcpyAsync(ctx->d_skips, B.hskip.data(), B.hskip.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                                  ctx->stream));
+        b->stage.put(ctx->stream, ctx->d_skips, B.hskip.data(), B.hskip.size() * sizeof(uint32_t));
         reset_batch(ctx, b->d_stats, (size_t)R * count * sizeof(sv_stats), obs ? b->d_obs : nullptr,
                     obs ? (size_t)R * count * 4 * sizeof(double) : 0);
         // A sweep runs on the fast-draw kernel (villain_sweep_hot_fr) when no replica's choice blocks of that sweep
@@ -252,18 +287,23 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         std::vector<char> hot_k(count, fr_hot);
         std::vector<std::vector<int32_t>> skipped(count);  // per sweep: replicas on the general kernel (ascending)
         if (fr_hot) {
-            std::vector<const std::vector<Block> *> hbr(R, nullptr);
+            // only the replicas on the int32 image or with host-planned descriptors can leave the fast kernel: the scan
+            // walks those (a scan of every replica and sweep, 65536 steps at config 5, cost ~0.1 ms of idle GPU per
+            // batch boundary, r5 profiles/r05_rep_idle*.txt)
+            std::vector<std::pair<int, const std::vector<Block> *>> special;
             size_t hi = 0;
-            for (int r = 0; r < R; r++)
-                if (B.hosted[r]) hbr[r] = &B.hb[hi++];
+            for (int r = 0; r < R; r++) {
+                const std::vector<Block> *h = B.hosted[r] ? &B.hb[hi++] : nullptr;
+                if (big[r] || h) special.push_back({r, h});
+            }
             for (int k = 0; k < count; k++)
-                for (int r = 0; r < R; r++) {
-                    bool gen = big[r] != 0;
-                    if (hbr[r])
-                        for (int bi = 2; bi < NB; bi++) gen |= bi != 6 && (*hbr[r])[(size_t)k * NB + bi].nskip != 0;
+                for (const auto &sp : special) {
+                    bool gen = big[sp.first] != 0;
+                    if (sp.second)
+                        for (int bi = 2; bi < NB; bi++) gen |= bi != 6 && (*sp.second)[(size_t)k * NB + bi].nskip != 0;
                     if (gen) {
                         hot_k[k] = 0;
-                        skipped[k].push_back(r);
+                        skipped[k].push_back(sp.first);
                     }
                 }
         }
@@ -286,9 +326,8 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
             B.hmap.insert(B.hmap.end(), skipped[k].begin(), skipped[k].end());
             split[k][3] = (int64_t)skipped[k].size();
         }
-        if (!B.hmap.empty())
-            SV_HIP(hipMemcpyAsync(b->d_map, B.hmap.data(), B.hmap.size() * sizeof(int32_t), hipMemcpyHostToDevice,
-                                  ctx->stream));
+        b->stage.put(ctx->stream, b->d_map, B.hmap.data(), B.hmap.size() * sizeof(int32_t));
+        b->stage.end(ctx->stream);
         // The batch goes out in chunks of CH sweeps: after chunk j is enqueued the host waits for chunk j - 1 (the
         // progress word the first launch of chunk j stores) and reads the host-mapped abort flag, so that a NumPy
         // Lemire rejection leaves at most ~2 CH launches queued behind it (each an early exit over every workgroup)
@@ -426,17 +465,16 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
                 cf[i] = c;
             }
             ctx->ensure_skips(allsk.size() + 1);
+            b->stage.begin();
             for (size_t i = 0; i < F.size(); i++) {
                 const size_t e = (size_t)F[i] * count + k;
-                SV_HIP(hipMemcpyAsync(b->d_blocks + e * NB, &fb[i * NB], NB * sizeof(Block), hipMemcpyHostToDevice,
-                                      ctx->stream));
+                b->stage.put(ctx->stream, b->d_blocks + e * NB, &fb[i * NB], NB * sizeof(Block));
                 SV_HIP(hipMemsetAsync(b->d_stats + e, 0, sizeof(sv_stats), ctx->stream));
                 if (obs) SV_HIP(hipMemsetAsync(b->d_obs + 4 * e, 0, 4 * sizeof(double), ctx->stream));
             }
-            if (!allsk.empty())
-                SV_HIP(hipMemcpyAsync(ctx->d_skips, allsk.data(), allsk.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                                      ctx->stream));
-            SV_HIP(hipMemcpyAsync(b->d_map, F.data(), F.size() * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+            b->stage.put(ctx->stream, ctx->d_skips, allsk.data(), allsk.size() * sizeof(uint32_t));
+            b->stage.put(ctx->stream, b->d_map, F.data(), F.size() * sizeof(int32_t));
+            b->stage.end(ctx->stream);
             clear_abort(ctx);
             SV_HIP(hipMemsetAsync(b->d_gate, 0x7f, sizeof(int32_t), ctx->stream));
             FArgs A;
@@ -658,6 +696,7 @@ int sv_replicas_destroy(sv_replicas *b) {
     (void)hipFree(b->d_obs);
     if (b->h_tail) (void)hipHostFree(b->h_tail);
     if (b->d_map) (void)hipFree(b->d_map);
+    b->stage.release();
     delete b;
     return rc;
 }

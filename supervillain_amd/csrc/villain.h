@@ -154,6 +154,23 @@ __host__ __device__ inline bool split_straddles(uint32_t s, int32_t Nt, int32_t 
     return !interior || (ca < xs && xs <= cb);
 }
 
+// strip b of a launch (strip table `tab` or uniform strips of TH rows, nsx column strips over the region's Wt columns)
+// in global coordinates: rows [tg0, tg1) (tg0 may be negative or tg1 beyond Nt: they wrap), columns [xg0, xg1), xg0
+// the strip's first column wrapped onto the torus (as villain_sweep_hot's X0s + x0)
+__host__ __device__ inline void split_strip(const FGeom &G, int nsx, int TH, const int32_t *tab, int b, int32_t &tg0,
+                                            int32_t &tg1, int32_t &xg0, int32_t &xg1) {
+    const int ix = tab ? tab[3 * b] : b % nsx;
+    const int32_t t0 = tab ? tab[3 * b + 1] : (b / nsx) * TH;
+    const int32_t t1 = tab ? tab[3 * b + 2] : (t0 + TH < G.Ht ? t0 + TH : G.Ht);
+    const int32_t x0 = (int32_t)((int64_t)ix * G.Wt / nsx), x1 = (int32_t)((int64_t)(ix + 1) * G.Wt / nsx);
+    tg0 = G.T0 + t0;
+    tg1 = G.T0 + t1;
+    int32_t g = (G.X0 + x0) % G.Nx;
+    if (g < 0) g += G.Nx;
+    xg0 = g;
+    xg1 = g + (x1 - x0);
+}
+
 // whether strip [t0, t1)'s rows (halo and base rows included) contain row qs or wrap around the torus: its rows then lie
 // on both sides of a switch in row qs, and the descriptors are chosen per row
 __host__ __device__ inline bool split_rows(int32_t qs, int32_t Nt, int32_t t0, int32_t t1) {
@@ -215,15 +232,15 @@ void launch_fused_batch(const FArgs &A, int grid, bool obs, hipStream_t stream);
 // villain_hot.hip: whether the fast-draw kernel covers the sweep whose 11 descriptors start at `blocks`,
 // and its launch (periodic single lattice or a domain tile, from the geometry)
 bool hot_ok(const VParams &P, const Block *blocks);
-// the split replay (villain_sweep_hot_split, periodic single lattices, 4 waves): whether it covers the sweep whose
+// the split replay (villain_sweep_hot_split, single lattices and domain tiles, 4 waves): whether it covers the sweep whose
 // descriptors start at `blocks` (<= 1 known rejected position per choice block), filling its SplitArgs; its launch
 // descriptors start at `blocks` (<= 1 known rejected position per choice block), filling S.s and the sweep's 11
 // descriptors after the switches (Bset)
 bool split_plan(const VParams &P, const Block *blocks, const uint32_t *skips, u128 inc, SplitArgs &S, Block *Bset);
 void launch_hot_split(const FArgs &A, const SplitArgs &S, int grid, hipStream_t stream);
-// fill S.nswap / S.swap: the skip-list strips (strip table `tab` of `grid` entries, or uniform strips of TH rows) moved
-// to the start of their XCD's range
-void split_order(SplitArgs &S, int32_t N, int nsx, int grid, const int32_t *tab, int TH);
+// fill S.nswap / S.swap: the skip-list strips of a launch over region G (strip table `tab` of `grid` entries, or uniform
+// strips of TH rows) moved to the start of their XCD's range
+void split_order(SplitArgs &S, const FGeom &G, int nsx, int TH, int grid, const int32_t *tab);
 // villain_sweep_hot's default descending strip table for H rows and nsx column strips ({ix, t0, t1} per strip)
 std::vector<int32_t> band_strips(int32_t H, int nsx);
 void launch_hot(const FArgs &A, int grid, hipStream_t stream);

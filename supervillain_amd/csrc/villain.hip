@@ -1151,8 +1151,8 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                 SplitArgs SA;
                 Block Bset[11];
                 if (!split_plan(P, bk, skipvec.data(), inc, SA, Bset)) continue;
-                split_order(SA, N, nsx, st->d_strips ? st->n_strips : grid, st->d_strips ? st->h_strips.data() : nullptr,
-                            TH);
+                split_order(SA, FGeom{N, N, 0, 0, N, N, N, V, 0}, nsx, TH, st->d_strips ? st->n_strips : grid,
+                            st->d_strips ? st->h_strips.data() : nullptr);
                 splits.push_back({k, SA});
                 split_off.push_back(blocks.size());
                 blocks.insert(blocks.end(), Bset, Bset + 11);

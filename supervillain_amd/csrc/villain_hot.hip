@@ -247,7 +247,7 @@ template <bool TILE, bool EDGE, bool FR = false, bool OBS = false, bool PH = fal
 __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, NWT> &Ls, int bl,
                                          const HotBand *hb = nullptr, const Block *blocksB = nullptr,
                                          const SplitSw *sw = nullptr) {
-    static_assert(!SPLIT || (!TILE && !FR && !PH && !SKIP && !BAND && NWT == 4), "split replays: periodic single lattices");
+    static_assert(!SPLIT || (!FR && !PH && !SKIP && !BAND && NWT == 4), "split replays: single lattices and tiles");
     static_assert(!(FR && TILE), "full-row replica strips are periodic");
     static_assert(!SKIP || (EDGE && !FR && !PH), "skip lists: the unpaired (edge) draws of single lattices and tiles");
     static_assert(NWT == 4 || (NWT == 8 && !FR && !PH), "8-wave strips: single lattices and tiles");
@@ -940,11 +940,13 @@ __global__ __launch_bounds__(NWT * 64) __attribute__((amdgpu_waves_per_eu(SV_HOT
 }
 
 
-// The replay of a sweep that met NumPy Lemire rejections, at most one per choice block (periodic single lattices):
-// a strip whose rows all lie on one side of each block's switch runs the hot kernel's draws with one descriptor per
-// block (paired on interior strips, a fwd/bwd pair at opposite pairing parities included); the strips whose rows contain
-// a switch's row or wrap around the torus run the skip-list body, dispatched first.  A replay thus costs about one hot
-// sweep instead of a general-kernel sweep (~1.9x).
+// The replay of a sweep that met NumPy Lemire rejections, at most one per choice block and two in all (single lattices
+// and domain tiles): a strip whose rows all lie on one side of each block's switch runs the hot kernel's draws with one
+// descriptor per block (paired on interior strips, a fwd/bwd pair at opposite pairing parities included), a strip
+// whose rows contain a switch's row or wrap around the torus picks them per row, and the few strips whose columns
+// straddle a switch's site run the skip-list body, moved to the head of their XCD's range.  A replay thus costs about
+// one hot sweep instead of a general-kernel sweep (~1.9x).
+template <bool TILE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4 ? 4 : 3))) void villain_sweep_hot_split(
     FArgs A, SplitArgs S) {
     __shared__ HotLDST<false, false, 4> Ls;
@@ -955,18 +957,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4
         if (lb == S.swap[i][0]) b = S.swap[i][1];
         else if (lb == S.swap[i][1]) b = S.swap[i][0];
     }
-    int ix, t0, t1;
-    if (A.strips) {
-        ix = A.strips[3 * b];
-        t0 = A.strips[3 * b + 1];
-        t1 = A.strips[3 * b + 2];
-    } else {
-        ix = b % A.nsx;
-        t0 = (b / A.nsx) * A.TH;
-        t1 = t0 + A.TH < A.G.Ht ? t0 + A.TH : A.G.Ht;
-    }
-    const int32_t x0 = (int32_t)((int64_t)ix * A.G.Nx / A.nsx), x1 = (int32_t)((int64_t)(ix + 1) * A.G.Nx / A.nsx);
-    const bool interior = x0 >= 4 && x1 + 2 < A.G.Nx;
+    int32_t tg0, tg1, xg0, xg1;  // the strip in global rows / columns
+    split_strip(A.G, A.nsx, A.TH, A.strips, b, tg0, tg1, xg0, xg1);
+    const bool interior = xg0 >= 4 && xg1 + 2 < A.G.Nx;
     bool straddle = false, rows = false;
     SplitSw sw;
     sw.qs[0] = sw.qs[1] = INT32_MAX;
@@ -977,21 +970,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4
     for (int i = 0; i < 8; i++) {
         if (S.s[i] == 0xFFFFFFFFu || k >= 2) continue;
         bool after = false;
-        straddle |= split_straddles(S.s[i], A.G.Nt, A.G.Nx, t0, t1, x0, x1, &sw.qs[k], &after);
-        rows |= split_rows(sw.qs[k], A.G.Nt, t0, t1);
+        straddle |= split_straddles(S.s[i], A.G.Nt, A.G.Nx, tg0, tg1, xg0, xg1, &sw.qs[k], &after);
+        rows |= split_rows(sw.qs[k], A.G.Nt, tg0, tg1);
         sw.blk[k] = (uint32_t)i;
         sw.after |= (uint32_t)after << k;
         k++;
     }
     if (__builtin_amdgcn_readfirstlane((int)straddle))
-        hot_body<false, true, false, false, false, 4, true>(A, Ls, b);
+        hot_body<TILE, true, false, false, false, 4, true>(A, Ls, b);
     else if (__builtin_amdgcn_readfirstlane((int)rows))
-        hot_body<false, true, false, false, false, 4, false, false, true, true>(A, Ls, b, nullptr, S.blocksB, &sw);
+        hot_body<TILE, true, false, false, false, 4, false, false, true, true>(A, Ls, b, nullptr, S.blocksB, &sw);
     else if (__builtin_amdgcn_readfirstlane((int)interior))
-        hot_body<false, false, false, false, false, 4, false, false, true>(A, Ls, b, nullptr, S.blocksB, &sw);
+        hot_body<TILE, false, false, false, false, 4, false, false, true>(A, Ls, b, nullptr, S.blocksB, &sw);
     else
-        hot_body<false, true, false, false, false, 4, false, false, true>(A, Ls, b, nullptr, S.blocksB, &sw);
+        hot_body<TILE, true, false, false, false, 4, false, false, true>(A, Ls, b, nullptr, S.blocksB, &sw);
 }
+template __global__ void villain_sweep_hot_split<false>(FArgs, SplitArgs);
+template __global__ void villain_sweep_hot_split<true>(FArgs, SplitArgs);
 
 // ---- multi-sweep band launches of small periodic lattices (BandArgs, villain.h)
 #ifndef SV_BAND_CAS
@@ -1215,7 +1210,7 @@ bool split_plan(const VParams &P, const Block *blocks, const uint32_t *skips, u1
     return true;
 }
 
-void split_order(SplitArgs &S, int32_t N, int nsx, int grid, const int32_t *tab, int TH) {
+void split_order(SplitArgs &S, const FGeom &G, int nsx, int TH, int grid, const int32_t *tab) {
     // logical blocks are dealt to the XCDs in contiguous ranges (logical_block), dispatched from the range's start; a
     // skip-list strip swaps places with the next not yet swapped strip at the start of its own XCD's range, so that the
     // XCD's set of strips (its share of the work) is unchanged
@@ -1223,13 +1218,12 @@ void split_order(SplitArgs &S, int32_t N, int nsx, int grid, const int32_t *tab,
     const int per = grid / 8, rem = grid % 8;
     int used[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int b = 0; b < grid && S.nswap < SPLIT_SWAPS; b++) {
-        const int ix = tab ? tab[3 * b] : b % nsx;
-        const int32_t t0 = tab ? tab[3 * b + 1] : (b / nsx) * TH;
-        const int32_t t1 = tab ? tab[3 * b + 2] : std::min(t0 + TH, N);
-        const int32_t x0 = (int32_t)((int64_t)ix * N / nsx), x1 = (int32_t)((int64_t)(ix + 1) * N / nsx);
+        int32_t tg0, tg1, xg0, xg1;
+        split_strip(G, nsx, TH, tab, b, tg0, tg1, xg0, xg1);
         bool st = false, after;
         int32_t qs;
-        for (int i = 0; i < 8 && !st; i++) st = S.s[i] != 0xFFFFFFFFu && split_straddles(S.s[i], N, N, t0, t1, x0, x1, &qs, &after);
+        for (int i = 0; i < 8 && !st; i++)
+            st = S.s[i] != 0xFFFFFFFFu && split_straddles(S.s[i], G.Nt, G.Nx, tg0, tg1, xg0, xg1, &qs, &after);
         if (!st) continue;
         int x = 0;
         while (x < 7 && b >= (x + 1) * per + std::min(x + 1, rem)) x++;
@@ -1242,9 +1236,11 @@ void split_order(SplitArgs &S, int32_t N, int nsx, int grid, const int32_t *tab,
 }
 
 void launch_hot_split(const FArgs &A, const SplitArgs &S, int grid, hipStream_t stream) {
-    villain_sweep_hot_split<<<grid, 4 * 64, 0, stream>>>(A, S);
+    const bool periodic =
+        A.G.org == 0 && A.G.pitch == A.G.Nx && A.G.T0 == 0 && A.G.X0 == 0 && A.G.Ht == A.G.Nt && A.G.Wt == A.G.Nx;
+    if (periodic) villain_sweep_hot_split<false><<<grid, 4 * 64, 0, stream>>>(A, S);
+    else villain_sweep_hot_split<true><<<grid, 4 * 64, 0, stream>>>(A, S);
 }
-
 
 // replica batch of full-row lattices: N <= 128 columns (one strip), N % 4 == 0 (row ranks start on whole words)
 bool hot_fr_ok(int32_t N) { return N <= RW && N % 4 == 0 && N >= 8; }
