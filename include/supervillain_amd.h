@@ -131,7 +131,7 @@ int sv_villain_run_philox(sv_villain *st, double kappa, int64_t W, double interv
  * Ensemble.generate's kept configurations, ensemble.py:89-92, overlapped with the sweeps that follow).
  * sv_villain_emit returns at once: the state as of every sweep queued so far is snapshotted on the device
  * (two alternating emission buffers) and copied to phi / n on a copy stream.  The host arrays must stay
- * valid and unread until sv_villain_emit_wait returns; register them with sv_host_register for a true DMA. */
+ * valid and unread until sv_villain_emit_wait returns; allocate them with sv_host_alloc for a true DMA. */
 int sv_villain_emit(sv_villain *st, double *phi, int64_t *n);
 int sv_villain_emit_wait(sv_villain *st);
 /* Deferred statistics: with on = 1, runs whose sweeps cannot meet a NumPy Lemire rejection (every bounded draw
@@ -140,8 +140,10 @@ int sv_villain_emit_wait(sv_villain *st);
  * calls synchronize as usual.  The stats arrays must stay valid until then. */
 int sv_ctx_set_deferred(sv_ctx *ctx, int32_t on);
 int sv_ctx_sync(sv_ctx *ctx);
-int sv_host_register(void *p, size_t bytes);   /* pin host memory (hipHostRegister) */
-int sv_host_unregister(void *p);
+/* Page-locked host memory owned by the library (hipHostMalloc): emission targets whose copies overlap the sweeps.
+ * The library never registers caller memory (page-locking arrays that share pages with other objects is unsafe). */
+int sv_host_alloc(size_t bytes, void **out);
+int sv_host_free(void *p);
 /* path: 0 = auto (fused two-colour sweep kernel for even N, per-colour kernels otherwise),
  *       1 = per-colour kernels (any N), 2 = fused (even N only). */
 int sv_villain_run(sv_villain *st, double kappa, int64_t W, double interval_phi, int64_t interval_n, int32_t sweeps,

@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 import supervillain_amd as sv  # noqa: E402
 from supervillain_amd.generator import villain as gv  # noqa: E402
 from supervillain_amd.generator.combining import KeepEvery  # noqa: E402
-from supervillain_amd.pipeline import DeviceChain, PinnedHost, device_program  # noqa: E402
+from supervillain_amd.pipeline import DeviceChain, device_program, pinned_empty  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument('--L', type=int, default=4096)
@@ -21,12 +21,11 @@ ap.add_argument('--keep', type=int, default=32)
 ap.add_argument('--steps', type=int, default=8)
 a = ap.parse_args()
 S = sv.Villain(sv.Lattice2D(a.L), 0.5, 1)
-phi = np.zeros((a.steps, 1, a.L, a.L))
-n = np.zeros((a.steps, 2, a.L, a.L), dtype=np.int64)
 t = time.perf_counter()
-pin = PinnedHost(phi, n)
+phi = pinned_empty((a.steps, 1, a.L, a.L), np.float64)
+n = pinned_empty((a.steps, 2, a.L, a.L), np.int64)
 t_pin = time.perf_counter() - t
-res = {'L': a.L, 'keep_every': a.keep, 'configs': a.steps, 'pinned': len(pin.pinned), 'pin_s': t_pin}
+res = {'L': a.L, 'keep_every': a.keep, 'configs': a.steps, 'pin_s': t_pin}
 for mode in ('advance_only', 'download', 'emit', 'advance_only'):
     G = gv.NeighborhoodUpdate(S)
     G.rng = np.random.default_rng(0)
@@ -45,6 +44,5 @@ for mode in ('advance_only', 'download', 'emit', 'advance_only'):
         ch.emit_wait()
     res[mode + '_ms_per_config'] = (time.perf_counter() - t) / a.steps * 1e3
     ch.close()
-pin.release()
 res['bytes_per_config'] = int(phi[0].nbytes + n[0].nbytes)
 print(json.dumps(res))

@@ -62,10 +62,10 @@ def lib():
         L.sv_villain_emit_wait.argtypes = [vp]
         L.sv_worldline_emit.argtypes = [vp, vp, vp]
         L.sv_worldline_emit_wait.argtypes = [vp]
-        L.sv_host_register.argtypes = [vp, ctypes.c_size_t]
+        L.sv_host_alloc.argtypes = [ctypes.c_size_t, P(vp)]
         L.sv_ctx_set_deferred.argtypes = [vp, i32]
         L.sv_ctx_sync.argtypes = [vp]
-        L.sv_host_unregister.argtypes = [vp]
+        L.sv_host_free.argtypes = [vp]
         L.sv_villain_run.argtypes = [vp, f64, i64, f64, i64, i32, P(SvRng), P(SvStats), i32]
         L.sv_villain_observables.argtypes = [vp, f64, vp]
         L.sv_villain_site_run.argtypes = [vp, f64, f64, i32, P(SvRng), P(SvStats)]
@@ -120,7 +120,7 @@ EXPORTED = ('sv_ctx_create', 'sv_ctx_destroy', 'sv_last_error', 'sv_device_count
             'sv_ctx_set_timing', 'sv_ctx_kernel_time', 'sv_ctx_sweep_counts', 'sv_ctx_band_counts', 'sv_ctx_block_counts', 'sv_ctx_split_counts', 'sv_ctx_set_multisweep', 'sv_ctx_set_table_cap', 'sv_ctx_table_purges', 'sv_hbm_copy', 'sv_rng_gather', 'sv_rng_scatter',
             'sv_villain_neighborhood', 'sv_villain_create', 'sv_villain_destroy', 'sv_villain_upload',
             'sv_villain_download', 'sv_villain_run', 'sv_villain_observables', 'sv_villain_emit', 'sv_villain_emit_wait', 'sv_villain_run_philox',
-            'sv_worldline_emit', 'sv_worldline_emit_wait', 'sv_host_register', 'sv_host_unregister',
+            'sv_worldline_emit', 'sv_worldline_emit_wait', 'sv_host_alloc', 'sv_host_free',
             'sv_ctx_set_deferred', 'sv_ctx_sync',
             'sv_villain_site_run', 'sv_villain_link_run', 'sv_villain_exact_run', 'sv_villain_cohomology_run', 'sv_worldline_create',
             'sv_worldline_destroy', 'sv_worldline_upload', 'sv_worldline_download', 'sv_worldline_coexact_run',

@@ -469,15 +469,19 @@ int sv_ctx_sync(sv_ctx *ctx) {
     }
 }
 
-int sv_host_register(void *p, size_t bytes) {
-    if (!p || !bytes) return -1;
-    if (hipHostRegister(p, bytes, hipHostRegisterDefault) != hipSuccess) return -2;
+int sv_host_alloc(size_t bytes, void **out) {
+    if (!out) return -1;
+    *out = nullptr;
+    if (!bytes) return -1;
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return -2;
+    *out = p;
     return 0;
 }
 
-int sv_host_unregister(void *p) {
+int sv_host_free(void *p) {
     if (!p) return -1;
-    return hipHostUnregister(p) == hipSuccess ? 0 : -2;
+    return hipHostFree(p) == hipSuccess ? 0 : -2;
 }
 
 int sv_villain_emit(sv_villain *st, double *phi, int64_t *n) {

@@ -13,7 +13,7 @@ import numpy as np
 from supervillain_amd.batch import Batch
 from supervillain_amd.configurations import Configurations
 from supervillain_amd.generator.combining import KeepEvery
-from supervillain_amd.pipeline import DeviceChain, PinnedHost, device_program
+from supervillain_amd.pipeline import DeviceChain, device_program, pinned_empty
 from supervillain_amd.store import ExtendableStore
 
 logger = logging.getLogger(__name__)
@@ -84,7 +84,11 @@ class Ensemble:
         ax, ay = Batch.as_array(fields[x]), Batch.as_array(fields[y])
         direct = (ax.dtype == chain.a.dtype and ay.dtype == chain.b.dtype and ax.shape[1:] == chain.a.shape
                   and ay.shape[1:] == chain.b.shape and ax.flags['C_CONTIGUOUS'] and ay.flags['C_CONTIGUOUS'])
-        pin = PinnedHost(ax, ay) if direct else None
+        if direct and isinstance(fields[x], Batch) and isinstance(fields[y], Batch):
+            # emissions land in library-owned page-locked storage (pipeline.pinned_empty), which the Batches keep
+            fields[x]._data, fields[y]._data = pinned_empty(ax.shape, ax.dtype), pinned_empty(ay.shape, ay.dtype)
+            ax, ay = fields[x]._data, fields[y]._data
+        done = 0
         try:
             chain.upload(seed)
             for i in progress(range(steps), desc='Generation'):
@@ -99,13 +103,13 @@ class Ensemble:
                     if direct:
                         chain.emit_wait()
                     writer.put(i + 1)
+                done = i + 1
             if direct:
                 chain.emit_wait()
         finally:
             if direct:
                 chain.emit_wait()
-            if pin is not None:
-                pin.release()
+                ax[done:], ay[done:] = 0, 0  # (after a failure: the draws never emitted read as the zeros they were)
             chain.close()
 
     def columns(self, start=0, stop=None):

@@ -143,25 +143,36 @@ class DeviceChain:
         return {x: self.a, y: self.b}
 
 
-class PinnedHost:
-    """Page-locks host arrays for the duration of a run (hipHostRegister), so that emissions into them are DMA
-    copies that overlap the sweeps; arrays the runtime refuses to pin are used as they are (copies still
-    land, without the overlap)."""
+class _PinnedBlock:
+    """Owner of one sv_host_alloc block; freed when the last numpy view of it is gone."""
 
-    def __init__(self, *arrays):
+    def __init__(self, ptr):
+        self.ptr = ptr
         self.lib = _native.lib()
-        self.pinned = []
-        for a in arrays:
-            if a.nbytes and a.flags['C_CONTIGUOUS'] and self.lib.sv_host_register(_native.ptr(a), a.nbytes) == 0:
-                self.pinned.append(a)
 
-    def release(self):
-        for a in self.pinned:
-            self.lib.sv_host_unregister(_native.ptr(a))
-        self.pinned = []
+    def __del__(self):
+        if self.ptr:
+            self.lib.sv_host_free(self.ptr)
+            self.ptr = None
 
-    def __enter__(self):
-        return self
 
-    def __exit__(self, *exc):
-        self.release()
+# below this an emission's copy is short enough that page-locking buys nothing
+PIN_MIN_BYTES = 1 << 20
+
+
+def pinned_empty(shape, dtype):
+    """An uninitialised C-contiguous array in page-locked memory the library owns (sv_host_alloc), so that
+    emissions into it are DMA copies that overlap the sweeps.  The memory is released when the array and every
+    view of it are gone.  Caller arrays are never page-locked in place: numpy storage shares pages with other
+    objects, and an overlapping registration can leave the runtime a stale device mapping for them.  Small arrays,
+    and a runtime that refuses the allocation, get ordinary memory (copies still land, without the overlap)."""
+    dtype = np.dtype(dtype)
+    nbytes = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
+    if nbytes < PIN_MIN_BYTES:
+        return np.empty(shape, dtype)
+    ptr = ctypes.c_void_p()
+    if _native.lib().sv_host_alloc(nbytes, ctypes.byref(ptr)) != 0 or not ptr.value:
+        return np.empty(shape, dtype)
+    raw = (ctypes.c_char * nbytes).from_address(ptr.value)
+    raw._owner = _PinnedBlock(ptr.value)
+    return np.frombuffer(raw, dtype=dtype).reshape(shape)
