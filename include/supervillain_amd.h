@@ -68,7 +68,7 @@ int sv_ctx_kernel_time(sv_ctx *ctx, double *ms_total, int64_t *launches);
  * launch.  Lets tests prove which kernel ran (e.g. the int32 fallback after |n| >= 2^14). */
 int sv_ctx_sweep_counts(sv_ctx *ctx, int64_t *hot, int64_t *fused, int64_t *generic);
 /* Diagnostic: of the hot sweeps since the last call (then reset), those run K at a time by the multi-sweep band
- * launches of small periodic lattices (villain_sweep_hot_band, SV_BAND_K), and the number of such launches. */
+ * launches of small periodic lattices (villain_sweep_hot_band), and the number of such launches. */
 int sv_ctx_band_counts(sv_ctx *ctx, int64_t *sweeps, int64_t *launches);
 /* Diagnostic: the same for the temporal-blocking launches (villain_sweep_block: K sweeps per launch, each workgroup
  * on its own block and deep-halo frame in LDS). */
@@ -78,12 +78,12 @@ int sv_ctx_block_counts(sv_ctx *ctx, int64_t *sweeps, int64_t *launches);
  * drawing each row from the block segment it lies in (the reference draws again, neighborhood.py:105-107). */
 int sv_ctx_split_counts(sv_ctx *ctx, int64_t *sweeps);
 /* Which multi-sweep launches small periodic lattices may use: 0 temporal blocks or else bands (default), 1 blocks
- * only, 2 bands only, 3 one sweep per launch; K: sweeps per temporal-blocking launch (0: the default; an even K runs
- * as K - 1, and K shrinks until the launch's frame fits; one sweep per launch is mode 3).  Returns -1 for another
+ * only, 2 bands only, 3 one sweep per launch; K: sweeps per multi-sweep launch, blocks or bands (0: the default, 3; an
+ * even K runs as K - 1, and K shrinks until the launch's frame fits; one sweep per launch is mode 3).  Returns -1 for another
  * mode or K outside {0, 3..15}. */
 int sv_ctx_set_multisweep(sv_ctx *ctx, int32_t mode, int32_t K);
-/* Diagnostic (tests): the context's PCG64 jump-table cache holds at most `cap` increments (0: the default, 1024 or
- * SV_MAX_TABLES); a full cache drains the device and is dropped.  sv_ctx_table_purges reports how often it was. */
+/* Diagnostic (tests): the context's PCG64 jump-table cache holds at most `cap` increments (0: the default,
+ * 1024); a full cache drains the device and is dropped.  sv_ctx_table_purges reports how often it was. */
 int sv_ctx_set_table_cap(sv_ctx *ctx, int32_t cap);
 int sv_ctx_table_purges(sv_ctx *ctx, int64_t *purges);
 /* Host-only: copy R NumPy PCG64 bit-generator states into (gather) or out of (scatter) sv_rng records, given

@@ -3,10 +3,7 @@
 
 #include "common.h"
 
-static bool alloc_log() {
-    static const bool on = getenv("SV_ALLOC_LOG") != nullptr;
-    return on;
-}
+static bool alloc_log() { return getenv("SV_ALLOC_LOG") != nullptr; }  // (read per call: tests set it in-process)
 
 hipError_t sv_log_malloc(void **p, size_t bytes, const char *site) {
     const hipError_t e = (hipMalloc)(p, bytes);

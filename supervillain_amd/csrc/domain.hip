@@ -551,14 +551,10 @@ int domain_th(const sv_domain *d, int nsx, int *nw8 = nullptr) {
     }();
     auto wgs = [&](int th) { return (int64_t)nsx * ((d->Ht + th - 1) / th); };
     const int64_t rounds = (wgs(52) + slots - 1) / slots;
-    const char *nwe = getenv("SV_HOT_NW");
     // (heights 8k - 3 / 4k + 1: a strip of TH rows takes ceil((TH + 3) / NW) row steps, fused_th; 37 rows of 8 waves
     // take the 5 steps 35 would, 40 took 6)
-    static const int th8 = [] {  // SV_DOMAIN_TH8: the 8-wave strip height (A/B measurements)
-        const char *e = getenv("SV_DOMAIN_TH8");
-        return e && atoi(e) >= 8 ? atoi(e) : 37;
-    }();
-    if (nw8 && !(nwe && atoi(nwe) == 4) && rounds == 1 && wgs(th8) <= slots / 2) {
+    constexpr int th8 = 37;
+    if (nw8 && rounds == 1 && wgs(th8) <= slots / 2) {
         *nw8 = 1;
         return th8;
     }
@@ -590,7 +586,7 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
     const int nsy = (d->Ht + TH - 1) / TH;
     const Affine adv[3] = {host_power(inc, (uint64_t)NWv * d->Nx), host_power(inc, (uint64_t)NWv * d->Nx / 2),
                            host_power(inc, (uint64_t)NWv * d->Nx / 4)};
-    const int hot_nw = nw8 ? 8 : hot_waves(TH);  // villain_sweep_hot with 8 rows per step (domain_th)
+    const int hot_nw = nw8 ? 8 : 4;  // villain_sweep_hot with 8 rows per step (domain_th)
     const Affine adv8[3] = {host_power(inc, 8 * (uint64_t)d->Nx), host_power(inc, 8 * (uint64_t)d->Nx / 2),
                             host_power(inc, 8 * (uint64_t)d->Nx / 4)};
     SkipMap skips;

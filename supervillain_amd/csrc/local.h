@@ -135,13 +135,9 @@ static inline int gcd_i(int64_t a, int64_t b) { return (int)std::gcd(a, b); }
 // Grid for a pass over `count` elements whose lanes advance by the whole grid: the stride is a
 // multiple of `mult` (and of 256) so that per-lane stream positions stay arithmetic.  Lanes take
 // about `iters` (default 2; measured flat from 1 to 16 at L=4096) elements each (one 4-level table jump amortized over them), the grid staying between
-// 2^17 lanes (2 waves per SIMD) and 2^19; SV_GS_ITERS overrides `iters` for experiments.
+// 2^17 lanes (2 waves per SIMD) and 2^19.
 static inline int grid_for(int64_t count, int64_t mult) {
-    static const int64_t iters = [] {
-        const char *e = getenv("SV_GS_ITERS");
-        const int64_t v = e ? atoll(e) : 2;
-        return v >= 1 ? v : 2;
-    }();
+    constexpr int64_t iters = 2;
     const int64_t target = std::min<int64_t>(1 << 19, std::max<int64_t>(1 << 17, count / iters));
     if (count <= target) return (int)std::max<int64_t>(1, (count + 255) / 256);
     const int64_t l = mult / gcd_i(mult, 256) * 256;  // lcm(mult, 256)

@@ -332,11 +332,9 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         // progress word the first launch of chunk j stores) and reads the host-mapped abort flag, so that a NumPy
         // Lemire rejection leaves at most ~2 CH launches queued behind it (each an early exit over every workgroup)
         // instead of the rest of the batch (r3: 220 early-exit launches, 1.1 ms, in a 200-sweep config-5 window)
-        static const int CH_env = [] {  // SV_REP_CHUNK overrides the chunk (0: the whole batch)
-            const char *e = getenv("SV_REP_CHUNK");
-            return e ? atoi(e) : 8;
-        }();
-        const int CH = CH_env > 0 ? CH_env : count;
+        const char *ch_env = getenv("SV_REP_CHUNK");  // overrides the chunk (0: the whole batch)
+        const int CH_set = ch_env ? atoi(ch_env) : 8;
+        const int CH = CH_set > 0 ? CH_set : count;
         *ctx->h_flag = 0;
         __atomic_store_n(ctx->h_prog, 0, __ATOMIC_RELEASE);  // (the previous batch has finished)
         int64_t launches = 0;  // kernel launches enqueued (a split sweep makes two): the timing's per-launch average

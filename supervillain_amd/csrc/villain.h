@@ -226,7 +226,6 @@ int fused_th(int32_t N, int nsx);  // rows per strip (SV_FUSED_TH overrides)
 // launch one tile-mode sweep with `grid` workgroups: villain_sweep_hot when `hot` (the sweep passes hot_ok),
 // villain_sweep_fused<4, true> otherwise
 void launch_fused_tile(const FArgs &A, int grid, hipStream_t stream, bool hot);
-int hot_waves(int TH);  // waves per workgroup of villain_sweep_hot for strips of TH rows (4, or 8)
 // launch villain_sweep_fused<4, false, obs> over a replica batch (grid = replicas * tiles_per_rep)
 void launch_fused_batch(const FArgs &A, int grid, bool obs, hipStream_t stream);
 // villain_hot.hip: whether the fast-draw kernel covers the sweep whose 11 descriptors start at `blocks`,

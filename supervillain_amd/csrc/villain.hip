@@ -626,15 +626,6 @@ void launch_fused_tile(const FArgs &A, int grid, hipStream_t stream, bool hot) {
     else villain_sweep_fused<4, true, false, false><<<grid, 4 * 64, 0, stream>>>(A);
 }
 
-// Waves per workgroup of villain_sweep_hot for strips of TH rows: SV_HOT_NW=8 (experiments) takes 8 when TH allows
-int hot_waves(int TH) {
-    static const int nw = [] {
-        const char *e = getenv("SV_HOT_NW");
-        return e && atoi(e) == 8 ? 8 : 4;
-    }();
-    return nw == 8 && TH % 8 == 0 ? 8 : 4;
-}
-
 
 void launch_fused_batch(const FArgs &A, int grid, bool obs, hipStream_t stream) {
     const bool fr = A.nsx == 1 && A.G.Nx <= RW;  // full-row strips
@@ -809,11 +800,7 @@ int fused_th(int32_t N, int nsx) {
         const int v = atoi(e);
         if (v >= 4) return v;
     }
-    static const int fill = [] {
-        const char *f = getenv("SV_FUSED_FILL");
-        const int v = f ? atoi(f) : 512;
-        return v > 0 ? v : 512;
-    }();
+    constexpr int fill = 512;
     int th = 53;
     while (th > 5 && (int64_t)nsx * ((N + th - 1) / th) < fill) th -= 4;
     return th;
@@ -960,27 +947,20 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
     // prologue rows included (8-row strips took two; L=256: 15.75 us per sweep at 4 rows / 4 waves, r369; 15.2 at
     // 8 rows / 8 waves; 13.5 at 5 rows, r3 -- 4 / 3 / 13 rows: 14.4 / 15.8 / 16.4)
     const bool small8 = !getenv("SV_FUSED_TH") && fused_th(N, nsx) <= 5 && NWv == 4;
-    static const int small_th = [] {  // SV_SMALL_TH: the 8-wave strip height on small lattices (experiments)
-        const char *e = getenv("SV_SMALL_TH");
-        return e && atoi(e) >= 1 ? atoi(e) : 5;
-    }();
-    const int TH = small8 ? small_th : fused_th(N, nsx);
+    const int TH = small8 ? 5 : fused_th(N, nsx);
     const int nsy = (N + TH - 1) / TH;
     const int grid = nsx * nsy;
     // sweeps per host round trip (SV_BATCH overrides): 64 measured best at L=4096; small lattices amortize the ~80 us
     // batch boundary (statistics read back, the next batch's reset and plan upload) over 256 (L=256, r4: 8.4-8.6 vs
     // 9.1-9.7 us per sweep wall, profiles/r04_block_l256_batch.txt)
-    static const int BATCH_env = [] {
-        const char *e = getenv("SV_BATCH");
-        return e && atoi(e) >= 1 ? atoi(e) : 0;
-    }();
-    const int BATCH = BATCH_env ? BATCH_env : (V <= (1 << 18) ? 256 : 64);
+    const char *batch_env = getenv("SV_BATCH");
+    const int BATCH = batch_env && atoi(batch_env) >= 1 ? atoi(batch_env) : (V <= (1 << 18) ? 256 : 64);
     // row-base advance maps for NW rows: NW*N metropolis draws, NW*N/2 ranks, NW*N/4 words
     if ((int64_t)NWv * N % 4) throw std::invalid_argument("fused path needs NW*N divisible by 4");
     const Affine adv[3] = {host_power(inc, (uint64_t)NWv * N), host_power(inc, (uint64_t)NWv * N / 2),
                            host_power(inc, (uint64_t)NWv * N / 4)};
     // villain_sweep_hot with 8 waves per workgroup (8 rows per step) when the strips allow it
-    const int hot_nw = small8 ? 8 : hot_waves(TH);
+    const int hot_nw = small8 ? 8 : 4;
     const Affine adv8[3] = {host_power(inc, 8 * (uint64_t)N), host_power(inc, 8 * (uint64_t)N / 2),
                             host_power(inc, 8 * (uint64_t)N / 4)};
     SkipMap skips;
@@ -1012,37 +992,25 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         }
     }
     // Small lattices: K sweeps per launch, one band of rows per XCD (villain_sweep_hot_band, BandArgs in villain.h).
-    // SV_BAND_K sets K (odd, at most BAND_MAXK; 0 disables); the band's workgroups must all be resident on its XCD.
+    // K (odd, at most BAND_MAXK) is sv_ctx_set_multisweep's, else 3; the band's workgroups must all be resident on its XCD.
     const int nbands = 8;
     int bandK = 0, bandP = 0;
     // Temporal blocking (villain_sweep_block, BlockArgs in villain.h) is preferred where it applies: bs x bs blocks (bs =
-    // N / 16, at least 4; SV_BLOCK_BS overrides) whose frame of K sweeps fits the lattice and the small-offset maps.
-    // sv_ctx_set_multisweep: 0 either (blocks first), 1 blocks only, 2 bands only, 3 neither.  SV_BLOCK_K sets K.
+    // N / 16, at least 4) whose frame of K sweeps fits the lattice and the small-offset maps.
+    // sv_ctx_set_multisweep: 0 either (blocks first), 1 blocks only, 2 bands only, 3 neither, and K (else 3).
     int blockK = 0, blockBS = 0;
     Affine block_step{};
-    static const int mode_env = [] {  // SV_MULTISWEEP: the mode of contexts that set none (experiments)
-        const char *e = getenv("SV_MULTISWEEP");
-        return e ? atoi(e) : 0;
-    }();
-    const int mode = ctx->multisweep ? ctx->multisweep : mode_env;
+    const int mode = ctx->multisweep;
     {
-        static const int bk_env = [] {
-            const char *e = getenv("SV_BLOCK_K");
-            return e ? atoi(e) : -1;
-        }();
-        static const int bs_env = [] {
-            const char *e = getenv("SV_BLOCK_BS");
-            return e ? atoi(e) : 0;
-        }();
         // one sweep's stream length in u64s (the buffered-half flags repeat from sweep to sweep when the bounded
         // words of a sweep are even in number; the launch checks every descriptor anyway)
         uint64_t S = 0, bounded = 0;
         for (const BlockSpec &b : specs) (b.kind == UNIFORM ? S : bounded) += b.count;
-        if ((mode == 0 || mode == 1) && bk_env != 0 && use_hot && hot_params_ok(P) && N % 2 == 0 && N <= 512 &&
+        if ((mode == 0 || mode == 1) && use_hot && hot_params_ok(P) && N % 2 == 0 && N <= 512 &&
             bounded % 2 == 0) {
-            int bs = bs_env > 0 ? bs_env : std::max(4, N / 16);
+            int bs = std::max(4, N / 16);
             while (bs > 2 && N % bs) bs--;
-            int K = std::min(ctx->block_k > 0 ? ctx->block_k : (bk_env > 0 ? bk_env : 3), BAND_MAXK);
+            int K = std::min(ctx->block_k > 0 ? ctx->block_k : 3, BAND_MAXK);
             if (K % 2 == 0) K--;
             if (N % bs == 0) {
                 for (; K >= 3; K -= 2) {
@@ -1058,10 +1026,6 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         }
     }
     {
-        static const int band_env = [] {
-            const char *e = getenv("SV_BAND_K");
-            return e ? atoi(e) : -1;
-        }();
         static const int cus = [] {
             int dev = 0, v = 0;
             if (hipGetDevice(&dev) != hipSuccess ||
@@ -1069,11 +1033,11 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                 v = 0;
             return v;
         }();
-        if (!blockK && (mode == 0 || mode == 2) && use_hot && small8 && hot_nw == 8 && band_env != 0 &&
+        if (!blockK && (mode == 0 || mode == 2) && use_hot && small8 && hot_nw == 8 &&
             !band_broken.load() && N % nbands == 0 && N <= 512) {
             const int own = N / nbands, per_xcd = band_residency() * (cus / nbands);
             // (K = 3 measured best at L=256, r4: 11.8 / 12.7 / 13.7 us per sweep at K = 3 / 5 / 7, 13.7 one per launch)
-            int K = std::min(band_env > 0 ? band_env : 3, BAND_MAXK);
+            int K = std::min(ctx->block_k > 0 ? ctx->block_k : 3, BAND_MAXK);
             if (K % 2 == 0) K--;
             for (; K >= 3; K -= 2) {
                 const int P = nsx * ((own + 5 * (K - 1) + TH - 1) / TH);

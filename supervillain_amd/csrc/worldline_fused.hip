@@ -542,8 +542,6 @@ static int wf_th(int32_t N, int nsx, int nw);
 // per CU, where 8 waves took 6 steps over 40 rows at 2 (L=1024: 43.8 -> 40.1 us per step; 16 waves over 25 / 33 / 57
 // rows: 57.0 / 68.0 / 47.8 us, two rounds or fewer CUs); used when one round of them covers at least 3/4 of the CUs
 static int wf_nw(int32_t Ht, int nsx) {
-    const char *e = getenv("SV_WF_NW");
-    if (e) return atoi(e) == 16 ? 16 : (atoi(e) == 8 ? 8 : 4);
     const int64_t g16 = (int64_t)nsx * ((Ht + 40) / 41);
     if (g16 >= 192 && g16 <= 256) return 16;
     const int th = wf_th(Ht, nsx, 8);
@@ -567,11 +565,7 @@ static int wf_th(int32_t N, int nsx, int nw) {
         while (th < N && (int64_t)nsx * ((N + th - 1) / th) > slots) th += 8;
         return th;
     }
-    static const int fill = [] {
-        const char *f = getenv("SV_WF_FILL");
-        const int v = f ? atoi(f) : 448;
-        return v > 0 ? v : 448;
-    }();
+    constexpr int fill = 448;
     int th = 64;
     while (th > 4 && (int64_t)nsx * ((N + th - 1) / th) < fill) th -= 4;
     return th;
