@@ -61,6 +61,10 @@ struct WFArgs {
     double Winv;  // 1 / W (W a power of two: x * Winv == x / W exactly)
     double c;     // 0.5 / kappa (coexact)
     double df[6], dfk[6];  // plaquette: df = cm - cv / W and df / kappa for index 3 jm + jv
+    // plaquette acceptance table (WF_KP): Sigma = ((f1 + f2) - f3) - f4 = S unit with the integer
+    // S = (m1 + m2 - m3 - m4) << sa + (vl + vu + vr + vd - 4 vc) << sb (unit = min(1, 1 / W)); ptab = 0: no table
+    double unit;
+    int32_t sa, sb, ptab;
     int32_t it;            // coexact: t in -it..-1, 1..it
     uint32_t kt, thrt;     // its choice count 2 it and Lemire threshold
     int32_t general;       // MODE 2 for every strip (wf_body)
@@ -69,9 +73,16 @@ struct WFArgs {
 // Column strip boundaries (uniform: narrower seam strips, whose MODE 1 row steps are ~11% longer, measured level, r4)
 __device__ __forceinline__ int32_t wf_xb(const WFArgs &A, int ix) { return (int32_t)((int64_t)ix * A.G.Wt / A.nsx); }
 
+// The plaquette pass's acceptance min(1, exp(-dS)), dS = dfk ((((f1 + f2) - f3) - f4) + 2 df) (plaquette.py via
+// plaquette_cb_gs), depends on the choice pair and on Sigma = ((f1 + f2) - f3) - f4 only, and Sigma is a small multiple
+// of unit = min(1, 1 / W) held exactly (f = m - dv / W, W a power of two): for |S| <= WF_KP it is read from a table
+// the prologue fills with the same expression (bit-identical), otherwise computed as before
+static constexpr int WF_KP = 63, WF_PT = 2 * WF_KP + 1;
+
 template <int NW>
 struct WFLDS {
     static constexpr int R = WFGeom<NW>::R;
+    double ptab[6 * WF_PT];
     int32_t m0[R][RW];
     int32_t m1[R][RW];
     int32_t v[R][RW];
@@ -149,6 +160,18 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
         Ls.dfk[threadIdx.x] = A.dfk[threadIdx.x];
     }
     if (threadIdx.x == 0) Ls.bad = 0;
+    for (int e = threadIdx.x; e < 6 * WF_PT; e += NW * 64) {
+        const int di = e / WF_PT, s = e % WF_PT - WF_KP;
+        double df = A.df[0], dfk = A.dfk[0];  // (selects: no dynamically indexed kernel argument)
+#pragma unroll
+        for (int k = 1; k < 6; k++) {
+            df = di == k ? A.df[k] : df;
+            dfk = di == k ? A.dfk[k] : dfk;
+        }
+        const double dS = dfk * (((double)s * A.unit) + 2.0 * df);
+        const double pr = sv_exp(-dS);
+        Ls.ptab[e] = pr > 1.0 ? 1.0 : pr;
+    }
     const double Winv = A.Winv, cc = A.c;
     const int32_t it = A.it;
     const uint32_t kt = A.kt, thrt = A.thrt;
@@ -346,15 +369,24 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
             const int32_t vc = s_v[s0][cx];
             // plaquette_cb_gs: f1 (0,q,x), f2 (1,q+1,x), f3 (0,q,x+1), f4 (1,q,x)
             const int32_t m_1 = s_m0[s0][cx], m_2 = s_m1[sp][cx], m_3 = s_m0[s0][cx + 1], m_4 = s_m1[s0][cx];
-            const double f1 = (double)m_1 - wf_dv0(vc, s_v[s0][cx - 1], Winv);
-            const double f2 = (double)m_2 - wf_dv1(s_v[sp][cx], vc, Winv);
-            const double f3 = (double)m_3 - wf_dv0(s_v[s0][cx + 1], vc, Winv);
-            const double f4 = (double)m_4 - wf_dv1(vc, s_v[sm][cx], Winv);
+            const int32_t vl = s_v[s0][cx - 1], vu = s_v[sp][cx], vr = s_v[s0][cx + 1], vd = s_v[sm][cx];
             const int di = 3 * (int)jm + (int)jv;
-            const double df = Ls.df[di], dfk = Ls.dfk[di];
-            const double dS = dfk * ((((f1 + f2) - f3) - f4) + 2.0 * df);
-            double pr = sv_exp(-dS);
-            pr = pr > 1.0 ? 1.0 : pr;
+            // (the int32 image bounds |m|, |v| < 2^30: the pair sums fit int32, the rest is 64-bit)
+            const int64_t S = (((int64_t)(m_1 + m_2) - (int64_t)(m_3 + m_4)) << A.sa) +
+                              (((int64_t)(vl + vu) + (int64_t)(vr + vd) - 4 * (int64_t)vc) << A.sb);
+            double pr;
+            if (A.ptab && (uint64_t)(S + WF_KP) < (uint64_t)WF_PT) {
+                pr = Ls.ptab[di * WF_PT + (int)S + WF_KP];
+            } else {
+                const double f1 = (double)m_1 - wf_dv0(vc, vl, Winv);
+                const double f2 = (double)m_2 - wf_dv1(vu, vc, Winv);
+                const double f3 = (double)m_3 - wf_dv0(vr, vc, Winv);
+                const double f4 = (double)m_4 - wf_dv1(vc, vd, Winv);
+                const double df = Ls.df[di], dfk = Ls.dfk[di];
+                const double dS = dfk * ((((f1 + f2) - f3) - f4) + 2.0 * df);
+                pr = sv_exp(-dS);
+                pr = pr > 1.0 ? 1.0 : pr;
+            }
             const bool acc = u < pr;
             if (q >= t0 && q < t1 && x >= x0 && x < x1) {
                 pacc += acc;
@@ -623,6 +655,15 @@ void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
             A.df[3 * jm + jv] = df;
             A.dfk[3 * jm + jv] = df / kappa;
         }
+    {
+        int ex = 0;
+        std::frexp(W_eff, &ex);  // W_eff = 2^(ex - 1)
+        const int lw = ex - 1;
+        A.sa = lw > 0 ? lw : 0;
+        A.sb = lw < 0 ? -lw : 0;
+        A.unit = lw > 0 ? A.Winv : 1.0;
+        A.ptab = lw >= -20 && lw <= 20;  // (shifts that keep S exact in 64 bits)
+    }
     A.it = (int32_t)it;
     A.kt = (uint32_t)(2 * it);
     A.thrt = (uint32_t)((0u - A.kt) % A.kt);
