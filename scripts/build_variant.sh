@@ -1,6 +1,6 @@
 #!/bin/bash
 # build a libsvhip.so variant with extra compile definitions (timing experiments):
-#   bash scripts/build_variant.sh NAME -DSV_K3=0 ...   ->  supervillain_amd/variants/libsvhip_NAME.so
+#   bash scripts/build_variant.sh NAME -DSV_WGTIME=1 ...   ->  supervillain_amd/variants/libsvhip_NAME.so
 set -e
 name=$1; shift
 cd $(dirname $0)/../supervillain_amd/csrc

@@ -111,24 +111,15 @@ __device__ __forceinline__ int32_t wrapN(int32_t v, int32_t N) {
     return v;
 }
 
-#ifndef SV_SKIP_FULLJUMP
-#define SV_SKIP_FULLJUMP 0
-#endif
-#ifndef SV_SCALAR_WAVE
-#define SV_SCALAR_WAVE 1
-#endif
 #ifndef SV_ABLATE
 #define SV_ABLATE 0  // timing experiments only: 1 = no exp, 2 = no RNG compositions, 4 = no wrapped-column jumps,
                      // 8 = no HBM stores, 16 = no HBM loads, 32 = no barriers, 64 = no choice draws,
                      // 256 / 512 = n kept in HBM as int32 / int16 (villain_sweep_hot; valid from a cold start only)
 #endif
-#ifndef SV_EXP_OCML
-#define SV_EXP_OCML 1
-#endif
 // d = a*b + c as the three-address v_fma_f64: the compiler writes ocml's Horner chain as v_fmac_f64 on a copy of
 // each hoisted coefficient (one v_mov_b64 per step); written out, the coefficients are read in place
 #ifndef SV_EXP_SCOEF
-#define SV_EXP_SCOEF 0  // coefficients as SGPR operands: 257 vs 253 us (r303), not kept
+#define SV_EXP_SCOEF 0  // coefficients as SGPR operands: villain_hot.hip sets it (18 VGPRs fewer at 4 waves per SIMD)
 #endif
 __device__ __forceinline__ double fma3(double a, double b, double c) {
     double d;
@@ -176,10 +167,8 @@ __device__ __forceinline__ double exp_ocml(double x) {
 __device__ __forceinline__ double sv_exp(double x) {
 #if SV_ABLATE & 1
     return 1.0 + x * 0.5;
-#elif SV_EXP_OCML
-    return exp_ocml(x);
 #else
-    return exp(x);
+    return exp_ocml(x);
 #endif
 }
 __device__ __forceinline__ u128 sv_apply(const Affine &f, u128 s) {
@@ -236,11 +225,7 @@ __device__ __forceinline__ u128 full_jump(const JumpTables *T, const Block *blk,
 // The same with the level tables' entries loaded together (digit 0's entry is the identity map): one memory round
 // trip instead of up to JUMP_LEVELS dependent ones, for the compositions with the identity maps of zero digits and 32
 // more live registers -- for the kernels' prologues (row bases), not their loops
-#ifndef SV_FLAT_JUMP
-#define SV_FLAT_JUMP 1
-#endif
 __device__ __forceinline__ u128 full_jump_flat(const JumpTables *T, const Block *blk, uint32_t pos) {
-#if SV_FLAT_JUMP
     Affine m[JUMP_LEVELS];
 #pragma unroll
     for (int l = 0; l < JUMP_LEVELS; l++) m[l] = T->level[l][(pos >> (l * JUMP_DIGIT_BITS)) & (JUMP_DIGITS - 1)];
@@ -249,9 +234,6 @@ __device__ __forceinline__ u128 full_jump_flat(const JumpTables *T, const Block 
     for (int l = 0; l < JUMP_LEVELS; l++) r = apply(m[l], r);
     __builtin_amdgcn_s_waitcnt(0);
     return r;
-#else
-    return full_jump(T, blk, pos);
-#endif
 }
 
 __device__ __forceinline__ u128 from_base(const JumpTables *T, const Block *blk, const SmallTab &sm, u128 base,
@@ -274,29 +256,17 @@ struct Rep {
     uint32_t id;
 };
 
-template <bool K3 = false>
 __device__ __forceinline__ int32_t choice_value(const FArgs &A, const Rep &RP, uint32_t word, uint32_t bidx,
                                                 uint32_t spos) {
-    if constexpr (K3) {
-        // choice((-1, 0, 1)) (interval_n = 1): 3x by one shift-add, Lemire threshold (2^32 - 3) % 3 = 1 (a
-        // rejection iff the low word is 0), the value a select instead of W * (idx - 1)
-        const uint64_t m = ((uint64_t)word << 1) + word;
-        if ((uint32_t)m == 0u) report(A.S, A.sweep, bidx, spos, RP.id);
-        const uint32_t idx = (uint32_t)(m >> 32);
-        const int32_t w = (int32_t)A.P.W;
-        return idx == 0 ? -w : (idx == 1 ? 0 : w);
-    } else {
-        bool rej;
-        const uint32_t idx = lemire(word, A.P.k, A.P.thr, &rej);
-        if (rej) report(A.S, A.sweep, bidx, spos, RP.id);
-        return (int32_t)A.P.W * ((int32_t)idx - (int32_t)A.P.interval_n);
-    }
+    bool rej;
+    const uint32_t idx = lemire(word, A.P.k, A.P.thr, &rej);
+    if (rej) report(A.S, A.sweep, bidx, spos, RP.id);
+    return (int32_t)A.P.W * ((int32_t)idx - (int32_t)A.P.interval_n);
 }
 
 // General draws: any strip (wrapped columns), skips, mismatched buffers.  6 compositions per site.
 // Columns of an edge strip that wrap around the lattice (global columns outside [xb, xb + RW)) draw
 // from the wave's second set of row bases `wb`, kept at global column xw, so no lane needs a full jump.
-template <bool K3 = false>
 __device__ __forceinline__ Draws draws_general(const FArgs &A, const Rep &RP, int c, bool active, int64_t gq, int64_t gx,
                                                int64_t xb, const u128 *bases, const SmallTab &sm, bool edge,
                                                int64_t xw, const u128 *wb) {
@@ -319,13 +289,6 @@ __device__ __forceinline__ Draws draws_general(const FArgs &A, const Rep &RP, in
         for (int q = 0; q < 4; q++) {
             const Block *B = &RP.blocks[bb + 1 + q];
             uint32_t word, spos = (uint32_t)rank;
-#if SV_SKIP_FULLJUMP  // (timing experiments: the round-2 form, a full table jump per draw of a block with skips)
-            if (B->nskip) {
-                spos = skip_pos(*B, A.skips, (uint32_t)rank);
-                word = bounded_word(T, *B, spos);
-                __builtin_amdgcn_s_waitcnt(0);
-            } else
-#endif
             {
                 // known rejected positions push this draw's stream position forward (skip_pos); the row base sits
                 // at the unshifted position of column xr, so the shifted word is still a small offset ahead of it
@@ -337,7 +300,7 @@ __device__ __forceinline__ Draws draws_general(const FArgs &A, const Rep &RP, in
                 word = (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
                 if (qq < 0) word = B->buf;  // has && rank == 0: the buffered half-word
             }
-            D.cn[q] = choice_value<K3>(A, RP, word, (uint32_t)(bb + 1 + q), spos);
+            D.cn[q] = choice_value(A, RP, word, (uint32_t)(bb + 1 + q), spos);
         }
     }
     return D;
@@ -347,19 +310,11 @@ __device__ __forceinline__ Draws draws_general(const FArgs &A, const Rep &RP, in
 // (half = 0), wrapping around the wave.  DPP wave rotates are one VALU move each (on gfx950 wave_ror:1 reads lane
 // i - 1 and wave_rol:1 lane i + 1, scripts/perf/dpp_check.hip) where ds_bpermute is an LDS round trip the draw
 // waits on.  All 64 lanes execute the draws (inactive sites only discard their results).
-#ifndef SV_DPP_PAIR
-#define SV_DPP_PAIR 1
-#endif
 __device__ __forceinline__ uint32_t pair_exchange(uint32_t send, uint32_t half, int lane) {
-#if SV_DPP_PAIR
     (void)lane;
     const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, 0x13C /* wave_ror:1 */, 0xF, 0xF, false);
     const uint32_t next = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, 0x134 /* wave_rol:1 */, 0xF, 0xF, false);
     return half ? prev : next;
-#else
-    const int partner = half ? ((lane - 1) & 63) : lane + 1;
-    return (uint32_t)__builtin_amdgcn_ds_bpermute(partner << 2, (int)send);
-#endif
 }
 
 // Fast draws for interior strips (no wrapped columns, no skips, equal buffers within each
@@ -421,31 +376,6 @@ __device__ __forceinline__ uint32_t fast_pack_g(const uint32_t *h4, int32_t lane
     return pk;
 }
 
-// The row bases are the same for every lane of a wave (one row per wave): held in SGPRs they feed the
-// 128-bit multiplies as scalar operands instead of occupying VGPRs.
-#ifndef SV_K3
-#define SV_K3 0  // choice((-1, 0, 1)) specialised at compile time: measured slower (329.5 vs 320.5 us, r92)
-#endif
-#ifndef SV_FR_FAST
-#define SV_FR_FAST 1
-#endif
-#ifndef SV_SCALAR_BASES
-#define SV_SCALAR_BASES 0  // measured slower: 339 vs 320 us per L=4096 sweep (SGPR spills, readfirstlane chains)
-#endif
-__device__ __forceinline__ u128 wave_uniform(u128 v) {
-#if SV_SCALAR_BASES
-    auto rf = [](uint64_t x) {
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
-        return ((uint64_t)hi << 32) | lo;
-    };
-    return u128{rf(v.lo), rf(v.hi)};
-#else
-    return v;
-#endif
-}
-
-template <bool K3 = false>
 __device__ __forceinline__ Draws draws_fastp(const FArgs &A, const Rep &RP, int c, bool active, int32_t lane,
                                              uint32_t pk, uint32_t rank, const u128 *bases, const SmallTab &sm) {
     const int bb = 1 + 5 * c;
@@ -471,15 +401,14 @@ __device__ __forceinline__ Draws draws_fastp(const FArgs &A, const Rep &RP, int 
             const uint32_t wf = half ? got : (uint32_t)X;
             const uint32_t wb = half ? (uint32_t)(X >> 32) : got;
             if (active) {
-                D.cn[2 * mu] = choice_value<K3>(A, RP, wf, (uint32_t)(bb + 1 + 2 * mu), rank);
-                D.cn[2 * mu + 1] = choice_value<K3>(A, RP, wb, (uint32_t)(bb + 2 + 2 * mu), rank);
+                D.cn[2 * mu] = choice_value(A, RP, wf, (uint32_t)(bb + 1 + 2 * mu), rank);
+                D.cn[2 * mu + 1] = choice_value(A, RP, wb, (uint32_t)(bb + 2 + 2 * mu), rank);
             }
         }
     }
     return D;
 }
 
-template <bool K3 = false>
 __device__ __forceinline__ Draws draws_fast(const FArgs &A, const Rep &RP, int c, const uint32_t *hasw, bool active,
                                             int32_t lane, uint32_t rowlin,
                                             uint32_t xs, uint32_t gx, uint32_t xb, const u128 *bases,
@@ -516,8 +445,8 @@ __device__ __forceinline__ Draws draws_fast(const FArgs &A, const Rep &RP, int c
             const uint32_t wf = half ? got : (uint32_t)X;
             const uint32_t wb = half ? (uint32_t)(X >> 32) : got;
             if (active) {
-                D.cn[2 * mu] = choice_value<K3>(A, RP, wf, (uint32_t)(bb + 1 + 2 * mu), rank);
-                D.cn[2 * mu + 1] = choice_value<K3>(A, RP, wb, (uint32_t)(bb + 2 + 2 * mu), rank);
+                D.cn[2 * mu] = choice_value(A, RP, wf, (uint32_t)(bb + 1 + 2 * mu), rank);
+                D.cn[2 * mu + 1] = choice_value(A, RP, wb, (uint32_t)(bb + 2 + 2 * mu), rank);
             }
         }
     }
@@ -580,22 +509,10 @@ __device__ __forceinline__ u128 hot_apply(const SmallTab &sm, uint32_t i, u128 b
 
 // NumPy random(): (x >> 11) * 2^-53, exactly: with m = x >> 11 = h 2^32 + l (h < 2^21),
 // m 2^-53 = h 2^-21 + l 2^-53; l 2^-53 is exact, and the fma's sum is m 2^-53 (53 significant bits)
-#ifndef SV_HOT_U53
-#define SV_HOT_U53 2  // 2: one 64-bit shift and an exact fma (r4, with villain_hot.hip's switches); 1: alignbit form
-#endif
-#ifndef SV_HOT_MUL24
-#define SV_HOT_MUL24 0
-#endif
 __device__ __forceinline__ double u53(uint64_t x) {
-    if (SV_HOT_U53 == 2) {
-        // one 64-bit shift gives both halves of m = x >> 11 (h < 2^21, l < 2^32); h 2^-21 + l 2^-53 is exact
-        const uint64_t m = x >> 11;
-        return __builtin_fma((double)(uint32_t)(m >> 32), 0x1p-21, (double)(uint32_t)m * 0x1p-53);
-    }
-    if (!SV_HOT_U53) return to_double(x);
-    const uint32_t h = (uint32_t)(x >> 43);
-    const uint32_t l = __builtin_amdgcn_alignbit((uint32_t)(x >> 32), (uint32_t)x, 11);
-    return __builtin_fma((double)h, 0x1p-21, (double)l * 0x1p-53);
+    // one 64-bit shift gives both halves of m = x >> 11 (h < 2^21, l < 2^32); h 2^-21 + l 2^-53 is exact
+    const uint64_t m = x >> 11;
+    return __builtin_fma((double)(uint32_t)(m >> 32), 0x1p-21, (double)(uint32_t)m * 0x1p-53);
 }
 
 

@@ -13,12 +13,6 @@
 #define SV_HD __host__ __device__ __forceinline__
 #endif
 
-#ifndef SV_XSL_ALIGNBIT
-#define SV_XSL_ALIGNBIT 1  // L=4096 sweep 320.9 -> 320.1 us (r91)
-#endif
-#ifndef SV_MAD128
-#define SV_MAD128 1  // L=4096 sweep 322.4 -> 321.0 us (r90, 2 repetitions)
-#endif
 
 namespace sv {
 
@@ -54,7 +48,7 @@ struct Affine {
     u128 A, C;
 };
 
-#if defined(__HIP_DEVICE_COMPILE__) && SV_MAD128
+#if defined(__HIP_DEVICE_COMPILE__)
 // low 128 bits of a*s + c by operand scanning on 32-bit limbs: 6 v_mad_u64_u32 + 4 v_mul_lo_u32 (the
 // generic form compiles to 12 multiplies), the addend folded into the partial sums
 __device__ __forceinline__ u128 mad128(u128 a, u128 s, u128 c) {
@@ -92,7 +86,7 @@ SV_HD Affine compose(const Affine &f, const Affine &g) {
 }
 
 SV_HD uint64_t xsl_rr(u128 s) {
-#if defined(__HIP_DEVICE_COMPILE__) && SV_XSL_ALIGNBIT
+#if defined(__HIP_DEVICE_COMPILE__)
     // rotate right by 32 as a half swap, then the rest with two 32-bit funnel shifts
     const uint64_t x = s.hi ^ s.lo;
     const uint32_t rot = (uint32_t)(s.hi >> 58);

@@ -31,10 +31,7 @@ struct PlanIn {
     uint32_t has, buf;
 };
 
-#ifndef SV_REP_BATCH
-#define SV_REP_BATCH 64
-#endif
-static constexpr int REP_BATCH = SV_REP_BATCH;
+static constexpr int REP_BATCH = 64;  // sweeps per batch (r4 A/B, profiles/r04_repbatch_ab.txt)
 static constexpr int NB = 11;  // blocks per sweep (even N: 2 colours)
 
 // u64 offset of block b inside a sweep (h = V/4 words per choice block)

@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256) void villain_pass_generic(VParams P, double *p
 
 // FR (full rows, periodic lattices of Nx <= 128): one strip spans the whole row, its LDS columns ARE
 // the lattice columns and neighbours wrap inside LDS -- no column halo, every lane busy at N = 128.
-template <int NW, bool TILE, bool REPS, bool OBS, bool FR, bool K3 = false>
+template <int NW, bool TILE, bool REPS, bool OBS, bool FR>
 __device__ __forceinline__ void sweep_body(const FArgs &A) {
     static_assert(!(FR && TILE), "full-row strips are for periodic lattices");
     constexpr int R = FusedGeom<NW>::R;
@@ -150,11 +150,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     const FGeom &Gm = A.G;
     const int32_t Nt = Gm.Nt, Nx = Gm.Nx;
     // the wave index is uniform: keep it (and all row / ring-slot arithmetic derived from it) scalar
-#if SV_SCALAR_WAVE
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
-#else
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#endif
     const int64_t V = Gm.plane;
     // global row of local row q; memory offset of local row q / local column c
     auto grow = [&](int32_t q) { return wrapN(Gm.T0 + q, Nt); };
@@ -231,7 +227,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
         // full-row strips (replica batches of N <= 128): every lane is busy, so the lane pairs that share a
         // choice word must not straddle the row -- true when the fwd/bwd blocks start on a whole word
         // (has == 0), which is the norm (each block draws an even V/2 half-words)
-        fastfr[c] = FR && SV_FR_FAST && B[0].nskip == 0 && B[1].nskip == 0 && B[2].nskip == 0 && B[3].nskip == 0 &&
+        fastfr[c] = FR && B[0].nskip == 0 && B[1].nskip == 0 && B[2].nskip == 0 && B[3].nskip == 0 &&
                     B[0].has == 0 && B[1].has == 0 && B[2].has == 0 && B[3].has == 0;
     }
 
@@ -382,16 +378,16 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             const bool active = row_ok && (FR ? x < w : x <= x1 + 1);
             u128 bs[6];
 #pragma unroll
-            for (int k = 0; k < 6; k++) bs[k] = wave_uniform(s_base[wave][k]);
+            for (int k = 0; k < 6; k++) bs[k] = s_base[wave][k];
             Draws D;
             if (fast[0])
-                D = draws_fastp<K3>(A, RL, 0, active, lane, pk0, ((uint32_t)gq * (uint32_t)Nx + (uint32_t)(X0s + x)) >> 1,
+                D = draws_fastp(A, RL, 0, active, lane, pk0, ((uint32_t)gq * (uint32_t)Nx + (uint32_t)(X0s + x)) >> 1,
                                 bs, s_small);
             else if (fastfr[0])
-                D = draws_fast<K3>(A, RL, 0, has_c0, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)xs, (uint32_t)x, 0u,
+                D = draws_fast(A, RL, 0, has_c0, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)xs, (uint32_t)x, 0u,
                                bs, s_small);
             else
-                D = draws_general<K3>(A, RL, 0, active, gq, wrapN(X0s + x, Nx), xb, bs, s_small, edge, xw,
+                D = draws_general(A, RL, 0, active, gq, wrapN(X0s + x, Nx), xb, bs, s_small, edge, xw,
                                   &s_base[wave][16]);
             if (active) {
                 const int lr = q - rbase;
@@ -457,16 +453,16 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
             const bool active = row_ok && (FR ? x < w : x <= x1);
             u128 bs[6];
 #pragma unroll
-            for (int k = 0; k < 6; k++) bs[k] = wave_uniform(s_base[wave][8 + k]);
+            for (int k = 0; k < 6; k++) bs[k] = s_base[wave][8 + k];
             Draws D;
             if (fast[1])
-                D = draws_fastp<K3>(A, RL, 1, active, lane, pk1, ((uint32_t)gq * (uint32_t)Nx + (uint32_t)(X0s + x)) >> 1,
+                D = draws_fastp(A, RL, 1, active, lane, pk1, ((uint32_t)gq * (uint32_t)Nx + (uint32_t)(X0s + x)) >> 1,
                                 bs, s_small);
             else if (fastfr[1])
-                D = draws_fast<K3>(A, RL, 1, has_c1, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)xs, (uint32_t)x, 0u,
+                D = draws_fast(A, RL, 1, has_c1, active, lane, (uint32_t)gq * (uint32_t)Nx, (uint32_t)xs, (uint32_t)x, 0u,
                                bs, s_small);
             else
-                D = draws_general<K3>(A, RL, 1, active, gq, wrapN(X0s + x, Nx), xb, bs, s_small, edge, xw,
+                D = draws_general(A, RL, 1, active, gq, wrapN(X0s + x, Nx), xb, bs, s_small, edge, xw,
                                   &s_base[wave][24]);
             if (active) {
                 const int lr = q - rbase;
@@ -540,9 +536,9 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
 }
 
 // 3 waves / SIMD (12 per CU, what the LDS ring allows): caps the kernel at 168 VGPRs
-template <int NW, bool TILE, bool REPS, bool FR, bool K3 = false>
+template <int NW, bool TILE, bool REPS, bool FR>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(3))) void villain_sweep_fused(FArgs A) {
-    sweep_body<NW, TILE, REPS, false, FR, K3>(A);
+    sweep_body<NW, TILE, REPS, false, FR>(A);
 }
 // replica batch with the inline observables fused into the row stores: held to 3 waves / SIMD
 template <bool FR>

@@ -30,12 +30,6 @@ __device__ uint64_t g_blktime[4096 * BLT];
 #define BLK_T(i) do { } while (0)
 #endif
 
-#ifndef SV_BLK_DRAW1
-#define SV_BLK_DRAW1 1  // the colour-1 draws made in the colour-0 pass (one round of lanes per colour)
-#endif
-#ifndef SV_BLK_FLATJUMP
-#define SV_BLK_FLATJUMP 1
-#endif
 // hot_draws_edge (fused.h) in 32-bit positions (N <= 512: every rank < 2^17): the frame's columns at or after xb draw
 // from the row's set A, its wrapped columns (gx < xb) from set B at column 0; words unpaired, equal buffered-half flags
 // within each fwd/bwd pair (hot_ok)
@@ -158,7 +152,7 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
         const uint32_t has = ty >= 2 ? A.blocks[blk].has : 0u;
         const uint32_t pos = (uint32_t)base_pos(ty, wrapN(FR0 + i, N), N, s ? 0 : xb, has);
         s_base[(i * 2 + s) * 12 + slot] =
-            SV_BLK_FLATJUMP ? full_jump_flat(A.T, &A.blocks[blk], pos) : full_jump(A.T, &A.blocks[blk], pos);
+            full_jump_flat(A.T, &A.blocks[blk], pos);
     }
     frame_store(threadIdx.x);
     for (int i0 = threadIdx.x + FU * NT; i0 < F * F; i0 += FU * NT) {  // (frames beyond FU sites per thread)
@@ -314,7 +308,8 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
         const std::integral_constant<int, 0> C0{};
         const std::integral_constant<int, 1> C1{};
         // (8-wave workgroups only: the 16-wave form must stay within 128 VGPRs)
-        if (SV_BLK_DRAW1 && NWT == 8 && nrows[0] * spr[0] <= NT && nrows[1] * spr[1] <= NT) {
+        // (the colour-1 draws made in the colour-0 pass: one round of lanes per colour)
+        if (NWT == 8 && nrows[0] * spr[0] <= NT && nrows[1] * spr[1] <= NT) {
             // one round of lanes per colour: the colour-1 draws (independent of the state) are made in the colour-0
             // pass, beside its site-update, and held in registers across the barrier
             int32_t q1, x1;

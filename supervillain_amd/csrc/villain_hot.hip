@@ -19,36 +19,18 @@
 // Exactness: every value that reaches phi or n is computed in the reference's operation order.
 // The residual r and dS reach nothing but exp(-dS); the `0.0 +` the reference's d() and face_sum() put in
 // front of them changes at most the sign of a zero, and exp(+-0) = 1.
-#ifndef SV_HOT_OCC4
-#define SV_HOT_OCC4 1  // 4 waves per SIMD: LDS <= 40 KB (6-row residual ring, int16 n image), <= 128 VGPRs
-#endif
-#if SV_HOT_OCC4 && !defined(SV_EXP_SCOEF)
+// 4 waves per SIMD: LDS <= 40 KB (6-row residual ring, int16 n image), <= 128 VGPRs
+#ifndef SV_EXP_SCOEF
 #define SV_EXP_SCOEF 1  // exp coefficients as SGPR operands (18 VGPRs fewer)
 #endif
 #include "fused.h"
 #include "philox.h"
 
-#ifndef SV_HOT_OFF32
-#define SV_HOT_OFF32 1  // row loads / stores by 32-bit byte offsets from the SGPR bases
-#endif
-#ifndef SV_HOT_ADV
-#define SV_HOT_ADV 1  // row bases advanced by the precomputed maps behind a wave-uniform test (r3xx A/B)
-#endif
-#ifndef SV_HOT_PH_OCC
-#define SV_HOT_PH_OCC 4  // the counter-based kernel (29.5 KB of LDS, 81 VGPRs): 4, 5 and 6 waves/SIMD measured flat (r336)
-#endif
-
-// r4 A/B (L=4096, two interleaved repetitions on one box, kernel us per sweep): base 221.8 / 225.3, the four
-// switches below together 218.7 / 221.2 (each alone within the noise); bit-exact (Villain, overflow, worldline suites)
-#ifndef SV_HOT_PF_EARLY
-#define SV_HOT_PF_EARLY 1  // the next row step's row loads issued right after the commit, before the step's barrier
-#endif
-#ifndef SV_HOT_I16
-#define SV_HOT_I16 1  // n read from LDS with sign-extending loads (the value made opaque after the load)
-#endif
-#ifndef SV_HOT_BSEL
-#define SV_HOT_BSEL 1  // paired words: each lane reads the base set it draws from (per-lane LDS address), no selects
-#endif
+// Measured and kept (r3-r4 A/Bs): row loads / stores by 32-bit byte offsets from the SGPR bases; row bases
+// advanced by precomputed maps behind a wave-uniform test; the next row step's loads issued right after the commit,
+// before the step's barrier; n read from LDS with sign-extending loads; each lane of a paired draw reading the one base
+// it composes with (r4: the last three with u53's one-shift form 221.8 / 225.3 -> 218.7 / 221.2 us per L=4096 sweep).
+// The counter-based kernel (29.5 KB of LDS, 81 VGPRs) runs at 4 waves per SIMD: 4, 5 and 6 measured flat (r336).
 
 #ifndef SV_WGTIME
 #define SV_WGTIME 0  // timing experiments: per-workgroup timestamps (sv_debug_wgtime)
@@ -67,28 +49,9 @@ __device__ uint64_t g_bandtime[8 * 128 * BT_SW * BT];
 __device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 #endif
 
-// Interior strips: the fwd/bwd blocks of a direction read the two halves of one u64 for two adjacent lanes
-// (draws_fastp in fused.h explains the packing of pk)
-__device__ __forceinline__ HotDraws hot_draws_paired(const FArgs &A, int32_t lane, uint32_t pk, const u128 *bs,
-                                                     const SmallTab &sm) {
-    HotDraws D;
-    D.u = u53(xsl_rr(hot_apply(sm, pk & (SMALL_LDS - 1), bs[0])));
-    D.dphi = A.P.lo_phi + A.P.range_phi * u53(xsl_rr(hot_apply(sm, (pk >> 7) & (SMALL_LDS - 1), bs[1])));
-#pragma unroll
-    for (int mu = 0; mu < 2; mu++) {
-        const uint32_t half = (pk >> (28 + mu)) & 1u;
-        const uint64_t X = xsl_rr(hot_apply(sm, (pk >> (14 + 7 * mu)) & (SMALL_LDS - 1), half ? bs[3 + 2 * mu] : bs[2 + 2 * mu]));
-        // lo lanes computed the fwd word (send its high half), hi lanes the bwd word (send its low half)
-        const uint32_t send = half ? (uint32_t)X : (uint32_t)(X >> 32);
-        const uint32_t got = pair_exchange(send, half, lane);
-        D.w[2 * mu] = half ? got : (uint32_t)X;
-        D.w[2 * mu + 1] = half ? (uint32_t)(X >> 32) : got;
-    }
-    return D;
-}
-
-// The same, each lane reading the one word base of each direction it composes with (bw: the wave's colour set in
-// LDS): a per-lane LDS address instead of two broadcast reads and four selects per direction (SV_HOT_BSEL)
+// Interior strips: the fwd/bwd blocks of a direction read the two halves of one u64 for two adjacent lanes (draws_fastp
+// in fused.h explains the packing of pk); each lane reads the one word base of each direction it composes with (bw:
+// the wave's colour set in LDS), a per-lane LDS address instead of two broadcast reads and four selects per direction
 __device__ __forceinline__ HotDraws hot_draws_paired_sel(const FArgs &A, int32_t lane, uint32_t pk, const u128 *bw,
                                                          const SmallTab &sm) {
     HotDraws D;
@@ -169,8 +132,8 @@ struct HotLDST {
     static constexpr int R = FusedGeom<NWL>::R;
     // the residuals r live from the colour-0 pass of step t (rows t+1..t+5) to the colour-1 pass of step t+4
     // (which reads row t+4 again): NW + 2 rows
-    static constexpr int RR = SV_HOT_OCC4 ? NWL + 2 : R;
-    using nint = std::conditional_t<SV_HOT_OCC4, int16_t, int32_t>;  // hot_ok / commit bound |n|
+    static constexpr int RR = NWL + 2;
+    using nint = int16_t;  // hot_ok / commit bound |n|
     double phi[R][RW];
     double r0[RR][RW];
     double r1[RR][RW];
@@ -256,7 +219,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     constexpr int R = HotLDST<PH, FR && OBS, NWT>::R, RR = HotLDST<PH, FR && OBS, NWT>::RR;
     // rows move by 32-bit byte offsets from the uniform bases: the hosts keep every offset below 2^32 on this kernel
     // (run_fused: 16 V < 2^32; domain tiles: 16 plane < 2^32; replica batches address within one replica of N <= 128)
-    constexpr bool OFF32 = SV_HOT_OFF32 && !PH && !(SV_ABLATE & (16 | 256 | 512 | 8));
+    constexpr bool OFF32 = !PH && !(SV_ABLATE & (16 | 256 | 512 | 8));
     constexpr int PF = RW / 64;
     auto &s_phi = Ls.phi;
     auto &s_r0 = Ls.r0;
@@ -465,7 +428,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
                     s_phi[slot][cc] = pf_phi[k] + 0.0;
                     const int32_t a = (int32_t)pf_n0[k], c = (int32_t)pf_n1[k];
                     // the int32 image must hold n exactly, with headroom for one sweep's changes
-                    constexpr int NB = SV_HOT_OCC4 ? 14 : 30;  // |n| < 2^NB, headroom for one sweep's 2|W| <= 2^13
+                    constexpr int NB = 14;  // |n| < 2^NB, headroom for one sweep's 2|W| <= 2^13
                     bad |= (uint32_t)((uint64_t)((pf_n0[k] >> NB) + 1) > 1) | (uint32_t)((uint64_t)((pf_n1[k] >> NB) + 1) > 1);
                     s_n0[slot][cc] = a;
                     s_n1[slot][cc] = c;
@@ -641,13 +604,8 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
             else
                 D = hot_draws_edge<false, true>(A, gq, wrapN(X0s + x, Nx), xb, two_sets ? xw : xb, &s_base[wave][8 * c],
                                                 &s_base[wave][(two_sets ? 16 : 0) + 8 * c], s_small, has4[c], buf_c[c]);
-        } else if constexpr (!edge && SV_HOT_BSEL) {
-            D = hot_draws_paired_sel(A, lane, c == 0 ? pk0 : pk1, &s_base[wave][8 * c], s_small);
         } else if constexpr (!edge) {
-            u128 bs[6];
-#pragma unroll
-            for (int k = 0; k < 6; k++) bs[k] = s_base[wave][8 * c + k];
-            D = hot_draws_paired(A, lane, c == 0 ? pk0 : pk1, bs, s_small);
+            D = hot_draws_paired_sel(A, lane, c == 0 ? pk0 : pk1, &s_base[wave][8 * c], s_small);
         } else {
             const uint32_t(*skl)[HOT_MAXSK] = nullptr;
             if constexpr (SKIP) skl = Ls.sk[c];
@@ -661,7 +619,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
             const uint64_t m = (uint64_t)D.w[j] * kc;
             rej |= (uint32_t)m < thr;
             // W * (index - interval_n), neighborhood.py:105-107: one v_mad_i32_i24 (hot_ok bounds |W|, k < 2^20)
-            cn[j] = SV_HOT_MUL24 ? __mul24((int32_t)(m >> 32), Wn) - nW : (int32_t)(m >> 32) * Wn - nW;
+            cn[j] = (int32_t)(m >> 32) * Wn - nW;
         }
         if (__builtin_expect(rej && active && !(SV_ABLATE & 2), 0)) {
             const uint32_t rank = (uint32_t)(((int64_t)gq * Nx + wrapN(X0s + x, Nx)) >> 1);
@@ -689,12 +647,11 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
 #endif
 
     const double hk = P.half_kappa;
-    if (SV_HOT_PF_EARLY) prefetch(tfirst + 3 + NW);
+    prefetch(tfirst + 3 + NW);
     for (int32_t t = tfirst; t < t1; t += NW) {
         if constexpr (POLL) {
             if (Ls.stop) return;
         }
-        if (!SV_HOT_PF_EARLY) prefetch(t + 3 + NW);
         store_rows(t - NW);
         // ---------------- colour 0 on row q = t+2+wave
         {
@@ -712,9 +669,8 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
                 const int cx = x - cofs, cp = cxp(cx), cm = cxm(cx);
                 const double ph = s_phi[s0][cx];
                 int32_t n_f0 = s_n0[s0][cx], n_b0 = s_n0[sm][cx], n_f1 = s_n1[s0][cx], n_b1 = s_n1[s0][cm];
-                if (SV_HOT_I16) {  // every later use takes the sign-extended value: ds_read_i16, no v_bfe_i32
-                    asm volatile("" : "+v"(n_f0), "+v"(n_b0), "+v"(n_f1), "+v"(n_b1));
-                }
+                // every later use takes the sign-extended value: ds_read_i16, no v_bfe_i32
+                asm volatile("" : "+v"(n_f0), "+v"(n_b0), "+v"(n_f1), "+v"(n_b1));
                 // r on the four links f0=(0,q,x), b0=(0,q-1,x), f1=(1,q,x), b1=(1,q,x-1) (neighborhood.py:91)
                 double r0[4];
                 r0[0] = (s_phi[sp][cx] - ph) - TWO_PI * (double)n_f0;
@@ -814,7 +770,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
             if (wave == 0 && lane == 0 && pv) Ls.stop = 1;
             if (wave == 0) pv = __hip_atomic_load(A.S.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (SV_HOT_PF_EARLY && t + NW < t1) prefetch(t + 3 + 2 * NW);
+        if (t + NW < t1) prefetch(t + 3 + 2 * NW);
         // The bases of the wave's two rows (brow1, brow1 + 1) move NW rows down.  Unless a row wraps around the
         // lattice or sits on global row 0 (where a buffered half-word clamps the word index), every block's
         // position moves by exactly its stride, so each base lane applies its precomputed advance map; the
@@ -823,7 +779,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
         brow1 += NW;
         if constexpr (PH) {
             // no row bases
-        } else if (SV_HOT_ADV && glo >= 1 && glo + NW + 1 < Nt && !(ROWM && sw->near(glo, NW + 2))) {
+        } else if (glo >= 1 && glo + NW + 1 < Nt && !(ROWM && sw->near(glo, NW + 2))) {
             if (base_lane) {
                 const int ai = bty == 0 ? 0 : (bty == 1 ? 1 : 2);
                 s_base[wave][lane] = mad128c(s_adv[ai].A, s_base[wave][lane], s_adv[ai].C);
@@ -921,7 +877,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
 }
 
 template <bool TILE, int NWT>
-__global__ __launch_bounds__(NWT * 64) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4 ? 4 : 3))) void villain_sweep_hot(FArgs A) {
+__global__ __launch_bounds__(NWT * 64) __attribute__((amdgpu_waves_per_eu(4))) void villain_sweep_hot(FArgs A) {
     __shared__ HotLDST<false, false, NWT> Ls;
     // the strip this workgroup owns (the same mapping hot_body makes), to pick the body
     int b = blockIdx.x;
@@ -947,7 +903,7 @@ __global__ __launch_bounds__(NWT * 64) __attribute__((amdgpu_waves_per_eu(SV_HOT
 // straddle a switch's site run the skip-list body, moved to the head of their XCD's range.  A replay thus costs about
 // one hot sweep instead of a general-kernel sweep (~1.9x).
 template <bool TILE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4 ? 4 : 3))) void villain_sweep_hot_split(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void villain_sweep_hot_split(
     FArgs A, SplitArgs S) {
     __shared__ HotLDST<false, false, 4> Ls;
     // the skip-list strips swap places with their XCD's first-dispatched strips (SplitArgs::swap)
@@ -989,9 +945,6 @@ template __global__ void villain_sweep_hot_split<false>(FArgs, SplitArgs);
 template __global__ void villain_sweep_hot_split<true>(FArgs, SplitArgs);
 
 // ---- multi-sweep band launches of small periodic lattices (BandArgs, villain.h)
-#ifndef SV_BAND_CAS
-#define SV_BAND_CAS 0  // poll the band barrier with compare-exchange (r4 A/B) instead of agent-scope loads
-#endif
 // The XCD-local barrier between two sweeps of a band: every wave's stores acknowledged by the L2, one arrival per
 // workgroup, then a spin (compare-exchange: a read-modify-write, so it executes in the L2 and never sees a stale L1
 // line) until the band's P workgroups have arrived, and this CU's L1 invalidated so that the next sweep's rows come
@@ -1007,16 +960,10 @@ __device__ __forceinline__ bool band_barrier(uint32_t *cnt, uint32_t target) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         int ok = 1;
         for (;;) {
-#if SV_BAND_CAS
-            uint32_t v = 0xFFFFFFFFu;
-            __hip_atomic_compare_exchange_strong(cnt, &v, 0xFFFFFFFFu, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
             // an agent-scope load misses the L1 and reads the L2 line the arrivals update; unlike a read-modify-write
             // it does not queue behind the other pollers in the L2's atomic unit (r4: CAS polling spread the barrier
             // passes of one band over ~4 us)
             const uint32_t v = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
             if (v >= target) break;
             if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000u) {  // 20 ms at 100 MHz
                 ok = 0;
@@ -1077,7 +1024,7 @@ __device__ __forceinline__ void band_sweeps(const FArgs &A, const BandArgs &B, H
 }
 
 template <int NWT>
-__global__ __launch_bounds__(NWT * 64) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4 ? 4 : 3))) void villain_sweep_hot_band(
+__global__ __launch_bounds__(NWT * 64) __attribute__((amdgpu_waves_per_eu(4))) void villain_sweep_hot_band(
     FArgs A, BandArgs B) {
     __shared__ HotLDST<false, false, NWT> Ls;
     __shared__ int32_t s_slot;
@@ -1117,7 +1064,7 @@ template __global__ void villain_sweep_hot<true, 8>(FArgs);
 
 // replica batches of full-row lattices (config 5), with or without the inline observables
 template <bool OBS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_OCC4 ? 4 : 3))) void villain_sweep_hot_fr(FArgs A) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void villain_sweep_hot_fr(FArgs A) {
     __shared__ HotLDST<false, OBS> Ls;
     // the replica this workgroup serves (the mapping hot_body makes), to pick the draw form
     int b = blockIdx.x;
@@ -1137,7 +1084,7 @@ template __global__ void villain_sweep_hot_fr<false>(FArgs);
 template __global__ void villain_sweep_hot_fr<true>(FArgs);
 
 // the counter-based mode on a periodic single lattice (every strip draws the same way)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SV_HOT_PH_OCC))) void villain_sweep_hot_ph(FArgs A) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void villain_sweep_hot_ph(FArgs A) {
     __shared__ HotLDST<true> Ls;
     hot_body<false, false, false, false, true>(A, Ls, logical_block());
 }
@@ -1164,7 +1111,7 @@ bool hot_params_ok(const VParams &P) {
     // the int16 n image: a row enters LDS with |n| < 2^14 (else OVERFLOW is reported) and each link changes at most
     // twice per sweep (once per colour) by |W (index - interval_n)| <= |W| interval_n, so |W| interval_n <= 2^13 keeps
     // every value within int16
-    if (SV_HOT_OCC4 && (aw > (1 << 12) || aw * P.interval_n > (1 << 13))) return false;
+    if ((aw > (1 << 12) || aw * P.interval_n > (1 << 13))) return false;
     return true;
 }
 

@@ -19,9 +19,6 @@
 // change_v pair; the host keeps the four pass kernels for the rest (worldline.hip).
 #include "fused.h"
 
-#ifndef SV_WF_PF0
-#define SV_WF_PF0 1  // the first prefetch of region rows issued before the prologue's row-base jumps
-#endif
 #ifndef SV_WFTIME
 #define SV_WFTIME 0  // timing experiments: per-workgroup timestamps of worldline_step_fused (sv_debug_wftime)
 #endif
@@ -268,9 +265,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     const int32_t tfirst = t0 - 7;
     int32_t brow = tfirst + 3 - bp + wave;
     u128 bases{0, 0};
-#if SV_WF_PF0
     prefetch(t0 - 5);  // the first region rows in flight while the row bases are jumped to
-#endif
     if (base_lane) bases = full_jump_flat(A.T, &A.blocks[bblk], (uint32_t)wf_base_pos(bbnd, grow(brow), N, bx, bhas));
     __builtin_amdgcn_s_waitcnt(0);
     if (base_lane) Ls.base[wave][lane] = bases;
@@ -464,7 +459,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     };
 
     for (int32_t ra = t0 - 5; ra < tfirst + AH; ra += NW) {
-        if (!SV_WF_PF0 || ra != t0 - 5) prefetch(ra);
+        if (ra != t0 - 5) prefetch(ra);
         commit(ra);
     }
     __syncthreads();
@@ -485,7 +480,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
         commit(t + AH);
         // The wave's four rows (t + wave .. t + 3 + wave) move NW rows down.  Unless one of them wraps around the
         // lattice or sits on global row 0 (where a buffered half-word clamps the word index), every block's position
-        // moves by exactly its stride: one precomputed map per base lane (villain_hot.hip's SV_HOT_ADV), the
+        // moves by exactly its stride: one precomputed map per base lane (as villain_hot.hip's), the
         // position arithmetic kept off the common path by a wave-uniform test.
         const int32_t glo = grow(t + wave);
         if (glo >= 1 && glo + NW + 3 < Nt) {
@@ -532,11 +527,10 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
 #endif
 }
 
-#ifndef SV_WF_OCC8
-#define SV_WF_OCC8 2  // waves per SIMD the 8-wave kernel is compiled for (4: two workgroups per CU, <= 128 VGPRs)
-#endif
+// the 8-wave kernel is compiled for 2 waves per SIMD (one workgroup per CU; two at <= 128 VGPRs measured slower, r386)
+constexpr int WF_OCC8 = 2;
 template <bool TILE, int NW>
-__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 8 ? SV_WF_OCC8 : 1))) void worldline_step_fused(WFArgs A) {
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 8 ? WF_OCC8 : 1))) void worldline_step_fused(WFArgs A) {
     __shared__ WFLDS<NW> Ls;
     int b = blockIdx.x;
     {
@@ -592,7 +586,7 @@ static int wf_th(int32_t N, int nsx, int nw) {
     }
     if (nw == 16) return 41;  // (16 k - 7 rows fill the last row step: the passes reach 7 rows past the strip)
     if (nw == 8) {
-        const int slots = 256 * (SV_WF_OCC8 >= 4 ? 2 : 1);
+        const int slots = 256 * (WF_OCC8 >= 4 ? 2 : 1);
         int th = 8;
         while (th < N && (int64_t)nsx * ((N + th - 1) / th) > slots) th += 8;
         return th;
