@@ -133,7 +133,7 @@ struct SplitArgs {
     uint32_t s[8];
     const Block *blocksB;
     int32_t nswap;
-    int32_t swap[SPLIT_SWAPS][2];  // logical block pairs exchanged (split_order)
+    int32_t swap[SPLIT_SWAPS][2];  // (logical slot, strip it runs) where the two differ (split_order)
 };
 // whether strip [t0, t1) x [x0, x1) of an Nt x Nx periodic lattice draws on both sides of the switch at site rank s
 // within one row (sites of rank >= s: linear index >= 2 s, one site of each colour per pair of sites): the switch's

@@ -906,13 +906,11 @@ template <bool TILE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void villain_sweep_hot_split(
     FArgs A, SplitArgs S) {
     __shared__ HotLDST<false, false, 4> Ls;
-    // the skip-list strips swap places with their XCD's first-dispatched strips (SplitArgs::swap)
+    // the skip-list strips run in their XCD's first-dispatched slots (SplitArgs::swap: slot -> strip where they differ)
     const int lb = logical_block();
     int b = lb;
-    for (int i = 0; i < S.nswap; i++) {
+    for (int i = 0; i < S.nswap; i++)
         if (lb == S.swap[i][0]) b = S.swap[i][1];
-        else if (lb == S.swap[i][1]) b = S.swap[i][0];
-    }
     int32_t tg0, tg1, xg0, xg1;  // the strip in global rows / columns
     split_strip(A.G, A.nsx, A.TH, A.strips, b, tg0, tg1, xg0, xg1);
     const bool interior = xg0 >= 4 && xg1 + 2 < A.G.Nx;
@@ -1158,13 +1156,17 @@ bool split_plan(const VParams &P, const Block *blocks, const uint32_t *skips, u1
 }
 
 void split_order(SplitArgs &S, const FGeom &G, int nsx, int TH, int grid, const int32_t *tab) {
-    // logical blocks are dealt to the XCDs in contiguous ranges (logical_block), dispatched from the range's start; a
-    // skip-list strip swaps places with the next not yet swapped strip at the start of its own XCD's range, so that the
-    // XCD's set of strips (its share of the work) is unchanged
+    // logical blocks are dealt to the XCDs in contiguous ranges (logical_block), dispatched from the range's start; the
+    // skip-list strips take the first slots of their own XCD's range and the strips there move to the slots they left,
+    // so that the XCD's set of strips (its share of the work) is unchanged.  The result is a permutation of the slots,
+    // sent as its non-identity entries (slot -> strip); a straddler already sitting in a head slot that another one is
+    // sent to is moved along with it (r5: an earlier pairwise-swap form ran one strip twice and another not at all then).
     S.nswap = 0;
     const int per = grid / 8, rem = grid % 8;
+    std::vector<int32_t> perm(grid), where(grid);  // slot -> strip, strip -> slot
+    for (int b = 0; b < grid; b++) perm[b] = where[b] = b;
     int used[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int b = 0; b < grid && S.nswap < SPLIT_SWAPS; b++) {
+    for (int b = 0; b < grid; b++) {
         int32_t tg0, tg1, xg0, xg1;
         split_strip(G, nsx, TH, tab, b, tg0, tg1, xg0, xg1);
         bool st = false, after;
@@ -1174,10 +1176,23 @@ void split_order(SplitArgs &S, const FGeom &G, int nsx, int TH, int grid, const 
         if (!st) continue;
         int x = 0;
         while (x < 7 && b >= (x + 1) * per + std::min(x + 1, rem)) x++;
-        const int a = x * per + std::min(x, rem) + used[x]++;
-        if (a >= b) continue;  // (already among the first)
-        S.swap[S.nswap][0] = a;
-        S.swap[S.nswap][1] = b;
+        const int a = x * per + std::min(x, rem) + used[x]++;  // the XCD's next head slot
+        const int pb = where[b];                               // where strip b sits now
+        if (pb == a) continue;
+        const int sa = perm[a];
+        perm[a] = b;
+        where[b] = a;
+        perm[pb] = sa;
+        where[sa] = pb;
+    }
+    for (int s = 0; s < grid; s++) {
+        if (perm[s] == s) continue;
+        if (S.nswap == SPLIT_SWAPS) {  // (more than the table holds: the identity, the order only costs time)
+            S.nswap = 0;
+            return;
+        }
+        S.swap[S.nswap][0] = s;
+        S.swap[S.nswap][1] = perm[s];
         S.nswap++;
     }
 }

@@ -91,3 +91,24 @@ def test_split_replay_natural_rejections_4096(oracle_lib):
     assert (phi == phi0).all() and (n == n0).all()
     assert G.rng.bit_generator.state == g.bit_generator.state
     assert nsplit >= 1
+
+
+@pytest.mark.parametrize('c,j', [(1, 3), (1, 2), (0, 3)])
+def test_split_replay_straddler_in_a_head_slot(c, j, oracle_lib):
+    """N = 2048 (663 strips: XCD ranges of 82 / 83): a rejection at row 300, column 517 makes straddling strips of which
+    one already sits in a head slot that another is sent to; the slot permutation must still run every strip once
+    (r5: the pairwise swaps ran one strip twice and left strip (rows 212-264, column strip 15) unswept)."""
+    N2 = 2048
+    V = N2 * N2
+    rank = (300 * N2 + 517) // 2
+    pos, half = V + c * (V // 2 + V) + V // 2 + j * (V // 4) + rank // 2, rank % 2
+    seed = 600 + 4 * c + j
+    r = np.random.default_rng(seed)
+    phi0, n0 = r.uniform(-np.pi, np.pi, (N2, N2)), r.integers(-2, 3, (2, N2, N2)).astype(np.int64)
+    G, phi, n, nsplit, counts = run(N2, 1, crafted_generator(seed, pos, half), phi0, n0)
+    g = crafted_generator(seed, pos, half)
+    st = oracle_lib.villain_neighborhood(N2, 0.5, 1, phi0, n0, 1, g)
+    assert st[0].rejections == 1
+    assert (phi == phi0).all() and (n == n0).all()
+    assert G.rng.bit_generator.state == g.bit_generator.state
+    assert nsplit == 1 and counts['fused'] == 0
