@@ -1,7 +1,7 @@
 # Full -m gpu suite (runtime error log on), smoke, the driver-form headline, the rejection window
 source scripts/gpu/guard.sh
 export TMPDIR=/tmp
-O=${OUT:-gpurun_out/r5_full3}
+O=${OUT:-gpurun_out/r5_full4}
 mkdir -p $O
 export AMD_LOG_LEVEL=1
 step tests timeout -k 10 900 python -u -m pytest tests -x -q --timeout 300 --timeout-method thread -m gpu > $O/tests.log 2>&1

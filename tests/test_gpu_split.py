@@ -112,3 +112,25 @@ def test_split_replay_straddler_in_a_head_slot(c, j, oracle_lib):
     assert (phi == phi0).all() and (n == n0).all()
     assert G.rng.bit_generator.state == g.bit_generator.state
     assert nsplit == 1 and counts['fused'] == 0
+
+
+@pytest.mark.parametrize('N2', [2048, 4096])
+def test_split_replay_random_positions(N2, oracle_lib):
+    """Forced rejections at seeded random (colour, block, rank) on the lattices whose strip tables differ from N = 1024's
+    (2048: 663 uniform strips; 4096: the per-XCD band schedule, 2992 strips): one sweep each, against the oracle."""
+    V = N2 * N2
+    pick = np.random.default_rng(N2)
+    for i in range(4):
+        c, j = int(pick.integers(0, 2)), int(pick.integers(0, 4))
+        rank = int(pick.integers(1, V // 2))
+        pos, half = V + c * (V // 2 + V) + V // 2 + j * (V // 4) + rank // 2, rank % 2
+        seed = 900 + 10 * i + N2 // 1024
+        r = np.random.default_rng(seed)
+        phi0, n0 = r.uniform(-np.pi, np.pi, (N2, N2)), r.integers(-2, 3, (2, N2, N2)).astype(np.int64)
+        G, phi, n, nsplit, counts = run(N2, 1, crafted_generator(seed, pos, half), phi0, n0)
+        g = crafted_generator(seed, pos, half)
+        st = oracle_lib.villain_neighborhood(N2, 0.5, 1, phi0, n0, 1, g)
+        assert st[0].rejections == 1
+        assert (phi == phi0).all() and (n == n0).all(), (N2, c, j, rank)
+        assert G.rng.bit_generator.state == g.bit_generator.state
+        assert nsplit == 1 and counts['fused'] == 0
