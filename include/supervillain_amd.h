@@ -307,6 +307,14 @@ int sv_replicas_upload(sv_replicas *b, const double *phi, const int64_t *n);
 int sv_replicas_download(sv_replicas *b, double *phi, int64_t *n);
 int sv_replicas_run(sv_replicas *b, double kappa, int64_t W, double interval_phi, int64_t interval_n, int32_t sweeps,
                     sv_rng *rngs, sv_stats *stats, double *obs);
+/* The same with the inline observables measured as the reference's observables report them, each (R, sweeps)
+ * row-major (torus_wrapping (R, sweeps, 2)): acceptance = acceptance_sum / V (G.acceptance's per-sweep increment),
+ * ActionDensity S / V and InternalEnergyDensity S / (V kappa) with S = kappa / 2 times the first sum (action.py:25-31,
+ * energy.py:25-30), WindingSquared the second sum / V (winding.py:30-37), TorusWrapping the n sums (wrapping.py:17-25).
+ * Written by the batch loop's copy-out, which overlaps the next batch's sweeps. */
+int sv_replicas_run_measured(sv_replicas *b, double kappa, int64_t W, double interval_phi, int64_t interval_n,
+                             int32_t sweeps, sv_rng *rngs, sv_stats *stats, double *acceptance, double *action_density,
+                             double *energy_density, double *winding_squared, int64_t *torus_wrapping);
 /* One-shot form over host arrays: phi (R, N, N) f64 and n (R, 2, N, N) int64 in/out, rngs[R] in/out,
  * stats[R * sweeps], inline_out (R * sweeps * 4, may be NULL) as sv_replicas_run's obs. */
 int sv_replicas_villain(sv_ctx *ctx, int32_t R, int32_t N, double kappa, int64_t W, double interval_phi,

@@ -107,6 +107,7 @@ def lib():
         L.sv_replicas_upload.argtypes = [vp, vp, vp]
         L.sv_replicas_download.argtypes = [vp, vp, vp]
         L.sv_replicas_run.argtypes = [vp, f64, i64, f64, i64, i32, vp, vp, vp]
+        L.sv_replicas_run_measured.argtypes = [vp, f64, i64, f64, i64, i32, vp, vp, vp, vp, vp, vp, vp]
         L.sv_replicas_villain.argtypes = [vp, i32, i32, f64, i64, f64, i64, vp, vp, i32, vp, vp, vp]
         L.sv_villain_worm_run.argtypes = [vp, f64, i64, i32, i64, P(SvRng), vp, vp]
         L.sv_replicas_worm_run.argtypes = [vp, f64, i64, i32, i64, vp, vp, vp]
@@ -133,7 +134,7 @@ EXPORTED = ('sv_ctx_create', 'sv_ctx_destroy', 'sv_last_error', 'sv_device_count
             'sv_domain_upload_worldline', 'sv_domain_download_worldline', 'sv_domain_run_worldline',
             'sv_domain_exchange_plan_worldline', 'sv_domain_message_layout_worldline',
             'sv_replicas_create', 'sv_replicas_destroy', 'sv_replicas_upload', 'sv_replicas_download',
-            'sv_replicas_run', 'sv_replicas_villain', 'sv_villain_worm_run', 'sv_replicas_worm_run', 'sv_worldline_worm_run',
+            'sv_replicas_run', 'sv_replicas_run_measured', 'sv_replicas_villain', 'sv_villain_worm_run', 'sv_replicas_worm_run', 'sv_worldline_worm_run',
             'sv_worldline_worm_batch')
 
 

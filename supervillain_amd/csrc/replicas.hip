@@ -202,8 +202,34 @@ struct RepBatch {
     std::vector<int32_t> hmap;
 };
 
-void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs, sv_stats *stats, double *obs) {
+// The measured form of the inline observables (sv_replicas_run_measured): what VillainReplicas.run returns, written
+// by the batch loop's copy-out (overlapped with the next batch) instead of by NumPy after the call
+struct MeasOut {
+    double *acceptance, *action, *energy, *w2;
+    int64_t *tw;
+    double kappa;
+};
+
+void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs, sv_stats *stats, double *obs,
+                  const MeasOut *mo = nullptr) {
     sv_ctx *ctx = b->ctx;
+    const bool inl = obs != nullptr || mo != nullptr;  // the inline observables are summed
+    // sweep k of replica r: its 4 raw sums (action sum, w2 sum, n0 sum, n1 sum) into the caller's arrays -- as they are
+    // (obs), or measured (mo: the operations of replicas.py's former NumPy post-processing, in its order)
+    auto put_obs = [&](int r, int64_t k, const double *raw) {
+        const size_t e = (size_t)r * sweeps + (size_t)k;
+        if (obs) {
+            std::memcpy(obs + e * 4, raw, 4 * sizeof(double));
+            return;
+        }
+        const double Vd = (double)b->V;
+        const double S = raw[0] * (mo->kappa / 2);
+        mo->energy[e] = S / (Vd * mo->kappa);
+        mo->action[e] = S / Vd;
+        mo->w2[e] = raw[1] / Vd;
+        mo->tw[2 * e] = (int64_t)raw[2];
+        mo->tw[2 * e + 1] = (int64_t)raw[3];
+    };
     const int R = b->R;
     const int64_t V = b->V;
     const int64_t counts[2] = {V / 2, V / 2};
@@ -275,8 +301,8 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         }
         ctx->ensure_skips(B.hskip.size() + 1);
         b->stage.put(ctx->stream, ctx->d_skips, B.hskip.data(), B.hskip.size() * sizeof(uint32_t));
-        reset_batch(ctx, b->d_stats, (size_t)R * count * sizeof(sv_stats), obs ? b->d_obs : nullptr,
-                    obs ? (size_t)R * count * 4 * sizeof(double) : 0);
+        reset_batch(ctx, b->d_stats, (size_t)R * count * sizeof(sv_stats), inl ? b->d_obs : nullptr,
+                    inl ? (size_t)R * count * 4 * sizeof(double) : 0);
         // A sweep runs on the fast-draw kernel (villain_sweep_hot_fr) when no replica's choice blocks of that sweep
         // carry a skip (the closed-form replicas have none; the host-planned ones are checked), else on the general
         // fused kernel.  Within a skip-free sweep a replica's four choice blocks start on the same half-word parity
@@ -363,9 +389,9 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
             A.rep_obs = 4 * count;
             A.Trep = b->d_Trep;
             A.advrep = b->d_adv;
-            A.obs = obs ? b->d_obs + 4 * k : nullptr;
+            A.obs = inl ? b->d_obs + 4 * k : nullptr;
             if (hot_k[k]) {
-                launch_hot_fr(A, R * tiles, obs != nullptr, ctx->stream);
+                launch_hot_fr(A, R * tiles, inl, ctx->stream);
                 ctx->sweeps_hot++;
                 launches++;
             } else if (split[k][3] > 0) {
@@ -377,13 +403,13 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
                 Ag.TH = 8;
                 Ag.nsy = (b->N + 7) / 8;
                 Ag.tiles_per_rep = nsx * Ag.nsy;
-                if (split[k][1] > 0) launch_hot_fr(Ah, (int)split[k][1] * tiles, obs != nullptr, ctx->stream);
-                launch_fused_batch(Ag, (int)split[k][3] * Ag.tiles_per_rep, obs != nullptr, ctx->stream);
+                if (split[k][1] > 0) launch_hot_fr(Ah, (int)split[k][1] * tiles, inl, ctx->stream);
+                launch_fused_batch(Ag, (int)split[k][3] * Ag.tiles_per_rep, inl, ctx->stream);
                 ctx->sweeps_hot += split[k][1] > 0;
                 ctx->sweeps_fused++;
                 launches += 1 + (split[k][1] > 0);
             } else {
-                launch_fused_batch(A, R * tiles, obs != nullptr, ctx->stream);
+                launch_fused_batch(A, R * tiles, inl, ctx->stream);
                 ctx->sweeps_fused++;
                 launches++;
             }
@@ -410,7 +436,7 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         const size_t st_bytes = (size_t)R * count * sizeof(sv_stats);
         SV_HIP(hipMemcpyAsync(tail, ctx->d_abort, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));  // + d_nreport
         SV_HIP(hipMemcpyAsync(tail + 64, b->d_stats, st_bytes, hipMemcpyDeviceToHost, ctx->stream));
-        if (obs)
+        if (inl)
             SV_HIP(hipMemcpyAsync(tail + 64 + st_bytes, b->d_obs, (size_t)R * count * 4 * sizeof(double),
                                   hipMemcpyDeviceToHost, ctx->stream));
     };
@@ -429,10 +455,10 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
                 dst[k] = src[k];
                 dst[k].proposed = V;
                 dst[k].rejections = none ? 0 : rejections_in(skips[r], B.sw + k, NB);
+                if (mo) mo->acceptance[(size_t)r * sweeps + B.sw + k] = src[k].acceptance_sum / (double)V;
             }
-            if (obs)
-                std::memcpy(obs + ((size_t)r * sweeps + B.sw) * 4, h_ob + (size_t)r * B.count * 4,
-                            (size_t)upto * 4 * sizeof(double));
+            if (inl)
+                for (int k = 0; k < upto; k++) put_obs(r, B.sw + k, h_ob + ((size_t)r * B.count + k) * 4);
         }
     };
 
@@ -465,7 +491,7 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
                 const size_t e = (size_t)F[i] * count + k;
                 b->stage.put(ctx->stream, b->d_blocks + e * NB, &fb[i * NB], NB * sizeof(Block));
                 SV_HIP(hipMemsetAsync(b->d_stats + e, 0, sizeof(sv_stats), ctx->stream));
-                if (obs) SV_HIP(hipMemsetAsync(b->d_obs + 4 * e, 0, 4 * sizeof(double), ctx->stream));
+                if (inl) SV_HIP(hipMemsetAsync(b->d_obs + 4 * e, 0, 4 * sizeof(double), ctx->stream));
             }
             b->stage.put(ctx->stream, ctx->d_skips, allsk.data(), allsk.size() * sizeof(uint32_t));
             b->stage.put(ctx->stream, b->d_map, F.data(), F.size() * sizeof(int32_t));
@@ -495,9 +521,9 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
             A.rep_obs = 4 * count;
             A.Trep = b->d_Trep;
             A.advrep = b->d_adv;
-            A.obs = obs ? b->d_obs + 4 * k : nullptr;
+            A.obs = inl ? b->d_obs + 4 * k : nullptr;
             A.rep_map = b->d_map;
-            launch_fused_batch(A, (int)F.size() * A.tiles_per_rep, obs != nullptr, ctx->stream);
+            launch_fused_batch(A, (int)F.size() * A.tiles_per_rep, inl, ctx->stream);
             ctx->sweeps_fused++;
             SV_HIP(hipGetLastError());
             AbortInfo a = read_abort(ctx);  // (synchronizes)
@@ -509,9 +535,12 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
                     SV_HIP(hipMemcpy(dst, b->d_stats + e, sizeof(sv_stats), hipMemcpyDeviceToHost));
                     dst->proposed = V;
                     dst->rejections = rejections_in(skips[r], B.sw + k, NB);
-                    if (obs)
-                        SV_HIP(hipMemcpy(obs + ((size_t)r * sweeps + B.sw + k) * 4, b->d_obs + 4 * e, 4 * sizeof(double),
-                                         hipMemcpyDeviceToHost));
+                    if (mo) mo->acceptance[(size_t)r * sweeps + B.sw + k] = dst->acceptance_sum / (double)V;
+                    if (inl) {
+                        double raw[4];
+                        SV_HIP(hipMemcpy(raw, b->d_obs + 4 * e, 4 * sizeof(double), hipMemcpyDeviceToHost));
+                        put_obs(r, B.sw + k, raw);
+                    }
                     cur[r] = cf[i];
                 }
                 return;
@@ -635,6 +664,25 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
     }
 }
 
+
+int replicas_run(sv_replicas *b, double kappa, int64_t W, double interval_phi, int64_t interval_n,
+                            int32_t sweeps, sv_rng *rngs, sv_stats *stats, double *obs, const MeasOut *mo) {
+    if (!b || !rngs || (sweeps > 0 && !stats)) return -1;
+    sv_ctx *ctx = b->ctx;
+    try {
+        if (sweeps < 0) throw std::invalid_argument("sweeps must be >= 0");
+        if (interval_n < 0 || interval_n > (1 << 20)) throw std::invalid_argument("interval_n out of range");
+        if ((W < 0 ? -W : W) * interval_n >= (1LL << 28)) throw std::invalid_argument("|W * interval_n| too large");
+        SV_HIP(hipSetDevice(ctx->device));
+        const VParams P = make_params(b->N, kappa, W, interval_phi, interval_n);
+        run_replicas(b, P, sweeps, rngs, stats, obs, mo);
+        return 0;
+    } catch (const std::exception &e) {
+        ctx->err = e.what();
+        return -2;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -735,20 +783,15 @@ int sv_replicas_download(sv_replicas *b, double *phi, int64_t *n) {
 
 int sv_replicas_run(sv_replicas *b, double kappa, int64_t W, double interval_phi, int64_t interval_n, int32_t sweeps,
                     sv_rng *rngs, sv_stats *stats, double *obs) {
-    if (!b || !rngs || (sweeps > 0 && !stats)) return -1;
-    sv_ctx *ctx = b->ctx;
-    try {
-        if (sweeps < 0) throw std::invalid_argument("sweeps must be >= 0");
-        if (interval_n < 0 || interval_n > (1 << 20)) throw std::invalid_argument("interval_n out of range");
-        if ((W < 0 ? -W : W) * interval_n >= (1LL << 28)) throw std::invalid_argument("|W * interval_n| too large");
-        SV_HIP(hipSetDevice(ctx->device));
-        const VParams P = make_params(b->N, kappa, W, interval_phi, interval_n);
-        run_replicas(b, P, sweeps, rngs, stats, obs);
-        return 0;
-    } catch (const std::exception &e) {
-        ctx->err = e.what();
-        return -2;
-    }
+    return replicas_run(b, kappa, W, interval_phi, interval_n, sweeps, rngs, stats, obs, nullptr);
+}
+
+int sv_replicas_run_measured(sv_replicas *b, double kappa, int64_t W, double interval_phi, int64_t interval_n,
+                             int32_t sweeps, sv_rng *rngs, sv_stats *stats, double *acceptance, double *action_density,
+                             double *energy_density, double *winding_squared, int64_t *torus_wrapping) {
+    if (sweeps > 0 && (!acceptance || !action_density || !energy_density || !winding_squared || !torus_wrapping)) return -1;
+    const MeasOut mo{acceptance, action_density, energy_density, winding_squared, torus_wrapping, kappa};
+    return replicas_run(b, kappa, W, interval_phi, interval_n, sweeps, rngs, stats, nullptr, &mo);
 }
 
 int sv_replicas_worm_run(sv_replicas *b, double kappa, int64_t W, int32_t worms, int64_t max_moves, sv_rng *rngs,

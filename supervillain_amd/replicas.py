@@ -84,31 +84,36 @@ class VillainReplicas:
         if len(rngs) != self.R:
             raise ValueError(f'need {self.R} generators')
         r, addrs = rngs_from_numpy(rngs)
-        st = np.zeros((self.R, max(sweeps, 1)), dtype=STATS_DTYPE)  # sv_stats[R][sweeps]
-        obs = np.zeros((self.R, max(sweeps, 1), 4)) if inline else None
-        self.ctx.check(_native.lib().sv_replicas_run(self.handle, self.kappa, self.W, self.interval_phi,
-                                                     self.interval_n, int(sweeps), r, _native.ptr(st),
-                                                     _native.ptr(obs) if inline else None), 'sv_replicas_run')
+        K = max(sweeps, 1)
+        st = np.empty((self.R, K), dtype=STATS_DTYPE)  # sv_stats[R][sweeps] (every entry written by the call)
+        # the measured arrays are filled by the library's copy-out of each batch, which overlaps the next batch's
+        # sweeps (and takes the arrays' first-touch page faults there), instead of NumPy after the call
+        acc = np.empty((self.R, K))
+        if inline:
+            act, energy, w2 = np.empty((self.R, K)), np.empty((self.R, K)), np.empty((self.R, K))
+            tw = np.empty((self.R, K, 2), dtype=np.int64)
+        else:
+            act = energy = w2 = np.empty((self.R, 0))
+            tw = np.empty((self.R, 0, 2), dtype=np.int64)
+        if inline:
+            rc = _native.lib().sv_replicas_run_measured(self.handle, self.kappa, self.W, self.interval_phi,
+                                                        self.interval_n, int(sweeps), r, _native.ptr(st),
+                                                        _native.ptr(acc), _native.ptr(act), _native.ptr(energy),
+                                                        _native.ptr(w2), _native.ptr(tw))
+            self.ctx.check(rc, 'sv_replicas_run_measured')
+        else:
+            self.ctx.check(_native.lib().sv_replicas_run(self.handle, self.kappa, self.W, self.interval_phi,
+                                                         self.interval_n, int(sweeps), r, _native.ptr(st), None),
+                           'sv_replicas_run')
         rngs_to_numpy(r, rngs, addrs)
-        V = self.N * self.N
         st = st[:, :sweeps]
-        # Views of the C-filled arrays, the arithmetic done in place: fresh arrays cost their page faults (at config
-        # 5's size ~1.5 MB each, together a few percent of the call); two are new (two quantities from one sum, and the
-        # integer wrapping sums)
-        acceptance = st['acceptance_sum']
-        acceptance /= V
-        stats = {'accepted': st['accepted'], 'acceptance': acceptance, 'rejections': st['rejections']}
+        if not inline:
+            acc = st['acceptance_sum'] / (self.N * self.N)
+        stats = {'accepted': st['accepted'], 'acceptance': acc[:, :sweeps], 'rejections': st['rejections']}
         if not inline:
             return stats, None
-        obs = obs[:, :sweeps]
-        S = obs[..., 0]
-        S *= self.kappa / 2
-        energy = S / (V * self.kappa)  # S / (V kappa), as the reference's InternalEnergyDensity
-        S /= V                         # S / V, ActionDensity
-        w2 = obs[..., 1]
-        w2 /= V
-        tw = obs[..., 2:4].astype(np.int64)  # integer sums, exact in f64 below 2^53 (an in-place cast measured slower)
-        return stats, {'ActionDensity': S, 'InternalEnergyDensity': energy, 'WindingSquared': w2, 'TorusWrapping': tw}
+        return stats, {'ActionDensity': act[:, :sweeps], 'InternalEnergyDensity': energy[:, :sweeps],
+                       'WindingSquared': w2[:, :sweeps], 'TorusWrapping': tw[:, :sweeps]}
 
 
 def worldline_worms(m, v, kappa, W, rngs, worms=1, max_moves=WORM_MAX_MOVES, device=None):
