@@ -225,6 +225,11 @@ def report(args, world, sites_per_step, sites_per_launch, elapsed, acc, avg_laun
         'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS,
                      'traffic': traffic_from_profiles(traffic_L) if kernel == 'villain_sweep_hot' else None,
+                     # (PMC counters cannot be read inside this process: they come from scripts/profile.sh's separate
+                     # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same command, per the guide's gfx950
+                     # corrections, folded into profiles/pmc_summary.json)
+                     'traffic_source': 'profiles/pmc_summary.json (rocprofv3 --pmc passes of this command, '
+                                       'scripts/profile.sh)' if kernel == 'villain_sweep_hot' else None,
                      'kernel': kernel, 'avg_launch_us': avg_launch_s * 1e6, 'launch_time_source': timing_source,
                      'alg_bytes_per_unit': alg_bytes,
                      'fused_min_bytes_per_unit': min_bytes,
