@@ -5,7 +5,9 @@ set -e
 name=$1; shift
 cd $(dirname $0)/../supervillain_amd/csrc
 mkdir -p ../variants/$name
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -mllvm --amdgpu-set-wave-priority -I../../include -I. $*"
+PRIO="-mllvm --amdgpu-set-wave-priority"
+[ "${NOPRIO:-0}" = 1 ] && PRIO=""  # (A/B: without the prologue wave-priority pass)
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math $PRIO -I../../include -I. $*"
 objs=""
 for f in capi plan mt19937 villain villain_hot villain_block villain_local worldline worldline_fused worldline_local domain replicas worm; do
   /opt/rocm/bin/hipcc $F -c $f.hip -o ../variants/$name/$f.o &
