@@ -1,0 +1,7 @@
+# per-workgroup timeline of config 3's worldline_step_fused, turned and plain layouts (variant built with -DSV_WFTIME=1)
+source scripts/gpu/guard.sh
+export TMPDIR=/tmp
+O=${OUT:-gpurun_out/r5_wftl2}
+mkdir -p $O
+step tl env SV_LIB_OVERRIDE=supervillain_amd/variants/libsvhip_wftime.so timeout -k 10 200 python -u scripts/perf/wg_timeline.py worldline 1024 > $O/timeline_turned.log 2>&1
+step tl0 env SV_WF_TURN=0 SV_LIB_OVERRIDE=supervillain_amd/variants/libsvhip_wftime.so timeout -k 10 200 python -u scripts/perf/wg_timeline.py worldline 1024 > $O/timeline_plain.log 2>&1

@@ -97,7 +97,37 @@ if mode == 'worldline':
         ctx.check(Lib.sv_worldline_plaquette_coexact_run(h, 0.5, 1.0, 1, 50, ctypes.byref(r), st), 'run')
         buf = np.zeros(65536 * 6, dtype=np.uint64)
         assert Lib.sv_debug_wftime(buf.ctypes.data, 65536) == 0
-        summarize(f'worldline L={L} call {k}', buf.reshape(65536, 6))
+        t = buf.reshape(65536, 6)
+        summarize(f'worldline L={L} call {k}', t)
+        # per strip: worldline_step_fused's XCD-aware slot -> strip mapping, nsx = ceil(L / 119) column strips
+        nsx = (L + 118) // 119
+        idx = np.nonzero(t[:, 0] > 0)[0]
+        G = len(idx)
+        per, rem = G // 8, G % 8
+        b = (idx & 7) * per + np.minimum(idx & 7, rem) + (idx >> 3)
+        nsy = (L + 40) // 41
+        if G != nsx * nsy:  # the turned layout: nsx - 1 interior columns of nsy strips, then the seam strips
+            ni = nsx - 1
+            ix = np.where(b < ni * nsy, 1 + b % ni, 0)
+            iy = np.where(b < ni * nsy, b // ni, b - ni * nsy)
+        else:
+            ix, iy = b % nsx, b // nsx
+        tt = t[idx]
+        t0 = int(tt[:, 0].min())
+        e, l0, l1, x = [(tt[:, i].astype(np.int64) - t0) * 0.01 for i in range(4)]
+        edge = (ix == 0) | ((ix == nsx - 1) & (G == nsx * nsy))
+        redge = (iy == 0) | (iy == np.where(ix == 0, iy[ix == 0].max(), iy[ix != 0].max()))
+        for nm, sel in (('interior', ~edge & ~redge), ('seam columns', edge & ~redge), ('seam rows', ~edge & redge),
+                        ('corners', edge & redge)):
+            if sel.any():
+                print(f'[worldline L={L} call {k}] {nm}: n={int(sel.sum())} loop p50 {np.median((l1 - l0)[sel]):.1f} '
+                      f'max {(l1 - l0)[sel].max():.1f}; prologue p50 {np.median((l0 - e)[sel]):.2f} (to bases '
+                      f'{np.median(((tt[:, 5].astype(np.int64) - t0) * 0.01 - e)[sel]):.2f}); epilogue p50 '
+                      f'{np.median((x - l1)[sel]):.2f}; exit p50 {np.median(x[sel]):.1f} max {x[sel].max():.1f}', flush=True)
+        last = np.argsort(x)[-8:]
+        print(f'[worldline L={L} call {k}] last exits (ix, iy, xcd, entry, loop, exit): ' + ' '.join(
+            f'({ix[j]},{iy[j]},{int((tt[j, 4] >> 32) & 0xF)},{e[j]:.1f},{(l1 - l0)[j]:.1f},{x[j]:.1f})' for j in last),
+            flush=True)
     sys.exit(0)
 if mode == 'single':
     L = int(sys.argv[2]) if len(sys.argv) > 2 else 4096

@@ -36,8 +36,8 @@ namespace svh {
 bool wf_usable(int32_t N, bool v_is_float, double W_eff, int64_t it);
 bool wf_fast(const sv::Block *blocks);
 void launch_wf(const sv::FGeom &G, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in,
-               int64_t *m_out, int64_t *v_out, const sv::Block *blocks, const uint32_t *skips, bool general,
-               const sv::JumpTables *T, const sv::Affine adv[6], void *pstat, void *cstat, sv::DevScratch S,
+               int64_t *m_out, int64_t *v_out, const sv::Block *blocks, const sv::Block *hblocks, const uint32_t *skips, bool general,
+               const sv::JumpTables *T, const sv::Affine adv[6], sv::u128 inc, void *pstat, void *cstat, sv::DevScratch S,
                uint32_t sweep, hipStream_t stream);
 }  // namespace svh
 
@@ -908,7 +908,7 @@ void run_wdomain(sv_domain *d, double kappa, double W_eff, int64_t it, int32_t s
             for (auto &Tl : d->tiles)
                 launch_wf(FGeom{d->Nt, d->Nx, Tl.T0, Tl.X0, d->Ht, d->Wt, d->pitch, d->plane, d->org}, kappa, W_eff, it,
                           Tl.n[in], (const int64_t *)Tl.phi[in], Tl.n[out], (int64_t *)Tl.phi[out],
-                          ctx->d_blocks + (size_t)k * nb, ctx->d_skips, general, T, adv,
+                          ctx->d_blocks + (size_t)k * nb, &blocks[(size_t)k * nb], ctx->d_skips, general, T, adv, inc,
                           Tl.stripes + (size_t)k * 2 * NSTRIPE, Tl.stripes + (size_t)k * 2 * NSTRIPE + NSTRIPE,
                           DevScratch{&Tl.sum->abort, &Tl.sum->nreport, Tl.sum->reports}, (uint32_t)k, ctx->stream);
             d->cur = out;

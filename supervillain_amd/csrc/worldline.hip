@@ -24,8 +24,8 @@ namespace svh {
 bool wf_usable(int32_t N, bool v_is_float, double W_eff, int64_t it);
 bool wf_fast(const sv::Block *blocks);
 void launch_wf(const sv::FGeom &G, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in,
-               int64_t *m_out, int64_t *v_out, const sv::Block *blocks, const uint32_t *skips, bool general,
-               const sv::JumpTables *T, const sv::Affine adv[6], void *pstat, void *cstat, sv::DevScratch S,
+               int64_t *m_out, int64_t *v_out, const sv::Block *blocks, const sv::Block *hblocks, const uint32_t *skips, bool general,
+               const sv::JumpTables *T, const sv::Affine adv[6], sv::u128 inc, void *pstat, void *cstat, sv::DevScratch S,
                uint32_t sweep, hipStream_t stream);
 }  // namespace svh
 
@@ -977,7 +977,7 @@ int sv_worldline_plaquette_coexact_run(sv_worldline *st, double kappa, double W_
                     const int64_t V = N * N;
                     svh::launch_wf(FGeom{(int32_t)N, (int32_t)N, 0, 0, (int32_t)N, (int32_t)N, N, V, 0}, kappa, W_eff,
                                    interval_t, st->m, (const int64_t *)st->v, st->m_alt, (int64_t *)st->v_alt,
-                                   blocks, ctx->d_skips, !svh::wf_fast(hblocks), T, adv, stat, stat + NSTRIPE,
+                                   blocks, hblocks, ctx->d_skips, !svh::wf_fast(hblocks), T, adv, inc, stat, stat + NSTRIPE,
                                    wscratch(ctx), k, ctx->stream);
                     std::swap(st->m, st->m_alt);
                     std::swap(st->v, st->v_alt);

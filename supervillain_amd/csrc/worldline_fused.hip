@@ -44,14 +44,20 @@ struct WFGeom {
 struct WFArgs {
     FGeom G;  // the periodic Nt x Nx lattice, or one domain tile with its ghost frame (villain.h)
     int32_t nsx, TH, nsy;
+    // periodic lattices (16 waves): the column strips turned left by rot columns, so that strip 0 alone holds the
+    // torus's column seam, in nsy_s row strips of ths rows (2 row steps: the seam strip's MODE 1 draws cost ~10% more
+    // a row step); ths = 0: the plain layout (strip 0 at column 0, the last strip's region wrapping as well)
+    int32_t rot, ths, nsy_s;
     const int64_t *m_in;
     const int64_t *v_in;
     int64_t *m_out;
     int64_t *v_out;
     const Block *blocks;  // 5 plaquette blocks ([0] metropolis, [1+2c] change_m, [2+2c] change_v), then 3 coexact
+    Block blk[8];         // the same descriptors by value: the prologue's row-base jumps start one load earlier
     const uint32_t *skips;  // known rejected stream positions (GENERAL mode)
     const JumpTables *T;  // ([5] metropolis, [6+c] t)
-    Affine adv[3];        // advance a row base by NW rows: [0] NW N draws, [2] NW N / 4 words
+    Affine adv[5];        // advance a row base by NW rows: [0] NW N draws, [2] NW N / 4 words; [3], [4]: the same
+                          // across the torus's row seam (NW N - V draws, (NW N - V) / 4 words: inverse maps)
     StatStripe *pstat, *cstat;
     DevScratch S;
     uint32_t sweep;
@@ -68,7 +74,25 @@ struct WFArgs {
 };
 
 // Column strip boundaries (uniform: narrower seam strips, whose MODE 1 row steps are ~11% longer, measured level, r4)
-__device__ __forceinline__ int32_t wf_xb(const WFArgs &A, int ix) { return (int32_t)((int64_t)ix * A.G.Wt / A.nsx); }
+__device__ __forceinline__ int32_t wf_xb(const WFArgs &A, int ix) {
+    return (int32_t)((int64_t)ix * A.G.Wt / A.nsx) - A.rot;
+}
+// launch slot -> strip (column ix, row iy, rows per strip); slots are dealt to the XCDs in contiguous runs
+__device__ __forceinline__ void wf_strip(const WFArgs &A, int &ix, int &iy, int &th) {
+    int b = blockIdx.x;
+    {
+        const int G = gridDim.x, per = G / 8, rem = G % 8;
+        const int xcd = b & 7, k = b >> 3;
+        b = xcd * per + (xcd < rem ? xcd : rem) + k;
+    }
+    if (A.ths) {
+        const int ni = A.nsx - 1;
+        if (b < ni * A.nsy) ix = 1 + b % ni, iy = b / ni, th = A.TH;
+        else ix = 0, iy = b - ni * A.nsy, th = A.ths;
+    } else {
+        ix = b % A.nsx, iy = b / A.nsx, th = A.TH;
+    }
+}
 
 // The plaquette pass's acceptance min(1, exp(-dS)), dS = dfk ((((f1 + f2) - f3) - f4) + 2 df) (plaquette.py via
 // plaquette_cb_gs), depends on the choice pair and on Sigma = ((f1 + f2) - f3) - f4 only, and Sigma is a small multiple
@@ -84,7 +108,7 @@ struct WFLDS {
     int32_t m1[R][RW];
     int32_t v[R][RW];
     SmallTab small;
-    Affine adv[3];
+    Affine adv[5];
     u128 base[NW][64];  // per wave: lane 8p + ty = block ty's base for pass p's row at xb; 32 + .. at xw
     double df[6], dfk[6];
     int32_t bad;
@@ -123,17 +147,12 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     const int32_t N = Gm.Nx, Nt = Gm.Nt;  // global row length (stream layout) and row count
     const int64_t V = Gm.plane;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
-    int b = blockIdx.x;
-    {
-        const int G = gridDim.x, per = G / 8, rem = G % 8;
-        const int xcd = b & 7, k = b >> 3;
-        b = xcd * per + (xcd < rem ? xcd : rem) + k;
-    }
-    const int ix = b % A.nsx, iy = b / A.nsx;
+    int ix, iy, TH;
+    wf_strip(A, ix, iy, TH);
     const int32_t x0 = wf_xb(A, ix), x1 = wf_xb(A, ix + 1);
     const int32_t w = x1 - x0;
-    const int32_t t0 = iy * A.TH;
-    const int32_t t1 = t0 + A.TH < Gm.Ht ? t0 + A.TH : Gm.Ht;
+    const int32_t t0 = iy * TH;
+    const int32_t t1 = t0 + TH < Gm.Ht ? t0 + TH : Gm.Ht;
     const int32_t rbase = t0 - 5;  // local row 0
     const int32_t cols = w + 9;
     const int32_t cofs = x0 - 5;   // LDS column of lattice column x is x - cofs
@@ -145,13 +164,13 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     const int32_t gx0 = Gm.X0 + x0;
     const int32_t xb = (N <= SMALL_LDS || gx0 - 5 < 0) ? 0 : gx0 - 5;
     const bool two_sets = EDGE && N > SMALL_LDS;
-    const int32_t xw = gx0 - 5 < 0 ? N - 5 : 0;
+    const int32_t xw = gx0 - 5 < 0 ? N + gx0 - 5 : 0;  // (gx0 >= -N / 2)
 
     for (int e = threadIdx.x; e < SMALL_LDS; e += NW * 64) {
         s_small.A[e] = A.T->small[e].A;
         s_small.C[e] = A.T->small[e].C;
     }
-    if (threadIdx.x < 3) Ls.adv[threadIdx.x] = A.adv[threadIdx.x];
+    if (threadIdx.x < 5) Ls.adv[threadIdx.x] = A.adv[threadIdx.x];
     if (threadIdx.x < 6) {
         Ls.df[threadIdx.x] = A.df[threadIdx.x];
         Ls.dfk[threadIdx.x] = A.dfk[threadIdx.x];
@@ -176,11 +195,11 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     uint32_t hasp[2], bufp[2][2], hast[2], buft[2];
 #pragma unroll
     for (int c = 0; c < 2; c++) {
-        hasp[c] = (uint32_t)__builtin_amdgcn_readfirstlane(A.blocks[1 + 2 * c].has);
-        bufp[c][0] = (uint32_t)__builtin_amdgcn_readfirstlane(A.blocks[1 + 2 * c].buf);
-        bufp[c][1] = (uint32_t)__builtin_amdgcn_readfirstlane(A.blocks[2 + 2 * c].buf);
-        hast[c] = (uint32_t)__builtin_amdgcn_readfirstlane(A.blocks[6 + c].has);
-        buft[c] = (uint32_t)__builtin_amdgcn_readfirstlane(A.blocks[6 + c].buf);
+        hasp[c] = A.blk[1 + 2 * c].has;
+        bufp[c][0] = A.blk[1 + 2 * c].buf;
+        bufp[c][1] = A.blk[2 + 2 * c].buf;
+        hast[c] = A.blk[6 + c].has;
+        buft[c] = A.blk[6 + c].buf;
     }
 
     // ---- register prefetch of region rows [ra, ra+NW): wave w moves row ra + w, lane l columns l, l + 64
@@ -239,11 +258,21 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
         if (SV_ABLATE & 8) return;  // timing experiments only: no HBM stores
         if (q >= t0 && q < t1) {
             const int slot = (q - rbase) % R;
-            const int64_t g0 = mrow(q) + x0;  // own sites never wrap
+            // own sites wrap only in the turned layout's seam strip (x0 < 0): column x0 + cc2 is the load column
+            // pf_gx[k] five on, wrapped (periodic lattices; a tile's own columns never wrap)
+            const int64_t g0 = TILE ? mrow(q) + x0 : mrow(q);
 #pragma unroll
             for (int k = 0; k < PF; k++) {
                 const int cc2 = lane + 64 * k;
                 if (cc2 < w) {
+                    if constexpr (!TILE) {
+                        const uint32_t c = (uint32_t)pf_gx[k] + 5u, cw = c >= (uint32_t)N ? c - (uint32_t)N : c;
+                        const uint32_t o = ((uint32_t)g0 + cw) * 8u;
+                        *(int64_t *)((char *)A.m_out + o) = (int64_t)s_m0[slot][cc2 + 5];
+                        *(int64_t *)((char *)A.m_out + (o + (uint32_t)V * 8u)) = (int64_t)s_m1[slot][cc2 + 5];
+                        *(int64_t *)((char *)A.v_out + o) = (int64_t)s_v[slot][cc2 + 5];
+                        continue;
+                    }
                     const uint32_t o = ((uint32_t)g0 + (uint32_t)cc2) * 8u;
                     *(int64_t *)((char *)A.m_out + o) = (int64_t)s_m0[slot][cc2 + 5];
                     *(int64_t *)((char *)A.m_out + (o + (uint32_t)V * 8u)) = (int64_t)s_m1[slot][cc2 + 5];
@@ -261,12 +290,24 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     const int32_t bx = lane >= 32 ? xw : xb;
     const int bblk = bp < 2 ? (bty == 0 ? 0 : bty + 2 * bp) : (bty == 0 ? 5 : 6 + (bp - 2));
     const bool bbnd = bty != 0;
-    const uint32_t bhas = (base_lane && bbnd) ? A.blocks[bblk].has : 0u;
+    Block kb;  // this lane's descriptor (selects: no dynamically indexed kernel argument)
+    {
+        uint64_t lo = A.blk[0].base_lo, hi = A.blk[0].base_hi;
+        uint32_t h = A.blk[0].has;
+#pragma unroll
+        for (int k = 1; k < 8; k++) {
+            lo = bblk == k ? A.blk[k].base_lo : lo;
+            hi = bblk == k ? A.blk[k].base_hi : hi;
+            h = bblk == k ? A.blk[k].has : h;
+        }
+        kb.base_lo = lo, kb.base_hi = hi, kb.has = h, kb.buf = 0, kb.nskip = 0, kb.skip0 = 0;
+    }
+    const uint32_t bhas = (base_lane && bbnd) ? kb.has : 0u;
     const int32_t tfirst = t0 - 7;
     int32_t brow = tfirst + 3 - bp + wave;
     u128 bases{0, 0};
     prefetch(t0 - 5);  // the first region rows in flight while the row bases are jumped to
-    if (base_lane) bases = full_jump_flat(A.T, &A.blocks[bblk], (uint32_t)wf_base_pos(bbnd, grow(brow), N, bx, bhas));
+    if (base_lane) bases = full_jump_flat(A.T, &kb, (uint32_t)wf_base_pos(bbnd, grow(brow), N, bx, bhas));
     __builtin_amdgcn_s_waitcnt(0);
     if (base_lane) Ls.base[wave][lane] = bases;
 #if SV_WFTIME
@@ -495,6 +536,8 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
             const int64_t p_new = wf_base_pos(bbnd, grow(brow + NW), N, bx, bhas);
             const int64_t step = bbnd ? (int64_t)NW * N / 4 : (int64_t)NW * N;
             if (p_new - p_old == step) bases = apply(Ls.adv[bbnd ? 2 : 0], bases);
+            else if (p_new - p_old == step - (bbnd ? (int64_t)Nt * N / 4 : (int64_t)Nt * N))
+                bases = apply(Ls.adv[bbnd ? 4 : 3], bases);  // the wave's rows wrapped around the torus
             else bases = full_jump(A.T, &A.blocks[bblk], (uint32_t)p_new);
             brow += NW;
             Ls.base[wave][lane] = bases;
@@ -532,13 +575,8 @@ constexpr int WF_OCC8 = 2;
 template <bool TILE, int NW>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 8 ? WF_OCC8 : 1))) void worldline_step_fused(WFArgs A) {
     __shared__ WFLDS<NW> Ls;
-    int b = blockIdx.x;
-    {
-        const int G = gridDim.x, per = G / 8, rem = G % 8;
-        const int xcd = b & 7, k = b >> 3;
-        b = xcd * per + (xcd < rem ? xcd : rem) + k;
-    }
-    const int ix = b % A.nsx;
+    int ix, iy, th;
+    wf_strip(A, ix, iy, th);
     const int32_t x0 = wf_xb(A, ix), x1 = wf_xb(A, ix + 1);
     const int32_t gx0 = A.G.X0 + x0;
     const bool interior = gx0 - 5 >= 0 && gx0 + (x1 - x0) + 4 <= A.G.Nx && A.G.Nx > SMALL_LDS;
@@ -613,9 +651,38 @@ bool wf_fast(const Block *blocks) {
     return true;
 }
 
+// compute units of the current device (the turned layout runs its strips in one round)
+static int cu_count() {
+    static const int n = [] {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 0;
+        return c;
+    }();
+    return n;
+}
+// SV_WF_TURN=0: the plain layout (A/B and tests), read per call
+static bool turn_off() {
+    const char *e = std::getenv("SV_WF_TURN");
+    return e && e[0] == '0';
+}
+
+// the inverse of s -> A s + C mod 2^128 (A odd): s -> A^-1 s - A^-1 C; A^-1 by Newton's iteration, each step doubling
+// the bits that are right (A A = 1 mod 8 to start)
+static Affine inverse(const Affine &f) {
+    u128 x = f.A;
+    for (int i = 0; i < 6; i++) {
+        const u128 ax = mul(f.A, x);
+        const u128 two_minus = add(u128{~ax.lo, ~ax.hi}, u128{3, 0});  // 2 - ax = ~ax + 1 + 2
+        x = mul(x, two_minus);
+    }
+    const u128 xc = mul(x, f.C);
+    return Affine{x, add(u128{~xc.lo, ~xc.hi}, u128{1, 0})};
+}
+
 void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int64_t *m_in, const int64_t *v_in,
-               int64_t *m_out, int64_t *v_out, const Block *blocks, const uint32_t *skips, bool general,
-               const JumpTables *T, const Affine adv[6], void *pstat, void *cstat, DevScratch S, uint32_t sweep,
+               int64_t *m_out, int64_t *v_out, const Block *blocks, const Block *hblocks, const uint32_t *skips, bool general,
+               const JumpTables *T, const Affine adv[6], u128 inc, void *pstat, void *cstat, DevScratch S, uint32_t sweep,
                hipStream_t stream) {
     if ((int64_t)G.Nt * G.Nx >= (int64_t(1) << 31))
         throw std::invalid_argument("worldline_step_fused addresses stream positions with 31 bits (V < 2^31)");
@@ -629,13 +696,35 @@ void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
     const int nw = wf_nw(G.Ht, A.nsx);
     A.TH = wf_th(G.Ht, A.nsx, nw);
     A.nsy = (G.Ht + A.TH - 1) / A.TH;
+    A.rot = A.ths = A.nsy_s = 0;
+    const bool tile = !(G.T0 == 0 && G.X0 == 0 && G.Ht == G.Nt && G.Wt == G.Nx && G.pitch == G.Nx && G.org == 0);
+    if (!tile && nw == 16 && G.Nx > SMALL_LDS && A.nsx >= 3 && !turn_off()) {
+        // the turned layout: strip 0 = [-rot, W - rot) holds the column seam (W = Nx / nsx); the other strips' regions
+        // stay within [0, Nx) (rot >= 5 and W - rot >= 5)
+        const int32_t W0 = G.Nx / A.nsx, rot = W0 / 2;
+        const int32_t ths = 25, nsy_s = (G.Ht + ths - 1) / ths;
+        if (rot >= 5 && W0 - rot >= 5 && (int64_t)(A.nsx - 1) * A.nsy + nsy_s <= cu_count()) {
+            A.rot = rot;
+            A.ths = ths;
+            A.nsy_s = nsy_s;
+        }
+    }
+    const int grid = A.ths ? (A.nsx - 1) * A.nsy + A.nsy_s : A.nsx * A.nsy;
     A.m_in = m_in;
     A.v_in = v_in;
     A.m_out = m_out;
     A.v_out = v_out;
     A.blocks = blocks;
+    for (int i = 0; i < 8; i++) A.blk[i] = hblocks[i];
     A.T = T;
     for (int i = 0; i < 3; i++) A.adv[i] = nw == 16 ? compose(adv[3 + i], adv[3 + i]) : adv[(nw == 8 ? 3 : 0) + i];
+    {
+        // NW rows on across the row seam moves a row's stream position back by V - NW N draws ((V - NW N) / 4 words;
+        // N even, so both are whole): the inverse of the forward maps
+        const uint64_t V = (uint64_t)G.Nt * (uint64_t)G.Nx, fw = (uint64_t)nw * (uint64_t)G.Nx;
+        A.adv[3] = V > fw ? inverse(host_power(inc, V - fw)) : Affine{{1, 0}, {0, 0}};
+        A.adv[4] = V > fw ? inverse(host_power(inc, (V - fw) / 4)) : Affine{{1, 0}, {0, 0}};
+    }
     A.pstat = (StatStripe *)pstat;
     A.cstat = (StatStripe *)cstat;
     A.S = S;
@@ -661,16 +750,15 @@ void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
     A.it = (int32_t)it;
     A.kt = (uint32_t)(2 * it);
     A.thrt = (uint32_t)((0u - A.kt) % A.kt);
-    const bool tile = !(G.T0 == 0 && G.X0 == 0 && G.Ht == G.Nt && G.Wt == G.Nx && G.pitch == G.Nx && G.org == 0);
     if (nw == 16) {
-        if (tile) worldline_step_fused<true, 16><<<A.nsx * A.nsy, 16 * 64, 0, stream>>>(A);
-        else worldline_step_fused<false, 16><<<A.nsx * A.nsy, 16 * 64, 0, stream>>>(A);
+        if (tile) worldline_step_fused<true, 16><<<grid, 16 * 64, 0, stream>>>(A);
+        else worldline_step_fused<false, 16><<<grid, 16 * 64, 0, stream>>>(A);
     } else if (nw == 8) {
-        if (tile) worldline_step_fused<true, 8><<<A.nsx * A.nsy, 8 * 64, 0, stream>>>(A);
-        else worldline_step_fused<false, 8><<<A.nsx * A.nsy, 8 * 64, 0, stream>>>(A);
+        if (tile) worldline_step_fused<true, 8><<<grid, 8 * 64, 0, stream>>>(A);
+        else worldline_step_fused<false, 8><<<grid, 8 * 64, 0, stream>>>(A);
     } else {
-        if (tile) worldline_step_fused<true, 4><<<A.nsx * A.nsy, 4 * 64, 0, stream>>>(A);
-        else worldline_step_fused<false, 4><<<A.nsx * A.nsy, 4 * 64, 0, stream>>>(A);
+        if (tile) worldline_step_fused<true, 4><<<grid, 4 * 64, 0, stream>>>(A);
+        else worldline_step_fused<false, 4><<<grid, 4 * 64, 0, stream>>>(A);
     }
 }
 
