@@ -106,26 +106,43 @@ if mode == 'worldline':
         per, rem = G // 8, G % 8
         b = (idx & 7) * per + np.minimum(idx & 7, rem) + (idx >> 3)
         nsy = (L + 40) // 41
-        if G != nsx * nsy:  # the turned layout: nsx - 1 interior columns of nsy strips, then the seam strips
-            ni = nsx - 1
-            ix = np.where(b < ni * nsy, 1 + b % ni, 0)
-            iy = np.where(b < ni * nsy, b // ni, b - ni * nsy)
+        ni = nsx - 1
+        tail = G == ni * (nsy + 1) + (L + 24) // 25  # the turned layout with the last row strip cut in two
+        turned = tail or G == ni * nsy + (L + 24) // 25
+        t0 = np.zeros(G, dtype=np.int64)
+        th = np.full(G, 41)
+        if turned:
+            ny = nsy - 1 if tail else nsy
+            ix = np.where(b < ni * ny, 1 + b % ni, 0)
+            t0 = np.where(b < ni * ny, (b // ni) * 41, 0)
+            if tail:
+                kk = b - ni * ny
+                inr = (b >= ni * ny) & (b < ni * (ny + 2))
+                half = (L - ny * 41 + 1) // 2
+                ix = np.where(inr, 1 + kk % ni, ix)
+                t0 = np.where(inr, ny * 41 + (kk // ni) * half, t0)
+                th = np.where(inr, half, th)
+            seam = b >= ni * (ny + 2 if tail else ny)
+            t0 = np.where(seam, (b - ni * (ny + 2 if tail else ny)) * 25, t0)
+            th = np.where(seam, 25, th)
         else:
-            ix, iy = b % nsx, b // nsx
+            ix, t0 = b % nsx, (b // nsx) * 41
+        t1 = np.minimum(t0 + th, L)
+        iy = t0  # (printed as the strip's first row)
         tt = t[idx]
-        t0 = int(tt[:, 0].min())
-        e, l0, l1, x = [(tt[:, i].astype(np.int64) - t0) * 0.01 for i in range(4)]
-        edge = (ix == 0) | ((ix == nsx - 1) & (G == nsx * nsy))
-        redge = (iy == 0) | (iy == np.where(ix == 0, iy[ix == 0].max(), iy[ix != 0].max()))
+        t0_ = int(tt[:, 0].min())
+        e, l0, l1, x = [(tt[:, i].astype(np.int64) - t0_) * 0.01 for i in range(4)]
+        edge = (ix == 0) | ((ix == nsx - 1) & (not turned))
+        redge = (t0 == 0) | (t1 == L)
         for nm, sel in (('interior', ~edge & ~redge), ('seam columns', edge & ~redge), ('seam rows', ~edge & redge),
                         ('corners', edge & redge)):
             if sel.any():
                 print(f'[worldline L={L} call {k}] {nm}: n={int(sel.sum())} loop p50 {np.median((l1 - l0)[sel]):.1f} '
                       f'max {(l1 - l0)[sel].max():.1f}; prologue p50 {np.median((l0 - e)[sel]):.2f} (to bases '
-                      f'{np.median(((tt[:, 5].astype(np.int64) - t0) * 0.01 - e)[sel]):.2f}); epilogue p50 '
+                      f'{np.median(((tt[:, 5].astype(np.int64) - t0_) * 0.01 - e)[sel]):.2f}); epilogue p50 '
                       f'{np.median((x - l1)[sel]):.2f}; exit p50 {np.median(x[sel]):.1f} max {x[sel].max():.1f}', flush=True)
         last = np.argsort(x)[-8:]
-        print(f'[worldline L={L} call {k}] last exits (ix, iy, xcd, entry, loop, exit): ' + ' '.join(
+        print(f'[worldline L={L} call {k}] last exits (ix, first row, xcd, entry, loop, exit): ' + ' '.join(
             f'({ix[j]},{iy[j]},{int((tt[j, 4] >> 32) & 0xF)},{e[j]:.1f},{(l1 - l0)[j]:.1f},{x[j]:.1f})' for j in last),
             flush=True)
     sys.exit(0)

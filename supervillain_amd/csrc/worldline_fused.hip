@@ -48,6 +48,9 @@ struct WFArgs {
     // torus's column seam, in nsy_s row strips of ths rows (2 row steps: the seam strip's MODE 1 draws cost ~10% more
     // a row step); ths = 0: the plain layout (strip 0 at column 0, the last strip's region wrapping as well)
     int32_t rot, ths, nsy_s;
+    // with the turned layout: the last interior row strip (fewer rows, and measured slowest) cut in two strips of
+    // tail rows (2 row steps each); 0: not cut
+    int32_t tail;
     const int64_t *m_in;
     const int64_t *v_in;
     int64_t *m_out;
@@ -77,21 +80,29 @@ struct WFArgs {
 __device__ __forceinline__ int32_t wf_xb(const WFArgs &A, int ix) {
     return (int32_t)((int64_t)ix * A.G.Wt / A.nsx) - A.rot;
 }
-// launch slot -> strip (column ix, row iy, rows per strip); slots are dealt to the XCDs in contiguous runs
-__device__ __forceinline__ void wf_strip(const WFArgs &A, int &ix, int &iy, int &th) {
+// launch slot -> strip (column ix, rows [t0, t1)); slots are dealt to the XCDs in contiguous runs
+__device__ __forceinline__ void wf_strip(const WFArgs &A, int &ix, int32_t &t0, int32_t &t1) {
     int b = blockIdx.x;
     {
         const int G = gridDim.x, per = G / 8, rem = G % 8;
         const int xcd = b & 7, k = b >> 3;
         b = xcd * per + (xcd < rem ? xcd : rem) + k;
     }
+    int32_t th;
     if (A.ths) {
-        const int ni = A.nsx - 1;
-        if (b < ni * A.nsy) ix = 1 + b % ni, iy = b / ni, th = A.TH;
-        else ix = 0, iy = b - ni * A.nsy, th = A.ths;
+        const int ni = A.nsx - 1, ny = A.tail ? A.nsy - 1 : A.nsy;
+        if (b < ni * ny) {
+            ix = 1 + b % ni, th = A.TH, t0 = (b / ni) * th;
+        } else if (b < ni * (ny + 2) && A.tail) {
+            const int k = b - ni * ny;
+            ix = 1 + k % ni, th = A.tail, t0 = ny * A.TH + (k / ni) * th;
+        } else {
+            ix = 0, th = A.ths, t0 = (b - ni * (A.tail ? ny + 2 : ny)) * th;
+        }
     } else {
-        ix = b % A.nsx, iy = b / A.nsx, th = A.TH;
+        ix = b % A.nsx, th = A.TH, t0 = (b / A.nsx) * th;
     }
+    t1 = t0 + th < A.G.Ht ? t0 + th : A.G.Ht;
 }
 
 // The plaquette pass's acceptance min(1, exp(-dS)), dS = dfk ((((f1 + f2) - f3) - f4) + 2 df) (plaquette.py via
@@ -147,12 +158,11 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     const int32_t N = Gm.Nx, Nt = Gm.Nt;  // global row length (stream layout) and row count
     const int64_t V = Gm.plane;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
-    int ix, iy, TH;
-    wf_strip(A, ix, iy, TH);
+    int ix;
+    int32_t t0, t1;
+    wf_strip(A, ix, t0, t1);
     const int32_t x0 = wf_xb(A, ix), x1 = wf_xb(A, ix + 1);
     const int32_t w = x1 - x0;
-    const int32_t t0 = iy * TH;
-    const int32_t t1 = t0 + TH < Gm.Ht ? t0 + TH : Gm.Ht;
     const int32_t rbase = t0 - 5;  // local row 0
     const int32_t cols = w + 9;
     const int32_t cofs = x0 - 5;   // LDS column of lattice column x is x - cofs
@@ -575,8 +585,9 @@ constexpr int WF_OCC8 = 2;
 template <bool TILE, int NW>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 8 ? WF_OCC8 : 1))) void worldline_step_fused(WFArgs A) {
     __shared__ WFLDS<NW> Ls;
-    int ix, iy, th;
-    wf_strip(A, ix, iy, th);
+    int ix;
+    int32_t t0, t1;
+    wf_strip(A, ix, t0, t1);
     const int32_t x0 = wf_xb(A, ix), x1 = wf_xb(A, ix + 1);
     const int32_t gx0 = A.G.X0 + x0;
     const bool interior = gx0 - 5 >= 0 && gx0 + (x1 - x0) + 4 <= A.G.Nx && A.G.Nx > SMALL_LDS;
@@ -667,6 +678,12 @@ static bool turn_off() {
     return e && e[0] == '0';
 }
 
+// SV_WF_TAIL=0: the last row strip not cut (A/B), read per call
+static bool tail_off() {
+    const char *e = std::getenv("SV_WF_TAIL");
+    return e && e[0] == '0';
+}
+
 // the inverse of s -> A s + C mod 2^128 (A odd): s -> A^-1 s - A^-1 C; A^-1 by Newton's iteration, each step doubling
 // the bits that are right (A A = 1 mod 8 to start)
 static Affine inverse(const Affine &f) {
@@ -696,7 +713,7 @@ void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
     const int nw = wf_nw(G.Ht, A.nsx);
     A.TH = wf_th(G.Ht, A.nsx, nw);
     A.nsy = (G.Ht + A.TH - 1) / A.TH;
-    A.rot = A.ths = A.nsy_s = 0;
+    A.rot = A.ths = A.nsy_s = A.tail = 0;
     const bool tile = !(G.T0 == 0 && G.X0 == 0 && G.Ht == G.Nt && G.Wt == G.Nx && G.pitch == G.Nx && G.org == 0);
     if (!tile && nw == 16 && G.Nx > SMALL_LDS && A.nsx >= 3 && !turn_off()) {
         // the turned layout: strip 0 = [-rot, W - rot) holds the column seam (W = Nx / nsx); the other strips' regions
@@ -707,9 +724,12 @@ void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
             A.rot = rot;
             A.ths = ths;
             A.nsy_s = nsy_s;
+            const int32_t rest = G.Ht - (A.nsy - 1) * A.TH, tail = (rest + 1) / 2;
+            if (A.nsy >= 2 && tail + 7 <= 32 && (int64_t)(A.nsx - 1) * (A.nsy + 1) + nsy_s <= cu_count() && !tail_off())
+                A.tail = tail;
         }
     }
-    const int grid = A.ths ? (A.nsx - 1) * A.nsy + A.nsy_s : A.nsx * A.nsy;
+    const int grid = A.ths ? (A.nsx - 1) * (A.tail ? A.nsy + 1 : A.nsy) + A.nsy_s : A.nsx * A.nsy;
     A.m_in = m_in;
     A.v_in = v_in;
     A.m_out = m_out;

@@ -47,19 +47,22 @@ def test_turned_layout_forced_rejection_at_config3(which, oracle_lib):
 @pytest.mark.parametrize('N,W', [(1024, 1.0), (960, 2.0), (1024, 0.5)])
 def test_turned_layout_equals_plain_layout(N, W, monkeypatch):
     """70 steps (across the 64-step batch) from a random v: the turned layout's fields, accepted counts, acceptance
-    sums and NumPy state equal the plain layout's (SV_WF_TURN=0, read per call) bit for bit."""
+    sums and NumPy state, with and without the last row strip cut in two (SV_WF_TAIL=0), equal the plain layout's
+    (SV_WF_TURN=0; both read per call) bit for bit."""
     v0 = np.random.default_rng(N).integers(-3, 4, (N, N)).astype(np.int64)
     m0 = np.zeros((2, N, N), dtype=np.int64)
     out = {}
-    for turn in ('1', '0'):
+    for turn, tail in (('1', '1'), ('1', '0'), ('0', '1')):
         monkeypatch.setenv('SV_WF_TURN', turn)
+        monkeypatch.setenv('SV_WF_TAIL', tail)
         gen = np.random.default_rng(9)
         m, v, st = _worldline_run(N, 0.5, W, m0, v0, 70, gen)
-        out[turn] = (m, v, [(s.accepted, s.acceptance_sum, s.rejections) for s in st], gen.bit_generator.state)
-    a, b = out['1'], out['0']
-    assert (a[0] == b[0]).all() and (a[1] == b[1]).all()
-    assert [x[0] for x in a[2]] == [x[0] for x in b[2]]
-    assert [x[2] for x in a[2]] == [x[2] for x in b[2]]
-    # (the float acceptance sums add the strips' partial sums in another order: equal within rounding)
-    np.testing.assert_allclose([x[1] for x in a[2]], [x[1] for x in b[2]], rtol=1e-12)
-    assert a[3] == b[3]
+        out[turn + tail] = (m, v, [(s.accepted, s.acceptance_sum, s.rejections) for s in st], gen.bit_generator.state)
+    for key in ('11', '10'):
+        a, b = out[key], out['01']
+        assert (a[0] == b[0]).all() and (a[1] == b[1]).all(), key
+        assert [x[0] for x in a[2]] == [x[0] for x in b[2]], key
+        assert [x[2] for x in a[2]] == [x[2] for x in b[2]], key
+        # (the float acceptance sums add the strips' partial sums in another order: equal within rounding)
+        np.testing.assert_allclose([x[1] for x in a[2]], [x[1] for x in b[2]], rtol=1e-12)
+        assert a[3] == b[3], key
