@@ -32,6 +32,9 @@
 // it composes with (r4: the last three with u53's one-shift form 221.8 / 225.3 -> 218.7 / 221.2 us per L=4096 sweep).
 // The counter-based kernel (29.5 KB of LDS, 81 VGPRs) runs at 4 waves per SIMD: 4, 5 and 6 measured flat (r336).
 
+#ifndef SV_HOT_SC1
+#define SV_HOT_SC1 0  // A/B: the domain tiles' row stores write-through (global_store sc1; the whole lattice: slower, r5)
+#endif
 #ifndef SV_WGTIME
 #define SV_WGTIME 0  // timing experiments: per-workgroup timestamps (sv_debug_wgtime)
 #endif
@@ -522,7 +525,15 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
                 if (cc < w) {
                     const int cx = FR ? cc : cc + 2;
                     const int64_t g = g0 + cc;
-                    if (OFF32) {
+                    if (OFF32 && SV_HOT_SC1 && TILE && !BAND) {
+                        const uint32_t o = ((uint32_t)g0 + (uint32_t)cc) * 8u;
+                        __hip_atomic_store((double *)((char *)phi_out + o), s_phi[slot][cx], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store((int64_t *)((char *)n_out + o), (int64_t)s_n0[slot][cx], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store((int64_t *)((char *)n_out + (o + (uint32_t)V * 8u)), (int64_t)s_n1[slot][cx],
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    } else if (OFF32) {
                         const uint32_t o = ((uint32_t)g0 + (uint32_t)cc) * 8u;
                         *(double *)((char *)phi_out + o) = s_phi[slot][cx];
                         *(int64_t *)((char *)n_out + o) = (int64_t)s_n0[slot][cx];
