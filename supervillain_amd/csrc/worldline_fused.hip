@@ -288,10 +288,13 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
                                            __HIP_MEMORY_SCOPE_AGENT);
                         continue;
                     }
-                    const uint32_t o = ((uint32_t)g0 + (uint32_t)cc2) * 8u;
-                    *(int64_t *)((char *)A.m_out + o) = (int64_t)s_m0[slot][cc2 + 5];
-                    *(int64_t *)((char *)A.m_out + (o + (uint32_t)V * 8u)) = (int64_t)s_m1[slot][cc2 + 5];
-                    *(int64_t *)((char *)A.v_out + o) = (int64_t)s_v[slot][cc2 + 5];
+                    const uint32_t o = ((uint32_t)g0 + (uint32_t)cc2) * 8u;  // (a tile: write-through as well)
+                    __hip_atomic_store((int64_t *)((char *)A.m_out + o), (int64_t)s_m0[slot][cc2 + 5], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store((int64_t *)((char *)A.m_out + (o + (uint32_t)V * 8u)), (int64_t)s_m1[slot][cc2 + 5],
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store((int64_t *)((char *)A.v_out + o), (int64_t)s_v[slot][cc2 + 5], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
         }
