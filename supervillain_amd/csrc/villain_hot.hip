@@ -525,8 +525,8 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
                     if (OFF32 && TILE && !BAND) {
                         // a domain tile (one short launch per sweep): write-through row stores (global_store sc1) leave
                         // no dirty L2 lines for the launch's end to write back (2048 x 1024 depth 4: 49.2 -> 47.8 us
-                        // per sweep, r5); on the whole lattice (many rounds of strips) they measured slower, and level for only its last
-                        // 256-1024 workgroups (r5)
+                        // per sweep, r5); on the whole lattice (many rounds of strips) they measured slower, and level
+                        // for only its last 256-1024 workgroups (r5)
                         const uint32_t o = ((uint32_t)g0 + (uint32_t)cc) * 8u;
                         __hip_atomic_store((double *)((char *)phi_out + o), s_phi[slot][cx], __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
