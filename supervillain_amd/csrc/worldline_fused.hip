@@ -76,7 +76,8 @@ struct WFArgs {
     int32_t general;       // MODE 2 for every strip (wf_body)
 };
 
-// Column strip boundaries (uniform: narrower seam strips, whose MODE 1 row steps are ~11% longer, measured level, r4)
+// Column strip boundaries: uniform widths (narrower seam strips measured level, r4), turned left by rot (r5: the
+// seam strip column then runs in short row strips instead)
 __device__ __forceinline__ int32_t wf_xb(const WFArgs &A, int ix) {
     return (int32_t)((int64_t)ix * A.G.Wt / A.nsx) - A.rot;
 }
