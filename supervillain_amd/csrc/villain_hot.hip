@@ -32,9 +32,6 @@
 // it composes with (r4: the last three with u53's one-shift form 221.8 / 225.3 -> 218.7 / 221.2 us per L=4096 sweep).
 // The counter-based kernel (29.5 KB of LDS, 81 VGPRs) runs at 4 waves per SIMD: 4, 5 and 6 measured flat (r336).
 
-#ifndef SV_FR_SC1
-#define SV_FR_SC1 0  // A/B: the replica batches' row stores write-through
-#endif
 #ifndef SV_WGTIME
 #define SV_WGTIME 0  // timing experiments: per-workgroup timestamps (sv_debug_wgtime)
 #endif
@@ -525,11 +522,11 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
                 if (cc < w) {
                     const int cx = FR ? cc : cc + 2;
                     const int64_t g = g0 + cc;
-                    if (OFF32 && (TILE || (SV_FR_SC1 && FR)) && !BAND) {
+                    if (OFF32 && TILE && !BAND) {
                         // a domain tile (one short launch per sweep): write-through row stores (global_store sc1) leave
                         // no dirty L2 lines for the launch's end to write back (2048 x 1024 depth 4: 49.2 -> 47.8 us
                         // per sweep, r5); on the whole lattice (many rounds of strips) they measured slower, and level
-                        // for only its last 256-1024 workgroups (r5)
+                        // for only its last 256-1024 workgroups and for the replica batches (r5)
                         const uint32_t o = ((uint32_t)g0 + (uint32_t)cc) * 8u;
                         __hip_atomic_store((double *)((char *)phi_out + o), s_phi[slot][cx], __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
