@@ -8,14 +8,16 @@ with the fields resident in HBM.
 
   N = 1: one L x L lattice on one GPU (the single-lattice fused sweep kernel).
   N > 1: one process per GPU (torch.distributed.run; `python bench.py --gpus N` launches it itself when
-         WORLD_SIZE is unset, before anything touches a GPU).  Weak scaling (north_star: >= 0.75 weak-scaling
-         efficiency at 8 GPUs): a (ty L) x (tx L) lattice domain-decomposed into ty x tx tiles of L x L (1x2,
-         2x2, 2x4 for N = 2, 4, 8), one tile per GPU, with RCCL halo exchanges -- every GPU sweeps an L = 4096
-         tile, the headline's per-GPU work.  --strong: BASELINE config 4 instead, the ONE L x L lattice cut
-         into the N tiles (strong scaling; the chain is bit-identical to the 1-GPU chain).  Each rank also
-         times its own tile alone as a periodic lattice (R1 of SURVEY.md 8(d)'s E_N = R_N / (N R1)),
-         reported under config.weak_scaling.  --tiles TYxTX on one GPU emulates a decomposition (strong unless
-         --weak).
+         WORLD_SIZE is unset, before anything touches a GPU).  BASELINE config 4 (the default): the ONE L x L
+         lattice the metric names (L=4096) cut into ty x tx tiles (1x2, 2x2, 2x4 for N = 2, 4, 8), one per GPU,
+         with RCCL halo exchanges (strong scaling; the chain is bit-identical to the 1-GPU chain).  --weak: an
+         L x L tile per GPU of a (ty L) x (tx L) lattice instead (north_star's weak-scaling efficiency), and the
+         metric names that lattice.  --tiles TYxTX on one GPU emulates a decomposition.
+         Every domain line also carries, under config.scaling_reference, rates timed after the same warm-up as
+         the main run (warm_up: W steps, then --warmup-s seconds) over at least --steps sweeps: R1 = this rank's
+         tile alone as a periodic lattice (E_N = R_N / (N R1)), and the single-lattice headline
+         path on one L x L lattice (the N = 1 line's kernel: for --weak the per-GPU R1, for strong the 1-GPU
+         rate of the whole problem).  An E_N above 1.02 is flagged (E_N_suspect) and printed to stderr.
 Rank 0 prints one JSON line.
 
 Secondary workloads (not the headline line; BASELINE.json configs 5 and 3):
@@ -80,9 +82,10 @@ def parse():
                          'the optional counter-based mode (SURVEY.md 8(b) sv_rng mode 1, a different chain)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-sweeps', type=int, default=5)
-    ap.add_argument('--weak', action='store_true', help='an L x L tile per GPU (weak scaling: the default for N > 1; '
-                                                        'with --tiles on one GPU, emulate that layout)')
-    ap.add_argument('--strong', action='store_true', help='N > 1: one L x L lattice decomposed over the N GPUs '
+    ap.add_argument('--weak', action='store_true', help='an L x L tile per GPU of a (ty L) x (tx L) lattice (weak '
+                                                        'scaling; with --tiles on one GPU, emulate that layout); the '
+                                                        'metric then names that lattice')
+    ap.add_argument('--strong', action='store_true', help='(the default) one L x L lattice decomposed over the N GPUs '
                                                           '(BASELINE config 4, strong scaling)')
     ap.add_argument('--warmup-s', type=float, default=1.0,
                     help='after the W warmup steps, keep warming (untimed) until this many seconds have passed: '
@@ -102,9 +105,8 @@ def parse():
     args = ap.parse_args()
     if args.strong and args.weak:
         ap.error('--strong and --weak exclude each other')
-    # weak scaling for N > 1 unless --strong; a one-GPU --tiles emulation is strong (config 4) unless --weak
-    gpus = args.gpus if args.gpus is not None else int(os.environ.get('WORLD_SIZE', '1'))
-    args.strong = args.strong or (gpus <= 1 and not args.weak)
+    # BASELINE config 4 (one L x L lattice over the GPUs, strong scaling) unless --weak
+    args.strong = not args.weak
     if args.workload in ('replicas', 'worms'):
         args.L = 128 if args.L == 4096 else args.L
         args.W = 2 if args.W == 1 else args.W
@@ -194,8 +196,34 @@ def kernel_time(Lib, ctx):
     return ms.value / 1e3 / max(launches.value, 1)
 
 
+HEADLINE_METRIC = 'lattice-site updates/sec (sweeps/s × L²), L=4096 Villain, 1→8 MI355X'  # BASELINE.json
+
+
+def lattice_metric(Nt, Nx, model='Villain', weak_tile=None,
+                   head='lattice-site updates/sec (sweeps/s × L²)', tail=', 1→8 MI355X'):
+    """The metric string of a line, naming the lattice it actually sweeps: BASELINE.json's metric verbatim for one
+    4096 x 4096 Villain lattice (the N = 1 headline and config 4's tiles of it), the same words with `L=N` for another
+    square lattice, and `NtxNx` (plus the per-GPU tile) for the weak-scaled lattices."""
+    if Nt == Nx and weak_tile is None:
+        return f'{head}, L={Nt} {model}{tail}'
+    what = f'{Nt}x{Nx} {model}'
+    if weak_tile is not None:
+        what += f' (weak scaling: one {weak_tile[0]}x{weak_tile[1]} tile per GPU)'
+    return f'{head.replace("L²", "Nt·Nx")}, {what}{tail}'
+
+
+def metric_lattice(metric):
+    """(Nt, Nx) named by a metric string (`L=N <model>` or `NtxNx <model>`), or None."""
+    import re
+    m = re.search(r'L=(\d+) (?:Villain|Worldline)', metric)
+    if m:
+        return int(m.group(1)), int(m.group(1))
+    m = re.search(r'(\d+)x(\d+) (?:Villain|Worldline)', metric)
+    return (int(m.group(1)), int(m.group(2))) if m else None
+
+
 def report(args, world, sites_per_step, sites_per_launch, elapsed, acc, avg_launch_s, config, traffic_L,
-           metric='lattice-site updates/sec (sweeps/s × L²), L=4096 Villain, 1→8 MI355X',
+           metric=HEADLINE_METRIC,
            unit='lattice-site updates/s', kernel='villain_sweep_hot', alg_bytes=SURVEY_BYTES_PER_SITE,
            min_bytes=FUSED_MIN_BYTES_PER_SITE, baseline=None, ctx=None, scaling=None):
     timing_source = 'hipEvents around the sweep launches'
@@ -205,8 +233,11 @@ def report(args, world, sites_per_step, sites_per_launch, elapsed, acc, avg_laun
         avg_launch_s = elapsed / max(args.steps, 1)
         timing_source = 'wall clock per step (no timed launch survived the rejections)'
     achieved = alg_bytes * sites_per_launch / avg_launch_s / 1e9
-    if 'L=4096 Villain' in metric and args.L != 4096:
-        metric = metric.replace('L=4096', f'L={args.L}')  # a non-headline size names itself
+    lat = config.get('lattice')
+    named = metric_lattice(metric)
+    if lat is not None and named is not None and tuple(lat) != named:
+        raise ValueError(f'bench.py: the metric names a {named[0]}x{named[1]} lattice but the run swept '
+                         f'{lat[0]}x{lat[1]}: {metric}')
     ceiling = copy_ceiling(ctx) if ctx is not None and not getattr(args, 'no_copy_ceiling', False) else None
     out = {
         'metric': metric,
@@ -359,7 +390,7 @@ def run_worms(args, world, rank, dist):
 def run_worldline_domain(args, world, rank, dist):
     """Config 3 decomposed (SURVEY.md 8(e)): one L x L Worldline lattice cut into ty x tx tiles (one per GPU;
     --weak: an L x L tile per GPU), one (v, m) halo exchange per Plaquette + Coexact step; R1 = one GPU running
-    one periodic tile alone, as for config 4."""
+    one periodic tile alone, as for config 4 (timed after the same warm-up, over at least --steps steps)."""
     from supervillain_amd import _native
     from supervillain_amd.domain import WorldlineDomain, tile_grid
     L = args.L
@@ -386,16 +417,13 @@ def run_worldline_domain(args, world, rank, dist):
     elapsed = max_over_ranks(dist, t1 - t0)
     avg_launch_s = kernel_time(Lib, dom.ctx)
     acc = sum(st[2 * i].accepted for i in range(args.steps)) / (args.steps * Nt * Nx)
+    rej = sum(s.rejections for s in st)
     ctx = dom.ctx
     dom.close()
     one = WorldlineDomain(Ht, Wt, (1, 1), **kw)
     one.cold()
     g1 = np.random.default_rng(1)
-    one.run(max(args.warmup, 5), g1)
-    k1 = max(args.steps, 20)
-    t = time.perf_counter()
-    one.run(k1, g1)
-    r1 = Ht * Wt * k1 / (time.perf_counter() - t)
+    r1, _ = timed_rate(lambda k: one.run(k, g1), Ht * Wt, args, dist)
     one.close()
     r1_mean = r1 if dist is None else _mean_over_ranks(dist, r1)
     if rank == 0:
@@ -405,11 +433,11 @@ def run_worldline_domain(args, world, rank, dist):
                               '(one per GPU), (v, m) halo exchange per step, bit-exact PCG64 replay',
                   'L': L, 'lattice': [Nt, Nx], 'tiles': [ty, tx], 'path': 'worldline-domain',
                   'parallelism': f'{ty}x{tx} domain decomposition over {world} GPU(s)',
-                  'weak_scaling': {'tile': [Ht, Wt], 'R1': r1_mean, 'E_N': value / (world * r1_mean),
-                                   'definition': 'E_N = R_N / (N R1), R1 = one GPU running one periodic tile '
-                                                 'of this size alone (SURVEY.md 8(d))'}}
+                  'lemire_rejections_in_timed_steps': int(rej),
+                  'scaling_reference': scaling_reference(value, world, r1_mean, [Ht, Wt], None, None, 'steps')}
         report(args, world, Nt * Nx, Nt * Nx // world, elapsed, acc, avg_launch_s, config, Ht,
-               metric=f'plaquette-steps/sec (Plaquette + Coexact sweep), L={L} Worldline, W={args.W}',
+               metric=lattice_metric(Nt, Nx, 'Worldline', None if args.strong else [Ht, Wt],
+                                     head='plaquette-steps/sec (Plaquette + Coexact sweep)', tail=f', W={args.W}'),
                unit='plaquette-steps/s', kernel='worldline_step_fused', alg_bytes=WORLDLINE_BYTES,
                min_bytes=WORLDLINE_BYTES, ctx=ctx)
 
@@ -495,7 +523,7 @@ def run_worldline(args, world, rank, dist):
             config = {'workload': f'L={L} Worldline: reference-order PlaquetteUpdate (the NumPy RandomState visit '
                                   'permutation, plaquette.py:35-104, bit-exact) + CoexactUpdate sweep per step, '
                                   f'W={args.W}, kappa={args.kappa}, PCG64 replay; level-scheduled launches',
-                      'L': L, 'path': 'worldline-reference-order', 'parallelism': 'single GPU',
+                      'L': L, 'lattice': [L, L], 'path': 'worldline-reference-order', 'parallelism': 'single GPU',
                       'visit_order': 'native MT19937 permutation (sv_mt19937_permutation), drawn on host threads while '
                                      'the device runs the previous steps'}
             # no single dominant kernel: the roofline line prices the whole step (both sweeps, 168 B) by its wall time
@@ -504,7 +532,7 @@ def run_worldline(args, world, rank, dist):
             config = {'workload': f'L={L} Worldline: checkerboard PlaquetteUpdate + CoexactUpdate sweep per step, '
                                   f'W={args.W}, kappa={args.kappa}, bit-exact PCG64 replay (one worldline_step_fused '
                                   'launch per step)',
-                      'L': L, 'path': 'worldline', 'parallelism': 'single GPU'}
+                      'L': L, 'lattice': [L, L], 'path': 'worldline', 'parallelism': 'single GPU'}
         report(args, world, world * L * L, L * L, elapsed, acc / (args.steps * L * L), step_kernel_s, config, L,
                metric=f'plaquette-steps/sec (Plaquette + Coexact sweep), L={L} Worldline, W={args.W}',
                unit='plaquette-steps/s',
@@ -620,6 +648,65 @@ def run_local(args, world, rank, dist):
     (Lib.sv_worldline_destroy if worldline else Lib.sv_villain_destroy)(h)
 
 
+def timed_rate(run, sites, args, dist):
+    """Sites per second of `run(k)` (k sweeps) after the main run's warm-up (warm_up: W steps, then --warmup-s
+    seconds), over max(--steps, 20) sweeps; returns (rate, run's result)."""
+    warm_up(run, args, dist)
+    k = max(args.steps, 20)
+    t = time.perf_counter()
+    out = run(k)
+    return sites * k / (time.perf_counter() - t), out
+
+
+def single_lattice_rate(L, args, dist):
+    """The N = 1 headline path (sv_villain_run on one periodic L x L lattice, villain_sweep_hot) on this rank's
+    GPU: (site-updates/s, NumPy Lemire rejections in the timed sweeps)."""
+    from supervillain_amd import _native
+    from supervillain_amd._abi import rng_from_numpy
+    Lib = _native.lib()
+    ctx = _native.context(_native.default_device())
+    h = ctypes.c_void_p()
+    ctx.check(Lib.sv_villain_create(ctx.handle, L, ctypes.byref(h)), 'sv_villain_create')
+    try:
+        ctx.check(Lib.sv_villain_upload(h, _native.ptr(np.zeros((L, L))), _native.ptr(np.zeros((2, L, L), np.int64))),
+                  'upload')
+        r = rng_from_numpy(np.random.default_rng(1))
+
+        def run(k):
+            st = _native.stats_array(k)
+            ctx.check(Lib.sv_villain_run(h, args.kappa, args.W, float(np.pi), 1, k, ctypes.byref(r), st, 2),
+                      'sv_villain_run')
+            return sum(st[i].rejections for i in range(k))
+
+        return timed_rate(run, L * L, args, dist)
+    finally:
+        Lib.sv_villain_destroy(h)
+
+
+E_N_FLAG = 1.02  # an efficiency above this is not physical: R1 was mismeasured (VERDICT r5 weak #2)
+
+
+def scaling_reference(value, world, r1, tile, single, single_rej, unit='sweeps'):
+    """config.scaling_reference of a domain line: R1 (this tile alone), E_N = R_N / (N R1), and the single-lattice
+    headline rate beside it; flags an E_N above E_N_FLAG (also on stderr)."""
+    e = value / (world * r1)
+    out = {'tile': tile, 'R1': r1, 'E_N': e, 'E_N_suspect': e > E_N_FLAG,
+           'definition': 'E_N = R_N / (N R1), R1 = one GPU running one periodic tile of this size alone (SURVEY.md '
+                         f'8(d)), timed after the main run\'s warm-up over max(--steps, 20) {unit}, mean over ranks'}
+    if single is not None:
+        out['single_lattice_rate'] = single
+        out['single_lattice_rejections_in_timed_steps'] = single_rej
+        out['E_N_vs_single_lattice'] = value / (world * single)
+        out['single_lattice_definition'] = ('the N = 1 headline path (sv_villain_run, villain_sweep_hot) on one '
+                                            'periodic L x L lattice per GPU, mean over ranks: for --weak the per-GPU R1 '
+                                            'of the headline kernel, for strong scaling the one-GPU rate of the whole '
+                                            'lattice')
+    if e > E_N_FLAG:
+        print(f'bench.py: E_N = {e:.3f} > {E_N_FLAG} (R1 = {r1:.4g}): the tile-alone reference is suspect',
+              file=sys.stderr, flush=True)
+    return out
+
+
 def run_domain(args, world, rank, local, dist):
     """N > 1 (or --tiles on one GPU): BASELINE config 4, one lattice domain-decomposed, RCCL halos."""
     from supervillain_amd import _native
@@ -651,20 +738,20 @@ def run_domain(args, world, rank, local, dist):
     elapsed = max_over_ranks(dist, t1 - t0)
     avg_launch_s = kernel_time(Lib, dom.ctx)
     acc = sum(s.accepted for s in st) / (args.steps * Nt * Nx)
+    rej = sum(s.rejections for s in st)
     ctx = dom.ctx
     dom.close()
 
-    # R1: this rank's tile alone, as a periodic Ht x Wt lattice on its own GPU, no exchange
+    # R1: this rank's tile alone, as a periodic Ht x Wt lattice on its own GPU, no exchange, timed
+    # after the same warm-up as the main run; then the single-lattice headline path on one L x L lattice
     one = VillainDomain(Ht, Wt, (1, 1), **kw)
     one.cold()
     g1 = np.random.default_rng(1)
-    one.run(max(args.warmup, 5), g1)
-    k1 = max(args.steps, 20)
-    t = time.perf_counter()
-    one.run(k1, g1)
-    r1 = Ht * Wt * k1 / (time.perf_counter() - t)
+    r1, _ = timed_rate(lambda k: one.run(k, g1), Ht * Wt, args, dist)
     one.close()
     r1_mean = r1 if dist is None else _mean_over_ranks(dist, r1)
+    single, single_rej = single_lattice_rate(L, args, dist)
+    single_mean = single if dist is None else _mean_over_ranks(dist, single)
 
     if rank == 0:
         value = args.steps * Nt * Nx / elapsed
@@ -674,12 +761,13 @@ def run_domain(args, world, rank, local, dist):
                   'L': L, 'lattice': [Nt, Nx], 'tiles': [ty, tx], 'path': 'domain',
                   # deep halos: K sweeps per halo exchange, ghost frame 2K / 3K deep
                   'sweeps_per_halo_exchange': ghost_frame(Nt, Nx, (ty, tx))[0] // 2,
-                  'parallelism': f'{ty}x{tx} domain decomposition over {world} GPU(s)',
-                  'weak_scaling': {'tile': [Ht, Wt], 'R1': r1_mean,
-                                   'E_N': value / (world * r1_mean),
-                                   'definition': 'E_N = R_N / (N R1), R1 = one GPU running one periodic tile '
-                                                 'of this size alone (SURVEY.md 8(d))'}}
-        report(args, world, Nt * Nx, Nt * Nx // world, elapsed, acc, avg_launch_s, config, Ht, ctx=ctx)
+                  'parallelism': f'{ty}x{tx} domain decomposition over {world} GPU(s)' +
+                                 ('' if world > 1 else ' (emulated: every tile on this GPU in turn)'),
+                  'lemire_rejections_in_timed_steps': int(rej),
+                  'scaling_reference': scaling_reference(value, world, r1_mean, [Ht, Wt], single_mean, int(single_rej))}
+        report(args, world, Nt * Nx, Nt * Nx // world, elapsed, acc, avg_launch_s, config, Ht, ctx=ctx,
+               metric=lattice_metric(Nt, Nx, weak_tile=None if args.strong else [Ht, Wt]),
+               kernel='villain_sweep_hot (tile)')
 
 
 def _mean_over_ranks(dist, x):
@@ -769,6 +857,8 @@ def main():
 
     warm_up(run, args)
     Lib.sv_ctx_set_timing(ctx.handle, 2 if args.event_timing == 'launch' else 1)
+    Lib.sv_ctx_block_counts(ctx.handle, None, None)  # (reset: count the timed sweeps' kernels only)
+    Lib.sv_ctx_band_counts(ctx.handle, None, None)
     t0 = time.perf_counter()
     st = run(args.steps)  # synchronous on return (stream synchronized)
     t1 = time.perf_counter()
@@ -785,12 +875,27 @@ def main():
     chain = ('bit-exact reference chain (PCG64 replay), fused two-colour sweep kernel (villain_sweep_hot)'
              if args.rng == 'pcg64' else 'counter-based Philox4x32-10 mode (a different chain from the reference\'s), '
              'fused two-colour sweep kernel (villain_sweep_hot_ph)')
+    # which kernel ran the timed sweeps: small lattices run K sweeps per launch (temporal blocks,
+    # villain_sweep_block; or the XCD bands, villain_sweep_hot_band), the rest villain_sweep_hot
+    blk, band = ctypes.c_int64(), ctypes.c_int64()
+    Lib.sv_ctx_block_counts(ctx.handle, ctypes.byref(blk), None)
+    Lib.sv_ctx_band_counts(ctx.handle, ctypes.byref(band), None)
+    kernel = 'villain_sweep_hot'
+    if args.rng == 'philox':
+        kernel = 'villain_sweep_hot_ph'
+    elif blk.value > 0:
+        kernel = 'villain_sweep_block'
+        chain = chain.replace('fused two-colour sweep kernel (villain_sweep_hot)',
+                              'temporal blocks of K sweeps per launch (villain_sweep_block)')
+    elif band.value > 0:
+        kernel = 'villain_sweep_hot_band'
+        chain = chain.replace('(villain_sweep_hot)', '(villain_sweep_hot_band: K sweeps per launch)')
     config = {'workload': f'L={L} Villain NeighborhoodUpdate sweep, kappa={args.kappa}, W={args.W}, ' + chain,
               'rng': args.rng,
               'L': L, 'lattice': [L, L], 'path': args.path, 'parallelism': 'single GPU',
               'lemire_rejections_in_timed_steps': int(rej)}
-    report(args, 1, L * L, L * L, t1 - t0, acc, avg_launch_s, config, L, ctx=ctx,
-           kernel='villain_sweep_hot' if args.rng == 'pcg64' else 'villain_sweep_hot_ph')
+    report(args, 1, L * L, L * L, t1 - t0, acc, avg_launch_s, config, L, ctx=ctx, kernel=kernel,
+           metric=lattice_metric(L, L))
     Lib.sv_villain_destroy(h)
 
 

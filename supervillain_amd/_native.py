@@ -10,7 +10,22 @@ import threading
 from supervillain_amd._abi import SvMT19937, SvPhilox, SvRng, SvStats
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get('SV_LIB_OVERRIDE') or os.path.join(_HERE, 'libsvhip.so')  # override: timing experiments
+LIB_PATH = os.path.join(_HERE, 'libsvhip.so')
+# Timing experiments (scripts/build_variant.sh) load an instrumented build of the same sources through
+# SV_LIB_OVERRIDE; only builds under the repository's variants/ directories are accepted.
+VARIANT_DIRS = (os.path.join(_HERE, 'variants'), os.path.join(os.path.dirname(_HERE), 'variants'))
+
+
+def lib_path():
+    """The library to load: libsvhip.so beside this file, or an experiment build named by SV_LIB_OVERRIDE that lies
+    under one of VARIANT_DIRS (anything else raises NativeError)."""
+    o = os.environ.get('SV_LIB_OVERRIDE')
+    if not o:
+        return LIB_PATH
+    p = os.path.realpath(o)
+    if not any(p.startswith(os.path.realpath(d) + os.sep) for d in VARIANT_DIRS):
+        raise NativeError(f'SV_LIB_OVERRIDE={o!r}: only experiment builds under {VARIANT_DIRS} are loaded')
+    return p
 _LIB = None
 _LOCK = threading.RLock()
 _CONTEXTS = {}
@@ -28,10 +43,11 @@ def lib():
     with _LOCK:
         if _LIB is not None:
             return _LIB
-        if not os.path.exists(LIB_PATH):
-            raise NativeError(f'{LIB_PATH} is missing; build it with `python -c "import __graft_entry__ as g; g.build()"` '
+        path = lib_path()
+        if not os.path.exists(path):
+            raise NativeError(f'{path} is missing; build it with `python -c "import __graft_entry__ as g; g.build()"` '
                               '(or `make -C supervillain_amd/csrc`).  There is no CPU fallback.')
-        L = ctypes.CDLL(LIB_PATH)
+        L = ctypes.CDLL(path)
         P = ctypes.POINTER
         i32, i64, f64, vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
         L.sv_ctx_create.argtypes = [ctypes.c_int, P(vp)]

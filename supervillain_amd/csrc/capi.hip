@@ -403,7 +403,7 @@ int sv_hbm_copy(sv_ctx *ctx, int64_t bytes, int32_t width, int32_t iters, double
         for (int u : {1, 2, 4, 8}) {
             const int grid = (int)((nvec + 256 * u - 1) / (256 * u));
             auto launch = [&]() {
-#define SV_COPY(T, UU) hbm_copy<T, UU><<<grid, 256, 0, ctx->stream>>>((const T *)a, (T *)b, nvec)
+#define SV_COPY(T, UU) hbm_copy<T, UU><<<grid, 256, 0, ctx->stream>>>((const T *)a, (T *)b, nvec), SV_LAUNCHED("hbm_copy", ctx->stream)
                 if (width == 16) {
                     if (u == 1) SV_COPY(uint4, 1); else if (u == 2) SV_COPY(uint4, 2); else if (u == 4) SV_COPY(uint4, 4); else SV_COPY(uint4, 8);
                 } else {
@@ -605,6 +605,16 @@ int sv_ctx_destroy(sv_ctx *ctx) {
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return e == hipSuccess ? 0 : -2;  // (the context is gone: the caller learns only that its last work failed)
+}
+
+extern "C++" {
+namespace sv {
+void launch_failed(const char *kernel, const char *stage, hipError_t e) {
+    const std::string m = std::string("SV_SYNC_CHECK: kernel ") + kernel + " failed at " + stage + ": " + hipGetErrorString(e);
+    fprintf(stderr, "[sv] %s\n", m.c_str());
+    throw std::runtime_error(m);
+}
+}  // namespace sv
 }
 
 const char *sv_last_error(sv_ctx *ctx) { return ctx ? ctx->err.c_str() : "no context"; }

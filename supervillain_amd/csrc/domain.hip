@@ -406,7 +406,7 @@ void exchange(sv_domain *d, hipStream_t stream) {
         HaloTable HS = d->H;
         for (int s = 0; s < NDIR; s++) HS.off[s] = T.soff[s];
         halo_pack<<<grid, threads, 0, stream>>>(T.phi[slot], T.n[slot], d->pitch, d->plane, d->org, HS, T.send,
-                                                     &T.sum->abort);
+                                                     &T.sum->abort), SV_LAUNCHED("halo_pack", stream);
     }
     // remote messages (one tile per rank in RCCL mode)
     if (d->comm) {
@@ -431,7 +431,7 @@ void exchange(sv_domain *d, hipStream_t stream) {
         }
         dim3 grid((unsigned)std::min<int64_t>((mx + threads - 1) / threads, 1024), NDIR);
         halo_unpack<<<grid, threads, 0, stream>>>(T.phi[slot], T.n[slot], d->pitch, d->plane, d->org, HR, src,
-                                                       &T.sum->abort);
+                                                       &T.sum->abort), SV_LAUNCHED("halo_unpack", stream);
     }
 }
 
@@ -641,7 +641,7 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
             a.ncand = &d->tiles[li].sum->ncand;
             a.cand = d->tiles[li].sum->cand;
             const uint64_t lanes = (a.hi - a.lo + SCAN_CHUNK - 1) / SCAN_CHUNK;
-            if (lanes) scan_rejections<<<(unsigned)((lanes + 255) / 256), 256, 0, stream>>>(a);
+            if (lanes) scan_rejections<<<(unsigned)((lanes + 255) / 256), 256, 0, stream>>>(a), SV_LAUNCHED("scan_rejections", stream);
         }
     };
     // the finds of every part (gathered summaries, global tile order), sorted; false if a part overflowed
@@ -913,7 +913,7 @@ void run_wdomain(sv_domain *d, double kappa, double W_eff, int64_t it, int32_t s
                           DevScratch{&Tl.sum->abort, &Tl.sum->nreport, Tl.sum->reports}, (uint32_t)k, ctx->stream);
             d->cur = out;
         }
-        for (auto &Tl : d->tiles) wd_fold<<<(2 * count + 63) / 64, 64, 0, ctx->stream>>>(Tl.stripes, Tl.sum->stats, 2 * count);
+        for (auto &Tl : d->tiles) wd_fold<<<(2 * count + 63) / 64, 64, 0, ctx->stream>>>(Tl.stripes, Tl.sum->stats, 2 * count), SV_LAUNCHED("wd_fold", ctx->stream);
         ctx->time_end(ev, count);
         SV_HIP(hipGetLastError());
         gather(d);

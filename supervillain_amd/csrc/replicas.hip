@@ -281,7 +281,7 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         b->stage.put(ctx->stream, b->d_plan, pin.data(), R * sizeof(PlanIn));
         const int64_t nplan = (int64_t)R * count * NB;
         plan_replicas<<<(unsigned)((nplan + 255) / 256), 256, 0, ctx->stream>>>(b->d_plan, b->d_Trep, b->d_blocks, R,
-                                                                                  count, (uint64_t)V);
+                                                                                  count, (uint64_t)V), SV_LAUNCHED("plan_replicas", ctx->stream);
         B.hskip.clear();
         B.hb.clear();
         B.hmap.clear();

@@ -619,16 +619,16 @@ int64_t rejections_in(const SkipMap &skips, int sweep, int nblocks) {
 
 void launch_fused_tile(const FArgs &A, int grid, hipStream_t stream, bool hot) {
     if (hot) launch_hot(A, grid, stream);
-    else villain_sweep_fused<4, true, false, false><<<grid, 4 * 64, 0, stream>>>(A);
+    else villain_sweep_fused<4, true, false, false><<<grid, 4 * 64, 0, stream>>>(A), SV_LAUNCHED("villain_sweep_fused<4, true, false, false>", stream);
 }
 
 
 void launch_fused_batch(const FArgs &A, int grid, bool obs, hipStream_t stream) {
     const bool fr = A.nsx == 1 && A.G.Nx <= RW;  // full-row strips
-    if (obs && fr) villain_sweep_fused_obs<true><<<grid, 4 * 64, 0, stream>>>(A);
-    else if (obs) villain_sweep_fused_obs<false><<<grid, 4 * 64, 0, stream>>>(A);
-    else if (fr) villain_sweep_fused<4, false, true, true><<<grid, 4 * 64, 0, stream>>>(A);
-    else villain_sweep_fused<4, false, true, false><<<grid, 4 * 64, 0, stream>>>(A);
+    if (obs && fr) villain_sweep_fused_obs<true><<<grid, 4 * 64, 0, stream>>>(A), SV_LAUNCHED("villain_sweep_fused_obs<true>", stream);
+    else if (obs) villain_sweep_fused_obs<false><<<grid, 4 * 64, 0, stream>>>(A), SV_LAUNCHED("villain_sweep_fused_obs<false>", stream);
+    else if (fr) villain_sweep_fused<4, false, true, true><<<grid, 4 * 64, 0, stream>>>(A), SV_LAUNCHED("villain_sweep_fused<4, false, true, true>", stream);
+    else villain_sweep_fused<4, false, true, false><<<grid, 4 * 64, 0, stream>>>(A), SV_LAUNCHED("villain_sweep_fused<4, false, true, false>", stream);
 }
 
 void farg_single(FArgs &A, int nsx, int nsy) {
@@ -756,7 +756,7 @@ void reset_batch(sv_ctx *ctx, void *a, size_t a_bytes, void *b, size_t b_bytes, 
     const int64_t na = (int64_t)(a_bytes / 8), nb = (int64_t)(b_bytes / 8), n = std::max(na, nb);
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 256));
     reset_batch_kernel<<<grid, 256, 0, ctx->stream>>>(ctx->d_abort, ctx->d_nreport, (uint64_t *)a, na, (uint64_t *)b, nb,
-                                                      gate);
+                                                      gate), SV_LAUNCHED("reset_batch_kernel", ctx->stream);
 }
 
 void clear_abort(sv_ctx *ctx) {
@@ -826,15 +826,15 @@ void run_generic(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, 
             upload_plan(ctx, blocks, skipvec);
             reset_batch(ctx, ctx->d_stats, sizeof(sv_stats));
             const int grid = (int)std::min<int64_t>((V + 255) / 256, 4096);
-            villain_phi_normalize<<<grid, 256, 0, ctx->stream>>>(st->N, phi, ctx->d_abort);
-            villain_r_init<<<grid, 256, 0, ctx->stream>>>(st->N, phi, n, st->r, ctx->d_abort);
+            villain_phi_normalize<<<grid, 256, 0, ctx->stream>>>(st->N, phi, ctx->d_abort), SV_LAUNCHED("villain_phi_normalize", ctx->stream);
+            villain_r_init<<<grid, 256, 0, ctx->stream>>>(st->N, phi, n, st->r, ctx->d_abort), SV_LAUNCHED("villain_r_init", ctx->stream);
             ctx->sweeps_generic++;
             for (int col = 0; col < st->ncol; col++) {
                 int64_t nc = st->count[col];
                 if (!nc) continue;
                 villain_pass_generic<<<(int)((nc + 255) / 256), 256, 0, ctx->stream>>>(
                     P, phi, n, st->r, st->sites + st->offset[col], nc, col, ctx->d_blocks, ctx->d_skips, T,
-                    ctx->d_stats, scratch(ctx), 0u);
+                    ctx->d_stats, scratch(ctx), 0u), SV_LAUNCHED("villain_pass_generic", ctx->stream);
             }
             SV_HIP(hipGetLastError());
             AbortInfo a = read_abort(ctx);
@@ -1259,7 +1259,7 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
                 ctx->sweeps_split++;
             } else {
                 ctx->sweeps_fused++;
-                villain_sweep_fused<4, false, false, false><<<grid, 4 * 64, 0, ctx->stream>>>(A);
+                villain_sweep_fused<4, false, false, false><<<grid, 4 * 64, 0, ctx->stream>>>(A), SV_LAUNCHED("villain_sweep_fused<4, false, false, false>", ctx->stream);
             }
             if (per_launch && seg) {
                 ctx->time_end(seg, step, k);
@@ -1704,7 +1704,7 @@ int sv_villain_observables(sv_villain *st, double kappa, double *out) {
         const int64_t V = (int64_t)st->N * st->N;
         const int grid = (int)std::min<int64_t>((V + 255) / 256, 2048);
         villain_observables_kernel<<<grid, 256, 0, ctx->stream>>>(st->N, kappa / 2.0, st->phi[st->cur], st->n[st->cur],
-                                                                   d);
+                                                                   d), SV_LAUNCHED("villain_observables_kernel", ctx->stream);
         SV_HIP(hipGetLastError());
         SV_HIP(hipMemcpyAsync(st->h_obs, d, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
         SV_HIP(hipStreamSynchronize(ctx->stream));

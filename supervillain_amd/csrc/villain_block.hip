@@ -416,8 +416,8 @@ void launch_block(const FArgs &A, const BlockArgs &B, hipStream_t stream) {
     (void)attr;
     // 16 waves when the first colour pass has more sites than 8 waves have lanes (F - 2 rows of (F - 1) / 2)
     const bool w16 = (F - 2) * ((F - 1) / 2) > 8 * 64;
-    if (w16) villain_sweep_block<16><<<B.nbx * B.nbx, 16 * 64, lds, stream>>>(A, B);
-    else villain_sweep_block<8><<<B.nbx * B.nbx, 8 * 64, lds, stream>>>(A, B);
+    if (w16) villain_sweep_block<16><<<B.nbx * B.nbx, 16 * 64, lds, stream>>>(A, B), SV_LAUNCHED("villain_sweep_block<16>", stream);
+    else villain_sweep_block<8><<<B.nbx * B.nbx, 8 * 64, lds, stream>>>(A, B), SV_LAUNCHED("villain_sweep_block<8>", stream);
 }
 
 }  // namespace svh

@@ -1212,22 +1212,22 @@ void split_order(SplitArgs &S, const FGeom &G, int nsx, int TH, int grid, const 
 void launch_hot_split(const FArgs &A, const SplitArgs &S, int grid, hipStream_t stream) {
     const bool periodic =
         A.G.org == 0 && A.G.pitch == A.G.Nx && A.G.T0 == 0 && A.G.X0 == 0 && A.G.Ht == A.G.Nt && A.G.Wt == A.G.Nx;
-    if (periodic) villain_sweep_hot_split<false><<<grid, 4 * 64, 0, stream>>>(A, S);
-    else villain_sweep_hot_split<true><<<grid, 4 * 64, 0, stream>>>(A, S);
+    if (periodic) villain_sweep_hot_split<false><<<grid, 4 * 64, 0, stream>>>(A, S), SV_LAUNCHED("villain_sweep_hot_split<false>", stream);
+    else villain_sweep_hot_split<true><<<grid, 4 * 64, 0, stream>>>(A, S), SV_LAUNCHED("villain_sweep_hot_split<true>", stream);
 }
 
 // replica batch of full-row lattices: N <= 128 columns (one strip), N % 4 == 0 (row ranks start on whole words)
 bool hot_fr_ok(int32_t N) { return N <= RW && N % 4 == 0 && N >= 8; }
 
 void launch_hot_fr(const FArgs &A, int grid, bool obs, hipStream_t stream) {
-    if (obs) villain_sweep_hot_fr<true><<<grid, 4 * 64, 0, stream>>>(A);
-    else villain_sweep_hot_fr<false><<<grid, 4 * 64, 0, stream>>>(A);
+    if (obs) villain_sweep_hot_fr<true><<<grid, 4 * 64, 0, stream>>>(A), SV_LAUNCHED("villain_sweep_hot_fr<true>", stream);
+    else villain_sweep_hot_fr<false><<<grid, 4 * 64, 0, stream>>>(A), SV_LAUNCHED("villain_sweep_hot_fr<false>", stream);
 }
 
-void launch_hot_ph(const FArgs &A, int grid, hipStream_t stream) { villain_sweep_hot_ph<<<grid, 4 * 64, 0, stream>>>(A); }
+void launch_hot_ph(const FArgs &A, int grid, hipStream_t stream) { villain_sweep_hot_ph<<<grid, 4 * 64, 0, stream>>>(A), SV_LAUNCHED("villain_sweep_hot_ph", stream); }
 
 void launch_hot_band(const FArgs &A, const BandArgs &B, hipStream_t stream) {
-    villain_sweep_hot_band<8><<<B.nbands * B.P, 8 * 64, 0, stream>>>(A, B);
+    villain_sweep_hot_band<8><<<B.nbands * B.P, 8 * 64, 0, stream>>>(A, B), SV_LAUNCHED("villain_sweep_hot_band<8>", stream);
 }
 
 int band_residency() {
@@ -1243,12 +1243,12 @@ void launch_hot(const FArgs &A, int grid, hipStream_t stream) {
     const bool periodic =
         A.G.org == 0 && A.G.pitch == A.G.Nx && A.G.T0 == 0 && A.G.X0 == 0 && A.G.Ht == A.G.Nt && A.G.Wt == A.G.Nx;
     if (A.hot_nw == 8) {
-        if (periodic) villain_sweep_hot<false, 8><<<grid, 8 * 64, 0, stream>>>(A);
-        else villain_sweep_hot<true, 8><<<grid, 8 * 64, 0, stream>>>(A);
+        if (periodic) villain_sweep_hot<false, 8><<<grid, 8 * 64, 0, stream>>>(A), SV_LAUNCHED("villain_sweep_hot<false, 8>", stream);
+        else villain_sweep_hot<true, 8><<<grid, 8 * 64, 0, stream>>>(A), SV_LAUNCHED("villain_sweep_hot<true, 8>", stream);
     } else if (periodic) {
-        villain_sweep_hot<false, 4><<<grid, 4 * 64, 0, stream>>>(A);
+        villain_sweep_hot<false, 4><<<grid, 4 * 64, 0, stream>>>(A), SV_LAUNCHED("villain_sweep_hot<false, 4>", stream);
     } else {
-        villain_sweep_hot<true, 4><<<grid, 4 * 64, 0, stream>>>(A);
+        villain_sweep_hot<true, 4><<<grid, 4 * 64, 0, stream>>>(A), SV_LAUNCHED("villain_sweep_hot<true, 4>", stream);
     }
 }
 

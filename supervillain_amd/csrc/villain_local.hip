@@ -489,8 +489,8 @@ int sv_villain_site_run(sv_villain *st, double kappa, double interval_phi, int32
             run_local(st, specs, sweeps, cur, inc, stats, false, false, false, [&](int k, const Block *B, sv_stats *ds) {
                 (void)k;
                 double *in = st->phi[st->cur], *out = st->snap_phi;
-                site_pp<0><<<grid, 256, 0, ctx->stream>>>(P, in, out, n, st->r, B, T, adv_m, adv_e, ds, ctx->d_abort);
-                site_pp<1><<<grid, 256, 0, ctx->stream>>>(P, in, out, n, st->r, B, T, adv_m, adv_e, ds, ctx->d_abort);
+                site_pp<0><<<grid, 256, 0, ctx->stream>>>(P, in, out, n, st->r, B, T, adv_m, adv_e, ds, ctx->d_abort), SV_LAUNCHED("site_pp<0>", ctx->stream);
+                site_pp<1><<<grid, 256, 0, ctx->stream>>>(P, in, out, n, st->r, B, T, adv_m, adv_e, ds, ctx->d_abort), SV_LAUNCHED("site_pp<1>", ctx->stream);
                 std::swap(st->phi[st->cur], st->snap_phi);
             });
             for (int k = 0; k < sweeps; k++) stats[k].proposed = V;
@@ -499,16 +499,16 @@ int sv_villain_site_run(sv_villain *st, double kappa, double interval_phi, int32
         }
         run_local(st, specs, sweeps, cur, inc, stats, false, true, false, [&](int k, const Block *B, sv_stats *ds) {
             (void)k;
-            local_dphi_init<<<gi, 256, 0, ctx->stream>>>(N, phi, st->r, 1, ctx->d_abort);
+            local_dphi_init<<<gi, 256, 0, ctx->stream>>>(N, phi, st->r, 1, ctx->d_abort), SV_LAUNCHED("local_dphi_init", ctx->stream);
             for (int c = 0; c < st->ncol; c++) {
                 const int64_t nc = st->count[c];
                 if (!nc) continue;
                 if (even)
                     site_pass<true><<<grid, 256, 0, ctx->stream>>>(P, phi, n, st->r, nullptr, nc, c, B, T, adv_m,
-                                                                   adv_e, ds, ctx->d_abort);
+                                                                   adv_e, ds, ctx->d_abort), SV_LAUNCHED("site_pass<true>", ctx->stream);
                 else
                     site_pass<false><<<(int)((nc + 255) / 256), 256, 0, ctx->stream>>>(
-                        P, phi, n, st->r, st->sites + st->offset[c], nc, c, B, T, adv_m, adv_e, ds, ctx->d_abort);
+                        P, phi, n, st->r, st->sites + st->offset[c], nc, c, B, T, adv_m, adv_e, ds, ctx->d_abort), SV_LAUNCHED("site_pass<false>", ctx->stream);
             }
         });
         for (int k = 0; k < sweeps; k++) stats[k].proposed = V;
@@ -549,11 +549,11 @@ int sv_villain_exact_run(sv_villain *st, double kappa, int64_t interval_z, int32
                 if (!nc) continue;
                 if (even)
                     exact_pass<true><<<grid, 256, 0, ctx->stream>>>(P, n, phi, nullptr, nc, c, B, ctx->d_skips, T,
-                                                                    adv_m, adv_half, ds, scratch(ctx), (uint32_t)k);
+                                                                    adv_m, adv_half, ds, scratch(ctx), (uint32_t)k), SV_LAUNCHED("exact_pass<true>", ctx->stream);
                 else
                     exact_pass<false><<<(int)((nc + 255) / 256), 256, 0, ctx->stream>>>(
                         P, n, phi, st->sites + st->offset[c], nc, c, B, ctx->d_skips, T, adv_m, adv_half, ds,
-                        scratch(ctx), (uint32_t)k);
+                        scratch(ctx), (uint32_t)k), SV_LAUNCHED("exact_pass<false>", ctx->stream);
             }
         });
         for (int k = 0; k < sweeps; k++) stats[k].proposed = V;
@@ -589,7 +589,7 @@ int sv_villain_link_run(sv_villain *st, double kappa, int64_t W, int64_t interva
         int64_t *n = st->n[st->cur];
         run_local(st, specs, sweeps, cur, inc, stats, P.thr != 0, false, true, [&](int k, const Block *B, sv_stats *ds) {
             link_sweep<<<grid, 256, 0, ctx->stream>>>(P, phi, n, B, ctx->d_skips, T, adv_u, adv_half, ds,
-                                                      scratch(ctx), (uint32_t)k);
+                                                      scratch(ctx), (uint32_t)k), SV_LAUNCHED("link_sweep", ctx->stream);
         });
         for (int k = 0; k < sweeps; k++) stats[k].proposed = 2 * V;
         store_cursor(cur, rng);
@@ -640,7 +640,7 @@ int sv_villain_cohomology_run(sv_villain *st, double kappa, int64_t interval_h, 
         ctx->time_begin(&ev);
         cohomology_run<<<1, 256, 0, ctx->stream>>>(st->N, kappa / 2.0, P.iv, P.k, P.thr, st->phi[st->cur],
                                                    st->n[st->cur], sweeps, (CohoRng *)d, (sv_stats *)(d + o_st),
-                                                   (const int32_t *)(d + o_lv), (const uint8_t *)(d + o_pg), plan);
+                                                   (const int32_t *)(d + o_lv), (const uint8_t *)(d + o_pg), plan), SV_LAUNCHED("cohomology_run", ctx->stream);
         ctx->time_end(ev, 1);
         SV_HIP(hipGetLastError());
         SV_HIP(hipMemcpyAsync(hb, d, o_lv, hipMemcpyDeviceToHost, ctx->stream));

@@ -588,7 +588,7 @@ void snapshot(sv_worldline *st, bool restore) {
         st->v_at_snap = st->v;
         if ((2 * V * sizeof(int64_t)) % 16 == 0 && vb % 16 == 0) {
             copy_pair<<<grid, 256, 0, ctx->stream>>>((uint4 *)st->snap_m, (const uint4 *)st->m, n0, (uint4 *)st->snap_v,
-                                                     (const uint4 *)st->v, n1);
+                                                     (const uint4 *)st->v, n1), SV_LAUNCHED("copy_pair", ctx->stream);
             SV_HIP(hipGetLastError());
         } else {
             SV_HIP(hipMemcpyAsync(st->snap_m, st->m, 2 * V * sizeof(int64_t), hipMemcpyDeviceToDevice, ctx->stream));
@@ -653,7 +653,7 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
                 launch(ctx->d_blocks + (size_t)k * nb, ss + (size_t)k * nstat * NSTRIPE, (uint32_t)k,
                        blocks.data() + (size_t)k * nb, k + 1 < count ? blocks.data() + (size_t)(k + 1) * nb : nullptr);
             ctx->time_end(ev, count);
-            fold_stripes<<<(count * nstat + 63) / 64, 64, 0, ctx->stream>>>(ss, ctx->d_stats, count * nstat);
+            fold_stripes<<<(count * nstat + 63) / 64, 64, 0, ctx->stream>>>(ss, ctx->d_stats, count * nstat), SV_LAUNCHED("fold_stripes", ctx->stream);
             SV_HIP(hipGetLastError());
             if (sw + count < sweeps) {  // (the device runs this batch meanwhile)
                 c_next = c;
@@ -717,10 +717,10 @@ void launch_coexact(sv_worldline *st, const WParams &P, const Block *blocks, Sta
         for (int c = 0; c < 2; c++) {
             if (st->v_is_float)
                 coexact_gs<true><<<P.grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips, T, stat,
-                                                                  wscratch(ctx), k);
+                                                                  wscratch(ctx), k), SV_LAUNCHED("coexact_gs<true>", ctx->stream);
             else
                 coexact_gs<false><<<P.grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips, T, stat,
-                                                                   wscratch(ctx), k);
+                                                                   wscratch(ctx), k), SV_LAUNCHED("coexact_gs<false>", ctx->stream);
         }
         return;
     }
@@ -730,10 +730,10 @@ void launch_coexact(sv_worldline *st, const WParams &P, const Block *blocks, Sta
         const int grid = (int)((nc + 255) / 256);
         if (st->v_is_float)
             coexact_pass<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->sites + st->offset[c], nc, c, blocks,
-                                                              ctx->d_skips, T, stat, wscratch(ctx), k);
+                                                              ctx->d_skips, T, stat, wscratch(ctx), k), SV_LAUNCHED("coexact_pass<true>", ctx->stream);
         else
             coexact_pass<false><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->sites + st->offset[c], nc, c, blocks,
-                                                               ctx->d_skips, T, stat, wscratch(ctx), k);
+                                                               ctx->d_skips, T, stat, wscratch(ctx), k), SV_LAUNCHED("coexact_pass<false>", ctx->stream);
     }
 }
 
@@ -745,10 +745,10 @@ void launch_plaquette_cb(sv_worldline *st, const WParams &P, const Block *blocks
         for (int c = 0; c < 2; c++) {
             if (st->v_is_float)
                 plaquette_cb_gs<true><<<P.grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips, T,
-                                                                       stat, wscratch(ctx), k);
+                                                                       stat, wscratch(ctx), k), SV_LAUNCHED("plaquette_cb_gs<true>", ctx->stream);
             else
                 plaquette_cb_gs<false><<<P.grid, 256, 0, ctx->stream>>>(P, st->m, st->v, c, blocks, ctx->d_skips, T,
-                                                                        stat, wscratch(ctx), k);
+                                                                        stat, wscratch(ctx), k), SV_LAUNCHED("plaquette_cb_gs<false>", ctx->stream);
         }
         return;
     }
@@ -758,10 +758,10 @@ void launch_plaquette_cb(sv_worldline *st, const WParams &P, const Block *blocks
         const int grid = (int)((nc + 255) / 256);
         if (st->v_is_float)
             plaquette_cb_pass<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->sites + st->offset[c], nc, c,
-                                                                   blocks, ctx->d_skips, T, stat, wscratch(ctx), k);
+                                                                   blocks, ctx->d_skips, T, stat, wscratch(ctx), k), SV_LAUNCHED("plaquette_cb_pass<true>", ctx->stream);
         else
             plaquette_cb_pass<false><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->sites + st->offset[c], nc, c,
-                                                                    blocks, ctx->d_skips, T, stat, wscratch(ctx), k);
+                                                                    blocks, ctx->d_skips, T, stat, wscratch(ctx), k), SV_LAUNCHED("plaquette_cb_pass<false>", ctx->stream);
     }
 }
 
@@ -1028,21 +1028,21 @@ void ordered_sweep(sv_worldline *st, double kappa, double W_eff, bool o32, u128 
         SV_HIP(hipMemsetAsync(st->lev, 0, V * sizeof(int32_t), ctx->stream));
         SV_HIP(hipMemsetAsync(st->lcnt, 0, (V + 2 + LFLAGS) * sizeof(int32_t), ctx->stream));
         if (o32)
-            order_positions<uint32_t><<<lgrid, 256, 0, ctx->stream>>>((const uint32_t *)st->ord64, V, st->pos, flags);
+            order_positions<uint32_t><<<lgrid, 256, 0, ctx->stream>>>((const uint32_t *)st->ord64, V, st->pos, flags), SV_LAUNCHED("order_positions<uint32_t>", ctx->stream);
         else
-            order_positions<int64_t><<<lgrid, 256, 0, ctx->stream>>>(st->ord64, V, st->pos, flags);
+            order_positions<int64_t><<<lgrid, 256, 0, ctx->stream>>>(st->ord64, V, st->pos, flags), SV_LAUNCHED("order_positions<int64_t>", ctx->stream);
         int32_t hf[LFLAGS];
         for (int it = 0;; it += LFLAGS - 2) {
             // relaxations in batches; a batch whose last relaxation changed nothing has converged
             if (it > 0) SV_HIP(hipMemsetAsync(flags + 2, 0, (LFLAGS - 2) * sizeof(int32_t), ctx->stream));
-            for (int j = 0; j < LFLAGS - 2; j++) order_levels<<<lgrid, 256, 0, ctx->stream>>>(N, st->pos, st->lev, flags, j);
+            for (int j = 0; j < LFLAGS - 2; j++) order_levels<<<lgrid, 256, 0, ctx->stream>>>(N, st->pos, st->lev, flags, j), SV_LAUNCHED("order_levels", ctx->stream);
             SV_HIP(hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, ctx->stream));
             SV_HIP(hipStreamSynchronize(ctx->stream));
             if (hf[0]) throw std::invalid_argument("order is not a permutation");
             if (!hf[LFLAGS - 1]) break;
             if (it > 2 * V) throw std::logic_error("order levels did not converge");
         }
-        order_level_counts<<<lgrid, 256, 0, ctx->stream>>>(st->lev, V, st->lcnt, flags);
+        order_level_counts<<<lgrid, 256, 0, ctx->stream>>>(st->lev, V, st->lcnt, flags), SV_LAUNCHED("order_level_counts", ctx->stream);
         int32_t nlev = 0;
         SV_HIP(hipMemcpyAsync(&nlev, flags + 1, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
         SV_HIP(hipStreamSynchronize(ctx->stream));
@@ -1052,7 +1052,7 @@ void ordered_sweep(sv_worldline *st, double kappa, double W_eff, bool o32, u128 
         SV_HIP(hipStreamSynchronize(ctx->stream));
         for (int l = 1; l <= nlev + 1; l++) start[l] += start[l - 1];  // start[l] = first slot of level l
         SV_HIP(hipMemcpyAsync(st->lcnt, start.data(), (nlev + 1) * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
-        order_level_lists<<<lgrid, 256, 0, ctx->stream>>>(st->lev, V, st->lcnt, st->order);
+        order_level_lists<<<lgrid, 256, 0, ctx->stream>>>(st->lev, V, st->lcnt, st->order), SV_LAUNCHED("order_level_lists", ctx->stream);
         std::vector<BlockSpec> specs = {{BOUNDED, (uint32_t)V}, {BOUNDED, (uint32_t)V}, {UNIFORM, (uint32_t)V}};
         SkipMap skips;
         std::vector<Block> blocks;
@@ -1069,9 +1069,9 @@ void ordered_sweep(sv_worldline *st, double kappa, double W_eff, bool o32, u128 
             StatStripe *ss = (StatStripe *)st->stripes;
             svh::reset_batch(ctx, ctx->d_stats, sizeof(sv_stats), ss, NSTRIPE * sizeof(StatStripe));
             if (st->v_is_float)
-                plaquette_f_init<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f);
+                plaquette_f_init<true><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f), SV_LAUNCHED("plaquette_f_init<true>", ctx->stream);
             else
-                plaquette_f_init<false><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f);
+                plaquette_f_init<false><<<grid, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f), SV_LAUNCHED("plaquette_f_init<false>", ctx->stream);
             for (int l = 1; l <= nlev; l++) {
                 const int32_t cnt = start[l + 1] - start[l];
                 if (!cnt) continue;
@@ -1079,13 +1079,13 @@ void ordered_sweep(sv_worldline *st, double kappa, double W_eff, bool o32, u128 
                 if (st->v_is_float)
                     plaquette_level<true><<<g, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f, st->order + start[l], cnt,
                                                                       st->pos, ctx->d_blocks, ctx->d_skips, T,
-                                                                      ss, wscratch(ctx));
+                                                                      ss, wscratch(ctx)), SV_LAUNCHED("plaquette_level<true>", ctx->stream);
                 else
                     plaquette_level<false><<<g, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f, st->order + start[l],
                                                                        cnt, st->pos, ctx->d_blocks, ctx->d_skips, T,
-                                                                       ss, wscratch(ctx));
+                                                                       ss, wscratch(ctx)), SV_LAUNCHED("plaquette_level<false>", ctx->stream);
             }
-            fold_stripes<<<1, 64, 0, ctx->stream>>>(ss, ctx->d_stats, 1);
+            fold_stripes<<<1, 64, 0, ctx->stream>>>(ss, ctx->d_stats, 1), SV_LAUNCHED("fold_stripes", ctx->stream);
             SV_HIP(hipGetLastError());
             if (!wcheck(ctx, reps)) {
                 cur = c;

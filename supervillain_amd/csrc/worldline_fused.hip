@@ -780,14 +780,14 @@ void launch_wf(const FGeom &G, double kappa, double W_eff, int64_t it, const int
     A.kt = (uint32_t)(2 * it);
     A.thrt = (uint32_t)((0u - A.kt) % A.kt);
     if (nw == 16) {
-        if (tile) worldline_step_fused<true, 16><<<grid, 16 * 64, 0, stream>>>(A);
-        else worldline_step_fused<false, 16><<<grid, 16 * 64, 0, stream>>>(A);
+        if (tile) worldline_step_fused<true, 16><<<grid, 16 * 64, 0, stream>>>(A), SV_LAUNCHED("worldline_step_fused<true, 16>", stream);
+        else worldline_step_fused<false, 16><<<grid, 16 * 64, 0, stream>>>(A), SV_LAUNCHED("worldline_step_fused<false, 16>", stream);
     } else if (nw == 8) {
-        if (tile) worldline_step_fused<true, 8><<<grid, 8 * 64, 0, stream>>>(A);
-        else worldline_step_fused<false, 8><<<grid, 8 * 64, 0, stream>>>(A);
+        if (tile) worldline_step_fused<true, 8><<<grid, 8 * 64, 0, stream>>>(A), SV_LAUNCHED("worldline_step_fused<true, 8>", stream);
+        else worldline_step_fused<false, 8><<<grid, 8 * 64, 0, stream>>>(A), SV_LAUNCHED("worldline_step_fused<false, 8>", stream);
     } else {
-        if (tile) worldline_step_fused<true, 4><<<grid, 4 * 64, 0, stream>>>(A);
-        else worldline_step_fused<false, 4><<<grid, 4 * 64, 0, stream>>>(A);
+        if (tile) worldline_step_fused<true, 4><<<grid, 4 * 64, 0, stream>>>(A), SV_LAUNCHED("worldline_step_fused<true, 4>", stream);
+        else worldline_step_fused<false, 4><<<grid, 4 * 64, 0, stream>>>(A), SV_LAUNCHED("worldline_step_fused<false, 4>", stream);
     }
 }
 

@@ -403,7 +403,7 @@ int sv_worldline_vortex_run(sv_worldline *st, double kappa, double W_eff, int64_
             ctx, specs, sweeps, cur, inc, stats, !vf && P.thr != 0, [&] { wl_copy(st, true, false, true); },
             [&] { wl_copy(st, false, false, true); },
             [&](int k, const Block *B, sv_stats *ds) {
-                if (vf) vortex_dv_init<<<gi, 256, 0, ctx->stream>>>(N, (const double *)st->v, st->f, ctx->d_abort);
+                if (vf) vortex_dv_init<<<gi, 256, 0, ctx->stream>>>(N, (const double *)st->v, st->f, ctx->d_abort), SV_LAUNCHED("vortex_dv_init", ctx->stream);
                 for (int c = 0; c < st->ncol; c++) {
                     const int64_t nc = st->count[c];
                     if (!nc) continue;
@@ -412,19 +412,19 @@ int sv_worldline_vortex_run(sv_worldline *st, double kappa, double W_eff, int64_
                     if (even && vf)
                         vortex_pass<true, true><<<g, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f, sites, nc, c, B,
                                                                           ctx->d_skips, T, adv_m, adv_p, ds,
-                                                                          scratch(ctx), (uint32_t)k);
+                                                                          scratch(ctx), (uint32_t)k), SV_LAUNCHED("vortex_pass<true, true>", ctx->stream);
                     else if (even)
                         vortex_pass<true, false><<<g, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f, sites, nc, c, B,
                                                                            ctx->d_skips, T, adv_m, adv_p, ds,
-                                                                           scratch(ctx), (uint32_t)k);
+                                                                           scratch(ctx), (uint32_t)k), SV_LAUNCHED("vortex_pass<true, false>", ctx->stream);
                     else if (vf)
                         vortex_pass<false, true><<<g, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f, sites, nc, c, B,
                                                                            ctx->d_skips, T, adv_m, adv_p, ds,
-                                                                           scratch(ctx), (uint32_t)k);
+                                                                           scratch(ctx), (uint32_t)k), SV_LAUNCHED("vortex_pass<false, true>", ctx->stream);
                     else
                         vortex_pass<false, false><<<g, 256, 0, ctx->stream>>>(P, st->m, st->v, st->f, sites, nc, c,
                                                                             B, ctx->d_skips, T, adv_m, adv_p, ds,
-                                                                            scratch(ctx), (uint32_t)k);
+                                                                            scratch(ctx), (uint32_t)k), SV_LAUNCHED("vortex_pass<false, false>", ctx->stream);
                 }
             });
         for (int k = 0; k < sweeps; k++) stats[k].proposed = V;
@@ -491,18 +491,18 @@ int sv_worldline_wrapping_run(sv_worldline *st, double kappa, double W_eff, int6
             ctx, specs, sweeps, cur, inc, stats, P.thr != 0, [&] { wl_copy(st, true, true, false); },
             [&] { wl_copy(st, false, true, false); },
             [&](int k, const Block *B, sv_stats *ds) {
-                wrap_draw<<<g2n, 256, 0, ctx->stream>>>(P, B, ctx->d_skips, T, cprop, scratch(ctx), (uint32_t)k);
+                wrap_draw<<<g2n, 256, 0, ctx->stream>>>(P, B, ctx->d_skips, T, cprop, scratch(ctx), (uint32_t)k), SV_LAUNCHED("wrap_draw", ctx->stream);
                 if (vf) {
-                    wrap_cols<true><<<gcols, 256, 0, ctx->stream>>>(P, st->m, st->v, cprop, dS, ctx->d_abort);
+                    wrap_cols<true><<<gcols, 256, 0, ctx->stream>>>(P, st->m, st->v, cprop, dS, ctx->d_abort), SV_LAUNCHED("wrap_cols<true>", ctx->stream);
                     wrap_rows<true><<<N, 256, 0, ctx->stream>>>(P, st->m, st->v, cprop, dS, lv, pg, nleaf,
-                                                                (int32_t)prog.size(), ctx->d_abort);
+                                                                (int32_t)prog.size(), ctx->d_abort), SV_LAUNCHED("wrap_rows<true>", ctx->stream);
                 } else {
-                    wrap_cols<false><<<gcols, 256, 0, ctx->stream>>>(P, st->m, st->v, cprop, dS, ctx->d_abort);
+                    wrap_cols<false><<<gcols, 256, 0, ctx->stream>>>(P, st->m, st->v, cprop, dS, ctx->d_abort), SV_LAUNCHED("wrap_cols<false>", ctx->stream);
                     wrap_rows<false><<<N, 256, 0, ctx->stream>>>(P, st->m, st->v, cprop, dS, lv, pg, nleaf,
-                                                                 (int32_t)prog.size(), ctx->d_abort);
+                                                                 (int32_t)prog.size(), ctx->d_abort), SV_LAUNCHED("wrap_rows<false>", ctx->stream);
                 }
-                wrap_metropolis<<<g2n, 256, 0, ctx->stream>>>(P, B, T, dS, accf, ds, ctx->d_abort);
-                wrap_apply<<<gapp, 256, 0, ctx->stream>>>(P, st->m, cprop, accf, ctx->d_abort);
+                wrap_metropolis<<<g2n, 256, 0, ctx->stream>>>(P, B, T, dS, accf, ds, ctx->d_abort), SV_LAUNCHED("wrap_metropolis", ctx->stream);
+                wrap_apply<<<gapp, 256, 0, ctx->stream>>>(P, st->m, cprop, accf, ctx->d_abort), SV_LAUNCHED("wrap_apply", ctx->stream);
             });
         for (int k = 0; k < sweeps; k++) stats[k].proposed = 2 * N;
         store_cursor(cur, rng);

@@ -296,8 +296,8 @@ void run_worms(sv_ctx *ctx, bool worldline, WormArgs A, sv_rng *rngs, int64_t *h
     hipEvent_t ev;
     ctx->time_begin(&ev);
     const unsigned grid = (unsigned)((R + 63) / 64);
-    if (worldline) worldline_worm<<<grid, 64, 0, ctx->stream>>>(A);
-    else villain_worm<<<grid, 64, 0, ctx->stream>>>(A);
+    if (worldline) worldline_worm<<<grid, 64, 0, ctx->stream>>>(A), SV_LAUNCHED("worldline_worm", ctx->stream);
+    else villain_worm<<<grid, 64, 0, ctx->stream>>>(A), SV_LAUNCHED("villain_worm", ctx->stream);
     ctx->time_end(ev, 1);
     SV_HIP(hipGetLastError());
     int32_t status = 0;

@@ -88,7 +88,7 @@ class Ensemble:
             # emissions land in library-owned page-locked storage (pipeline.pinned_empty), which the Batches keep
             fields[x]._data, fields[y]._data = pinned_empty(ax.shape, ax.dtype), pinned_empty(ay.shape, ay.dtype)
             ax, ay = fields[x]._data, fields[y]._data
-        done = 0
+        done = landed = 0  # draws queued for emission / confirmed landed by emit_wait
         try:
             chain.upload(seed)
             for i in progress(range(steps), desc='Generation'):
@@ -99,18 +99,25 @@ class Ensemble:
                         fields[k][i] = v
                 else:
                     self.configuration[i] = chain.download() | obs
+                done = i + 1
                 if writer is not None and (i + 1) % stream_every == 0:
                     if direct:
                         chain.emit_wait()
+                        landed = done
                     writer.put(i + 1)
-                done = i + 1
             if direct:
                 chain.emit_wait()
+                landed = done
         finally:
-            if direct:
-                chain.emit_wait()
-                ax[done:], ay[done:] = 0, 0  # (after a failure: the draws never emitted read as the zeros they were)
-            chain.close()
+            try:
+                if direct and landed < done:
+                    chain.emit_wait()  # (a failure before the loop's last wait: land what was queued, if possible)
+                    landed = done
+            finally:
+                if direct:
+                    # the pinned storage is uninitialised (pinned_empty): rows no confirmed emission wrote read as zeros
+                    ax[landed:], ay[landed:] = 0, 0
+                chain.close()
 
     def columns(self, start=0, stop=None):
         """The ensemble's draws [start, stop) as store columns: configuration fields, index, weight."""

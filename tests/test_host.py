@@ -2,6 +2,8 @@
 
 The Ensemble/KeepEvery/Sequentially logic is exercised with an oracle-backed stand-in generator
 (test-only) and compared with golden vectors captured from the reference's own Ensemble.generate."""
+import os
+
 import numpy as np
 import pytest
 
@@ -213,3 +215,40 @@ def test_bench_json_contract(capsys):
     c = d['cpu_baseline']
     assert c['cores'] >= 1 and c['kind'] == 'port' and c['value'] > 0 and c['value_1core'] > 0
     assert abs(d['value'] - 10 * 4096 * 4096 / 3.2e-3) < 1e-3 * d['value']
+
+
+def test_bench_metric_names_the_lattice(capsys, monkeypatch):
+    """a line's metric names the lattice the run swept -- BASELINE.json's metric verbatim for one
+    L=4096 lattice (N = 1 and config 4's tiles of it, the default for --gpus N), the (ty L) x (tx L) lattice for
+    --weak -- and report() refuses a line whose metric and config.lattice disagree."""
+    import json
+    import sys
+    import types
+    import bench
+    with open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'BASELINE.json')) as f:
+        baseline_metric = json.load(f)['metric']
+    assert bench.lattice_metric(4096, 4096) == bench.HEADLINE_METRIC == baseline_metric
+    assert bench.metric_lattice(baseline_metric) == (4096, 4096)
+    weak = bench.lattice_metric(8192, 16384, weak_tile=[4096, 4096])
+    assert bench.metric_lattice(weak) == (8192, 16384) and 'L=4096' not in weak
+    assert bench.metric_lattice(bench.lattice_metric(256, 256)) == (256, 256)
+    wl = bench.lattice_metric(2048, 4096, 'Worldline', [1024, 1024], head='plaquette-steps/sec (x)', tail=', W=1')
+    assert bench.metric_lattice(wl) == (2048, 4096)
+    # the scaling default: config 4 (strong) for --gpus N unless --weak
+    for argv, strong in ((['--gpus', '8'], True), (['--gpus', '8', '--weak'], False), (['--tiles', '2x4'], True),
+                         (['--tiles', '2x4', '--weak'], False), ([], True)):
+        monkeypatch.setattr(sys, 'argv', ['bench.py'] + argv)
+        assert bench.parse().strong is strong, argv
+    args = types.SimpleNamespace(steps=10, warmup=2, strong=True, no_cpu_baseline=True, L=4096, kappa=0.5, W=1)
+    with pytest.raises(ValueError):
+        bench.report(args, 8, 8192 * 16384, 4096 * 4096, 1.0, 0.004, 3e-4, {'workload': 'x', 'lattice': [8192, 16384]},
+                     4096)  # the headline metric on the weak lattice
+    bench.report(args, 8, 4096 * 4096, 2048 * 1024, 1.0, 0.004, 3e-5, {'workload': 'x', 'lattice': [4096, 4096]}, 2048)
+    d = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert d['metric'] == baseline_metric and d['scaling'] == 'strong' and d['n_gpus'] == 8
+    # an efficiency above 1.02 is flagged
+    ref = bench.scaling_reference(8.5e11, 8, 1.0e11, [2048, 1024], 7.0e10, 0)
+    assert ref['E_N_suspect'] and abs(ref['E_N'] - 1.0625) < 1e-12
+    assert 'suspect' in capsys.readouterr().err
+    ref = bench.scaling_reference(6.0e11, 8, 1.0e11, [2048, 1024], 7.0e10, 0)
+    assert not ref['E_N_suspect'] and abs(ref['E_N_vs_single_lattice'] - 6.0e11 / 5.6e11) < 1e-12
