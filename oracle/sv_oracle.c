@@ -48,6 +48,56 @@ typedef struct {
     int64_t rejections;    /* Lemire rejections met in this sweep (diagnostic) */
 } sv_stats;
 
+/* ---------------------------------------------------------------- exact acceptance sums
+ * The sweep statistic acceptance_sum sums the per-proposal Metropolis probabilities (neighborhood.py:118,
+ * coexact.py:117, plaquette.py:88; the reference adds NumPy pairwise sums per colour).  It is kept here as the
+ * exact sum of the probabilities rounded to 2^-103, T(p) = round(p 2^51) 2^52 + round(r 2^103) with r = p - (p
+ * rounded to 2^-51), accumulated as three 38-bit limb sums and turned into a double by the same function as
+ * libsvhip.so (supervillain_amd/csrc/common.h fx_add / fx_value): the device's value whatever its launch geometry,
+ * within ~2 ulp of the exact sum of the p, so within rounding of the reference's pairwise sums.  The running sum
+ * of the sv_stats being filled lives beside it (thread-local); a cleared or different sv_stats restarts it. */
+#define FX_LIMB ((UINT64_C(1) << 38) - 1)
+static _Thread_local const sv_stats *fx_owner;
+static _Thread_local uint64_t fx_w[3];
+static _Thread_local double fx_last;
+static double fx_value(uint64_t w0, uint64_t w1, uint64_t w2) {
+    w1 += w0 >> 38;
+    w0 &= FX_LIMB;
+    w2 += w1 >> 38;
+    w1 &= FX_LIMB;
+    return ((double)w2 * 0x1p76 + (double)w1 * 0x1p38 + (double)w0) * 0x1p-103;
+}
+/* T(p) for p in [0, 1] as three limbs (added to w) */
+static void fx_term_limbs(double p, uint64_t w[3]) {
+    const double x = p + 2.0;
+    uint64_t bx;
+    memcpy(&bx, &x, sizeof bx);
+    const uint64_t a = bx - UINT64_C(0x4000000000000000); /* round(p 2^51) */
+    const double r = p - (x - 2.0);                       /* exact, |r| <= 2^-52 */
+    const double y = fma(r, 0x1p103, 0x1.8p52);
+    int64_t by;
+    memcpy(&by, &y, sizeof by);
+    const int64_t b = by - INT64_C(0x4338000000000000); /* round(r 2^103) */
+    const u128 T = ((u128)a << 52) + (u128)(__int128)b;
+    w[0] += (uint64_t)T & FX_LIMB;
+    w[1] += (uint64_t)(T >> 38) & FX_LIMB;
+    w[2] += (uint64_t)(T >> 76);
+}
+static double exact_acceptance_add_w(const sv_stats *st, const uint64_t add[3]) {
+    if (fx_owner != st || st->acceptance_sum != fx_last) {
+        fx_owner = st;
+        fx_w[0] = fx_w[1] = fx_w[2] = 0;
+    }
+    for (int i = 0; i < 3; i++) fx_w[i] += add[i];
+    fx_last = fx_value(fx_w[0], fx_w[1], fx_w[2]);
+    return fx_last;
+}
+static double exact_acceptance_add(const sv_stats *st, double p) {
+    uint64_t w[3] = {0, 0, 0};
+    fx_term_limbs(p, w);
+    return exact_acceptance_add_w(st, w);
+}
+
 /* ---------------------------------------------------------------- PCG64 (NumPy) */
 static const u128 PCG_MULT = (((u128)0x2360ED051FC65DA4ULL) << 64) | (u128)0x4385DF649FCCF645ULL;
 
@@ -283,7 +333,7 @@ static void villain_sweep(int64_t Nt, int64_t Nx, double kappa, int64_t W, doubl
             int a = metro[s] < p;
             acc[s] = a;
             st->accepted += a;
-            st->acceptance_sum += p;
+            st->acceptance_sum = exact_acceptance_add(st, p);
         }
         for (int64_t i = 0; i < nc; i++) { /* :121-125 */
             int64_t s = sites[i];
@@ -453,7 +503,7 @@ int sv_o_villain_neighborhood_philox(int32_t N, double kappa, int64_t W, double 
                 int a = metro[s] < p;
                 acc[s] = a;
                 st->accepted += a;
-                st->acceptance_sum += p;
+                st->acceptance_sum = exact_acceptance_add(st, p);
             }
             free(dS_l);
             for (int64_t i = 0; i < nc; i++) {
@@ -563,7 +613,7 @@ int sv_o_worldline_coexact(int32_t N_, double kappa, double Weff, int64_t interv
                 p = p > 1.0 ? 1.0 : p;
                 int a = metro[x] < p;
                 st->accepted += a;
-                st->acceptance_sum += p;
+                st->acceptance_sum = exact_acceptance_add(st, p);
                 if (a) { /* :120 (links of same-colour plaquettes are disjoint) */
                     m[x] += t;
                     m[xe1] -= t;
@@ -609,7 +659,7 @@ int sv_o_worldline_plaquette_seq(int32_t N_, double kappa, double Weff, int64_t 
         double p = exp(-dS);
         p = p < 0.0 ? 0.0 : p;
         p = p > 1.0 ? 1.0 : p;
-        st->acceptance_sum += p;
+        st->acceptance_sum = exact_acceptance_add(st, p);
         if (met[i] < p) {
             m[x] += cm[i];
             m[V + xm] += cm[i];
@@ -694,7 +744,7 @@ int sv_o_worldline_plaquette_cb(int32_t N_, double kappa, double Weff, int64_t *
                 double p = exp(-dS);
                 p = p < 0.0 ? 0.0 : p;
                 p = p > 1.0 ? 1.0 : p;
-                st->acceptance_sum += p;
+                st->acceptance_sum = exact_acceptance_add(st, p);
                 if (metro[x] < p) {
                     m[x] += cm[i];
                     m[V + xm] += cm[i];
@@ -785,7 +835,7 @@ int sv_o_villain_site(int32_t N, double kappa, double interval_phi, double *phi,
                 p = p > 1.0 ? 1.0 : p;
                 acc[s] = metro[s] < p;
                 st->accepted += acc[s];
-                st->acceptance_sum += p;
+                st->acceptance_sum = exact_acceptance_add(st, p);
             }
             for (int64_t i = 0; i < nc; i++) cphi[sites[i]] *= (double)acc[sites[i]];             /* :111 */
             for (int64_t s = 0; s < V; s++) phi[s] = phi[s] + cphi[s];                              /* :112 */
@@ -827,7 +877,7 @@ int sv_o_villain_link(int32_t N, double kappa, int64_t W, int64_t interval_n, co
             const double u = pcg_uniform(&g, 0.0, 1.0);
             const int a = u < p[l];
             st->accepted += a;
-            st->acceptance_sum += p[l];
+            st->acceptance_sum = exact_acceptance_add(st, p[l]);
             if (a) n[l] += cn[l];
         }
         st->proposed = 2 * V;
@@ -877,7 +927,7 @@ int sv_o_villain_exact(int32_t N, double kappa, int64_t interval_z, const double
                 p = p > 1.0 ? 1.0 : p;
                 acc[s] = metro[s] < p;
                 st->accepted += acc[s];
-                st->acceptance_sum += p;
+                st->acceptance_sum = exact_acceptance_add(st, p);
             }
             for (int64_t i = 0; i < nc; i++) z[sites[i]] *= acc[sites[i]];                         /* :114 */
             for (int mu = 0; mu < 2; mu++)                                                          /* :115 */
@@ -923,7 +973,7 @@ int sv_o_villain_cohomology(int32_t N, double kappa, int64_t interval_h, const d
                 for (int64_t i = 0; i < N; i++) n[mu * V + (mu == 0 ? i : i * N)] += h;
                 st->accepted += 1;
             }
-            st->acceptance_sum += p;
+            st->acceptance_sum += p;  /* (two terms, added in order as the device does) */
         }
         st->proposed = 2;
     }
@@ -999,7 +1049,7 @@ int sv_o_worldline_vortex(int32_t N, double kappa, double Weff, int64_t interval
                 p = p > 1.0 ? 1.0 : p;
                 const int acc = metro[s] < p;
                 st->accepted += acc;
-                st->acceptance_sum += p;
+                st->acceptance_sum = exact_acceptance_add(st, p);
                 /* v[x] += vals * accepted; delta_v patched with the same sparse delta (:129-131) */
                 if (v_is_float) {
                     const double ap = a * (double)acc;
@@ -1070,7 +1120,7 @@ int sv_o_worldline_wrapping(int32_t N, double kappa, double Weff, int64_t interv
                 const double p = prob[mu * N + j];
                 const int acc = u < p;
                 st->accepted += acc;
-                st->acceptance_sum += p;
+                st->acceptance_sum = exact_acceptance_add(st, p);
                 if (acc) {
                     const int64_t c = cm[mu * N + j];
                     if (mu == 0)
@@ -1318,8 +1368,8 @@ int sv_o_villain_neighborhood_mt(int32_t N_, double kappa, int64_t W, double int
                     dSl[mu * V + s] = (half_kappa * cr) * ((2.0 * r[mu * V + s]) + cr);
                 }
             int64_t accepted = 0;
-            double psum = 0.0;
-#pragma omp parallel for num_threads(threads) reduction(+ : accepted, psum)
+            uint64_t fx0 = 0, fx1 = 0, fx2 = 0; /* the exact acceptance limb sums (order-free) */
+#pragma omp parallel for num_threads(threads) reduction(+ : accepted, fx0, fx1, fx2)
             for (int64_t i = 0; i < nc; i++) {
                 const int64_t s = sites[i];
                 double dS = 0.0;
@@ -1333,10 +1383,15 @@ int sv_o_villain_neighborhood_mt(int32_t N_, double kappa, int64_t W, double int
                 const double u = (double)(raw[s] >> 11) * (1.0 / 9007199254740992.0);
                 acc[s] = u < p;
                 accepted += acc[s];
-                psum += p;
+                uint64_t w[3] = {0, 0, 0};
+                fx_term_limbs(p, w);
+                fx0 += w[0];
+                fx1 += w[1];
+                fx2 += w[2];
             }
             st->accepted += accepted;
-            st->acceptance_sum += psum;
+            const uint64_t add[3] = {fx0, fx1, fx2};
+            st->acceptance_sum = exact_acceptance_add_w(st, add);
 #pragma omp parallel for num_threads(threads)
             for (int64_t i = 0; i < nc; i++) {
                 const int64_t s = sites[i];

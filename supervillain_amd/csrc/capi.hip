@@ -122,6 +122,7 @@ bool sv_ctx::defer_stats(sv_stats *dst, int64_t count) {
         SV_HIP(hipHostMalloc((void **)&h_stage, stage_cap * sizeof(sv_stats), hipHostMallocDefault));
         SV_HIP(hipHostMalloc((void **)&h_stage_abort, abort_cap * sizeof(int32_t), hipHostMallocDefault));
     }
+    svh::finalize_stats(d_stats, count, stream);
     SV_HIP(hipMemcpyAsync(h_stage + stage_used, d_stats, count * sizeof(sv_stats), hipMemcpyDeviceToHost, stream));
     SV_HIP(hipMemcpyAsync(h_stage_abort + abort_used, d_abort, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
     landings.push_back(Landing{dst, stage_used, count, abort_used});

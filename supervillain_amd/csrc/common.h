@@ -5,6 +5,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -213,8 +214,8 @@ struct sv_villain {
     char *d_aux = nullptr;         // small per-call device block (CohomologyUpdate: rng | stats | plan)
     char *h_aux = nullptr;         // its pinned host image
     size_t aux_cap = 0;
-    double *d_obs = nullptr;       // inline observables: 4 device sums (coarse-grained hipMalloc)
-    double *h_obs = nullptr;       // and their pinned host image
+    unsigned long long *d_obs = nullptr;  // inline observables: the OBS_WORDS exact words (coarse-grained hipMalloc)
+    unsigned long long *h_obs = nullptr;  // and their pinned host image
     int32_t *d_strips = nullptr;   // villain_sweep_hot's strip table (strip_schedule), n_strips entries of 3
     int32_t n_strips = 0;
     std::vector<int32_t> h_strips;  // (its host copy: the split replay orders its straddling strips first)
@@ -293,6 +294,105 @@ inline void launch_check(const char *kernel, hipStream_t s) {
 }
 }  // namespace sv
 #define SV_LAUNCHED(kernel, stream) (sv::sync_check_on() ? sv::launch_check(kernel, stream) : (void)0)
+
+// Exact Metropolis acceptance sums (the float statistics must not depend on the launch geometry).
+// A proposal's acceptance probability p in [0, 1] enters as T(p) = round(p 2^103), an integer, in two parts: x = p +
+// 2.0 lies in the binade [2, 4) (ulp 2^-51), so bits(x) = 0x4000000000000000 + round(p 2^51) and a = x - 2.0 is p
+// rounded to 2^-51; the remainder r = p - a is exact (|r| <= 2^-52) and fma(r, 2^103, 1.5 2^52) holds round(r 2^103)
+// in its low bits.  T(p) = round(p 2^51) 2^52 + round(r 2^103): resolution 2^-103 (~1e-31) per proposal.  A lane
+// keeps the raw bits of x summed modulo 2^64 (after k < 2^11 terms the low 62 bits are the exact sum of the round(p
+// 2^51)) and the round(r 2^103) in an int64 (fx_add: four f64 and six integer operations).  It flushes its exact value
+// sum T (< 2^114) as three 38-bit limbs, so every later addition -- over lanes, waves, workgroups, strips, tiles,
+// replica batches, launches -- is an integer addition whose result does not depend on its order, and the statistic
+// is fx_value(limb sums): the same double whatever the strip heights, layouts, tile grids or replica counts of the run,
+// within ~2 ulp of the exact sum of the p (the reference's NumPy pairwise sums are within rounding of it too).
+// On the device a stats slot holds the three limb sums in its host-owned fields until it is finalized (stats_finalize,
+// or fx_value on the host for the domain summaries): proposed = limb 0, rejections = limb 1, acceptance_sum's bits =
+// limb 2.
+namespace sv {
+constexpr uint64_t FX_LANE_MASK = (uint64_t(1) << 62) - 1, FX_LIMB = (uint64_t(1) << 38) - 1;
+struct AccFx {
+    uint64_t a = 0;  // raw bits of p + 2.0, summed mod 2^64
+    int64_t b = 0;   // round(r 2^103), summed
+};
+__device__ __forceinline__ void fx_add(AccFx &s, double p) {
+    const double x = p + 2.0;
+    s.a += (uint64_t)__double_as_longlong(x);
+    const double r = p - (x - 2.0);
+    s.b += (int64_t)__double_as_longlong(__builtin_fma(r, 0x1p103, 0x1.8p52)) - (int64_t)0x4338000000000000ll;
+}
+// the same, the lane's two words kept in LDS slots of its own (no-return LDS adds: no registers held across a loop)
+__device__ __forceinline__ void fx_add_lds(unsigned long long *a, unsigned long long *b, double p) {
+    const double x = p + 2.0;
+    atomicAdd(a, (unsigned long long)__double_as_longlong(x));
+    const double r = p - (x - 2.0);
+    atomicAdd(b, (unsigned long long)(__double_as_longlong(__builtin_fma(r, 0x1p103, 0x1.8p52)) -
+                                      (long long)0x4338000000000000ll));
+}
+// a lane's exact value sum T = (a mod 2^62) 2^52 + b (>= 0, < 2^114) as three 38-bit limbs
+__device__ __forceinline__ void fx_limbs(const AccFx &s, unsigned long long &w0, unsigned long long &w1,
+                                         unsigned long long &w2) {
+    const unsigned __int128 T = ((unsigned __int128)(s.a & FX_LANE_MASK) << 52) + (unsigned __int128)(__int128)s.b;
+    w0 = (uint64_t)T & FX_LIMB;
+    w1 = (uint64_t)(T >> 38) & FX_LIMB;
+    w2 = (uint64_t)(T >> 76);
+}
+// device word i of a stats slot: 0 accepted, 1..3 the acceptance limbs (proposed, rejections, acceptance_sum's bits)
+__device__ __forceinline__ unsigned long long *stat_word(sv_stats *st, int i) {
+    return i == 0 ? (unsigned long long *)&st->accepted
+         : i == 1 ? (unsigned long long *)&st->proposed
+         : i == 2 ? (unsigned long long *)&st->rejections
+                  : (unsigned long long *)&st->acceptance_sum;
+}
+__host__ __device__ __forceinline__ uint64_t stat_limb(const sv_stats &st, int i) {  // i = 0, 1, 2
+    if (i == 0) return (uint64_t)st.proposed;
+    if (i == 1) return (uint64_t)st.rejections;
+    uint64_t w;
+    memcpy(&w, &st.acceptance_sum, sizeof w);
+    return w;
+}
+// the statistic from the three limb sums (each < 2^64): a deterministic function of the exact total T 2^-103
+__host__ __device__ __forceinline__ double fx_value(uint64_t w0, uint64_t w1, uint64_t w2) {
+    w1 += w0 >> 38;
+    w0 &= FX_LIMB;
+    w2 += w1 >> 38;
+    w1 &= FX_LIMB;
+    return ((double)w2 * 0x1p76 + (double)w1 * 0x1p38 + (double)w0) * 0x1p-103;
+}
+
+// Exact inline observables (same reason).  A site's action term t = l0^2 + l1^2 (l the link residuals, in the
+// reference's operation order) enters as round(t 2^40) when t < 2^12 (|l| < 45; at kappa >= 0.05 a larger residual
+// has Boltzmann weight below e^-100), else as a double added to the big-term word in arrival order -- the one case
+// whose sum still depends on the launch geometry.  The resolution is 2^-41 per site (an absolute error below 2^-41 V
+// on the action sum: relative 1e-13 or less in any state whose mean t exceeds 0.005).  A lane holds at most 256 such
+// values (< 2^60) and flushes them as 32-bit halves (lo, hi).  The integer observables (sum dn^2, sum n0, sum n1) are
+// integer sums.
+// Per (replica, sweep) the OBS_WORDS words are: the action (lo, hi), sum dn^2, sum n0, sum n1 (two's complement),
+// the big-term double; obs_raw() turns them into the 4 raw sums of the C-ABI {sum l^2, sum dn^2, sum n0, sum n1}.
+constexpr int OBS_WORDS = 6;
+constexpr double ACT_LIMIT = 4096.0;
+__device__ __forceinline__ uint64_t act_fx(double t) {  // t in [0, ACT_LIMIT)
+    // t 2^40 + 2^52 rounded once (t 2^40 is exact): the double's low bits are round(t 2^40)
+    return (uint64_t)__double_as_longlong(__builtin_fma(t, 0x1p40, 0x1p52)) - 0x4330000000000000ull;
+}
+__host__ __device__ __forceinline__ double act_value(uint64_t lo, uint64_t hi) {
+    const uint64_t h = hi + (lo >> 32), l = lo & 0xffffffffull;
+    return ((double)h * 4294967296.0 + (double)l) * 0x1p-40;
+}
+inline void obs_raw(const unsigned long long *w, double *raw) {
+    double big;
+    std::memcpy(&big, &w[5], sizeof big);
+    raw[0] = act_value(w[0], w[1]) + big;
+    raw[1] = (double)w[2];
+    raw[2] = (double)(int64_t)w[3];
+    raw[3] = (double)(int64_t)w[4];
+}
+}  // namespace sv
+namespace svh {
+// the exact acceptance limbs of n device stats slots -> their acceptance_sum (villain.hip); enqueued before every copy
+// of device statistics to the host (a finalized slot is marked and left alone by a second finalize)
+void finalize_stats(sv_stats *d, int64_t n, hipStream_t stream);
+}  // namespace svh
 
 // The drain at the start of every sv_*_destroy: the work queued on the context stream (and on `side`, an object's
 // own stream) ends before anything is freed.  A failure there is the failure of work queued earlier -- by this

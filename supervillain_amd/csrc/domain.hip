@@ -211,14 +211,14 @@ __global__ __launch_bounds__(256) void scan_rejections(ScanArgs a) {
 __global__ void wd_fold(const StatStripe *ss, sv_stats *out, int count) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= count) return;
-    unsigned long long a = 0;
-    double p = 0.0;
+    unsigned long long a = 0, w[3] = {0, 0, 0};
     for (int j = 0; j < NSTRIPE; j++) {
         a += ss[k * NSTRIPE + j].acc;
-        p += ss[k * NSTRIPE + j].psum;
+        for (int i = 0; i < 3; i++) w[i] += ss[k * NSTRIPE + j].pw[i];
     }
-    out[k].accepted = (int64_t)a;
-    out[k].acceptance_sum = p;
+    // the exact acceptance limbs (common.h) in the slot's words: summed over tiles on the host
+    *stat_word(&out[k], 0) = a;
+    for (int i = 0; i < 3; i++) *stat_word(&out[k], 1 + i) = w[i];
 }
 
 }  // namespace sv
@@ -503,10 +503,12 @@ void fill_stats(const sv_domain *d, const SkipMap &skips, int nb, int sw, int co
     const int64_t V = (int64_t)d->Nt * d->Nx;
     for (int k = 0; k < count; k++) {
         sv_stats s{0, V, 0.0, 0};
+        uint64_t w[3] = {0, 0, 0};  // the tiles' exact acceptance limbs (common.h): the single lattice's statistic
         for (const Summary &S : d->host_sum) {  // global tile order: identical on every rank
             s.accepted += S.stats[k].accepted;
-            s.acceptance_sum += S.stats[k].acceptance_sum;
+            for (int i = 0; i < 3; i++) w[i] += stat_limb(S.stats[k], i);
         }
+        s.acceptance_sum = fx_value(w[0], w[1], w[2]);
         s.rejections = rejections_in(skips, sw + k, nb);
         stats[sw + k] = s;
     }
@@ -877,10 +879,12 @@ void run_wdomain(sv_domain *d, double kappa, double W_eff, int64_t it, int32_t s
         for (int k = 0; k < count; k++)
             for (int j = 0; j < 2; j++) {
                 sv_stats st{0, V, 0.0, 0};
+                uint64_t w[3] = {0, 0, 0};  // exact acceptance limbs (common.h)
                 for (const Summary &S : d->host_sum) {
                     st.accepted += S.stats[2 * k + j].accepted;
-                    st.acceptance_sum += S.stats[2 * k + j].acceptance_sum;
+                    for (int i = 0; i < 3; i++) w[i] += stat_limb(S.stats[2 * k + j], i);
                 }
+                st.acceptance_sum = fx_value(w[0], w[1], w[2]);
                 for (int bi = j == 0 ? 0 : 5; bi < (j == 0 ? 5 : nb); bi++) {
                     auto itk = skips.find({sw + k, bi});
                     if (itk != skips.end()) st.rejections += (int64_t)itk->second.size();

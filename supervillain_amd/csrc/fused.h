@@ -70,28 +70,24 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-// One atomic pair per WORKGROUP (every thread must call this): same-address atomics from thousands
-// of waves serialize in one L2 channel.
-__device__ __forceinline__ void flush_stats(sv_stats *st, int64_t acc, double psum) {
-    __shared__ unsigned long long s_acc[16];
-    __shared__ double s_ps[16];
-    unsigned long long a = (unsigned long long)acc;
-    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
-    psum = wave_sum(psum);
-    if ((threadIdx.x & 63) == 0) {
-        s_acc[threadIdx.x >> 6] = a;
-        s_ps[threadIdx.x >> 6] = psum;
-    }
+// One atomic quadruple per WORKGROUP (every thread must call this): same-address atomics from thousands of waves
+// serialize in one L2 channel.  psum is the lane's exact acceptance sum (common.h), flushed as three limbs into the
+// slot's host-owned words.
+template <int MAXW = 16>  // (waves per workgroup: the LDS it takes counts against the replica kernel's 4th workgroup)
+__device__ __forceinline__ void flush_stats(sv_stats *st, int64_t acc, const AccFx &psum) {
+    __shared__ unsigned long long s_w[4][MAXW];
+    unsigned long long w[4];
+    w[0] = (unsigned long long)acc;
+    fx_limbs(psum, w[1], w[2], w[3]);
+    for (int o = 32; o > 0; o >>= 1)
+        for (int i = 0; i < 4; i++) w[i] += __shfl_xor(w[i], o);
+    if ((threadIdx.x & 63) == 0)
+        for (int i = 0; i < 4; i++) s_w[i][threadIdx.x >> 6] = w[i];
     __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long ta = 0;
-        double tp = 0.0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); w++) {
-            ta += s_acc[w];
-            tp += s_ps[w];
-        }
-        atomicAdd((unsigned long long *)&st->accepted, ta);
-        unsafeAtomicAdd(&st->acceptance_sum, tp);  // hardware f64 atomic (coarse-grained HBM)
+    if (threadIdx.x < 4) {
+        unsigned long long t = 0;
+        for (int v = 0; v < (int)(blockDim.x >> 6); v++) t += s_w[threadIdx.x][v];
+        atomicAdd(stat_word(st, threadIdx.x), t);
     }
 }
 
@@ -516,11 +512,6 @@ __device__ __forceinline__ double u53(uint64_t x) {
 }
 
 
-__device__ __forceinline__ double wsum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
 
 // Per-sweep statistics are accumulated in NSTRIPE stripes (one 128-B line each) picked by workgroup:
 // thousands of short waves adding into ONE address serialize in one L2 channel (measured: ~200 us
@@ -528,18 +519,20 @@ __device__ __forceinline__ double wsum(double v) {
 static constexpr int NSTRIPE = 16;
 struct StatStripe {
     unsigned long long acc;
-    double psum;
-    uint64_t pad[14];
+    unsigned long long pw[3];  // the exact acceptance limbs (common.h)
+    uint64_t pad[12];
 };
 
-__device__ __forceinline__ void wflush(StatStripe *ss, int64_t acc, double psum) {
-    unsigned long long a = (unsigned long long)acc;
-    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
-    psum = wsum(psum);
+__device__ __forceinline__ void wflush(StatStripe *ss, int64_t acc, const AccFx &psum) {
+    unsigned long long w[4];
+    w[0] = (unsigned long long)acc;
+    fx_limbs(psum, w[1], w[2], w[3]);
+    for (int o = 32; o > 0; o >>= 1)
+        for (int i = 0; i < 4; i++) w[i] += __shfl_xor(w[i], o);
     if ((threadIdx.x & 63) == 0) {
         StatStripe *st = ss + ((blockIdx.x + blockIdx.y * 7 + (threadIdx.x >> 6) * 3) & (NSTRIPE - 1));
-        atomicAdd(&st->acc, a);
-        unsafeAtomicAdd(&st->psum, psum);  // hardware f64 atomic (coarse-grained HBM)
+        atomicAdd(&st->acc, w[0]);
+        for (int i = 0; i < 3; i++) atomicAdd(&st->pw[i], w[1 + i]);
     }
 }
 

@@ -70,33 +70,22 @@ __device__ __forceinline__ uint32_t bnd_word_slow(const JumpTables *T, const Blo
     return (qq & 1) ? (uint32_t)(X >> 32) : (uint32_t)X;
 }
 
-__device__ __forceinline__ double lwave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
 
-// One atomic pair per workgroup (all threads call it).
-__device__ __forceinline__ void lflush(sv_stats *st, int64_t acc, double psum) {
-    __shared__ unsigned long long s_acc[16];
-    __shared__ double s_ps[16];
-    unsigned long long a = (unsigned long long)acc;
-    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
-    psum = lwave_sum(psum);
-    if ((threadIdx.x & 63) == 0) {
-        s_acc[threadIdx.x >> 6] = a;
-        s_ps[threadIdx.x >> 6] = psum;
-    }
+// One atomic quadruple per workgroup (all threads call it); psum is the lane's exact acceptance sum (common.h).
+__device__ __forceinline__ void lflush(sv_stats *st, int64_t acc, const AccFx &psum) {
+    __shared__ unsigned long long s_w[4][16];
+    unsigned long long w[4];
+    w[0] = (unsigned long long)acc;
+    fx_limbs(psum, w[1], w[2], w[3]);
+    for (int o = 32; o > 0; o >>= 1)
+        for (int i = 0; i < 4; i++) w[i] += __shfl_xor(w[i], o);
+    if ((threadIdx.x & 63) == 0)
+        for (int i = 0; i < 4; i++) s_w[i][threadIdx.x >> 6] = w[i];
     __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long ta = 0;
-        double tp = 0.0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); w++) {
-            ta += s_acc[w];
-            tp += s_ps[w];
-        }
-        atomicAdd((unsigned long long *)&st->accepted, ta);
-        unsafeAtomicAdd(&st->acceptance_sum, tp);
+    if (threadIdx.x < 4) {
+        unsigned long long t = 0;
+        for (int v = 0; v < (int)(blockDim.x >> 6); v++) t += s_w[threadIdx.x][v];
+        atomicAdd(stat_word(st, threadIdx.x), t);
     }
 }
 
@@ -142,6 +131,8 @@ static inline int grid_for(int64_t count, int64_t mult) {
     if (count <= target) return (int)std::max<int64_t>(1, (count + 255) / 256);
     const int64_t l = mult / gcd_i(mult, 256) * 256;  // lcm(mult, 256)
     int64_t S = std::max<int64_t>(1, target / l) * l;
+    // at most 1024 grid-stride iterations per lane: a lane's exact acceptance sum must stay below 2^11 terms (common.h)
+    S = std::max<int64_t>(S, (count + 1024 * l - 1) / (1024 * l) * l);
     return (int)(S / 256);
 }
 
@@ -219,6 +210,7 @@ static inline void run_batches(sv_ctx *ctx, const std::vector<BlockSpec> &specs,
             continue;
         }
         if (!may_reject) queue_abort_copy(ctx);
+        finalize_stats(ctx->d_stats, count, ctx->stream);
         SV_HIP(hipMemcpyAsync(stats + sw, ctx->d_stats, count * sizeof(sv_stats), hipMemcpyDeviceToHost, ctx->stream));
         SV_HIP(hipStreamSynchronize(ctx->stream));
         if (!may_reject) {

@@ -97,7 +97,7 @@ struct sv_replicas {
     PlanIn *d_plan = nullptr;
     Block *d_blocks = nullptr;
     sv_stats *d_stats = nullptr;
-    double *d_obs = nullptr;
+    unsigned long long *d_obs = nullptr;  // per (replica, sweep): the OBS_WORDS exact observable words (common.h)
     std::vector<std::pair<uint64_t, uint64_t>> incs;  // current per-replica increments
     // pinned batch tail: abort flag, report count, then the batch's statistics and observables (one DMA each,
     // one synchronization)
@@ -216,8 +216,10 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
     const bool inl = obs != nullptr || mo != nullptr;  // the inline observables are summed
     // sweep k of replica r: its 4 raw sums (action sum, w2 sum, n0 sum, n1 sum) into the caller's arrays -- as they are
     // (obs), or measured (mo: the operations of replicas.py's former NumPy post-processing, in its order)
-    auto put_obs = [&](int r, int64_t k, const double *raw) {
+    auto put_obs = [&](int r, int64_t k, const unsigned long long *words) {
         const size_t e = (size_t)r * sweeps + (size_t)k;
+        double raw[4];
+        obs_raw(words, raw);  // the exact words -> the 4 raw sums (common.h)
         if (obs) {
             std::memcpy(obs + e * 4, raw, 4 * sizeof(double));
             return;
@@ -253,7 +255,7 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
     // on they run on the general fused kernel's int32 image, beside the others (the split launches below)
     std::vector<char> big(R, 0);
     // pinned batch tails, two slots: batch k+1 is enqueued before batch k's statistics are copied out
-    const size_t slot_bytes = 64 + (size_t)R * REP_BATCH * (sizeof(sv_stats) + 4 * sizeof(double));
+    const size_t slot_bytes = 64 + (size_t)R * REP_BATCH * (sizeof(sv_stats) + OBS_WORDS * sizeof(unsigned long long));
     if (b->tail_cap < 2 * slot_bytes) {
         SV_HIP(hipStreamSynchronize(ctx->stream));
         if (b->h_tail) SV_HIP(hipHostFree(b->h_tail));
@@ -302,7 +304,7 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         ctx->ensure_skips(B.hskip.size() + 1);
         b->stage.put(ctx->stream, ctx->d_skips, B.hskip.data(), B.hskip.size() * sizeof(uint32_t));
         reset_batch(ctx, b->d_stats, (size_t)R * count * sizeof(sv_stats), inl ? b->d_obs : nullptr,
-                    inl ? (size_t)R * count * 4 * sizeof(double) : 0);
+                    inl ? (size_t)R * count * OBS_WORDS * sizeof(unsigned long long) : 0);
         // A sweep runs on the fast-draw kernel (villain_sweep_hot_fr) when no replica's choice blocks of that sweep
         // carry a skip (the closed-form replicas have none; the host-planned ones are checked), else on the general
         // fused kernel.  Within a skip-free sweep a replica's four choice blocks start on the same half-word parity
@@ -386,10 +388,10 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
             A.rep_blocks = count * NB;
             A.rep_field = V;
             A.rep_stat = count;
-            A.rep_obs = 4 * count;
+            A.rep_obs = OBS_WORDS * count;
             A.Trep = b->d_Trep;
             A.advrep = b->d_adv;
-            A.obs = inl ? b->d_obs + 4 * k : nullptr;
+            A.obs = inl ? b->d_obs + OBS_WORDS * k : nullptr;
             if (hot_k[k]) {
                 launch_hot_fr(A, R * tiles, inl, ctx->stream);
                 ctx->sweeps_hot++;
@@ -435,9 +437,10 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
         char *tail = b->h_tail + slot * slot_bytes;
         const size_t st_bytes = (size_t)R * count * sizeof(sv_stats);
         SV_HIP(hipMemcpyAsync(tail, ctx->d_abort, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));  // + d_nreport
+        finalize_stats(b->d_stats, (int64_t)R * count, ctx->stream);
         SV_HIP(hipMemcpyAsync(tail + 64, b->d_stats, st_bytes, hipMemcpyDeviceToHost, ctx->stream));
         if (inl)
-            SV_HIP(hipMemcpyAsync(tail + 64 + st_bytes, b->d_obs, (size_t)R * count * 4 * sizeof(double),
+            SV_HIP(hipMemcpyAsync(tail + 64 + st_bytes, b->d_obs, (size_t)R * count * OBS_WORDS * sizeof(unsigned long long),
                                   hipMemcpyDeviceToHost, ctx->stream));
     };
     // --- keep sweeps [B.sw, B.sw + good) of a finished batch: statistics and observables into the caller's arrays
@@ -445,7 +448,7 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
     auto keep = [&](const RepBatch &B, int good, const std::vector<char> *fail = nullptr) {
         const char *tail = b->h_tail + B.slot * slot_bytes;
         const sv_stats *h_st = (const sv_stats *)(tail + 64);
-        const double *h_ob = (const double *)(tail + 64 + (size_t)R * B.count * sizeof(sv_stats));
+        const unsigned long long *h_ob = (const unsigned long long *)(tail + 64 + (size_t)R * B.count * sizeof(sv_stats));
         for (int r = 0; r < R; r++) {
             const bool none = skips[r].empty();
             sv_stats *dst = stats + (size_t)r * sweeps + B.sw;
@@ -458,7 +461,7 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
                 if (mo) mo->acceptance[(size_t)r * sweeps + B.sw + k] = src[k].acceptance_sum / (double)V;
             }
             if (inl)
-                for (int k = 0; k < upto; k++) put_obs(r, B.sw + k, h_ob + ((size_t)r * B.count + k) * 4);
+                for (int k = 0; k < upto; k++) put_obs(r, B.sw + k, h_ob + ((size_t)r * B.count + k) * OBS_WORDS);
         }
     };
 
@@ -491,7 +494,7 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
                 const size_t e = (size_t)F[i] * count + k;
                 b->stage.put(ctx->stream, b->d_blocks + e * NB, &fb[i * NB], NB * sizeof(Block));
                 SV_HIP(hipMemsetAsync(b->d_stats + e, 0, sizeof(sv_stats), ctx->stream));
-                if (inl) SV_HIP(hipMemsetAsync(b->d_obs + 4 * e, 0, 4 * sizeof(double), ctx->stream));
+                if (inl) SV_HIP(hipMemsetAsync(b->d_obs + OBS_WORDS * e, 0, OBS_WORDS * sizeof(unsigned long long), ctx->stream));
             }
             b->stage.put(ctx->stream, ctx->d_skips, allsk.data(), allsk.size() * sizeof(uint32_t));
             b->stage.put(ctx->stream, b->d_map, F.data(), F.size() * sizeof(int32_t));
@@ -518,10 +521,10 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
             A.rep_blocks = count * NB;
             A.rep_field = V;
             A.rep_stat = count;
-            A.rep_obs = 4 * count;
+            A.rep_obs = OBS_WORDS * count;
             A.Trep = b->d_Trep;
             A.advrep = b->d_adv;
-            A.obs = inl ? b->d_obs + 4 * k : nullptr;
+            A.obs = inl ? b->d_obs + OBS_WORDS * k : nullptr;
             A.rep_map = b->d_map;
             launch_fused_batch(A, (int)F.size() * A.tiles_per_rep, inl, ctx->stream);
             ctx->sweeps_fused++;
@@ -532,14 +535,16 @@ void run_replicas(sv_replicas *b, const VParams &P, int32_t sweeps, sv_rng *rngs
                     const int r = F[i];
                     const size_t e = (size_t)r * count + k;
                     sv_stats *dst = stats + (size_t)r * sweeps + B.sw + k;
-                    SV_HIP(hipMemcpy(dst, b->d_stats + e, sizeof(sv_stats), hipMemcpyDeviceToHost));
+                    finalize_stats(b->d_stats + e, 1, ctx->stream);
+                    SV_HIP(hipMemcpyAsync(dst, b->d_stats + e, sizeof(sv_stats), hipMemcpyDeviceToHost, ctx->stream));
+                    SV_HIP(hipStreamSynchronize(ctx->stream));
                     dst->proposed = V;
                     dst->rejections = rejections_in(skips[r], B.sw + k, NB);
                     if (mo) mo->acceptance[(size_t)r * sweeps + B.sw + k] = dst->acceptance_sum / (double)V;
                     if (inl) {
-                        double raw[4];
-                        SV_HIP(hipMemcpy(raw, b->d_obs + 4 * e, 4 * sizeof(double), hipMemcpyDeviceToHost));
-                        put_obs(r, B.sw + k, raw);
+                        unsigned long long words[OBS_WORDS];
+                        SV_HIP(hipMemcpy(words, b->d_obs + OBS_WORDS * e, sizeof words, hipMemcpyDeviceToHost));
+                        put_obs(r, B.sw + k, words);
                     }
                     cur[r] = cf[i];
                 }
@@ -711,7 +716,7 @@ int sv_replicas_create(sv_ctx *ctx, int32_t R, int32_t N, sv_replicas **out) {
         SV_HIP(hipMalloc(&b->d_plan, R * sizeof(PlanIn)));
         SV_HIP(hipMalloc(&b->d_blocks, (size_t)R * REP_BATCH * NB * sizeof(Block)));
         SV_HIP(hipMalloc(&b->d_stats, (size_t)R * REP_BATCH * sizeof(sv_stats)));
-        SV_HIP(hipMalloc(&b->d_obs, (size_t)R * REP_BATCH * 4 * sizeof(double)));
+        SV_HIP(hipMalloc(&b->d_obs, (size_t)R * REP_BATCH * OBS_WORDS * sizeof(unsigned long long)));
         SV_HIP(hipMalloc(&b->d_gate, sizeof(int32_t)));
         *out = b;
         return 0;

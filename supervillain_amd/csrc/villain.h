@@ -69,7 +69,7 @@ struct FArgs {
     int32_t rep_obs;                // obs entries per replica
     const JumpTables *const *Trep;  // per-replica tables, or nullptr (all use T)
     const Affine *advrep;           // per-replica adv[3], or nullptr (all use adv)
-    double *obs;                    // OBS kernels: per replica {sum (d phi - 2 pi n)^2, sum (dn)^2, sum n0, sum n1}
+    unsigned long long *obs;        // OBS kernels: per replica the OBS_WORDS exact observable words (common.h)
     // villain_sweep_hot: per strip (in the XCD-aware logical order) its column strip and rows {ix, t0, t1}, or null
     // (uniform strips of TH rows); lets the strips of the last rounds of slots be shorter (strip_schedule)
     const int32_t *strips = nullptr;
@@ -182,8 +182,9 @@ __host__ __device__ inline bool split_rows(int32_t qs, int32_t Nt, int32_t t0, i
 __host__ __device__ inline int32_t block_frame(int32_t bs, int32_t K) { return bs + 5 * (K - 1) + 5; }
 __host__ __device__ inline size_t block_lds_bytes(int32_t F) {
     // small-offset maps, row bases [F][2 sets][2 colours][6], phi / r0 / r1 (f64) and n0 / n1 (int32) per frame
-    // site, per-sweep statistics (16 + 16 words), the overflow flag and the choice-block descriptors (16 sweeps x 8)
-    return 2 * 16 * (size_t)SMALL_LDS + (size_t)F * 24 * 16 + (size_t)F * F * 32 + 256 + 16 + 16 * 8 * 8;
+    // site, per-sweep statistics (16 x 4 words: count, exact acceptance limbs), the overflow flag and the choice-block
+    // descriptors (16 sweeps x 8)
+    return 2 * 16 * (size_t)SMALL_LDS + (size_t)F * 24 * 16 + (size_t)F * F * 32 + 512 + 16 + 16 * 8 * 8;
 }
 
 // (FArgs::progress) the launch has started: every earlier launch of its stream has finished
@@ -216,6 +217,7 @@ VParams make_params(int32_t N, double kappa, int64_t W, double interval_phi, int
 int absorb_reports(const AbortInfo &a, int first, SkipMap &skips);
 DevScratch scratch(sv_ctx *ctx);
 AbortInfo read_abort(sv_ctx *ctx);  // synchronizes the stream
+
 void clear_abort(sv_ctx *ctx);
 // Before a batch, in ONE launch: the abort flag and report count, and up to two arrays (multiples of 8 bytes) zeroed
 // -- each small hipMemsetAsync is a blit of its own on the queue (~4.5 us of GPU time apiece in the Hammer traces)

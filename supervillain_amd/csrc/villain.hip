@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void villain_pass_generic(VParams P, double *p
     const int64_t N = P.N, V = N * N;
     int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     int64_t acc_count = 0;
-    double psum = 0.0;
+    AccFx psum;  // exact acceptance sum (common.h)
     if (i < nc) {
         const int64_t s = sites[i];
         const int64_t t = s / N, x = s - t * N;
@@ -103,7 +103,7 @@ __global__ __launch_bounds__(256) void villain_pass_generic(VParams P, double *p
         p = p > 1.0 ? 1.0 : p;
         const int acc = u < p;
         acc_count = acc;
-        psum = p;
+        fx_add(psum, p);
         const double cphi = dphi * (double)acc;
         phi[s] = phi[s] + cphi;
         const double dcp_f = 0.0 + (0.0 - cphi);
@@ -141,7 +141,8 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     __shared__ Affine s_adv[3];
     __shared__ u128 s_base[NW][32];  // per wave: [8c + ty] = block ty's base for the colour-c row; [16 + ..] at xw
     __shared__ int32_t s_bad;
-    __shared__ double s_obs[4];  // OBS: workgroup sums of the inline observables
+    __shared__ unsigned long long s_obsw[5];  // OBS: the workgroup's exact observable words (common.h)
+    __shared__ double s_obig;                 // OBS: its action terms t >= ACT_LIMIT
     __shared__ Block s_blk[11];  // this sweep's descriptors (LDS: no vector-memory waits in the loop)
 
     note_progress(A);
@@ -209,7 +210,8 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     const Rep RL{s_blk, RP.T, RP.id};  // the loop's view (valid after the prologue barrier)
     if (threadIdx.x < 3) s_adv[threadIdx.x] = REPS ? A.advrep[3 * rep + threadIdx.x] : A.adv[threadIdx.x];
     if (threadIdx.x == 0) s_bad = 0;
-    if (OBS && threadIdx.x < 4) s_obs[threadIdx.x] = 0.0;
+    if (OBS && threadIdx.x < 5) s_obsw[threadIdx.x] = 0;
+    if (OBS && threadIdx.x == 5) s_obig = 0.0;
 
     // the buffered-half flags of the fwd choice blocks (mu = 0, 1) per colour, kept in SGPRs: reading
     // them from the descriptors inside the loop would put a vmcnt(0) wait behind the row prefetch
@@ -307,13 +309,14 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
     }
 
     int64_t acc_count = 0;
-    double psum = 0.0;
+    AccFx psum;  // exact acceptance sum (common.h)
 
     // coalesced stores of finished rows [ra, ra+NW) (clipped to the tile) from the ring: wave w
     // stores row ra + w, lane l columns l and l + 64
     auto store_rows = [&](int32_t ra) {
         const int32_t q = ra + wave;
-        double o_act = 0.0, o_w2 = 0.0, o_n0 = 0.0, o_n1 = 0.0;  // OBS partials (integers exact in f64)
+        unsigned long long o_act = 0, o_w2 = 0;  // OBS partials: exact action values (common.h), integer sums
+        int64_t o_n0 = 0, o_n1 = 0;
         if (q >= t0 && q < t1) {
             const int slot = (q - rbase) % R;
             const int64_t g0 = mrow(q) + x0;  // tile sites never wrap
@@ -335,26 +338,29 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
                         const double ph = s_phi[slot][cx];
                         const double l0 = (0.0 + (s_phi[slot1][cx] - ph)) - TWO_PI * (double)s_n0[slot][cx];
                         const double l1 = (0.0 + (s_phi[slot][cxp(cx)] - ph)) - TWO_PI * (double)s_n1[slot][cx];
-                        o_act += l0 * l0 + l1 * l1;
+                        const double t = l0 * l0 + l1 * l1;
+                        if (t < ACT_LIMIT) o_act += act_fx(t);
+                        else atomicAdd(&s_obig, t);
                         const int64_t dn = ((int64_t)s_n1[slot1][cx] - s_n1[slot][cx]) -
                                            ((int64_t)s_n0[slot][cxp(cx)] - s_n0[slot][cx]);
-                        o_w2 += (double)(dn * dn);
-                        o_n0 += (double)s_n0[slot][cx];
-                        o_n1 += (double)s_n1[slot][cx];
+                        o_w2 += (unsigned long long)(dn * dn);
+                        o_n0 += s_n0[slot][cx];
+                        o_n1 += s_n1[slot][cx];
                     }
                 }
             }
         }
         if (OBS) {
-            o_act = wave_sum(o_act);
-            o_w2 = wave_sum(o_w2);
-            o_n0 = wave_sum(o_n0);
-            o_n1 = wave_sum(o_n1);
+            // integer sums (a row's action values < 2^59): the same words in any order (common.h)
+            unsigned long long w[4] = {o_act, o_w2, (unsigned long long)o_n0, (unsigned long long)o_n1};
+            for (int o = 32; o > 0; o >>= 1)
+                for (int i = 0; i < 4; i++) w[i] += __shfl_xor(w[i], o);
             if (lane == 0) {
-                atomicAdd(&s_obs[0], o_act);
-                atomicAdd(&s_obs[1], o_w2);
-                atomicAdd(&s_obs[2], o_n0);
-                atomicAdd(&s_obs[3], o_n1);
+                atomicAdd(&s_obsw[0], w[0] & 0xffffffffull);
+                atomicAdd(&s_obsw[1], w[0] >> 32);
+                atomicAdd(&s_obsw[2], w[1]);
+                atomicAdd(&s_obsw[3], w[2]);
+                atomicAdd(&s_obsw[4], w[3]);
             }
         }
     };
@@ -424,7 +430,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
                 const bool own = q >= q_lo && q < q_hi && (FR || (x >= c_lo && x < c_hi));
                 if (own) {  // count each site once; colour-0 phi is final after this pass
                     acc_count += acc;
-                    psum += p;
+                    fx_add(psum, p);
                 }
                 const double cphi = D.dphi * (double)acc;
                 s_phi[s0][cx] = (ph + cphi) + 0.0;  // final colour-0 phi (the colour-1 pass adds +0.0)
@@ -492,7 +498,7 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
                 const int acc = D.u < p;
                 if (q >= q_lo && q < q_hi && (FR || (x >= c_lo && x < c_hi))) {
                     acc_count += acc;
-                    psum += p;
+                    fx_add(psum, p);
                 }
                 const double cphi = D.dphi * (double)acc;
                 s_phi[s0][cx] = (ph + 0.0) + cphi;
@@ -528,10 +534,12 @@ __device__ __forceinline__ void sweep_body(const FArgs &A) {
         // |n| too large for the int32 LDS image: the host falls back to the generic path
         report(A.S, A.sweep, OVERFLOW_BLOCK, 0, (uint32_t)rep);
     }
-    flush_stats(REPS ? A.stat + (int64_t)rep * A.rep_stat : A.stat, acc_count, psum);
+    flush_stats<NW>(REPS ? A.stat + (int64_t)rep * A.rep_stat : A.stat, acc_count, psum);
     if (OBS) {
         __syncthreads();
-        if (threadIdx.x < 4) unsafeAtomicAdd(&A.obs[(int64_t)rep * A.rep_obs + threadIdx.x], s_obs[threadIdx.x]);
+        unsigned long long *ow = A.obs + (int64_t)rep * A.rep_obs;
+        if (threadIdx.x < 5 && s_obsw[threadIdx.x]) atomicAdd(&ow[threadIdx.x], s_obsw[threadIdx.x]);
+        if (threadIdx.x == 5 && s_obig != 0.0) unsafeAtomicAdd((double *)&ow[5], s_obig);
     }
 }
 
@@ -556,10 +564,12 @@ template __global__ void villain_sweep_fused_obs<true>(FArgs);
 // ================================================================================================
 // observables (fused reductions over the current state)
 // ================================================================================================
-__global__ void villain_observables_kernel(int32_t N, double half_kappa, const double *phi, const int64_t *n,
-                                           double *out) {
+__global__ void villain_observables_kernel(int32_t N, const double *phi, const int64_t *n, unsigned long long *out) {
+    // the exact observable words of the state (common.h OBS_WORDS; the launch gives every thread <= 256 sites)
     const int64_t V = (int64_t)N * N;
-    double s_act = 0.0, s_w2 = 0.0, s_n0 = 0.0, s_n1 = 0.0;
+    unsigned long long q = 0, w2 = 0;
+    int64_t s_n0 = 0, s_n1 = 0;
+    double big = 0.0;
     for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < V; s += (int64_t)gridDim.x * blockDim.x) {
         int64_t t = s / N, x = s - t * N;
         int64_t f0 = ((t + 1 == N) ? 0 : t + 1) * N + x;
@@ -567,23 +577,35 @@ __global__ void villain_observables_kernel(int32_t N, double half_kappa, const d
         double p = phi[s];
         double l0 = (0.0 + (phi[f0] - p)) - TWO_PI * (double)n[s];
         double l1 = (0.0 + (phi[f1] - p)) - TWO_PI * (double)n[V + s];
-        s_act += l0 * l0 + l1 * l1;
+        const double a = l0 * l0 + l1 * l1;
+        if (a < ACT_LIMIT) q += act_fx(a);
+        else big += a;
         // (dn)_01[x] = (n1[x+e0] - n1[x]) - (n0[x+e1] - n0[x])   (d on 1-forms, rows (0,1,0,+1),(0,0,1,-1))
         int64_t dn = (n[V + f0] - n[V + s]) - (n[f1] - n[s]);
-        s_w2 += (double)(dn * dn);
-        s_n0 += (double)n[s];
-        s_n1 += (double)n[V + s];
+        w2 += (unsigned long long)(dn * dn);
+        s_n0 += n[s];
+        s_n1 += n[V + s];
     }
-    s_act = wave_sum(s_act);
-    s_w2 = wave_sum(s_w2);
-    s_n0 = wave_sum(s_n0);
-    s_n1 = wave_sum(s_n1);
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&out[0], half_kappa * s_act);
-        atomicAdd(&out[1], s_w2);
-        atomicAdd(&out[2], s_n0);
-        atomicAdd(&out[3], s_n1);
-    }
+    unsigned long long w[5] = {q & 0xffffffffull, q >> 32, w2, (unsigned long long)s_n0, (unsigned long long)s_n1};
+    for (int o = 32; o > 0; o >>= 1)
+        for (int i = 0; i < 5; i++) w[i] += __shfl_xor(w[i], o);
+    if ((threadIdx.x & 63) == 0)
+        for (int i = 0; i < 5; i++)
+            if (w[i]) atomicAdd(&out[i], w[i]);
+    if (big != 0.0) unsafeAtomicAdd((double *)&out[5], big);
+}
+
+
+// the exact acceptance limbs of each slot (its proposed, rejections and acceptance_sum words on the device, common.h)
+// into its acceptance_sum; a finalized slot is marked (rejections = -1) and left alone by a second finalize
+__global__ void stats_finalize(sv_stats *s, int64_t n) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (s[i].rejections == -1) return;  // (finalized already: limb 1 never reaches 2^63)
+    const uint64_t w0 = stat_limb(s[i], 0), w1 = stat_limb(s[i], 1), w2 = stat_limb(s[i], 2);
+    s[i].acceptance_sum = fx_value(w0, w1, w2);
+    s[i].proposed = 0;
+    s[i].rejections = -1;  // (every landing overwrites it on the host)
 }
 
 }  // namespace sv
@@ -703,6 +725,11 @@ AbortInfo read_abort(sv_ctx *ctx) {
 // the batch -- after an abort, `landed` points at them (the sweeps before the failing one are kept from there), and
 // only a batch with more than TAIL_REPORTS reports needs a second copy
 static constexpr size_t TAIL_HEAD = 16 + TAIL_REPORTS * sizeof(Report);  // 256 B
+void finalize_stats(sv_stats *d, int64_t n, hipStream_t stream) {
+    if (n <= 0) return;
+    stats_finalize<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(d, n), SV_LAUNCHED("stats_finalize", stream);
+}
+
 AbortInfo read_abort_stats(sv_ctx *ctx, int count, sv_stats *stats, const sv_stats **landed = nullptr) {
     const size_t bytes = TAIL_HEAD + (size_t)count * sizeof(sv_stats);
     if (bytes > ctx->tail_cap) {
@@ -716,6 +743,7 @@ AbortInfo read_abort_stats(sv_ctx *ctx, int count, sv_stats *stats, const sv_sta
     const Report *h_rep = (const Report *)(ctx->h_tail + 16);
     sv_stats *h_st = (sv_stats *)(ctx->h_tail + TAIL_HEAD);
     SV_HIP(hipMemcpyAsync(ctx->h_tail, ctx->d_abort, TAIL_HEAD, hipMemcpyDeviceToHost, ctx->stream));  // + d_nreport, reports
+    finalize_stats(ctx->d_stats, count, ctx->stream);
     SV_HIP(hipMemcpyAsync(h_st, ctx->d_stats, count * sizeof(sv_stats), hipMemcpyDeviceToHost, ctx->stream));
     SV_HIP(hipStreamSynchronize(ctx->stream));
     AbortInfo a;
@@ -846,6 +874,7 @@ void run_generic(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, 
             SV_HIP(hipMemcpyAsync(phi, st->snap_phi, V * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
             SV_HIP(hipMemcpyAsync(n, st->snap_n, 2 * V * sizeof(int64_t), hipMemcpyDeviceToDevice, ctx->stream));
         }
+        finalize_stats(ctx->d_stats, 1, ctx->stream);
         SV_HIP(hipMemcpyAsync(&stats[sw], ctx->d_stats, sizeof(sv_stats), hipMemcpyDeviceToHost, ctx->stream));
         SV_HIP(hipStreamSynchronize(ctx->stream));
         stats[sw].proposed = V;
@@ -1696,19 +1725,25 @@ int sv_villain_observables(sv_villain *st, double kappa, double *out) {
         // persistent device sums + pinned host image: a stream-ordered DMA, then a host copy after the sync
         // (a pooled hipMallocAsync buffer read back into pageable memory once returned zeros)
         if (!st->d_obs) {
-            SV_HIP(hipMalloc((void **)&st->d_obs, 4 * sizeof(double)));
-            SV_HIP(hipHostMalloc((void **)&st->h_obs, 4 * sizeof(double), hipHostMallocDefault));
+            SV_HIP(hipMalloc((void **)&st->d_obs, OBS_WORDS * sizeof(unsigned long long)));
+            SV_HIP(hipHostMalloc((void **)&st->h_obs, OBS_WORDS * sizeof(unsigned long long), hipHostMallocDefault));
         }
-        double *d = st->d_obs;
-        SV_HIP(hipMemsetAsync(d, 0, 4 * sizeof(double), ctx->stream));
+        unsigned long long *d = st->d_obs;
+        SV_HIP(hipMemsetAsync(d, 0, OBS_WORDS * sizeof(unsigned long long), ctx->stream));
         const int64_t V = (int64_t)st->N * st->N;
-        const int grid = (int)std::min<int64_t>((V + 255) / 256, 2048);
-        villain_observables_kernel<<<grid, 256, 0, ctx->stream>>>(st->N, kappa / 2.0, st->phi[st->cur], st->n[st->cur],
-                                                                   d), SV_LAUNCHED("villain_observables_kernel", ctx->stream);
+        // <= 256 sites per thread (the exact action values of a thread stay below 2^60)
+        const int grid = (int)std::max<int64_t>(std::min<int64_t>((V + 255) / 256, 2048), (V + 65535) / 65536);
+        villain_observables_kernel<<<grid, 256, 0, ctx->stream>>>(st->N, st->phi[st->cur], st->n[st->cur], d),
+            SV_LAUNCHED("villain_observables_kernel", ctx->stream);
         SV_HIP(hipGetLastError());
-        SV_HIP(hipMemcpyAsync(st->h_obs, d, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipMemcpyAsync(st->h_obs, d, OBS_WORDS * sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
         SV_HIP(hipStreamSynchronize(ctx->stream));
-        memcpy(out, st->h_obs, 4 * sizeof(double));
+        double raw[4];
+        obs_raw(st->h_obs, raw);
+        out[0] = kappa / 2.0 * raw[0];  // S = kappa / 2 sum (d phi - 2 pi n)^2 (villain.py:51-66)
+        out[1] = raw[1];
+        out[2] = raw[2];
+        out[3] = raw[3];
         return 0;
     } catch (const std::exception &e) {
         st->ctx->err = e.what();

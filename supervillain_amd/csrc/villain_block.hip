@@ -83,14 +83,11 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
     int32_t *s_n0 = reinterpret_cast<int32_t *>(s_r1 + F * F);
     int32_t *s_n1 = s_n0 + F * F;
     unsigned long long *s_acc = reinterpret_cast<unsigned long long *>(s_n1 + F * F);
-    double *s_ps = reinterpret_cast<double *>(s_acc + 16);
-    int32_t *s_bad = reinterpret_cast<int32_t *>(s_ps + 16);
+    // per sweep j: s_acc[4 j + i], i = 0 accepted, 1..3 the exact acceptance limbs (common.h)
+    int32_t *s_bad = reinterpret_cast<int32_t *>(s_acc + 64);
 
     int32_t *s_desc = s_bad + 4;  // [j][c][q]: choice block q of colour c in sweep j, {has, buf}
-    if (threadIdx.x < 16) {
-        s_acc[threadIdx.x] = 0;
-        s_ps[threadIdx.x] = 0.0;
-    }
+    if (threadIdx.x < 64) s_acc[threadIdx.x] = 0;
     if (threadIdx.x == 0) *s_bad = 0;
 
     // The prologue's loads are issued in the order they are consumed (the small-offset maps, the descriptors, the
@@ -185,7 +182,7 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
             }
         if (j == 0) BLK_T(2);
         int32_t acc_count = 0;
-        double psum = 0.0;
+        AccFx psum;  // exact acceptance sum (common.h)
 
         // colour c on rows qlo..qhi and columns xlo..xhi (inclusive): villain_sweep_hot's ranges around the decided
         // region [ra, rb) x [ca, cb) -- colour 0 one row / column further on every side, colour 1 one further below
@@ -258,7 +255,7 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
                 const bool acc = D.u < p;
                 if (own) {
                     acc_count += acc;
-                    psum += p;
+                    fx_add(psum, p);
                 }
                 if (acc) {
                     // neighborhood.py:124-129: phi += change_phi, n += change_n, r += d(change_phi) - 2 pi change_n
@@ -294,7 +291,7 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
                 const bool acc = D.u < p;
                 if (own) {
                     acc_count += acc;
-                    psum += p;
+                    fx_add(psum, p);
                 }
                 if (acc) {
                     s_phi[s0] = s_phi[s0] + D.dphi;
@@ -350,13 +347,14 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
 
         // the sweep's statistics (per wave into the workgroup's slot j; added to the sweep's sv_stats at the end)
         {
-            unsigned long long a = (unsigned long long)acc_count;
-            for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
-            const double ps = wave_sum(psum);
-            if ((threadIdx.x & 63) == 0 && (a || ps != 0.0)) {
-                atomicAdd(&s_acc[j], a);
-                atomicAdd(&s_ps[j], ps);
-            }
+            unsigned long long w[4];
+            w[0] = (unsigned long long)acc_count;
+            fx_limbs(psum, w[1], w[2], w[3]);
+            for (int o = 32; o > 0; o >>= 1)
+                for (int i = 0; i < 4; i++) w[i] += __shfl_xor(w[i], o);
+            if ((threadIdx.x & 63) == 0)
+                for (int i = 0; i < 4; i++)
+                    if (w[i]) atomicAdd(&s_acc[4 * j + i], w[i]);
         }
         // the own block into the sweep's output buffer
         {
@@ -385,10 +383,8 @@ __global__ __launch_bounds__(NWT * 64) void villain_sweep_block(FArgs A, BlockAr
     }
     __syncthreads();
     if (*s_bad && threadIdx.x == 0) report(A.S, A.sweep, OVERFLOW_BLOCK, 0);
-    if ((int)threadIdx.x < K && (s_acc[threadIdx.x] || s_ps[threadIdx.x] != 0.0)) {
-        atomicAdd((unsigned long long *)&A.stat[threadIdx.x].accepted, s_acc[threadIdx.x]);
-        unsafeAtomicAdd(&A.stat[threadIdx.x].acceptance_sum, s_ps[threadIdx.x]);
-    }
+    if ((int)threadIdx.x < 4 * K && s_acc[threadIdx.x])
+        atomicAdd(stat_word(&A.stat[threadIdx.x >> 2], threadIdx.x & 3), s_acc[threadIdx.x]);
     BLK_T(15);
 }
 template __global__ void villain_sweep_block<8>(FArgs, BlockArgs);

@@ -123,7 +123,7 @@ struct HotEmpty {};
 // same sums held in registers spilled (r353); full-row strips never need the second set of row bases, which makes
 // the room.  n0 and n1 sums share one 64-bit word (n0 + 2^32 n1, two's complement).
 struct ObsLane {
-    double act[256];
+    unsigned long long act[256];  // exact action values round(t 2^40) (common.h)
     unsigned long long w2[256];
     unsigned long long npk[256];
 };
@@ -148,12 +148,12 @@ struct HotLDST {
     // SKIP: per colour and choice block, its known rejected stream positions (not in the replica-observables layout,
     // which needs every byte for its fourth workgroup per CU)
     std::conditional_t<OBSL, HotEmpty, uint32_t[2][4][HOT_MAXSK]> sk;
-    double obs[4];     // OBS: the workgroup's sums of the inline observables
+    unsigned long long obsw[5];  // OBS: the workgroup's exact observable words (common.h OBS_WORDS, but the big term)
+    double obig;                 // OBS: the workgroup's action terms t >= ACT_LIMIT (common.h)
     std::conditional_t<OBSL, ObsLane, HotEmpty> ol;
     // band launches (8-wave workgroups): the workgroup's statistics per sweep of the launch, flushed once at its end
     struct BandStats {
-        unsigned long long acc[16];
-        double ps[16];
+        unsigned long long w[16][4];  // per sweep: accepted, the exact acceptance limbs (common.h)
     };
     std::conditional_t<NWL == 8, BandStats, HotEmpty> bst;
 };
@@ -315,9 +315,10 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     }
     if (threadIdx.x == 0) s_bad = 0;
     if (POLL && threadIdx.x == 0) Ls.stop = 0;
-    if (OBS && threadIdx.x < 4) Ls.obs[threadIdx.x] = 0.0;
+    if (OBS && threadIdx.x < 5) Ls.obsw[threadIdx.x] = 0;
+    if (OBS && threadIdx.x == 5) Ls.obig = 0.0;
     if constexpr (FR && OBS) {  // this lane's running sums (only this lane touches its slots)
-        Ls.ol.act[threadIdx.x] = 0.0;
+        Ls.ol.act[threadIdx.x] = 0;
         Ls.ol.w2[threadIdx.x] = 0;
         Ls.ol.npk[threadIdx.x] = 0;
     }
@@ -505,12 +506,12 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     }
 
     int64_t acc_count = 0;
-    double psum = 0.0;
+    AccFx psum;  // exact acceptance sum (common.h)
 
     auto store_rows = [&](int32_t ra) {
         if (SV_ABLATE & 8) return;
         const int32_t q = ra + wave;
-        double o_act = 0.0;  // OBS partials of this row step
+        unsigned long long o_act = 0;  // OBS partials of this row step (exact action values, common.h)
         int64_t o_w2 = 0;
         int32_t o_n0 = 0, o_n1 = 0;
         if (q >= t0 && q < t1) {
@@ -559,7 +560,9 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
                         const double ph = s_phi[slot][cx];
                         const double l0 = (0.0 + (s_phi[slot1][cx] - ph)) - TWO_PI * (double)s_n0[slot][cx];
                         const double l1 = (0.0 + (s_phi[slot][cxp(cx)] - ph)) - TWO_PI * (double)s_n1[slot][cx];
-                        o_act += l0 * l0 + l1 * l1;
+                        const double t = l0 * l0 + l1 * l1;
+                        if (__builtin_expect(t < ACT_LIMIT, 1)) o_act += act_fx(t);
+                        else atomicAdd(&Ls.obig, t);
                         // |n| <= 2^15 on the int16 image, so |dn| < 2^17 fits int32 and dn^2 needs 64 bits
                         const int32_t dn = ((int32_t)s_n1[slot1][cx] - s_n1[slot][cx]) - ((int32_t)s_n0[slot][cxp(cx)] - s_n0[slot][cx]);
                         o_w2 += (int64_t)dn * dn;
@@ -705,7 +708,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
                 const bool acc = D.u < p;
                 if (q >= q_lo && q < q_hi && (FR || (x >= c_lo && x < c_hi))) {
                     acc_count += acc;
-                    psum += p;
+                    fx_add(psum, p);
                 }
                 double wr[4] = {r0[0], r0[1], r0[2], r0[3]};
                 if (__builtin_amdgcn_ballot_w64(acc)) {
@@ -764,7 +767,7 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
                 const bool acc = D.u < p;
                 if (q >= q_lo && q < q_hi && (FR || (x >= c_lo && x < c_hi))) {
                     acc_count += acc;
-                    psum += p;
+                    fx_add(psum, p);
                 }
                 if (__builtin_amdgcn_ballot_w64(acc)) {
                     if (acc) {
@@ -837,15 +840,15 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
     if (s_bad && threadIdx.x == 0) report(A.S, sweep_id, OVERFLOW_BLOCK, 0, (uint32_t)rep);
     if constexpr (BAND) {
         // into the workgroup's per-sweep slots (LDS); band_sweeps adds them to the sweeps' statistics at the end
-        unsigned long long a = (unsigned long long)acc_count;
-        for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
-        const double ps = wave_sum(psum);
-        if (lane == 0) {
-            atomicAdd(&Ls.bst.acc[hb->j], a);
-            atomicAdd(&Ls.bst.ps[hb->j], ps);
-        }
+        unsigned long long w[4];
+        w[0] = (unsigned long long)acc_count;
+        fx_limbs(psum, w[1], w[2], w[3]);
+        for (int o = 32; o > 0; o >>= 1)
+            for (int i = 0; i < 4; i++) w[i] += __shfl_xor(w[i], o);
+        if (lane == 0)
+            for (int i = 0; i < 4; i++) atomicAdd(&Ls.bst.w[hb->j][i], w[i]);
     } else {
-        flush_stats(FR ? A.stat + (int64_t)rep * A.rep_stat : A.stat, acc_count, psum);
+        flush_stats<NWT>(FR ? A.stat + (int64_t)rep * A.rep_stat : A.stat, acc_count, psum);
     }
 #if SV_WGTIME
     __builtin_amdgcn_s_waitcnt(0);
@@ -875,16 +878,21 @@ __device__ __forceinline__ void hot_body(const FArgs &A, HotLDST<PH, FR && OBS, 
         const uint64_t pk = Ls.ol.npk[threadIdx.x];
         const int32_t a_n0 = (int32_t)(uint32_t)pk;
         const int64_t a_n1 = (int64_t)(pk - (uint64_t)(int64_t)a_n0) >> 32;
-        const double w_act = wave_sum(Ls.ol.act[threadIdx.x]), w_w2 = wave_sum((double)Ls.ol.w2[threadIdx.x]);
-        const double w_n0 = wave_sum((double)a_n0), w_n1 = wave_sum((double)a_n1);
-        if (lane == 0) {
-            atomicAdd(&Ls.obs[0], w_act);
-            atomicAdd(&Ls.obs[1], w_w2);
-            atomicAdd(&Ls.obs[2], w_n0);
-            atomicAdd(&Ls.obs[3], w_n1);
-        }
+        const uint64_t q = Ls.ol.act[threadIdx.x];  // < 2^60: 2 sites x 128 rows of round(t 2^40) < 2^52
+        // integer sums over the workgroup: the same words in any order (common.h)
+        unsigned long long w[5] = {q & 0xffffffffull, q >> 32, Ls.ol.w2[threadIdx.x], (uint64_t)(int64_t)a_n0,
+                                   (uint64_t)a_n1};
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+            for (int i = 0; i < 5; i++) w[i] += __shfl_xor(w[i], o);
+        if (lane == 0)
+#pragma unroll
+            for (int i = 0; i < 5; i++) atomicAdd(&Ls.obsw[i], w[i]);
         __syncthreads();
-        if (threadIdx.x < 4) unsafeAtomicAdd(&A.obs[(int64_t)rep * A.rep_obs + threadIdx.x], Ls.obs[threadIdx.x]);
+        unsigned long long *ow = A.obs + (int64_t)rep * A.rep_obs;
+        if (threadIdx.x < 5 && Ls.obsw[threadIdx.x]) atomicAdd(&ow[threadIdx.x], Ls.obsw[threadIdx.x]);
+        if (threadIdx.x == 5 && Ls.obig != 0.0) unsafeAtomicAdd((double *)&ow[5], Ls.obig);
     }
 }
 
@@ -1003,8 +1011,7 @@ __device__ __forceinline__ void band_sweeps(const FArgs &A, const BandArgs &B, H
         t1 = r < nr ? R0 + (r + 1) * H / nr : 0;
     };
     if (threadIdx.x < 16) {
-        Ls.bst.acc[threadIdx.x] = 0;
-        Ls.bst.ps[threadIdx.x] = 0.0;
+        for (int i = 0; i < 4; i++) Ls.bst.w[threadIdx.x][i] = 0;
     }
     for (int j = 0; j < B.K; j++) {
         int32_t t0, t1, n0 = 0, n1 = 0;
@@ -1024,13 +1031,10 @@ __device__ __forceinline__ void band_sweeps(const FArgs &A, const BandArgs &B, H
         if (threadIdx.x == 0 && (band * B.P + i) < 8 * 128) g_bandtime[BT * (size_t)((band * B.P + i) * BT_SW + j) + 5] = rt_now();
 #endif
     }
-    // the launch's statistics: one lane per sweep (each sweep's sum over workgroups is order-free for the count;
-    // the acceptance sums add in any order, as flush_stats' atomics do)
+    // the launch's statistics: one lane per sweep (integer sums: order-free, the acceptance words too)
     __syncthreads();
-    if (threadIdx.x < B.K && (Ls.bst.acc[threadIdx.x] || Ls.bst.ps[threadIdx.x] != 0.0)) {
-        atomicAdd((unsigned long long *)&A.stat[threadIdx.x].accepted, Ls.bst.acc[threadIdx.x]);
-        unsafeAtomicAdd(&A.stat[threadIdx.x].acceptance_sum, Ls.bst.ps[threadIdx.x]);
-    }
+    if (threadIdx.x < 4 * B.K && Ls.bst.w[threadIdx.x >> 2][threadIdx.x & 3])
+        atomicAdd(stat_word(&A.stat[threadIdx.x >> 2], threadIdx.x & 3), Ls.bst.w[threadIdx.x >> 2][threadIdx.x & 3]);
 }
 
 template <int NWT>

@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void site_pass(LParams P, double *phi, const i
     const Block BM = blocks[0], BD = blocks[1 + color];
     UniLane um{u128{0, 0}, false}, ud{u128{0, 0}, false};
     int64_t acc_count = 0;
-    double psum = 0.0;
+    AccFx psum;  // exact acceptance sum (common.h)
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nc; e += S) {
         const int64_t s = EVEN ? even_site(e, N, color) : sites[e];
         if (!EVEN) um.init = ud.init = false;
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) void site_pass(LParams P, double *phi, const i
         const double p = clip01(exp(-dS));
         const int acc = u < p;
         acc_count += acc;
-        psum += p;
+        fx_add(psum, p);
         const double cphi = dph * (double)acc;
         phi[s] = phi[s] + cphi;
         const double dcf = 0.0 + (0.0 - cphi), dcb = 0.0 + (cphi - 0.0);
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void site_pp(LParams P, const double *phi_in, 
     const Block BM = blocks[0], BD = blocks[1 + PASS];
     UniLane um{u128{0, 0}, false}, ud{u128{0, 0}, false};
     int64_t acc_count = 0;
-    double psum = 0.0;
+    AccFx psum;  // exact acceptance sum (common.h)
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nc; e += S) {
         const int64_t s = even_site(e, N, PASS);
         const double u = 0.0 + 1.0 * to_double(um.next(T, BM, (uint32_t)s, adv_m));
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256) void site_pp(LParams P, const double *phi_in, 
         const double p = clip01(exp(-dS));
         const int acc = u < p;
         acc_count += acc;
-        psum += p;
+        fx_add(psum, p);
         const double cphi = dph * (double)acc;
         if (PASS == 0) {
             phi_out[s] = (ps + cphi) + 0.0;
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void exact_pass(LParams P, int64_t *n, const d
     UniLane um{u128{0, 0}, false};
     BndLane uz{u128{0, 0}, false};
     int64_t acc_count = 0;
-    double psum = 0.0;
+    AccFx psum;  // exact acceptance sum (common.h)
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nc; e += S) {
         const int64_t s = EVEN ? even_site(e, N, color) : sites[e];
         if (!EVEN) um.init = uz.init = false;
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(256) void exact_pass(LParams P, int64_t *n, const d
         const double p = clip01(exp(-dS));
         const int acc = u < p;
         acc_count += acc;
-        psum += p;
+        fx_add(psum, p);
         if (acc) {
 #pragma unroll
             for (int q4 = 0; q4 < 4; q4++) n[L[q4]] = nv[q4] + ((q4 & 1) ? cn_b : cn_f);
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(256) void link_sweep(LParams P, const double *phi, 
     UniLane uu{u128{0, 0}, false};
     BndLane uc{u128{0, 0}, false};
     int64_t acc_count = 0;
-    double psum = 0.0;
+    AccFx psum;  // exact acceptance sum (common.h)
     for (int64_t l = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; l < 2 * V; l += S) {
         uint32_t q = (uint32_t)l, w;
         if (slow) w = bnd_word_slow(T, BC, skips, (uint32_t)l, &q);
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(256) void link_sweep(LParams P, const double *phi, 
         const double u = 0.0 + 1.0 * to_double(uu.next(T, BU, (uint32_t)l, adv_u));
         const int acc = u < p;
         acc_count += acc;
-        psum += p;
+        fx_add(psum, p);
         if (acc) n[l] = nl + cn;
     }
     lflush(stat, acc_count, psum);

@@ -64,14 +64,14 @@ __device__ __forceinline__ uint32_t wbounded(const JumpTables *T, const Block &b
 __global__ void fold_stripes(const StatStripe *ss, sv_stats *out, int count) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= count) return;
-    unsigned long long a = 0;
-    double p = 0.0;
+    unsigned long long a = 0, w[3] = {0, 0, 0};
     for (int j = 0; j < NSTRIPE; j++) {
         a += ss[k * NSTRIPE + j].acc;
-        p += ss[k * NSTRIPE + j].psum;
+        for (int i = 0; i < 3; i++) w[i] += ss[k * NSTRIPE + j].pw[i];
     }
-    out[k].accepted = (int64_t)a;
-    out[k].acceptance_sum = p;
+    // the exact acceptance limbs (common.h) in the slot's words, finalized before the slot lands
+    *stat_word(&out[k], 0) = a;
+    for (int i = 0; i < 3; i++) *stat_word(&out[k], 1 + i) = w[i];
 }
 
 // delta(v)/W on link (mu, s) of a D=2 two-form v, exactly as reference_delta + coexact.py:80:
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void coexact_pass(WParams P, int64_t *m, const
     const int64_t N = P.N, V = N * N;
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     int64_t acc_count = 0;
-    double psum = 0.0;
+    AccFx psum;  // exact acceptance sum (common.h)
     if (i < nc) {
         const int64_t x = sites[i];
         int64_t tt, xx;
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void coexact_pass(WParams P, int64_t *m, const
         p = p > 1.0 ? 1.0 : p;
         const int acc = u < p;
         acc_count = acc;
-        psum = p;
+        fx_add(psum, p);
         if (acc) {  // delta_sparse(..., t*accepted, out=m): m0[x]+=t, m0[x+e1]-=t, m1[x]-=t, m1[x+e0]+=t
             m[x] += t;
             m[xe1] -= t;
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(256) void plaquette_cb_pass(WParams P, int64_t *m, 
     const int64_t N = P.N, V = N * N;
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     int64_t acc_count = 0;
-    double psum = 0.0;
+    AccFx psum;  // exact acceptance sum (common.h)
     if (i < nc) {
         const int64_t x = sites[i];
         int64_t tt, xx;
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(256) void plaquette_cb_pass(WParams P, int64_t *m, 
         p = p > 1.0 ? 1.0 : p;
         const int acc = u < p;
         acc_count = acc;
-        psum = p;
+        fx_add(psum, p);
         if (acc) {
             m[x] += cm;
             m[V + xm] += cm;
@@ -242,7 +242,7 @@ __global__ __launch_bounds__(256) void coexact_gs(WParams P, int64_t *m, const v
     loc::UniLane um{u128{0, 0}, false};
     loc::BndLane bt{u128{0, 0}, false};
     int64_t acc_count = 0;
-    double psum = 0.0;
+    AccFx psum;  // exact acceptance sum (common.h)
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nc; e += G) {
         const int64_t x = loc::even_site(e, N, color);
         int64_t tt, xx;
@@ -273,7 +273,7 @@ __global__ __launch_bounds__(256) void coexact_gs(WParams P, int64_t *m, const v
         const double p = loc::clip01(exp(-dS));
         const int acc = u < p;
         acc_count += acc;
-        psum += p;
+        fx_add(psum, p);
         if (acc) {
             m[x] += t;
             m[xe1] -= t;
@@ -298,7 +298,7 @@ __global__ __launch_bounds__(256) void plaquette_cb_gs(WParams P, int64_t *m, vo
     loc::UniLane um{u128{0, 0}, false};
     loc::BndLane bm{u128{0, 0}, false}, bv{u128{0, 0}, false};
     int64_t acc_count = 0;
-    double psum = 0.0;
+    AccFx psum;  // exact acceptance sum (common.h)
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nc; e += G) {
         const int64_t x = loc::even_site(e, N, color);
         int64_t tt, xx;
@@ -328,7 +328,7 @@ __global__ __launch_bounds__(256) void plaquette_cb_gs(WParams P, int64_t *m, vo
         const double p = loc::clip01(exp(-dS));
         const int acc = u < p;
         acc_count += acc;
-        psum += p;
+        fx_add(psum, p);
         if (acc) {
             m[x] += cm;
             m[V + xm] += cm;
@@ -365,7 +365,7 @@ __global__ __launch_bounds__(256) void plaquette_level(WParams P, int64_t *m, vo
     const int64_t N = P.N, V = N * N;
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     int64_t acc_count = 0;
-    double psum = 0.0;
+    AccFx psum;  // exact acceptance sum (common.h)
     if (i < count) {
         const int64_t x = list[i];
         int64_t tt, xx;
@@ -383,7 +383,7 @@ __global__ __launch_bounds__(256) void plaquette_level(WParams P, int64_t *m, vo
         double p = exp(-dS);
         p = p < 0.0 ? 0.0 : p;
         p = p > 1.0 ? 1.0 : p;
-        psum = p;
+        fx_add(psum, p);
         if (met < p) {
             m[x] += cm;
             m[V + xm] += cm;
@@ -667,6 +667,7 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
             }
             // the batch's statistics travel with the abort check (one synchronization per batch, not two); an
             // aborted batch's copy is simply overwritten by its replay's
+            svh::finalize_stats(ctx->d_stats, (int64_t)count * nstat, ctx->stream);
             SV_HIP(hipMemcpyAsync(stats + (size_t)sw * nstat, ctx->d_stats, (size_t)count * nstat * sizeof(sv_stats),
                                   hipMemcpyDeviceToHost, ctx->stream));
             if (!wcheck(ctx, reps)) {
@@ -687,6 +688,7 @@ void run_colour_sweeps(sv_worldline *st, const std::vector<BlockSpec> &specs, in
         const bool deferred = !may_reject && ctx->defer_stats(stats + (size_t)sw * nstat, (int64_t)count * nstat);
         if (!may_reject && !deferred) svh::loc::queue_abort_copy(ctx);
         if (!deferred && !stats_landed) {
+            svh::finalize_stats(ctx->d_stats, (int64_t)count * nstat, ctx->stream);
             SV_HIP(hipMemcpyAsync(stats + (size_t)sw * nstat, ctx->d_stats, (size_t)count * nstat * sizeof(sv_stats),
                                   hipMemcpyDeviceToHost, ctx->stream));
             SV_HIP(hipStreamSynchronize(ctx->stream));
@@ -1094,6 +1096,7 @@ void ordered_sweep(sv_worldline *st, double kappa, double W_eff, bool o32, u128 
             wabsorb(reps, 0, skips);
             snapshot(st, true);
         }
+        svh::finalize_stats(ctx->d_stats, 1, ctx->stream);
         SV_HIP(hipMemcpyAsync(stats, ctx->d_stats, sizeof(sv_stats), hipMemcpyDeviceToHost, ctx->stream));
         SV_HIP(hipStreamSynchronize(ctx->stream));
         stats->proposed = V;

@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256) void vortex_pass(VxParams P, const int64_t *m,
     UniLane um{u128{0, 0}, false}, up{u128{0, 0}, false};
     BndLane bp{u128{0, 0}, false};
     int64_t acc_count = 0;
-    double psum = 0.0;
+    AccFx psum;  // exact acceptance sum (common.h)
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nc; e += S) {
         const int64_t s = EVEN ? wl_site(e, N, color) : sites[e];
         if (!EVEN) um.init = up.init = bp.init = false;
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256) void vortex_pass(VxParams P, const int64_t *m,
         const double p = clip01(exp(-dS));
         const int acc = u < p;
         acc_count += acc;
-        psum += p;
+        fx_add(psum, p);
         if (VF) {
             const double ap = a * (double)acc;
             double *vf = (double *)vv;
@@ -298,14 +298,14 @@ __global__ __launch_bounds__(256) void wrap_metropolis(WrParams P, const Block *
     if (*(volatile const int32_t *)abort) return;
     const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     int64_t acc_count = 0;
-    double psum = 0.0;
+    AccFx psum;  // exact acceptance sum (common.h)
     if (j < 2 * (int64_t)P.N) {
         const double p = clip01(exp(-dS[j]));
         const double u = 0.0 + 1.0 * to_double(xsl_rr(jump(T, lbase(blocks[1]), (uint32_t)j)));
         const int acc = u < p;
         accf[j] = acc;
         acc_count = acc;
-        psum = p;
+        fx_add(psum, p);
     }
     lflush(stat, acc_count, psum);
 }

@@ -255,6 +255,14 @@ def single_lattice(N, kappa, W, phi0, n0, sweeps, gen):
     return np.asarray(cfg['phi'])[0], np.asarray(cfg['n']), G
 
 
+def exact_acceptance(st, V):
+    """NeighborhoodUpdate.acceptance folded from these statistics the way the generator folds them"""
+    acc = 0.
+    for s in st:
+        acc += s.acceptance_sum / V
+    return acc
+
+
 @pytest.mark.parametrize('tiles', [(2, 4), (1, 8)])
 def test_equals_single_lattice_at_scale(tiles):
     """L=1024 (interior strips take the fast draw path): decomposed == single-lattice fused kernel."""
@@ -266,6 +274,7 @@ def test_equals_single_lattice_at_scale(tiles):
     assert (phi == p).all() and (n == m).all()
     assert gen.bit_generator.state == G.rng.bit_generator.state
     assert sum(s.accepted for s in st) == G.accepted
+    assert exact_acceptance(st, N * N) == G.acceptance  # (exact sums: the tile grid cannot enter them)
 
 
 @pytest.mark.parametrize('batch', ['', '5', 'predict'])
@@ -285,6 +294,7 @@ def test_natural_rejections_bench_size(batch, monkeypatch):
     assert (phi == p).all() and (n == m).all()
     assert gen.bit_generator.state == G.rng.bit_generator.state
     assert sum(s.accepted for s in st) == G.accepted
+    assert exact_acceptance(st, N * N) == G.acceptance  # (exact sums: the tile grid cannot enter them)
 
 
 @pytest.mark.parametrize('tiles', [(1, 2), (2, 1)])
@@ -301,6 +311,7 @@ def test_two_rank_layouts_at_scale(tiles):
     assert (phi == p).all() and (n == m).all()
     assert gen.bit_generator.state == G.rng.bit_generator.state
     assert sum(s.accepted for s in st) == G.accepted
+    assert exact_acceptance(st, N * N) == G.acceptance  # (exact sums: the tile grid cannot enter them)
 
 
 @pytest.mark.parametrize('predict', ['0', '1'])

@@ -58,3 +58,71 @@ def test_replica_inline_vs_reference(group):
         for s in range(sweeps):
             _check({k: obs[k][r, s] for k in obs}, c, s, f'{group} replica {r}')
         assert (state_of(gens[r]) == c['rng1']).all()
+
+
+def _replica_run(R, N, kappa, W, sweeps, phi0, n0, seeds, streams=1):
+    B = VillainReplicas(R, N, kappa, W, streams=streams)
+    try:
+        B.upload(phi0, n0)
+        gens = [s if isinstance(s, np.random.Generator) else np.random.default_rng(s) for s in seeds]
+        stats, obs = B.run(sweeps, gens, inline=True)
+        phi, n = B.download()
+    finally:
+        B.close()
+    return phi, n, stats, obs, [g.bit_generator.state for g in gens]
+
+
+def test_golden_chains_inside_a_config5_batch():
+    """the n128w2 reference chains embedded in a 1024-replica batch (config 5's shape: 64-row strips,
+    the batch's other replicas hot-started from their own seeds) give the reference's observables at 1e-12, and the
+    same values bit for bit as the small batch of test_replica_inline_vs_reference (32-row strips): the sums are exact
+    (supervillain_amd/csrc/common.h), so the launch geometry cannot enter them."""
+    chains = observable_groups()['n128w2']
+    R, N, kappa, W, sweeps = 1024, 128, chains[0]['kappa'], chains[0]['W'], chains[0]['sweeps']
+    r = np.random.default_rng(77)
+    phi0 = r.uniform(-np.pi, np.pi, (R, N, N))
+    n0 = (W * r.integers(-2, 3, (R, 2, N, N))).astype(np.int64)
+    seeds = [1000 + i for i in range(R)]
+    for i, c in enumerate(chains):
+        phi0[i], n0[i] = observable_start(c)
+        seeds[i] = generator_from(c['rng0'])
+    _, _, st_big, obs_big, states = _replica_run(R, N, kappa, W, sweeps, phi0, n0, seeds)
+    k = len(chains)
+    _, _, st_small, obs_small, _ = _replica_run(k, N, kappa, W, sweeps, phi0[:k].copy(), n0[:k].copy(),
+                                                [generator_from(c['rng0']) for c in chains])
+    for i, c in enumerate(chains):
+        for s in range(sweeps):
+            _check({q: obs_big[q][i, s] for q in obs_big}, c, s, f'n128w2 replica {i} of 1024')
+        assert (state_of(seeds[i]) == c['rng1']).all()
+    for q in obs_big:
+        assert (np.asarray(obs_big[q][:k]) == np.asarray(obs_small[q])).all(), q
+    for q in ('accepted', 'acceptance', 'rejections'):
+        assert (np.asarray(st_big[q][:k]) == np.asarray(st_small[q])).all(), q
+
+
+@pytest.mark.parametrize('R', [37, 1024])
+def test_one_batch_equals_two_half_batches(R):
+    """VERDICT r5 next #2, done-when: a replica batch and the same replicas run as two half-batches (another replica
+    count, so other strip heights and launch widths) give the same fields, statistics and inline observables bit for
+    bit -- what lets config 5 run as half-batches on two streams."""
+    N, kappa, W, sweeps = 128, 0.5, 2, 6
+    r = np.random.default_rng(R)
+    phi0 = r.uniform(-np.pi, np.pi, (R, N, N))
+    n0 = (W * r.integers(-2, 3, (R, 2, N, N))).astype(np.int64)
+    seeds = [5000 + i for i in range(R)]
+    whole = _replica_run(R, N, kappa, W, sweeps, phi0, n0, seeds)
+    two = _replica_run(R, N, kappa, W, sweeps, phi0, n0, seeds, streams=2)  # (VillainReplicas' two-stream form)
+    for x, y in zip(whole[:2] + whole[4:], two[:2] + two[4:]):
+        assert np.array_equal(x, y) if isinstance(x, np.ndarray) else x == y
+    for i in (2, 3):
+        for q in whole[i]:
+            assert np.array_equal(whole[i][q], two[i][q]), q
+    h = R // 2
+    a = _replica_run(h, N, kappa, W, sweeps, phi0[:h].copy(), n0[:h].copy(), seeds[:h])
+    b = _replica_run(R - h, N, kappa, W, sweeps, phi0[h:].copy(), n0[h:].copy(), seeds[h:])
+    assert (whole[0] == np.concatenate([a[0], b[0]])).all() and (whole[1] == np.concatenate([a[1], b[1]])).all()
+    for q in whole[2]:
+        assert (np.asarray(whole[2][q]) == np.concatenate([np.asarray(a[2][q]), np.asarray(b[2][q])])).all(), q
+    for q in whole[3]:
+        assert (np.asarray(whole[3][q]) == np.concatenate([np.asarray(a[3][q]), np.asarray(b[3][q])])).all(), q
+    assert whole[4] == a[4] + b[4]
