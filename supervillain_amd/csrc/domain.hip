@@ -775,7 +775,9 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
                 if (split_i[k] >= 0) {
                     SplitArgs SA = splits[split_i[k]];
                     SA.blocksB = ctx->d_blocks + split_off[split_i[k]];
-                    split_order(SA, A.G, A.nsx, A.TH, grid, A.strips);
+                    // (tiles run uniform strips: no strip table -- split_order reads one on the host, never A.strips,
+                    // which is a device pointer)
+                    split_order(SA, A.G, A.nsx, A.TH, grid, nullptr);
                     launch_hot_split(A, SA, grid, ctx->stream);
                     ctx->sweeps_split++;
                 } else {

@@ -523,17 +523,34 @@ struct StatStripe {
     uint64_t pad[12];
 };
 
+#ifndef SV_WFLUSH_WG
+#define SV_WFLUSH_WG 0  // timing experiments: 1 = the workgroup's waves summed in LDS first, one stripe per workgroup
+#endif
 __device__ __forceinline__ void wflush(StatStripe *ss, int64_t acc, const AccFx &psum) {
     unsigned long long w[4];
     w[0] = (unsigned long long)acc;
     fx_limbs(psum, w[1], w[2], w[3]);
     for (int o = 32; o > 0; o >>= 1)
         for (int i = 0; i < 4; i++) w[i] += __shfl_xor(w[i], o);
+#if SV_WFLUSH_WG
+    __shared__ unsigned long long s_w[4][16];
+    if ((threadIdx.x & 63) == 0)
+        for (int i = 0; i < 4; i++) s_w[i][threadIdx.x >> 6] = w[i];
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        unsigned long long t = 0;
+        for (int v = 0; v < (int)(blockDim.x >> 6); v++) t += s_w[threadIdx.x][v];
+        StatStripe *st = ss + ((blockIdx.x + blockIdx.y * 7) & (NSTRIPE - 1));
+        if (t) atomicAdd(threadIdx.x == 0 ? &st->acc : &st->pw[threadIdx.x - 1], t);
+    }
+    __syncthreads();
+#else
     if ((threadIdx.x & 63) == 0) {
         StatStripe *st = ss + ((blockIdx.x + blockIdx.y * 7 + (threadIdx.x >> 6) * 3) & (NSTRIPE - 1));
         atomicAdd(&st->acc, w[0]);
         for (int i = 0; i < 3; i++) atomicAdd(&st->pw[i], w[1 + i]);
     }
+#endif
 }
 
 

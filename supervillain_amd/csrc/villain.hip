@@ -1117,7 +1117,10 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             blocks.swap(blocks_next);
             skipvec.swap(skipvec_next);
             c = c_next;
-        } else if (skips.empty() && V <= (1 << 18) && count >= 4 * 3 * std::max(bandK, 1)) {
+        } else if ((skips.empty() || skips.rbegin()->first.first < sw + 3 * std::max(bandK, 1)) && V <= (1 << 18) &&
+                   count >= 4 * 3 * std::max(bandK, 1)) {
+            // (known skips only in the first part -- the replay after an abort starts the batch -- so the re-plan after
+            // a rejection leaves the GPU idle for the first part's plan only, r6)
             part = 3 * std::max(bandK, 1);
             plan_sweeps(ctx, c, inc, specs, sw, part, skips, blocks, skipvec);
             ctx->ensure_blocks((size_t)count * nb);  // (the second part must not move d_blocks under the first launches)
@@ -1160,8 +1163,14 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         // (~5 us each) instead of the rest of the batch.  r5, scripts/perf/reject_window.py 4096 20 150, two runs each
         // (profiles/r05_chunk_ab.txt): extra per call that meets a rejection 0.270 / 0.274 ms whole, 0.225 / 0.228 ms in
         // chunks of 2, 0.241 / 0.254 in chunks of 4; clean calls level (4.38-4.40 ms).  Small lattices are enqueued whole
-        // (their sweeps are a few us: the host would pace the GPU).
-        const int CH = V >= (int64_t(1) << 22) ? 2 : count;
+        // (their sweeps are a few us: the host would pace the GPU).  Host cost: the calling thread polls the progress word
+        // for the length of the batch (std::this_thread::yield between polls, so other runnable threads get the core):
+        // one host core per large-lattice call, the price of the ~5 us early exit.
+        // Multi-sweep launches (temporal blocks, XCD bands) go out four launches (~90 us at L=256) at a time behind the
+        // progress word too: a rejection then leaves at most ~8 early-exit launches queued instead of the rest of a
+        // 256-sweep batch (r5: ~0.32 ms, ~41 sweeps, per rejection at L=256); four launches take the host ~20 us to
+        // enqueue, well inside the chunk before them.
+        const int CH = V >= (int64_t(1) << 22) ? 2 : (bandK ? 4 * bandK : count);
         int launched = count;
         *ctx->h_flag = 0;
         __atomic_store_n(ctx->h_prog, 0, __ATOMIC_RELEASE);  // (the previous batch's launches have all finished)
@@ -1387,16 +1396,20 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
         // concurrently; past MAX_REPORTS the reports are dropped in arrival order, so the earliest failing sweep (the
         // gate's atomic minimum) may have lost all of its reports.  Then the sweeps before the gate stand and the
         // rest of the call runs one sweep per launch, whose reports name the rejections anew.
+        // (its own flag: a genuine BAND_FAIL_BLOCK report that arrives with more than MAX_REPORTS reports still takes the
+        // process-wide band_broken path below)
+        bool truncated = false;
         if (a.raw > (uint32_t)MAX_REPORTS && band_gate) {
             int32_t g = INT32_MAX;
             SV_HIP(hipMemcpy(&g, band_gate, sizeof(int32_t), hipMemcpyDeviceToHost));
             if (g >= 0 && (uint32_t)g < first_bad) {
                 first_bad = (uint32_t)g;
                 overflow = false;
-                band_fail = true;  // (the band-failure path: keep the sweeps before it, multi-sweep launches off)
+                band_fail = false;
+                truncated = true;  // (keep the sweeps before the gate, multi-sweep launches off for this call)
             }
         }
-        if (band_fail && a.raw > (uint32_t)MAX_REPORTS) {
+        if (truncated) {
             // (truncated reports, above: multi-sweep launches off for the rest of this call only)
             const int bad = (int)first_bad;
             if (bad > 0) {

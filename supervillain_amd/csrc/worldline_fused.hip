@@ -112,6 +112,10 @@ __device__ __forceinline__ void wf_strip(const WFArgs &A, int &ix, int32_t &t0, 
 // the prologue fills with the same expression (bit-identical), otherwise computed as before
 static constexpr int WF_KP = 63, WF_PT = 2 * WF_KP + 1;
 
+#ifndef SV_WFFX
+#define SV_WFFX 0  // timing experiments: the exact acceptance words in LDS (0), in registers (1), not kept (2: wrong sums)
+#endif
+
 template <int NW>
 struct WFLDS {
     static constexpr int R = WFGeom<NW>::R;
@@ -125,7 +129,9 @@ struct WFLDS {
     double df[6], dfk[6];
     // per lane: the exact acceptance words of the Plaquette (0, 1) and Coexact (2, 3) passes (common.h), in LDS: two
     // AccFx in registers pushed the 16-wave loop past 128 VGPRs (r6: 34.8 -> 42.2 us per L=1024 step)
+#if SV_WFFX == 0
     unsigned long long fx[4][NW * 64];
+#endif
     int32_t bad;
 };
 
@@ -145,10 +151,6 @@ __device__ __forceinline__ double wf_dv1(int32_t vs, int32_t vn, double Winv) { 
 // MODE 0: interior strip, paired plaquette words; 1: edge strip (rows wrap), unpaired words from two base sets;
 // 2: GENERAL, a step with known Lemire rejections (skip lists) or unequal buffered-half flags: bounded words by
 // a full table jump at their skip-adjusted stream position (the rare replay of a rejected step)
-#ifndef SV_WFFX
-#define SV_WFFX 0  // timing experiments: the exact acceptance words in LDS (0), in registers (1), not kept (2: wrong sums)
-#endif
-
 template <bool TILE, int MODE, int NW>
 __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     constexpr bool EDGE = MODE != 0;
@@ -372,7 +374,9 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
 #if SV_WFFX == 1
     AccFx ppsum_r, cpsum_r;
 #endif
+#if SV_WFFX == 0
     for (int i = 0; i < 4; i++) Ls.fx[i][threadIdx.x] = 0;  // (only this lane touches its slots)
+#endif
 
     // uniform draw and bounded word at stream offsets of row q's base (set A or, for wrapped columns, set B)
     auto draw_u = [&](const u128 &base, uint32_t off) { return u53(xsl_rr(hot_apply(s_small, off & (SMALL_LDS - 1), base))); };
@@ -594,6 +598,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
 #if SV_WFFX == 1
     ppsum = ppsum_r;
     cpsum = cpsum_r;
+#elif SV_WFFX == 2
 #else
     ppsum.a = Ls.fx[0][threadIdx.x];
     ppsum.b = (int64_t)Ls.fx[1][threadIdx.x];

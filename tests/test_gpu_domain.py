@@ -19,10 +19,11 @@ def hot(Nt, Nx, W, seed):
 
 
 def run_domain(Nt, Nx, tiles, kappa, W, phi0, n0, sweeps, gen, chunks=(None,), interval_phi=np.pi, interval_n=1,
-               rccl=False):
+               rccl=False, split=None):
     dom = VillainDomain(Nt, Nx, tiles, kappa, W, interval_phi, interval_n, unique_id=unique_id() if rccl else None)
     try:
         dom.upload(phi0, n0)
+        dom.ctx.split_counts()  # (reset)
         stats = []
         left = sweeps
         for c in chunks:
@@ -30,6 +31,8 @@ def run_domain(Nt, Nx, tiles, kappa, W, phi0, n0, sweeps, gen, chunks=(None,), i
             stats += dom.run(k, gen)
             left -= k
         assert left == 0
+        if split is not None:
+            split.append(dom.ctx.split_counts())  # sweeps replayed on villain_sweep_hot_split (tile mode)
         phi, n = dom.download()
     finally:
         dom.close()
@@ -126,13 +129,17 @@ def test_deep_halo_depths(depth, tiles, oracle_lib, monkeypatch):
     pos, half = 4 * V + V + V // 2 + 11, 0  # sweep 1, a colour-0 choice block
     phi0, n0 = hot(N, N, 1, 99)
     gen = crafted_generator(5, pos, half)
-    phi, n, st = run_domain(N, N, tiles, 0.45, 1, phi0, n0, 11, gen)
+    split = []
+    phi, n, st = run_domain(N, N, tiles, 0.45, 1, phi0, n0, 11, gen, split=split)
     g = crafted_generator(5, pos, half)
     p, m = phi0.copy(), n0.copy()
     st_ref = oracle_lib.villain_neighborhood(N, 0.45, 1, p, m, 11, g)
     assert sum(s.rejections for s in st_ref) >= 1
     assert_same(phi, n, st, gen, p, m, st_ref, g)
     assert [s.rejections for s in st] == [s.rejections for s in st_ref]
+    # the replay of the failing sweep ran on the split kernel in tile mode, at depth 1 and at the deeper frames of
+    # the K > 1 groups (shifted region origins) alike
+    assert split[0] >= 1, split
 
 
 @pytest.mark.parametrize('tiles', [(2, 2), (2, 4)])

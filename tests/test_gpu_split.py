@@ -134,3 +134,73 @@ def test_split_replay_random_positions(N2, oracle_lib):
         assert (phi == phi0).all() and (n == n0).all(), (N2, c, j, rank)
         assert G.rng.bit_generator.state == g.bit_generator.state
         assert nsplit == 1 and counts['fused'] == 0
+
+
+PCG_MULT = 0x2360ED051FC65DA44385DF649FCCF645
+M128 = (1 << 128) - 1
+
+
+def crafted_two(seed, p1, half1, p2, half2):
+    """A Generator(PCG64) whose raw outputs p1 < p2 (p2 - p1 odd) have their low (half=0) or high (half=1) 32 bits zero:
+    two NumPy Lemire rejections in one sweep.  The state at output p1 is crafted as crafted_generator does; the
+    increment is then solved for so that the state at p2 = A^d s1 + (sum_{i<d} A^i) inc takes the crafted form too
+    (that sum is odd for odd d, so invertible mod 2^128; the free high word picks an odd increment)."""
+    from tests.golden import _MINV
+    d = p2 - p1
+    assert d > 0 and d % 2 == 1
+    out = {0: 0xDEADBEEF00000000, 1: 0x00000000DEADBEEF}
+    h1 = (0x0123456789ABCDEF ^ (seed * 0x9E3779B1)) & ((1 << 58) - 1)
+    s1 = (h1 << 64) | (h1 ^ out[half1])
+    Ad, coef, a = 1, 0, 1
+    for _ in range(d):
+        coef = (coef + a) & M128
+        a = (a * PCG_MULT) & M128
+    Ad = a
+    inv = pow(coef, -1, 1 << 128)
+    for t in range(1 << 16):
+        h2 = ((0x0FEDCBA987654321 ^ (seed * 0x85EBCA6B)) + t) & ((1 << 58) - 1)
+        s2 = (h2 << 64) | (h2 ^ out[half2])
+        inc = ((s2 - Ad * s1) * inv) & M128
+        if inc & 1:
+            break
+    s = s1
+    for _ in range(p1 + 1):
+        s = ((s - inc) * _MINV) & M128
+    g = np.random.default_rng(seed)
+    st = g.bit_generator.state
+    st['state']['state'] = s
+    st['state']['inc'] = inc
+    st['has_uint32'] = 0
+    st['uinteger'] = 0
+    g.bit_generator.state = st
+    return g
+
+
+@pytest.mark.parametrize('case', ['same row', 'different rows', 'both colours'])
+def test_split_replay_two_rejections_in_one_sweep(case, oracle_lib):
+    """split_plan takes up to two rejected words per sweep (one each in two choice blocks), and the replay
+    switches descriptors per row for both.  Two crafted rejections in one sweep -- in two blocks of one colour on the
+    same row, on different rows, and one in each colour -- replayed on the split kernel, against the oracle."""
+    V = N * N
+    (c1, j1, r1), (c2, j2, r2) = {
+        'same row': ((0, 0, (517 * N + 300) // 2), (0, 2, (517 * N + 600) // 2)),
+        'different rows': ((0, 1, (100 * N + 40) // 2), (0, 3, (700 * N + 900) // 2)),
+        'both colours': ((0, 2, (333 * N + 123) // 2), (1, 1, (801 * N + 77) // 2)),
+    }[case]
+    p1, h1 = word_of(N, c1, j1, r1, 0)
+    p2, h2 = word_of(N, c2, j2, r2, 0)
+    if (p2 - p1) % 2 == 0:  # (the increment solve needs an odd distance: the next word of the same block)
+        r2 += 2
+        p2, h2 = word_of(N, c2, j2, r2, 0)
+    seed = {'same row': 71, 'different rows': 72, 'both colours': 73}[case]
+    phi0, n0 = hot(N, 1, seed)
+    gen = crafted_two(seed, p1, h1, p2, h2)
+    G, phi, n, nsplit, counts = run(N, 2, gen, phi0, n0)
+    g = crafted_two(seed, p1, h1, p2, h2)
+    p, m = phi0.copy(), n0.copy()
+    st = oracle_lib.villain_neighborhood(N, 0.5, 1, p, m, 2, g)
+    assert st[0].rejections == 2, [s.rejections for s in st]
+    assert (phi == p).all() and (n == m).all(), case
+    assert G.rng.bit_generator.state == g.bit_generator.state
+    assert G.accepted == sum(s.accepted for s in st)
+    assert nsplit >= 1 and counts['fused'] == 0, (case, nsplit, counts)
