@@ -18,3 +18,6 @@ for r in 1 2; do
 done
 cat $O/rej_*.log
 for f in $O/*.json; do python scripts/summ_line.py $f; done
+step dt timeout -k 10 300 env SV_DEBUG_TIMING=1 python -u bench.py --tiles 2x4 --steps 40 --warmup 5 --no-cpu-baseline --no-copy-ceiling > $O/tiles_dbg.json 2> $O/tiles_dbg.err
+tail -40 $O/tiles_dbg.err
+python scripts/summ_line.py $O/tiles_dbg.json

@@ -22,11 +22,10 @@ for l in lines:
         files[int(m.group(1))] = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(path)) if d == '.' else d, f)) \
             if not d.startswith('/') else os.path.join(d, f)
 src_dir = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', '..', 'supervillain_amd', 'csrc')
-for k, v in list(files.items()):
-    if not os.path.exists(v):
-        cand = os.path.join(src_dir, os.path.basename(v))
-        if os.path.exists(cand):
-            files[k] = cand
+for k, v in list(files.items()):  # (relative .file entries: the library's sources)
+    cand = os.path.join(src_dir, os.path.basename(v))
+    if os.path.exists(cand) and not v.startswith(('/usr', '/opt')):
+        files[k] = cand
 
 start = next(i for i, l in enumerate(lines) if l.startswith(kern + ':'))
 end = next(i for i in range(start, len(lines)) if lines[i].startswith('.Lfunc_end') and i > start)
@@ -59,7 +58,7 @@ def ranges(fname):
     for i, l in enumerate(text):
         m = re.search(r'auto\s+(\w+)\s*=\s*\[', l)
         name = m.group(1) if m else None
-        if name is None and re.search(r'__device__|__global__|__host__', l):
+        if name is None and re.search(r'__device__|__global__|__host__|SV_HD', l):
             m = re.search(r'\b(\w+)\s*\((?!.*;\s*$)', l.split('//')[0])
             name = m.group(1) if m else None
         if not name or name in ('if', 'for', 'while', 'switch', 'launch_bounds', '__launch_bounds__', 'attribute',
@@ -118,6 +117,8 @@ def klass(mn):
 
 
 CATEGORY = [  # (substring of the owner, category)
+    ('mad_kk', 'PCG64 composition'), ('mad_k', 'PCG64 composition'), ('mad_n', 'PCG64 composition'),
+    ('fma3', 'exp'), ('base_pos', 'row-base advance'), ('wrapN', 'index wrap (wrapN)'), ('jump', 'row-base advance'),
     ('hot_apply', 'PCG64 composition'), ('mad128', 'PCG64 composition'), ('apply', 'PCG64 composition'),
     ('compose', 'PCG64 composition'), ('xsl_rr', 'XSL-RR output'), ('u53', 'u53 / uniform'),
     ('to_double', 'u53 / uniform'), ('exp_ocml', 'exp'), ('sv_exp', 'exp'), ('lemire', 'Lemire'),
@@ -135,32 +136,49 @@ def category(own):
     return own
 
 
-loops = []
-for i, (mn, s, _) in enumerate(insts):
-    if mn.startswith(('s_cbranch', 's_branch')):
-        tgt = s.split()[-1]
-        if tgt in labels and labels[tgt] <= i:
-            loops.append((labels[tgt], i))
-seen = []
-for a, b in sorted(loops, key=lambda x: x[1] - x[0], reverse=True):
-    if any(a >= x and b <= y for x, y in seen):
+# natural loops from the compiler's block annotations ("Loop: Header=BBx" / "Loop Header"): the row loops of the
+# kernel's bodies are the two largest (interior strips and edge strips)
+blocks, cur, loc = [], None, (None, 0)
+for l in lines[start:end]:
+    s = l.split(';')[0].strip()
+    m = re.match(r'\.loc\s+(\d+)\s+(\d+)', s)
+    if m:
+        loc = (int(m.group(1)), int(m.group(2)))
         continue
-    seen.append((a, b))
-    if len(seen) > nloops:
-        break
-    body = insts[a:b + 1]
+    m = re.match(r'^(\.LBB\S+):', s)
+    if m:
+        mm = re.search(r'Loop: Header=(\S+)', l)
+        h = mm.group(1) if mm else ('BB' + m.group(1)[4:] if 'Loop Header' in l else None)
+        cur = [m.group(1), h, []]
+        blocks.append(cur)
+        continue
+    if not s or s.startswith('.') or cur is None:
+        continue
+    cur[2].append((s.split()[0], s, loc))
+sizes = collections.Counter()
+for b in blocks:
+    if b[1]:
+        sizes[b[1]] += len(b[2])
+for H, n in sizes.most_common(nloops):
     per = collections.defaultdict(collections.Counter)
     cat = collections.defaultdict(collections.Counter)
-    for mn, s, lc in body:
-        o = owner(lc)
-        k = klass(mn)
-        per[o][k] += 1
-        cat[category(o)][k] += 1
     tot = collections.Counter()
-    for c in per.values():
-        tot.update(c)
-    print(f'loop [{a}, {b}]: {len(body)} instructions: ' + ', '.join(f'{k} {v}' for k, v in sorted(tot.items())))
-    print('  by category (valu + valu64 | lds | vmem | salu):')
+    rare = collections.Counter()
+    for b in blocks:
+        if b[1] != H:
+            continue
+        is_rare = any(owner(lc).endswith(':report') or mn.startswith('global_atomic') for mn, _, lc in b[2])
+        for mn, s, lc in b[2]:
+            o, k = owner(lc), klass(mn)
+            tot[k] += 1
+            if is_rare:
+                rare[k] += 1
+                continue
+            per[o][k] += 1
+            cat[category(o)][k] += 1
+    print(f'loop {H}: {n} instructions: ' + ', '.join(f'{k} {v}' for k, v in sorted(tot.items())) +
+          f'; in blocks that report a rejection (rare): ' + ', '.join(f'{k} {v}' for k, v in sorted(rare.items())))
+    print('  by category, common blocks (valu + valu64 | lds | vmem | salu):')
     for c, cnt in sorted(cat.items(), key=lambda kv: -(kv[1]['valu'] + kv[1]['valu64'])):
-        print(f'    {c:40s} {cnt["valu"] + cnt["valu64"]:5d} ({cnt["valu64"]:4d} 64-bit) | {cnt["lds"]:4d} | '
+        print(f'    {c:44s} {cnt["valu"] + cnt["valu64"]:5d} ({cnt["valu64"]:4d} 64-bit) | {cnt["lds"]:4d} | '
               f'{cnt["vmem"]:3d} | {cnt["salu"]:4d}')

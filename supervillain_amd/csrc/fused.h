@@ -524,7 +524,7 @@ struct StatStripe {
 };
 
 #ifndef SV_WFLUSH_WG
-#define SV_WFLUSH_WG 0  // timing experiments: 1 = the workgroup's waves summed in LDS first, one stripe per workgroup
+#define SV_WFLUSH_WG 1  // 1: the workgroup's waves summed in LDS first, one stripe per workgroup (0: per wave, r5)
 #endif
 __device__ __forceinline__ void wflush(StatStripe *ss, int64_t acc, const AccFx &psum) {
     unsigned long long w[4];

@@ -215,6 +215,7 @@ void plan_sweeps(sv_ctx *ctx, Cursor &cur, u128 inc, const std::vector<BlockSpec
 void upload_plan(sv_ctx *ctx, const std::vector<Block> &blocks, const std::vector<uint32_t> &skipvec);
 VParams make_params(int32_t N, double kappa, int64_t W, double interval_phi, int64_t interval_n);
 int absorb_reports(const AbortInfo &a, int first, SkipMap &skips);
+void drop_later_skips(SkipMap &skips, const std::pair<int, int> &key);  // (skips after key: stale)
 DevScratch scratch(sv_ctx *ctx);
 AbortInfo read_abort(sv_ctx *ctx);  // synchronizes the stream
 

@@ -794,12 +794,23 @@ void clear_abort(sv_ctx *ctx) {
 
 // Add the rejected positions of the earliest reported (sweep, block) to the skip map.
 // Returns that sweep index (relative to the batch start).
+// Skips of later choice blocks (of this sweep or a later one) were found against descriptors that did not yet know the
+// skip just added: it moves every later block's start one half-word on, so their rejected words sit one position lower
+// now.  They are dropped and found again, at their true positions, by the replay (r6: two rejections in one sweep whose
+// later block's was found first -- the early stop left the earlier one unreported -- kept a stale skip and replayed the
+// sweep wrong; tests/test_gpu_split.py two-rejection cases).  Skips within one block are positions in that block's own
+// stream and stay valid.
+void drop_later_skips(SkipMap &skips, const std::pair<int, int> &key) {
+    skips.erase(skips.upper_bound(key), skips.end());
+}
+
 int absorb_reports(const AbortInfo &a, int first, SkipMap &skips) {
     if (a.reports.empty()) throw std::runtime_error("device aborted without a rejection report");
     std::pair<uint32_t, uint32_t> best{~0u, ~0u};
     for (const Report &r : a.reports)
         if (std::make_pair(r.sweep, r.block) < best) best = {r.sweep, r.block};
-    auto &lst = skips[{first + (int)best.first, (int)best.second}];
+    const std::pair<int, int> key{first + (int)best.first, (int)best.second};
+    auto &lst = skips[key];
     const size_t before = lst.size();
     for (const Report &r : a.reports)
         if (r.sweep == best.first && r.block == best.second) lst.push_back(r.pos);
@@ -807,6 +818,7 @@ int absorb_reports(const AbortInfo &a, int first, SkipMap &skips) {
     lst.erase(std::unique(lst.begin(), lst.end()), lst.end());
     // a replay that meets only positions it already skips would repeat forever: a kernel drew a skipped word
     if (lst.size() == before) throw std::logic_error("rejection replay made no progress (a skipped word was drawn)");
+    drop_later_skips(skips, key);
     return (int)best.first;
 }
 
@@ -1487,7 +1499,11 @@ bool run_fused(sv_villain *st, const VParams &P, int32_t sweeps, Cursor &cur, u1
             return false;
         }
         const int bad = absorb_reports(a, sw, skips);
-        if (dbg) fprintf(stderr, "[sv] abort at sweep %d of %d\n", bad, count);
+        if (dbg) {
+            fprintf(stderr, "[sv] abort at sweep %d of %d; reports:", bad, count);
+            for (const Report &r : a.reports) fprintf(stderr, " (sweep %u block %u pos %u)", r.sweep, r.block, r.pos);
+            fprintf(stderr, "\n");
+        }
         // sweeps before `bad` in this batch are valid: keep them
         if (bad > 0) {
             Cursor c2 = cur;

@@ -534,11 +534,13 @@ int wabsorb(const std::vector<Report> &reps, int first, SkipMap &skips) {
     std::pair<uint32_t, uint32_t> best{~0u, ~0u};
     for (const Report &r : reps)
         if (std::make_pair(r.sweep, r.block) < best) best = {r.sweep, r.block};
-    auto &lst = skips[{first + (int)best.first, (int)best.second}];
+    const std::pair<int, int> key{first + (int)best.first, (int)best.second};
+    auto &lst = skips[key];
     for (const Report &r : reps)
         if (r.sweep == best.first && r.block == best.second) lst.push_back(r.pos);
     std::sort(lst.begin(), lst.end());
     lst.erase(std::unique(lst.begin(), lst.end()), lst.end());
+    svh::drop_later_skips(skips, key);  // (later blocks' skips were found against the old block starts: stale)
     return (int)best.first;
 }
 
