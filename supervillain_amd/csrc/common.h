@@ -296,16 +296,17 @@ inline void launch_check(const char *kernel, hipStream_t s) {
 #define SV_LAUNCHED(kernel, stream) (sv::sync_check_on() ? sv::launch_check(kernel, stream) : (void)0)
 
 // Exact Metropolis acceptance sums (the float statistics must not depend on the launch geometry).
-// A proposal's acceptance probability p in [0, 1] enters as T(p) = round(p 2^103), an integer, in two parts: x = p +
-// 2.0 lies in the binade [2, 4) (ulp 2^-51), so bits(x) = 0x4000000000000000 + round(p 2^51) and a = x - 2.0 is p
-// rounded to 2^-51; the remainder r = p - a is exact (|r| <= 2^-52) and fma(r, 2^103, 1.5 2^52) holds round(r 2^103)
-// in its low bits.  T(p) = round(p 2^51) 2^52 + round(r 2^103): resolution 2^-103 (~1e-31) per proposal.  A lane
-// keeps the raw bits of x summed modulo 2^64 (after k < 2^11 terms the low 62 bits are the exact sum of the round(p
-// 2^51)) and the round(r 2^103) in an int64 (fx_add: four f64 and six integer operations).  It flushes its exact value
-// sum T (< 2^114) as three 38-bit limbs, so every later addition -- over lanes, waves, workgroups, strips, tiles,
-// replica batches, launches -- is an integer addition whose result does not depend on its order, and the statistic
-// is fx_value(limb sums): the same double whatever the strip heights, layouts, tile grids or replica counts of the run,
-// within ~2 ulp of the exact sum of the p (the reference's NumPy pairwise sums are within rounding of it too).
+// A proposal's acceptance probability p in [0, 1] enters as the integer round(p 2^51): x = p + 2.0 lies in the binade
+// [2, 4) (ulp 2^-51), so bits(x) = 0x4000000000000000 + round(p 2^51) (round to nearest even).  A lane adds the raw bits
+// modulo 2^64 (fx_add: one f64 add and one 64-bit integer add per proposal); after k < 2^11 terms the low 62 bits are
+// the exact sum of its k values (the k 2^62 of the exponents only touch bits 62 and 63).  It flushes that sum, scaled to
+// T = sum 2^52 (the 2^-103 grid the three-limb words use), as three 38-bit limbs, so every later addition -- over lanes,
+// waves, workgroups, strips, tiles, replica batches, launches -- is an integer addition whose result does not depend on
+// its order, and the statistic is fx_value(limb sums) = T 2^-103: the same double whatever the strip heights, layouts,
+// tile grids or replica counts of the run.  Resolution: 2^-52 per proposal, absolute (the sweep's sum is within
+// 2^-52 x proposals of the exact sum of the p: relative 1e-15 at any acceptance rate above 0.1%).  The oracle keeps
+// the 2^-103 grid (oracle/sv_oracle.c fx_term_limbs), within rounding of the reference's pairwise sums at any rate; a
+// second, 2^-103 level here measured 1.5% on the headline sweep and 5% on config 3 (r6) and is not kept.
 // On the device a stats slot holds the three limb sums in its host-owned fields until it is finalized (stats_finalize,
 // or fx_value on the host for the domain summaries): proposed = limb 0, rejections = limb 1, acceptance_sum's bits =
 // limb 2.
@@ -313,26 +314,12 @@ namespace sv {
 constexpr uint64_t FX_LANE_MASK = (uint64_t(1) << 62) - 1, FX_LIMB = (uint64_t(1) << 38) - 1;
 struct AccFx {
     uint64_t a = 0;  // raw bits of p + 2.0, summed mod 2^64
-    int64_t b = 0;   // round(r 2^103), summed
 };
-__device__ __forceinline__ void fx_add(AccFx &s, double p) {
-    const double x = p + 2.0;
-    s.a += (uint64_t)__double_as_longlong(x);
-    const double r = p - (x - 2.0);
-    s.b += (int64_t)__double_as_longlong(__builtin_fma(r, 0x1p103, 0x1.8p52)) - (int64_t)0x4338000000000000ll;
-}
-// the same, the lane's two words kept in LDS slots of its own (no-return LDS adds: no registers held across a loop)
-__device__ __forceinline__ void fx_add_lds(unsigned long long *a, unsigned long long *b, double p) {
-    const double x = p + 2.0;
-    atomicAdd(a, (unsigned long long)__double_as_longlong(x));
-    const double r = p - (x - 2.0);
-    atomicAdd(b, (unsigned long long)(__double_as_longlong(__builtin_fma(r, 0x1p103, 0x1.8p52)) -
-                                      (long long)0x4338000000000000ll));
-}
-// a lane's exact value sum T = (a mod 2^62) 2^52 + b (>= 0, < 2^114) as three 38-bit limbs
+__device__ __forceinline__ void fx_add(AccFx &s, double p) { s.a += (uint64_t)__double_as_longlong(p + 2.0); }
+// a lane's exact value sum T = (a mod 2^62) 2^52 (< 2^114) as three 38-bit limbs
 __device__ __forceinline__ void fx_limbs(const AccFx &s, unsigned long long &w0, unsigned long long &w1,
                                          unsigned long long &w2) {
-    const unsigned __int128 T = ((unsigned __int128)(s.a & FX_LANE_MASK) << 52) + (unsigned __int128)(__int128)s.b;
+    const unsigned __int128 T = (unsigned __int128)(s.a & FX_LANE_MASK) << 52;
     w0 = (uint64_t)T & FX_LIMB;
     w1 = (uint64_t)(T >> 38) & FX_LIMB;
     w2 = (uint64_t)(T >> 76);

@@ -112,10 +112,6 @@ __device__ __forceinline__ void wf_strip(const WFArgs &A, int &ix, int32_t &t0, 
 // the prologue fills with the same expression (bit-identical), otherwise computed as before
 static constexpr int WF_KP = 63, WF_PT = 2 * WF_KP + 1;
 
-#ifndef SV_WFFX
-#define SV_WFFX 0  // timing experiments: the exact acceptance words in LDS (0), in registers (1), not kept (2: wrong sums)
-#endif
-
 template <int NW>
 struct WFLDS {
     static constexpr int R = WFGeom<NW>::R;
@@ -127,11 +123,6 @@ struct WFLDS {
     Affine adv[5];
     u128 base[NW][64];  // per wave: lane 8p + ty = block ty's base for pass p's row at xb; 32 + .. at xw
     double df[6], dfk[6];
-    // per lane: the exact acceptance words of the Plaquette (0, 1) and Coexact (2, 3) passes (common.h), in LDS: two
-    // AccFx in registers pushed the 16-wave loop past 128 VGPRs (r6: 34.8 -> 42.2 us per L=1024 step)
-#if SV_WFFX == 0
-    unsigned long long fx[4][NW * 64];
-#endif
     int32_t bad;
 };
 
@@ -371,12 +362,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
     }
 
     int32_t pacc = 0, cacc = 0;  // (a lane's counts stay below 2^11)
-#if SV_WFFX == 1
-    AccFx ppsum_r, cpsum_r;
-#endif
-#if SV_WFFX == 0
-    for (int i = 0; i < 4; i++) Ls.fx[i][threadIdx.x] = 0;  // (only this lane touches its slots)
-#endif
+    AccFx ppsum, cpsum;          // exact acceptance sums (common.h)
 
     // uniform draw and bounded word at stream offsets of row q's base (set A or, for wrapped columns, set B)
     auto draw_u = [&](const u128 &base, uint32_t off) { return u53(xsl_rr(hot_apply(s_small, off & (SMALL_LDS - 1), base))); };
@@ -459,11 +445,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
             const bool acc = u < pr;
             if (q >= t0 && q < t1 && x >= x0 && x < x1) {
                 pacc += acc;
-#if SV_WFFX == 0
-                fx_add_lds(&Ls.fx[0][threadIdx.x], &Ls.fx[1][threadIdx.x], pr);
-#elif SV_WFFX == 1
-                fx_add(ppsum_r, pr);
-#endif
+                fx_add(ppsum, pr);
             }
             if (__builtin_amdgcn_ballot_w64(acc)) {
                 if (acc) {
@@ -523,11 +505,7 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
             const bool acc = u < pr;
             if (q >= t0 && q < t1 && x >= x0 && x < x1) {
                 cacc += acc;
-#if SV_WFFX == 0
-                fx_add_lds(&Ls.fx[2][threadIdx.x], &Ls.fx[3][threadIdx.x], pr);
-#elif SV_WFFX == 1
-                fx_add(cpsum_r, pr);
-#endif
+                fx_add(cpsum, pr);
             }
             if (__builtin_amdgcn_ballot_w64(acc)) {
                 if (acc) {  // delta_sparse(t accepted): m0[x] += t, m0[x+e1] -= t, m1[x] -= t, m1[x+e0] += t
@@ -594,17 +572,6 @@ __device__ __forceinline__ void wf_body(const WFArgs &A, WFLDS<NW> &Ls) {
         store_rows(tl);
     }
     if (Ls.bad && threadIdx.x == 0) report(A.S, A.sweep, OVERFLOW_BLOCK, 0, 0);
-    AccFx ppsum, cpsum;
-#if SV_WFFX == 1
-    ppsum = ppsum_r;
-    cpsum = cpsum_r;
-#elif SV_WFFX == 2
-#else
-    ppsum.a = Ls.fx[0][threadIdx.x];
-    ppsum.b = (int64_t)Ls.fx[1][threadIdx.x];
-    cpsum.a = Ls.fx[2][threadIdx.x];
-    cpsum.b = (int64_t)Ls.fx[3][threadIdx.x];
-#endif
     wflush(A.pstat, pacc, ppsum);
     wflush(A.cstat, cacc, cpsum);
 #if SV_WFTIME
