@@ -964,11 +964,15 @@ template __global__ void villain_sweep_hot_split<true>(FArgs, SplitArgs);
 
 // ---- multi-sweep band launches of small periodic lattices (BandArgs, villain.h)
 // The XCD-local barrier between two sweeps of a band: every wave's stores acknowledged by the L2, one arrival per
-// workgroup, then a spin (compare-exchange: a read-modify-write, so it executes in the L2 and never sees a stale L1
-// line) until the band's P workgroups have arrived, and this CU's L1 invalidated so that the next sweep's rows come
-// from the L2.  Workgroup-scope atomics stay in the XCD's own L2, which every member of the band shares; nothing here
-// crosses XCDs (the cross-XCD barrier of round 2 paid an L2 write-back per workgroup and cost more than the launch it
-// saved).  A barrier that has waited 20 ms (the band's workgroups not all resident) gives up.
+// workgroup, then a spin until the band's P workgroups have arrived.  Workgroup-scope atomics stay in the XCD's own L2,
+// which every member of the band shares; nothing here crosses XCDs (the cross-XCD barrier of round 2 paid an L2
+// write-back per workgroup and cost more than the launch it saved).  The next sweep's rows come from the L2 because
+// no CU has them in its L1: sweep j reads buffer j, which this launch reads in no other sweep, and a launch starts with
+// its L1s invalidated.  (The `buffer_inv sc0` below is a workgroup-scope invalidate and does NOT drop L1 lines
+// -- measured, profiles/r06_xcd_barrier.txt: a re-read of a line after the first is stale; an L1-bypassing re-read
+// costs nothing extra, `buffer_inv sc1` 1.7 us per barrier.)  1.0 us per barrier with 32 workgroups per XCD against
+// 12.8 for the device-wide form (r6).  A barrier that has waited 20 ms (the band's workgroups not all resident)
+// gives up.
 __device__ __forceinline__ bool band_barrier(uint32_t *cnt, uint32_t target) {
     __shared__ int32_t s_ok;
     __builtin_amdgcn_s_waitcnt(0);
