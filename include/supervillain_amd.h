@@ -256,6 +256,21 @@ int sv_domain_unique_id(uint8_t *id /* SV_UNIQUE_ID_BYTES */);
 int sv_domain_create(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t nranks,
                      int32_t rank, const uint8_t *unique_id, sv_domain **out);
 int sv_domain_destroy(sv_domain *d);
+/* The same multi-rank domain with its two collectives carried by the caller instead of RCCL (an engine extension:
+ * the reference runs one process).  Per halo exchange the library copies this rank's packed messages to host
+ * memory and calls xfer(user, nsend, sends, sendbuf, nrecv, recvs, recvbuf): sends / recvs are {peer, offset,
+ * words} triples (offsets and sizes in uint64 words of sendbuf / recvbuf, the sv_domain_message_layout grouping),
+ * and xfer returns 0 once every message has been sent and received.  Per batch it calls gather(user, local, all,
+ * bytes): `all` receives every rank's `bytes`-byte batch summary in rank order (an all-gather).  Both must be called
+ * collectively on every rank (e.g. torch.distributed over gloo); a non-zero return fails the run.  model: 0
+ * Villain (then sv_domain_run), 1 Worldline (sv_domain_run_worldline).  For checking the multi-rank protocol where
+ * RCCL cannot run (two ranks on one GPU), not for speed. */
+typedef int (*sv_xfer_fn)(void *user, int32_t nsend, const int64_t *sends, const uint64_t *sendbuf, int32_t nrecv,
+                          const int64_t *recvs, uint64_t *recvbuf);
+typedef int (*sv_gather_fn)(void *user, const void *local, void *all, int64_t bytes);
+int sv_domain_create_hosted(sv_ctx *ctx, int32_t model, int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x,
+                            int32_t nranks, int32_t rank, sv_xfer_fn xfer, sv_gather_fn gather, void *user,
+                            sv_domain **out);
 /* Global (Nt, Nx) row-major host arrays; each rank copies its own tiles.  phi == NULL: cold start. */
 int sv_domain_upload(sv_domain *d, const double *phi, const int64_t *n);
 int sv_domain_download(sv_domain *d, double *phi, int64_t *n);

@@ -28,6 +28,10 @@ def lib_path():
     return p
 _LIB = None
 _LOCK = threading.RLock()
+# sv_domain_create_hosted's callbacks (include/supervillain_amd.h sv_xfer_fn, sv_gather_fn)
+XFER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p,
+                           ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p)
+GATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
 _CONTEXTS = {}
 
 
@@ -113,6 +117,7 @@ def lib():
         L.sv_domain_exchange_plan.argtypes = [i32, i32, i32, i32, i32, vp]
         L.sv_domain_message_layout.argtypes = [i32, i32, i32, i32, i32, vp]
         L.sv_domain_create_worldline.argtypes = [vp, i32, i32, i32, i32, i32, i32, vp, P(vp)]
+        L.sv_domain_create_hosted.argtypes = [vp, i32, i32, i32, i32, i32, i32, i32, XFER_FN, GATHER_FN, vp, P(vp)]
         L.sv_domain_upload_worldline.argtypes = [vp, vp, vp]
         L.sv_domain_download_worldline.argtypes = [vp, vp, vp]
         L.sv_domain_run_worldline.argtypes = [vp, f64, f64, i64, i32, P(SvRng), P(SvStats)]
@@ -147,6 +152,7 @@ EXPORTED = ('sv_ctx_create', 'sv_ctx_destroy', 'sv_last_error', 'sv_device_count
             'sv_worldline_vortex_run', 'sv_worldline_wrapping_run',
             'sv_domain_unique_id', 'sv_domain_create', 'sv_domain_destroy', 'sv_domain_upload', 'sv_domain_download',
             'sv_domain_run', 'sv_domain_exchange_plan', 'sv_domain_message_layout', 'sv_domain_create_worldline',
+            'sv_domain_create_hosted',
             'sv_domain_upload_worldline', 'sv_domain_download_worldline', 'sv_domain_run_worldline',
             'sv_domain_exchange_plan_worldline', 'sv_domain_message_layout_worldline',
             'sv_replicas_create', 'sv_replicas_destroy', 'sv_replicas_upload', 'sv_replicas_download',

@@ -266,6 +266,12 @@ struct sv_domain {
     ncclComm_t comm = nullptr;
     bool loopback = false;              // 1 rank, 1 tile, halos through RCCL to itself (tests the RCCL path)
     Summary *gathered = nullptr;        // device, nranks summaries (RCCL mode)
+    // hosted transport (sv_domain_create_hosted): the caller's callbacks carry the messages and the all-gather
+    sv_xfer_fn xfer = nullptr;
+    sv_gather_fn gatherfn = nullptr;
+    void *user = nullptr;
+    uint64_t *h_send = nullptr, *h_recv = nullptr;  // page-locked message staging
+    Summary *h_local = nullptr;                      // page-locked: this rank's summary
     std::vector<Summary> host_sum;
 };
 
@@ -409,7 +415,19 @@ void exchange(sv_domain *d, hipStream_t stream) {
                                                      &T.sum->abort), SV_LAUNCHED("halo_pack", stream);
     }
     // remote messages (one tile per rank in RCCL mode)
-    if (d->comm) {
+    if (d->xfer) {
+        // hosted transport: this rank's packed messages through host memory and the caller's callback
+        sv_domain_tile &T = d->tiles[0];
+        SV_HIP(hipMemcpyAsync(d->h_send, T.send, d->msg_words * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
+        SV_HIP(hipStreamSynchronize(stream));
+        std::vector<int64_t> sd, rv;
+        for (const auto &m : T.sends) sd.insert(sd.end(), {m[0], m[1], m[2]});
+        for (const auto &m : T.recvs) rv.insert(rv.end(), {m[0], m[1], m[2]});
+        if (d->xfer(d->user, (int32_t)T.sends.size(), sd.data(), d->h_send, (int32_t)T.recvs.size(), rv.data(),
+                    d->h_recv) != 0)
+            throw std::runtime_error("the hosted halo exchange failed (sv_xfer_fn returned non-zero)");
+        SV_HIP(hipMemcpyAsync(T.recv, d->h_recv, d->msg_words * sizeof(uint64_t), hipMemcpyHostToDevice, stream));
+    } else if (d->comm) {
         sv_domain_tile &T = d->tiles[0];
         check_nccl(ncclGroupStart(), "ncclGroupStart");
         for (const auto &m : T.sends)
@@ -440,6 +458,13 @@ void gather(sv_domain *d) {
     sv_ctx *ctx = d->ctx;
     const int ntiles = d->ty * d->tx;
     d->host_sum.resize(ntiles);
+    if (d->gatherfn) {
+        SV_HIP(hipMemcpyAsync(d->h_local, d->tiles[0].sum, sizeof(Summary), hipMemcpyDeviceToHost, ctx->stream));
+        SV_HIP(hipStreamSynchronize(ctx->stream));
+        if (d->gatherfn(d->user, d->h_local, d->host_sum.data(), (int64_t)sizeof(Summary)) != 0)
+            throw std::runtime_error("the hosted all-gather failed (sv_gather_fn returned non-zero)");
+        return;
+    }
     if (d->comm) {
         check_nccl(ncclAllGather(d->tiles[0].sum, d->gathered, sizeof(Summary), ncclChar, d->comm, ctx->stream),
                    "ncclAllGather");
@@ -525,7 +550,7 @@ void fill_stats(const sv_domain *d, const SkipMap &skips, int nb, int sw, int co
 int domain_batch_q(const sv_domain *d, double q) {
     if (const char *e = getenv("SV_DOMAIN_BATCH")) return std::max(1, std::min(DOMAIN_BATCH, atoi(e)));
     if (q <= 0) return DOMAIN_BATCH;
-    const double o = 0.3, r = d->comm ? 0.17 : 0.05;  // measured: RCCL exchange ~50 us, batch ~100 us, sweep 330 us
+    const double o = 0.3, r = d->nranks > 1 || d->comm ? 0.17 : 0.05;  // measured: RCCL exchange ~50 us, batch ~100 us, sweep 330 us
     const int B = (int)std::lround(std::sqrt(2.0 * o / (q * r)));
     return std::max(4, std::min(DOMAIN_BATCH, B));
 }
@@ -601,7 +626,7 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
     // rejections cost there.  SV_DOMAIN_PREDICT=1 / 0 forces it on / off.
     const char *np_env = getenv("SV_DOMAIN_PREDICT");
     const bool predict = P.k > 1 && P.thr > 0 && V >= 256 &&
-                         (np_env ? np_env[0] == '1' : (d->comm != nullptr && d->nranks > 1));
+                         (np_env ? np_env[0] == '1' : d->nranks > 1);
     // unpredicted batches stay short (an abort drains the rest of the batch); predicted ones run the full 64
     const int batch = domain_batch(d, P), full = predict && !getenv("SV_DOMAIN_BATCH") ? DOMAIN_BATCH : batch;
     auto &pred = d->pred;
@@ -629,9 +654,9 @@ void run_domain(sv_domain *d, const VParams &P, int32_t sweeps, Cursor &cur, u12
         }
         SV_HIP(hipMemcpyAsync(d->d_scan, h_scan.data(), n * sizeof(u128), hipMemcpyHostToDevice, stream));
         const uint64_t total = (uint64_t)n * 2 * ((uint64_t)V + 2 * SCAN_MARGIN);
-        const int parts = d->comm ? d->nranks : (int)d->tiles.size();
+        const int parts = d->nranks > 1 ? d->nranks : (int)d->tiles.size();
         for (size_t li = 0; li < d->tiles.size(); li++) {
-            const int me = d->comm ? d->rank : (int)li;
+            const int me = d->nranks > 1 ? d->rank : (int)li;
             ScanArgs a;
             a.s_k = d->d_scan;
             a.T = T;
@@ -1050,7 +1075,8 @@ int sv_domain_message_layout_worldline(int32_t Nt, int32_t Nx, int32_t tiles_t, 
 }
 
 static int domain_create(sv_ctx *ctx, int model, int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x,
-                         int32_t nranks, int32_t rank, const uint8_t *unique_id, sv_domain **out) {
+                         int32_t nranks, int32_t rank, const uint8_t *unique_id, sv_domain **out,
+                         sv_xfer_fn xfer = nullptr, sv_gather_fn gatherfn = nullptr, void *user = nullptr) {
     if (!ctx || !out) return -1;
     *out = nullptr;
     sv_domain *d = new sv_domain();
@@ -1058,6 +1084,9 @@ static int domain_create(sv_ctx *ctx, int model, int32_t Nt, int32_t Nx, int32_t
         SV_HIP(hipSetDevice(ctx->device));
         d->ctx = ctx;
         d->model = model;
+        d->xfer = xfer;
+        d->gatherfn = gatherfn;
+        d->user = user;
         d->ghost = model == 1 ? WORLDLINE_GHOST : VILLAIN_GHOST;
         d->Nt = Nt;
         d->Nx = Nx;
@@ -1069,7 +1098,10 @@ static int domain_create(sv_ctx *ctx, int model, int32_t Nt, int32_t Nx, int32_t
         if (nranks < 1 || rank < 0 || rank >= nranks) throw std::invalid_argument("bad rank / nranks");
         if (nranks > 1 && nranks != tiles_t * tiles_x)
             throw std::invalid_argument("with several ranks, each rank owns exactly one tile (nranks == tiles_t * tiles_x)");
-        if (nranks > 1 && !unique_id) throw std::invalid_argument("a unique id (sv_domain_unique_id on rank 0) is required");
+        if ((xfer == nullptr) != (gatherfn == nullptr)) throw std::invalid_argument("a hosted transport needs both callbacks");
+        if (xfer && unique_id) throw std::invalid_argument("a hosted transport takes no RCCL unique id");
+        if (nranks > 1 && !unique_id && !xfer)
+            throw std::invalid_argument("a unique id (sv_domain_unique_id on rank 0) is required");
         d->loopback = nranks == 1 && unique_id != nullptr;
         if (d->loopback && tiles_t * tiles_x != 1) throw std::invalid_argument("RCCL loopback mode needs a 1 x 1 tile grid");
         geometry(d);
@@ -1091,7 +1123,14 @@ static int domain_create(sv_ctx *ctx, int model, int32_t Nt, int32_t Nx, int32_t
             SV_HIP(hipMemset(T.sum, 0, sizeof(Summary)));
             if (model == 1) SV_HIP(hipMalloc(&T.stripes, (size_t)DOMAIN_BATCH * 2 * NSTRIPE * sizeof(StatStripe)));
         }
-        if (nranks > 1 || d->loopback) {
+        if (xfer) {
+            SV_HIP(hipHostMalloc((void **)&d->h_send, std::max<int64_t>(d->msg_words, 1) * sizeof(uint64_t),
+                                 hipHostMallocDefault));
+            SV_HIP(hipHostMalloc((void **)&d->h_recv, std::max<int64_t>(d->msg_words, 1) * sizeof(uint64_t),
+                                 hipHostMallocDefault));
+            SV_HIP(hipHostMalloc((void **)&d->h_local, sizeof(Summary), hipHostMallocDefault));
+            std::memset(d->h_recv, 0, std::max<int64_t>(d->msg_words, 1) * sizeof(uint64_t));
+        } else if (nranks > 1 || d->loopback) {
             ncclUniqueId u;
             std::memcpy(u.internal, unique_id, NCCL_UNIQUE_ID_BYTES);
             check_nccl(ncclCommInitRank(&d->comm, nranks, u, rank), "ncclCommInitRank");
@@ -1112,8 +1151,22 @@ int sv_domain_create(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tiles_t, int32
     return domain_create(ctx, 0, Nt, Nx, tiles_t, tiles_x, nranks, rank, unique_id, out);
 }
 
-int sv_domain_create_worldline(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t nranks,
-                               int32_t rank, const uint8_t *unique_id, sv_domain **out) {
+static int worldline_limits(sv_ctx *ctx, int32_t Nt, int32_t Nx);
+static int worldline_tile_limit(sv_ctx *ctx, int rc, sv_domain **out);
+
+int sv_domain_create_hosted(sv_ctx *ctx, int32_t model, int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x,
+                            int32_t nranks, int32_t rank, sv_xfer_fn xfer, sv_gather_fn gather, void *user,
+                            sv_domain **out) {
+    if (!xfer || !gather || (model != 0 && model != 1)) {
+        if (ctx) ctx->err = "sv_domain_create_hosted: model 0 or 1 and both callbacks are required";
+        return -2;
+    }
+    if (model == 1 && worldline_limits(ctx, Nt, Nx) != 0) return -2;
+    const int rc = domain_create(ctx, model, Nt, Nx, tiles_t, tiles_x, nranks, rank, nullptr, out, xfer, gather, user);
+    return model == 1 ? worldline_tile_limit(ctx, rc, out) : rc;
+}
+
+static int worldline_limits(sv_ctx *ctx, int32_t Nt, int32_t Nx) {
     if (Nt % 2 || Nx % 2) {
         if (ctx) ctx->err = "the Worldline decomposition needs even lattice extents";
         return -2;
@@ -1124,7 +1177,11 @@ int sv_domain_create_worldline(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tile
         if (ctx) ctx->err = "the Worldline decomposition needs Nt * Nx < 2^31 (worldline_step_fused's 31-bit positions)";
         return -2;
     }
-    const int rc = domain_create(ctx, 1, Nt, Nx, tiles_t, tiles_x, nranks, rank, unique_id, out);
+    return 0;
+}
+
+// (a Worldline domain whose tiles exceed worldline_step_fused's 32-bit row offsets is refused after its geometry is known)
+static int worldline_tile_limit(sv_ctx *ctx, int rc, sv_domain **out) {
     if (rc == 0 && (*out)->plane >= (int64_t(1) << 28)) {
         (void)sv_domain_destroy(*out);
         *out = nullptr;
@@ -1133,6 +1190,12 @@ int sv_domain_create_worldline(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tile
         return -2;
     }
     return rc;
+}
+
+int sv_domain_create_worldline(sv_ctx *ctx, int32_t Nt, int32_t Nx, int32_t tiles_t, int32_t tiles_x, int32_t nranks,
+                               int32_t rank, const uint8_t *unique_id, sv_domain **out) {
+    if (worldline_limits(ctx, Nt, Nx) != 0) return -2;
+    return worldline_tile_limit(ctx, domain_create(ctx, 1, Nt, Nx, tiles_t, tiles_x, nranks, rank, unique_id, out), out);
 }
 
 int sv_domain_destroy(sv_domain *d) {
@@ -1149,6 +1212,9 @@ int sv_domain_destroy(sv_domain *d) {
         (void)hipFree(T.stripes);
     }
     if (d->comm) (void)ncclCommDestroy(d->comm);
+    if (d->h_send) (void)hipHostFree(d->h_send);
+    if (d->h_recv) (void)hipHostFree(d->h_recv);
+    if (d->h_local) (void)hipHostFree(d->h_local);
     (void)hipFree(d->gathered);
     (void)hipFree(d->d_scan);
     if (d->scan_stream) (void)hipStreamDestroy(d->scan_stream);

@@ -85,32 +85,105 @@ def message_layout(Nt, Nx, tiles, rank, model='villain'):
             'words': o[p + 16:p + 24], 'msg_words': o[p + 24]}
 
 
+class HostTransport:
+    """The two collectives of a multi-rank domain carried by torch.distributed on host memory instead of RCCL
+    (sv_domain_create_hosted): the halo messages as one isend / irecv per distinct peer, the batch summaries as an
+    all_gather.  Any backend that moves CPU tensors will do (gloo).  For checking the multi-rank protocol where RCCL
+    cannot run -- two ranks on one GPU -- not for speed.  Default process group only (peers are its ranks)."""
+
+    def __init__(self):
+        import torch
+        import torch.distributed as dist
+        self._torch, self._dist = torch, dist
+        self.error = None  # the first exception a callback met (the library then fails the run)
+        self.xfer = _native.XFER_FN(self._xfer)
+        self.gather = _native.GATHER_FN(self._gather)
+
+    def _xfer(self, user, nsend, sends, sendbuf, nrecv, recvs, recvbuf):
+        try:
+            torch, dist = self._torch, self._dist
+            reqs, landed = [], []
+            for i in range(nsend):
+                peer, off, words = sends[3 * i], sends[3 * i + 1], sends[3 * i + 2]
+                msg = np.frombuffer((ctypes.c_int64 * words).from_address(sendbuf + 8 * off), dtype=np.int64).copy()
+                reqs.append(dist.isend(torch.from_numpy(msg), dst=int(peer)))
+            for i in range(nrecv):
+                peer, off, words = recvs[3 * i], recvs[3 * i + 1], recvs[3 * i + 2]
+                t = torch.empty(int(words), dtype=torch.int64)
+                reqs.append(dist.irecv(t, src=int(peer)))
+                landed.append((off, words, t))
+            for r in reqs:
+                r.wait()
+            for off, words, t in landed:
+                ctypes.memmove(recvbuf + 8 * off, t.numpy().ctypes.data, 8 * words)
+            return 0
+        except Exception as e:  # (an exception cannot cross the C frames: report it, fail the run)
+            self.error = self.error or e
+            return 1
+
+    def _gather(self, user, local, out, nbytes):
+        try:
+            torch, dist = self._torch, self._dist
+            mine = torch.from_numpy(np.frombuffer((ctypes.c_uint8 * nbytes).from_address(local), dtype=np.uint8).copy())
+            parts = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(dist.get_world_size())]
+            dist.all_gather(parts, mine)
+            for r, t in enumerate(parts):
+                ctypes.memmove(out + r * nbytes, t.numpy().ctypes.data, nbytes)
+            return 0
+        except Exception as e:
+            self.error = self.error or e
+            return 1
+
+
 class VillainDomain:
     """An Nt x Nx Villain (phi, n) state cut into tiles, resident in HBM."""
+    _model = 0  # sv_domain_create_hosted's model
 
     def __init__(self, Nt, Nx=None, tiles=(1, 1), kappa=0.5, W=1, interval_phi=np.pi, interval_n=1, *,
-                 device=None, nranks=1, rank=0, unique_id=None):
+                 device=None, nranks=1, rank=0, unique_id=None, transport=None):
         Nx = Nt if Nx is None else Nx
         self.Nt, self.Nx, self.tiles = int(Nt), int(Nx), (int(tiles[0]), int(tiles[1]))
         self.kappa, self.W, self.interval_phi, self.interval_n = float(kappa), int(W), float(interval_phi), int(interval_n)
         self.nranks, self.rank = int(nranks), int(rank)
         self.ctx = _native.context(_native.default_device() if device is None else device)
-        uid = None
-        if unique_id is not None:
-            uid = (ctypes.c_uint8 * UNIQUE_ID_BYTES).from_buffer_copy(bytes(unique_id))
+        self._create(unique_id, transport, 'sv_domain_create')
+
+    def _create(self, unique_id, transport, name):
         h = ctypes.c_void_p()
-        self.ctx.check(_native.lib().sv_domain_create(self.ctx.handle, self.Nt, self.Nx, self.tiles[0], self.tiles[1],
-                                                      self.nranks, self.rank, uid, ctypes.byref(h)),
-                       'sv_domain_create')
+        self._transport = transport  # (the callbacks must outlive the domain)
+        if transport is not None:
+            rc = _native.lib().sv_domain_create_hosted(self.ctx.handle, self._model, self.Nt, self.Nx, self.tiles[0],
+                                                       self.tiles[1], self.nranks, self.rank, transport.xfer,
+                                                       transport.gather, None, ctypes.byref(h))
+            self.ctx.check(rc, 'sv_domain_create_hosted')
+        else:
+            uid = None
+            if unique_id is not None:
+                uid = (ctypes.c_uint8 * UNIQUE_ID_BYTES).from_buffer_copy(bytes(unique_id))
+            self.ctx.check(getattr(_native.lib(), name)(self.ctx.handle, self.Nt, self.Nx, self.tiles[0], self.tiles[1],
+                                                        self.nranks, self.rank, uid, ctypes.byref(h)), name)
         self.handle = h
 
+    def _check_run(self, rc, name):
+        t = getattr(self, '_transport', None)
+        if rc != 0 and t is not None and t.error is not None:
+            raise _native.NativeError(f'{name}: the host transport failed: {t.error!r}') from t.error
+        self.ctx.check(rc, name)
+
     @classmethod
-    def distributed(cls, Nt, Nx=None, tiles=None, group=None, **kw):
-        """One tile per rank of the (already initialised) default torch.distributed group; any backend
-        (gloo is enough: it only carries the 128-byte RCCL id)."""
+    def distributed(cls, Nt, Nx=None, tiles=None, group=None, transport='rccl', **kw):
+        """One tile per rank of the (already initialised) default torch.distributed group.  transport='rccl': halos
+        over RCCL (any backend for the group: gloo is enough, it only carries the 128-byte RCCL id); 'host': both
+        collectives over the group itself through host memory (HostTransport; default group only)."""
         import torch.distributed as dist
         world, rank = dist.get_world_size(group), dist.get_rank(group)
         tiles = tile_grid(world) if tiles is None else tiles
+        if transport == 'host':
+            if group is not None:
+                raise ValueError('the host transport runs on the default process group')
+            return cls(Nt, Nx, tiles, nranks=world, rank=rank, transport=HostTransport(), **kw)
+        if transport != 'rccl':
+            raise ValueError(f"transport must be 'rccl' or 'host', not {transport!r}")
         box = [unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0, group=group)
         return cls(Nt, Nx, tiles, nranks=world, rank=rank, unique_id=box[0], **kw)
@@ -145,8 +218,8 @@ class VillainDomain:
         Collective when nranks > 1.  Returns per-sweep global stats."""
         r = rng_from_numpy(rng)
         st = _native.stats_array(max(sweeps, 1))
-        self.ctx.check(_native.lib().sv_domain_run(self.handle, self.kappa, self.W, self.interval_phi, self.interval_n,
-                                                   int(sweeps), ctypes.byref(r), st), 'sv_domain_run')
+        self._check_run(_native.lib().sv_domain_run(self.handle, self.kappa, self.W, self.interval_phi, self.interval_n,
+                                                    int(sweeps), ctypes.byref(r), st), 'sv_domain_run')
         rng_to_numpy(r, rng)
         return [st[i] for i in range(sweeps)]
 
@@ -156,22 +229,16 @@ class WorldlineDomain(VillainDomain):
     the CoexactUpdate sweep of sv_worldline_plaquette_coexact_run (the config-3 step), one halo exchange per
     step (sv_domain_*_worldline).  Integer v; W a power of two."""
 
+    _model = 1
+
     def __init__(self, Nt, Nx=None, tiles=(1, 1), kappa=0.5, W=1, interval_t=1, *, device=None, nranks=1, rank=0,
-                 unique_id=None):
+                 unique_id=None, transport=None):
         Nx = Nt if Nx is None else Nx
         self.Nt, self.Nx, self.tiles = int(Nt), int(Nx), (int(tiles[0]), int(tiles[1]))
         self.kappa, self.W, self.interval_t = float(kappa), float(W), int(interval_t)
         self.nranks, self.rank = int(nranks), int(rank)
         self.ctx = _native.context(_native.default_device() if device is None else device)
-        uid = None
-        if unique_id is not None:
-            uid = (ctypes.c_uint8 * UNIQUE_ID_BYTES).from_buffer_copy(bytes(unique_id))
-        h = ctypes.c_void_p()
-        self.ctx.check(_native.lib().sv_domain_create_worldline(self.ctx.handle, self.Nt, self.Nx, self.tiles[0],
-                                                                self.tiles[1], self.nranks, self.rank, uid,
-                                                                ctypes.byref(h)),
-                       'sv_domain_create_worldline')
-        self.handle = h
+        self._create(unique_id, transport, 'sv_domain_create_worldline')
 
     def cold(self):
         self.ctx.check(_native.lib().sv_domain_upload_worldline(self.handle, None, None), 'sv_domain_upload_worldline')
@@ -194,9 +261,9 @@ class WorldlineDomain(VillainDomain):
         2 * steps global stats ({Plaquette, Coexact} per step)."""
         r = rng_from_numpy(rng)
         st = _native.stats_array(max(2 * steps, 1))
-        self.ctx.check(_native.lib().sv_domain_run_worldline(self.handle, self.kappa, self.W, self.interval_t,
-                                                             int(steps), ctypes.byref(r), st),
-                       'sv_domain_run_worldline')
+        self._check_run(_native.lib().sv_domain_run_worldline(self.handle, self.kappa, self.W, self.interval_t,
+                                                              int(steps), ctypes.byref(r), st),
+                        'sv_domain_run_worldline')
         rng_to_numpy(r, rng)
         return [st[i] for i in range(2 * steps)]
 

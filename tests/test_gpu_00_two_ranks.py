@@ -1,7 +1,10 @@
-"""Two real ranks on one GPU: the multi-rank RCCL code (per-peer ncclSend / ncclRecv pairs between two processes,
-the batch-summary ncclAllGather over two ranks, rank-ordered group calls) against the single-process tile emulation,
-bit for bit, for a Villain and a Worldline 1 x 2 decomposition (config 4 and config 3 as two GPUs would run them),
-with NumPy Lemire rejections forced into the chain (the abort / replay protocol across ranks).
+"""Two real ranks on one GPU: the multi-rank domain code (per-peer halo messages between two processes, the
+batch-summary all-gather over two ranks, the abort / replay decision taken on every rank) against the single-process
+tile emulation, bit for bit, for a Villain and a Worldline 1 x 2 decomposition (config 4 and config 3 as two GPUs would
+run them), with NumPy Lemire rejections forced into the chain (the abort spreading across real ranks).  transport
+'rccl': RCCL's ncclSend / ncclRecv and ncclAllGather; 'host': the same two collectives through host memory over the
+gloo group (HostTransport, sv_domain_create_hosted) -- every other part of the multi-rank path (one tile per process,
+pack / unpack kernels, the message layout per peer, the gathered summaries, rejection prediction) is the RCCL run's.
 
 This file sorts FIRST among the -m gpu tests on purpose: the two ranks are started (spawn: fresh interpreters) before
 the test process itself has touched the GPU -- a process that has initialised the GPU must not start new programs.
@@ -21,8 +24,10 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, model, out):
+def _worker(rank, world, port, model, transport, predict, out):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), SV_DEVICE='0', SV_DOMAIN_BATCH='4')
+    if predict is not None:  # rejection prediction (on by default with several ranks) or the abort / replay protocol
+        os.environ['SV_DOMAIN_PREDICT'] = predict
     import torch.distributed as dist
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
@@ -36,7 +41,7 @@ def _worker(rank, world, port, model, out):
             phi0 = np.random.default_rng(4).uniform(-np.pi, np.pi, (Nt, Nx))
             n0 = np.random.default_rng(5).integers(-2, 3, (2, Nt, Nx)).astype(np.int64)
             make = lambda **kw: VillainDomain(Nt, Nx, (1, 2), kappa=0.5, W=1, **kw)  # noqa: E731
-            dist_make = lambda: VillainDomain.distributed(Nt, Nx, (1, 2), kappa=0.5, W=1)  # noqa: E731
+            dist_make = lambda: VillainDomain.distributed(Nt, Nx, (1, 2), kappa=0.5, W=1, transport=transport)  # noqa: E731
         else:
             Nt, Nx, steps = 64, 128, 6
             V = Nt * Nx
@@ -45,10 +50,12 @@ def _worker(rank, world, port, model, out):
             phi0 = np.random.default_rng(6).integers(-3, 4, (Nt, Nx)).astype(np.int64)
             n0 = np.zeros((2, Nt, Nx), dtype=np.int64)
             make = lambda **kw: WorldlineDomain(Nt, Nx, (1, 2), kappa=0.5, W=1, **kw)  # noqa: E731
-            dist_make = lambda: WorldlineDomain.distributed(Nt, Nx, (1, 2), kappa=0.5, W=1)  # noqa: E731
+            dist_make = lambda: WorldlineDomain.distributed(Nt, Nx, (1, 2), kappa=0.5, W=1, transport=transport)  # noqa: E731
         try:
             dom = dist_make()
         except Exception as e:  # RCCL refusing two ranks on one device lands here (ncclCommInitRank)
+            if transport != 'rccl':
+                raise
             with open(f'{out}.refused', 'w') as f:
                 f.write(f'rank {rank}: {e}')
             return
@@ -98,20 +105,25 @@ def _worker(rank, world, port, model, out):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize('transport,predict', [('rccl', None), ('host', '0'), ('host', '1')])
 @pytest.mark.parametrize('model', ['villain', 'worldline'])
-def test_two_ranks_one_gpu(model, tmp_path):
+def test_two_ranks_one_gpu(model, transport, predict, tmp_path):
+    """predict '0': the forced rejection aborts the batch on the rank that meets it, the abort reaches the other rank
+    in the halo messages and the gathered summaries, and both replay; '1': the scan split over the two ranks finds it
+    first and both plan around it."""
     import time
 
     import torch.multiprocessing as mp
     out = str(tmp_path / model)
-    ctx = mp.start_processes(_worker, args=(2, _free_port(), model, out), nprocs=2, join=False, start_method='spawn')
+    ctx = mp.start_processes(_worker, args=(2, _free_port(), model, transport, predict, out), nprocs=2, join=False,
+                             start_method='spawn')
     deadline = time.time() + 240  # a rendezvous that never completes must not hang the suite
     while not ctx.join(timeout=5):
         if time.time() > deadline:
             for p in ctx.processes:
                 p.kill()
             pytest.fail('two-rank run did not finish in 240 s')
-    if os.path.exists(f'{out}.refused'):
+    if transport == 'rccl' and os.path.exists(f'{out}.refused'):
         pytest.xfail('RCCL refused two ranks on one device: ' + open(f'{out}.refused').read())
     assert not os.path.exists(f'{out}.error'), open(f'{out}.error').read()
     assert open(f'{out}.result').read() == 'ok'
