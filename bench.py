@@ -93,6 +93,10 @@ def parse():
     ap.add_argument('--no-copy-ceiling', action='store_true', help='skip the measured copy-kernel HBM ceiling')
     ap.add_argument('--tiles', default=None, help='tile grid TYxTX (default from N); with N=1 emulates the '
                                                    'decomposition on one GPU')
+    ap.add_argument('--transport', default='rccl', choices=['rccl', 'host'],
+                    help="N > 1 domain lines: halos over RCCL (the default), or 'host' (sv_domain_create_hosted over the "
+                         'gloo group: a rehearsal of the N-rank path where RCCL cannot run, e.g. N ranks on one GPU '
+                         'with SV_DEVICE=0; not a performance line)')
     ap.add_argument('--workload', default='villain', choices=['villain', 'replicas', 'worldline', 'site', 'link', 'exact',
                                                               'cohomology', 'hammer', 'vortex', 'wrapping', 'wlhammer',
                                                               'worms', 'ranks'])
@@ -417,7 +421,8 @@ def run_worldline_domain(args, world, rank, dist):
     Nt, Nx = (L, L) if args.strong else (ty * L, tx * L)
     Ht, Wt = Nt // ty, Nx // tx
     kw = dict(kappa=args.kappa, W=args.W)
-    dom = WorldlineDomain.distributed(Nt, Nx, (ty, tx), **kw) if world > 1 else WorldlineDomain(Nt, Nx, (ty, tx), **kw)
+    dom = (WorldlineDomain.distributed(Nt, Nx, (ty, tx), transport=args.transport, **kw) if world > 1
+           else WorldlineDomain(Nt, Nx, (ty, tx), **kw))
     dom.cold()
     gen = np.random.default_rng(0)
     Lib = _native.lib()
@@ -448,6 +453,7 @@ def run_worldline_domain(args, world, rank, dist):
                               f'W={args.W}, kappa={args.kappa}, domain-decomposed into {ty}x{tx} tiles of {Ht}x{Wt} '
                               '(one per GPU), (v, m) halo exchange per step, bit-exact PCG64 replay',
                   'L': L, 'lattice': [Nt, Nx], 'tiles': [ty, tx], 'path': 'worldline-domain',
+                  'halo_transport': args.transport if world > 1 else 'none (one process)',
                   'parallelism': f'{ty}x{tx} domain decomposition over {world} GPU(s)',
                   'lemire_rejections_in_timed_steps': int(rej),
                   'scaling_reference': scaling_reference(value, world, r1_mean, [Ht, Wt], None, None, 'steps')}
@@ -741,7 +747,7 @@ def run_domain(args, world, rank, local, dist):
     Ht, Wt = Nt // ty, Nx // tx
     kw = dict(kappa=args.kappa, W=args.W)  # device: $SV_DEVICE, else $LOCAL_RANK
     if world > 1:
-        dom = VillainDomain.distributed(Nt, Nx, (ty, tx), **kw)
+        dom = VillainDomain.distributed(Nt, Nx, (ty, tx), transport=args.transport, **kw)
     else:
         dom = VillainDomain(Nt, Nx, (ty, tx), **kw)
     dom.cold()
@@ -780,6 +786,7 @@ def run_domain(args, world, rank, local, dist):
                               f'domain-decomposed into {ty}x{tx} tiles of {Ht}x{Wt} (one per GPU), RCCL halo '
                               'exchange, bit-exact reference chain (PCG64 replay)',
                   'L': L, 'lattice': [Nt, Nx], 'tiles': [ty, tx], 'path': 'domain',
+                  'halo_transport': args.transport if world > 1 else 'none (one process)',
                   # deep halos: K sweeps per halo exchange, ghost frame 2K / 3K deep
                   'sweeps_per_halo_exchange': ghost_frame(Nt, Nx, (ty, tx))[0] // 2,
                   'parallelism': f'{ty}x{tx} domain decomposition over {world} GPU(s)' +
@@ -837,7 +844,17 @@ def main():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        dist.init_process_group('gloo', rank=rank, world_size=world)
+        # gloo prints its connection messages on stdout ("[Gloo] Rank 0 is connected to ..."), interleaved across the
+        # ranks: they go to stderr, so that stdout carries rank 0's one JSON line only
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group('gloo', rank=rank, world_size=world)
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     if args.workload != 'villain':
         fn = {'replicas': run_replicas, 'worldline': run_worldline, 'worms': run_worms,
               'ranks': run_ranks}.get(args.workload, run_local)

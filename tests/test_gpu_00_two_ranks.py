@@ -127,3 +127,26 @@ def test_two_ranks_one_gpu(model, transport, predict, tmp_path):
         pytest.xfail('RCCL refused two ranks on one device: ' + open(f'{out}.refused').read())
     assert not os.path.exists(f'{out}.error'), open(f'{out}.error').read()
     assert open(f'{out}.result').read() == 'ok'
+
+
+@pytest.mark.parametrize('workload', ['villain', 'worldline'])
+def test_bench_two_ranks_hosted(workload):
+    """`bench.py --gpus 2` end to end -- its own torch.distributed.run launch, one rank per process, the domain line,
+    R1 and the single-lattice reference on every rank, max over ranks, rank 0's JSON line -- with both ranks on the one
+    GPU (SV_DEVICE=0) and the halos over the hosted transport (RCCL refuses two ranks on one device).  A rehearsal of
+    the driver's N > 1 runs, not a measurement.  (Started, like the test above, before this process touches the GPU.)"""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SV_DEVICE='0', MASTER_ADDR='127.0.0.1')
+    cmd = [sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2', '--transport', 'host', '--steps', '4',
+           '--warmup', '1', '--warmup-s', '0', '--no-cpu-baseline', '--no-copy-ceiling', '--L', '512',
+           '--workload', workload]
+    p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([s for s in p.stdout.splitlines() if s.startswith('{')][-1])
+    assert line['n_gpus'] == 2 and line['steps'] == 4 and line['value'] > 0
+    cfg = line['config']
+    assert cfg['halo_transport'] == 'host' and cfg['tiles'] == [1, 2] and cfg['lattice'] == [512, 512]
+    assert '512' in line['metric'] and cfg['scaling_reference']['R1'] > 0
