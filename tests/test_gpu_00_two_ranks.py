@@ -24,7 +24,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, model, transport, predict, out):
+def _worker(rank, world, port, model, transport, predict, out, tiles=(1, 2)):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), SV_DEVICE='0', SV_DOMAIN_BATCH='4')
     if predict is not None:  # rejection prediction (on by default with several ranks) or the abort / replay protocol
         os.environ['SV_DOMAIN_PREDICT'] = predict
@@ -40,8 +40,8 @@ def _worker(rank, world, port, model, transport, predict, out):
             gen = lambda: crafted_generator(pos, pos, 1)  # noqa: E731
             phi0 = np.random.default_rng(4).uniform(-np.pi, np.pi, (Nt, Nx))
             n0 = np.random.default_rng(5).integers(-2, 3, (2, Nt, Nx)).astype(np.int64)
-            make = lambda **kw: VillainDomain(Nt, Nx, (1, 2), kappa=0.5, W=1, **kw)  # noqa: E731
-            dist_make = lambda: VillainDomain.distributed(Nt, Nx, (1, 2), kappa=0.5, W=1, transport=transport)  # noqa: E731
+            make = lambda **kw: VillainDomain(Nt, Nx, tiles, kappa=0.5, W=1, **kw)  # noqa: E731
+            dist_make = lambda: VillainDomain.distributed(Nt, Nx, tiles, kappa=0.5, W=1, transport=transport)  # noqa: E731
         else:
             Nt, Nx, steps = 64, 128, 6
             V = Nt * Nx
@@ -49,8 +49,8 @@ def _worker(rank, world, port, model, transport, predict, out):
             gen = lambda: crafted_generator(pos, pos, 1)  # noqa: E731
             phi0 = np.random.default_rng(6).integers(-3, 4, (Nt, Nx)).astype(np.int64)
             n0 = np.zeros((2, Nt, Nx), dtype=np.int64)
-            make = lambda **kw: WorldlineDomain(Nt, Nx, (1, 2), kappa=0.5, W=1, **kw)  # noqa: E731
-            dist_make = lambda: WorldlineDomain.distributed(Nt, Nx, (1, 2), kappa=0.5, W=1, transport=transport)  # noqa: E731
+            make = lambda **kw: WorldlineDomain(Nt, Nx, tiles, kappa=0.5, W=1, **kw)  # noqa: E731
+            dist_make = lambda: WorldlineDomain.distributed(Nt, Nx, tiles, kappa=0.5, W=1, transport=transport)  # noqa: E731
         try:
             dom = dist_make()
         except Exception as e:  # RCCL refusing two ranks on one device lands here (ncclCommInitRank)
@@ -69,18 +69,21 @@ def _worker(rank, world, port, model, transport, predict, out):
             a, b = dom.download()
         finally:
             dom.close()
-        res = [None, None]
+        res = [None] * world
         dist.all_gather_object(res, (a, b, [(s.accepted, s.rejections) for s in st], g.bit_generator.state))
         if rank == 0:
             a = res[0][0].copy()
             b = res[0][1].copy()
-            half = Nx // 2
-            if model == 'villain':  # phi (Nt, Nx), n (2, Nt, Nx): rank 1 owns columns [half, Nx)
-                a[:, half:] = res[1][0][:, half:]
-                b[:, :, half:] = res[1][1][:, :, half:]
-            else:  # m (2, Nt, Nx), v (Nt, Nx)
-                a[:, :, half:] = res[1][0][:, :, half:]
-                b[:, half:] = res[1][1][:, half:]
+            Ht, Wt = Nt // tiles[0], Nx // tiles[1]
+            for r in range(1, world):  # rank r owns tile r (row-major): rows [iy Ht, +Ht), columns [ix Wt, +Wt)
+                ys = slice(r // tiles[1] * Ht, (r // tiles[1] + 1) * Ht)
+                xs = slice(r % tiles[1] * Wt, (r % tiles[1] + 1) * Wt)
+                if model == 'villain':  # phi (Nt, Nx), n (2, Nt, Nx)
+                    a[ys, xs] = res[r][0][ys, xs]
+                    b[:, ys, xs] = res[r][1][:, ys, xs]
+                else:  # m (2, Nt, Nx), v (Nt, Nx)
+                    a[:, ys, xs] = res[r][0][:, ys, xs]
+                    b[ys, xs] = res[r][1][ys, xs]
             ref = make()
             try:
                 if model == 'villain':
@@ -93,7 +96,7 @@ def _worker(rank, world, port, model, transport, predict, out):
             finally:
                 ref.close()
             ok = ((a == a2).all() and (b == b2).all() and res[0][2] == [(s.accepted, s.rejections) for s in st2]
-                  and res[1][2] == res[0][2] and res[0][3] == g2.bit_generator.state == res[1][3]
+                  and all(res[r][2] == res[0][2] and res[r][3] == g2.bit_generator.state for r in range(world))
                   and sum(r for _, r in res[0][2]) >= 1)
             with open(f'{out}.result', 'w') as f:
                 f.write('ok' if ok else f'mismatch: stats {res[0][2]} vs {[(s.accepted, s.rejections) for s in st2]}')
@@ -125,6 +128,28 @@ def test_two_ranks_one_gpu(model, transport, predict, tmp_path):
             pytest.fail('two-rank run did not finish in 240 s')
     if transport == 'rccl' and os.path.exists(f'{out}.refused'):
         pytest.xfail('RCCL refused two ranks on one device: ' + open(f'{out}.refused').read())
+    assert not os.path.exists(f'{out}.error'), open(f'{out}.error').read()
+    assert open(f'{out}.result').read() == 'ok'
+
+
+@pytest.mark.parametrize('tiles', [(2, 2), (2, 4)])
+@pytest.mark.parametrize('model', ['villain', 'worldline'])
+def test_more_ranks_one_gpu_hosted(model, tiles, tmp_path):
+    """The same with 4 and 8 ranks (2 x 2, 2 x 4: every rank exchanges with several peers, corners included, the
+    8-rank layout of BASELINE config 4) over the hosted transport, rejection prediction on (the multi-rank default)."""
+    import time
+
+    import torch.multiprocessing as mp
+    out = str(tmp_path / model)
+    world = tiles[0] * tiles[1]
+    ctx = mp.start_processes(_worker, args=(world, _free_port(), model, 'host', None, out, tiles), nprocs=world,
+                             join=False, start_method='spawn')
+    deadline = time.time() + 240
+    while not ctx.join(timeout=5):
+        if time.time() > deadline:
+            for p in ctx.processes:
+                p.kill()
+            pytest.fail(f'{world}-rank run did not finish in 240 s')
     assert not os.path.exists(f'{out}.error'), open(f'{out}.error').read()
     assert open(f'{out}.result').read() == 'ok'
 
