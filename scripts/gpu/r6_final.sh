@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 O=${OUT:-gpurun_out/r6_final}
 mkdir -p $O/bench
 export AMD_LOG_LEVEL=1
-step tests timeout -k 10 700 python -u -m pytest tests -q --timeout 300 --timeout-method thread -m gpu -p no:cacheprovider > $O/tests.log 2>&1
+step tests timeout -k 10 900 python -u -m pytest tests -q --timeout 300 --timeout-method thread -m gpu -p no:cacheprovider > $O/tests.log 2>&1
 tail -3 $O/tests.log
 grep -E "[0-9]+ passed" $O/tests.log > /dev/null && ! grep -E "[0-9]+ (failed|errors?)( |,|$)" $O/tests.log > /dev/null || { echo "[tests] not green"; exit 1; }
 unset AMD_LOG_LEVEL
