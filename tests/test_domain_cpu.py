@@ -201,3 +201,54 @@ def test_rccl_blocks_line_up(tiles, model, size):
             assert sum(L['words'][s] for s in dirs) == words
             for s in dirs:
                 assert L['soff'][s] - off == lay[b]['roff'][s] - roff
+
+
+def _hosted_worker(rank, world, port, tiles, errfile):
+    import ctypes
+
+    import torch.distributed as dist
+    from supervillain_amd.domain import HostTransport
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        Nt, Nx = 24 * tiles[0], 24 * tiles[1]
+        lay = message_layout(Nt, Nx, tiles, rank)
+        t = HostTransport()
+        # the library's call: this rank's messages {peer, offset, words} over host buffers, through the C callback
+        send = np.zeros(lay['msg_words'], dtype=np.uint64)
+        for peer, o, w in lay['sends']:
+            send[o:o + w] = (np.uint64(rank) << np.uint64(48)) + (np.uint64(peer) << np.uint64(32)) + np.arange(w, dtype=np.uint64)
+        recv = np.zeros(lay['msg_words'], dtype=np.uint64)
+        flat = lambda lst: (ctypes.c_int64 * max(1, 3 * len(lst)))(*[v for m in lst for v in m])  # noqa: E731
+        rc = t.xfer(None, len(lay['sends']), flat(lay['sends']), send.ctypes.data, len(lay['recvs']),
+                    flat(lay['recvs']), recv.ctypes.data)
+        assert rc == 0 and t.error is None, t.error
+        for peer, o, w in lay['recvs']:  # what the peer sent to this rank, in its own layout
+            exp = (np.uint64(peer) << np.uint64(48)) + (np.uint64(rank) << np.uint64(32)) + np.arange(w, dtype=np.uint64)
+            np.testing.assert_array_equal(recv[o:o + w], exp)
+        # the batch-summary all-gather: every rank's bytes, in rank order
+        nbytes = 40
+        mine = np.full(nbytes, rank + 1, dtype=np.uint8)
+        out = np.zeros(world * nbytes, dtype=np.uint8)
+        assert t.gather(None, mine.ctypes.data, out.ctypes.data, nbytes) == 0
+        np.testing.assert_array_equal(out, np.repeat(np.arange(1, world + 1, dtype=np.uint8), nbytes))
+    except Exception as e:
+        with open(errfile, 'a') as f:
+            f.write(f'rank {rank}: {e!r}\n')
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('tiles', [(1, 2), (2, 2)])
+def test_host_transport_callbacks(tiles, tmp_path):
+    """HostTransport (sv_domain_create_hosted's callbacks over gloo) moves each rank's per-peer messages to the offsets
+    the receivers' layout names, and all-gathers the batch summaries in rank order -- driven through the same ctypes
+    function pointers the library calls (the GPU suite runs it inside real multi-rank domains)."""
+    import torch.multiprocessing as mp
+    errfile = str(tmp_path / 'err.txt')
+    world = tiles[0] * tiles[1]
+    mp.start_processes(_hosted_worker, args=(world, _free_port(), tiles, errfile), nprocs=world, join=True,
+                       start_method='spawn')
+    assert not os.path.exists(errfile), open(errfile).read()
