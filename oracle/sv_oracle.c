@@ -53,9 +53,11 @@ typedef struct {
  * coexact.py:117, plaquette.py:88; the reference adds NumPy pairwise sums per colour).  It is kept here as the
  * exact sum of the probabilities rounded to 2^-103, T(p) = round(p 2^51) 2^52 + round(r 2^103) with r = p - (p
  * rounded to 2^-51), accumulated as three 38-bit limb sums and turned into a double by the same function as
- * libsvhip.so (supervillain_amd/csrc/common.h fx_add / fx_value): the device's value whatever its launch geometry,
- * within ~2 ulp of the exact sum of the p, so within rounding of the reference's pairwise sums.  The running sum
- * of the sv_stats being filled lives beside it (thread-local); a cleared or different sv_stats restarts it. */
+ * libsvhip.so (supervillain_amd/csrc/common.h fx_value): within ~2 ulp of the exact sum of the p, so within rounding
+ * of the reference's pairwise sums.  The device keeps only the first level, round(p 2^51) per proposal (one integer
+ * add, common.h fx_add), so device and oracle agree within 2^-52 per proposal (the GPU tests: 1e-12 relative), and
+ * the device's value is the same for every launch geometry.  The running sum of the sv_stats being filled lives
+ * beside it (thread-local); a cleared or different sv_stats restarts it. */
 #define FX_LIMB ((UINT64_C(1) << 38) - 1)
 static _Thread_local const sv_stats *fx_owner;
 static _Thread_local uint64_t fx_w[3];
